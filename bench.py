@@ -1,0 +1,172 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): images/sec for the whole node, SD2.1
+512x512, 50-step txt2img, batch 4 per GPU (bf16), plus p50 job latency.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one complete txt2img job per GPU: prompt encoding (OpenCLIP-H,
+CFG batch), 50 DPM-Solver++(2M) Karras denoising steps of the full SD2.1 UNet
+(865.9M params) on the CFG batch of 8 latents 64x64, VAE decode 512x512, uint8
+D2H, and JPEG/base64/sha256 result-envelope encoding (overlapped with the next
+job on a host thread, joined before the clock stops).  Data-parallel over GPUs
+(one process per GPU, weak scaling: 4 images per GPU per step); weights are
+random-init on every rank and distributed with a sharded RCCL all_gather
+(outside the timed region); each rank's final latents are all-gathered to
+every rank over xGMI (split-job assembly, inside the timed region).
+
+``--impl reference`` runs the same models with plain PyTorch ops (hipBLASLt
+GEMMs, MIOpen channels-last convs, SDPA) = the diffusers-style eager baseline
+("reference-on-MI355X") for the A/B.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+METRIC = ("images/sec (whole node) SD2.1 512×512 50-step txt2img at 1/2/4/8 MI355X; "
+          "p50 job latency")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4, help="images per GPU per job")
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--denoise-steps", type=int, default=50)
+    ap.add_argument("--family", default="sd21")
+    ap.add_argument("--impl", default="hip", choices=["hip", "reference"])
+    ap.add_argument("--guidance", type=float, default=7.5)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--device", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from chiaswarm_amd import ops
+    from chiaswarm_amd.output.processor import OutputProcessor
+    from chiaswarm_amd.parallel import comm
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+    from chiaswarm_amd.schedulers import get_scheduler
+
+    rank, local_rank, world = comm.init_distributed()
+    on_gpu = torch.cuda.is_available() and args.device != "cpu"
+    device = torch.device("cuda", local_rank) if on_gpu else torch.device("cpu")
+    if on_gpu:
+        torch.cuda.set_device(device)
+        torch.backends.cudnn.benchmark = True
+    ops.set_mode(args.impl)
+    if args.impl == "hip" and on_gpu:
+        ops._lib.load()  # fail loudly: the HIP path must be the one measured
+
+    t_load = time.perf_counter()
+    pipe = StableDiffusion(args.family, device=device, seed=1234)
+    if args.no_graphs:
+        pipe.use_graphs = False
+    # sharded RCCL distribution of the (random-init) weights to every GPU
+    for m in [pipe.unet, pipe.vae] + pipe.text_encoders:
+        comm.allgather_module(m)
+    load_s = time.perf_counter() - t_load
+
+    pool = cf.ThreadPoolExecutor(max_workers=2)
+    prompts = ["a photograph of an astronaut riding a horse", "a watercolor fox in a snowy forest",
+               "a cyberpunk city street at night, neon", "a bowl of ramen, studio lighting"]
+
+    def job(i):
+        g = torch.Generator(device=device).manual_seed(1000 * rank + i)
+        sched = get_scheduler("DPMSolverMultistepScheduler", prediction_type=pipe.family.prediction_type)
+        out = pipe(prompt=prompts[i % len(prompts)], negative_prompt="blurry, low quality",
+                   num_inference_steps=args.denoise_steps, guidance_scale=args.guidance,
+                   num_images_per_prompt=args.batch, height=args.res, width=args.res,
+                   generator=g, scheduler=sched)
+        gathered = comm.all_gather_tensor(out.latents.contiguous())  # split-job assembly over xGMI
+
+        def encode(images=out.images):
+            op = OutputProcessor(["primary"], "image/jpeg")
+            op.add_outputs(images)
+            return op.get_results()
+
+        return pool.submit(encode), out.timings, gathered.shape
+
+    futs = []
+    for i in range(args.warmup):
+        f, _, _ = job(i)
+        f.result()
+    if on_gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+    lat = []
+    timings = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ts = time.perf_counter()
+        f, tm, _ = job(args.warmup + i)
+        futs.append(f)
+        if on_gpu:
+            torch.cuda.synchronize()
+        lat.append(time.perf_counter() - ts)
+        timings.append(tm)
+    for f in futs:
+        f.result()
+    if on_gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+    elapsed = comm.max_over_ranks(time.perf_counter() - t0)
+    p50 = comm.max_over_ranks(statistics.median(lat))
+
+    images = args.batch * args.steps * world
+    ips = images / elapsed
+    if rank == 0:
+        phase = {k: round(1000 * statistics.median([t[k] for t in timings]), 2) for k in timings[0]}
+        rec = {
+            "metric": METRIC,
+            "value": round(ips, 4),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if on_gpu else "fp32",
+            "data": "synthetic prompts, random-init weights (no checkpoints offline)",
+            "config": {
+                "model": "SD2.1 (stable-diffusion-2-1-base arch: UNet 865.9M + OpenCLIP-H 340.4M + VAE 83.7M)",
+                "global_batch": args.batch * world,
+                "seq_len": (args.res // 8) ** 2,
+                "parallelism": f"dp{world}",
+                "resolution": f"{args.res}x{args.res}",
+                "denoise_steps": args.denoise_steps,
+                "scheduler": "DPMSolverMultistepScheduler (karras)",
+                "guidance_scale": args.guidance,
+                "impl": args.impl,
+                "hip_graphs": (not args.no_graphs) and args.impl == "hip",
+            },
+            "p50_job_latency_ms": round(1000 * p50, 1),
+            "phase_ms_median": phase,
+            "model_load_s": round(load_s, 2),
+        }
+        print(json.dumps(rec), flush=True)
+    pool.shutdown()
+    if comm.is_dist():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,333 @@
+"""Building blocks shared by every model family (UNet, VAE, ControlNet, CLIP,
+RRDBNet ...).  Parameter names follow the diffusers / transformers state-dict
+key layout so real safetensors checkpoints load unchanged (SURVEY.md §7.1
+"state_dict keys compatible with diffusers/HF safetensors"); the compute path
+uses *packed* copies made once by ``prepare()`` (NHWC conv weights, fused QKV,
+interleaved GEGLU, batched time-embedding projections).
+
+Reference behaviour these mirror: the diffusers pipelines invoked at
+swarm/diffusion/diffusion_func.py:96 (UNet / VAE / text encoder forward).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class Prepared(nn.Module):
+    """Mixin: ``prepare()`` builds packed inference buffers from parameters."""
+
+    def prepare(self):  # pragma: no cover - overridden
+        pass
+
+
+def prepare_model(model: nn.Module) -> nn.Module:
+    """Build packed buffers for every sub-module (call after loading weights)."""
+    for m in model.modules():
+        if isinstance(m, Prepared):
+            m.prepare()
+    if hasattr(model, "prepare_self"):
+        model.prepare_self()
+    return model
+
+
+class Linear(nn.Linear, Prepared):
+    """nn.Linear whose forward runs the MFMA GEMM (fused bias/act/residual)."""
+
+    def forward(self, x, residual=None, act=None):  # type: ignore[override]
+        return ops.gemm(x, self.weight, self.bias, residual=residual, act=act)
+
+
+class Conv2d(nn.Conv2d, Prepared):
+    """NHWC conv.  ``weight`` keeps the PyTorch [Cout, Cin, kh, kw] layout for
+    state-dict compatibility; ``wp`` is the packed [Cout, kh, kw, Cin] copy the
+    implicit-GEMM kernel reads."""
+
+    def prepare(self):
+        self.wp = ops.pack_conv_weight(self.weight.detach())
+
+    def _wp(self):
+        wp = getattr(self, "wp", None)
+        if wp is None or wp.device != self.weight.device or wp.dtype != self.weight.dtype:
+            self.prepare()
+        return self.wp
+
+    def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None):  # type: ignore[override]
+        kh, kw = self.kernel_size
+        if kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x:
+            w2 = self.weight.view(self.out_channels, self.in_channels)
+            y = ops.gemm(x, w2, self.bias, residual=residual)
+            if bias2d is not None:
+                y = y + bias2d[:, None, None, :].to(y.dtype)
+            return y
+        pad = self.padding[0] if padding is None else padding
+        return ops.conv2d(x, self._wp(), self.bias, self.stride[0], pad, residual=residual,
+                          up2x=up2x, bias2d=bias2d)
+
+
+class GroupNorm(nn.GroupNorm):
+    def forward(self, x, silu=False):  # type: ignore[override]
+        return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu=silu)
+
+
+class LayerNorm(nn.LayerNorm):
+    def forward(self, x):  # type: ignore[override]
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+# ----------------------------------------------------------------------------
+# Attention (self / cross), diffusers naming: to_q / to_k / to_v / to_out.0
+# ----------------------------------------------------------------------------
+class Attention(Prepared):
+    def __init__(self, query_dim, heads, dim_head, cross_dim=None, bias=False, out_bias=True,
+                 norm_groups=None, norm_eps=1e-6, residual=False):
+        super().__init__()
+        inner = heads * dim_head
+        self.heads, self.dim_head = heads, dim_head
+        self.is_cross = cross_dim is not None
+        kv_dim = cross_dim if cross_dim is not None else query_dim
+        self.to_q = Linear(query_dim, inner, bias=bias)
+        self.to_k = Linear(kv_dim, inner, bias=bias)
+        self.to_v = Linear(kv_dim, inner, bias=bias)
+        self.to_out = nn.ModuleList([Linear(inner, query_dim, bias=out_bias)])
+        self.group_norm = GroupNorm(norm_groups, query_dim, eps=norm_eps) if norm_groups else None
+        self.residual = residual
+        self.scale = 1.0 / math.sqrt(dim_head)
+
+    def prepare(self):
+        q, k, v = self.to_q, self.to_k, self.to_v
+        if self.is_cross:
+            self.w_kv = torch.cat([k.weight, v.weight], 0).detach()
+            self.b_kv = torch.cat([k.bias, v.bias], 0).detach() if k.bias is not None else None
+        else:
+            self.w_qkv = torch.cat([q.weight, k.weight, v.weight], 0).detach()
+            self.b_qkv = (torch.cat([q.bias, k.bias, v.bias], 0).detach()
+                          if q.bias is not None else None)
+
+    def _ensure(self):
+        attr = "w_kv" if self.is_cross else "w_qkv"
+        w = getattr(self, attr, None)
+        if w is None or w.device != self.to_q.weight.device or w.dtype != self.to_q.weight.dtype:
+            self.prepare()
+
+    def context_kv(self, ctx):
+        """K/V of a cross-attention for a fixed context: [B, Skv, 2, H, D].
+        Constant over all denoising steps -> computed once per request."""
+        self._ensure()
+        b, s, _ = ctx.shape
+        kv = ops.gemm(ctx, self.w_kv, self.b_kv)
+        return kv.view(b, s, 2, self.heads, self.dim_head)
+
+    def forward(self, x, ctx=None, kv=None, residual=None, causal=False):
+        """x: [B, S, C].  ``residual`` is added in the out-projection epilogue."""
+        self._ensure()
+        b, s, _ = x.shape
+        h, d = self.heads, self.dim_head
+        if self.is_cross:
+            q = self.to_q(x).view(b, s, h, d)
+            if kv is None:
+                kv = self.context_kv(ctx)
+            k, v = kv[:, :, 0], kv[:, :, 1]
+        else:
+            qkv = ops.gemm(x, self.w_qkv, self.b_qkv).view(b, s, 3, h, d)
+            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o = ops.attention(q, k, v, self.scale, causal=causal)
+        return self.to_out[0](o.reshape(b, s, h * d), residual=residual)
+
+
+class SpatialSelfAttention(Attention):
+    """Single-head VAE mid-block attention on NHWC maps (GroupNorm + residual)."""
+
+    def __init__(self, channels, norm_groups=32, eps=1e-6):
+        super().__init__(channels, 1, channels, bias=True, norm_groups=norm_groups, norm_eps=eps)
+
+    def forward(self, x):  # type: ignore[override]
+        b, hh, ww, c = x.shape
+        hN = self.group_norm(x).view(b, hh * ww, c)
+        out = super().forward(hN, residual=x.view(b, hh * ww, c))
+        return out.view(b, hh, ww, c)
+
+
+class GEGLU(Prepared):
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = Linear(dim_in, dim_out * 2)
+
+    def prepare(self):
+        self.wp, self.bp = ops.pack_geglu(self.proj.weight.detach(),
+                                          self.proj.bias.detach() if self.proj.bias is not None else None)
+
+    def forward(self, x):
+        wp = getattr(self, "wp", None)
+        if wp is None or wp.device != self.proj.weight.device or wp.dtype != self.proj.weight.dtype:
+            self.prepare()
+        return ops.gemm(x, self.wp, self.bp, act="geglu")
+
+
+class FeedForward(nn.Module):
+    """diffusers FeedForward(GEGLU): keys ff.net.0.proj / ff.net.2."""
+
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Identity(), Linear(inner, dim)])
+
+    def forward(self, x, residual=None):
+        return self.net[2](self.net[0](x), residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, heads, dim_head, cross_dim):
+        super().__init__()
+        self.norm1 = LayerNorm(dim)
+        self.attn1 = Attention(dim, heads, dim_head)
+        self.norm2 = LayerNorm(dim)
+        self.attn2 = Attention(dim, heads, dim_head, cross_dim=cross_dim)
+        self.norm3 = LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+    def forward(self, x, ctx=None, kv=None):
+        x = self.attn1(self.norm1(x), residual=x)
+        x = self.attn2(self.norm2(x), ctx=ctx, kv=kv, residual=x)
+        x = self.ff(self.norm3(x), residual=x)
+        return x
+
+
+class Transformer2D(nn.Module):
+    """Spatial transformer: GN -> proj_in -> N x BasicTransformerBlock -> proj_out (+x)."""
+
+    def __init__(self, channels, heads, cross_dim, layers=1, linear_proj=True, groups=32):
+        super().__init__()
+        dim_head = channels // heads
+        self.norm = GroupNorm(groups, channels, eps=1e-6)
+        self.linear_proj = linear_proj
+        if linear_proj:
+            self.proj_in = Linear(channels, channels)
+            self.proj_out = Linear(channels, channels)
+        else:
+            self.proj_in = Conv2d(channels, channels, 1)
+            self.proj_out = Conv2d(channels, channels, 1)
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(channels, heads, dim_head, cross_dim) for _ in range(layers)])
+
+    def cross_modules(self):
+        return [blk.attn2 for blk in self.transformer_blocks]
+
+    def forward(self, x, ctx=None, kvs=None):
+        b, hh, ww, c = x.shape
+        h = self.norm(x)
+        h = self.proj_in(h).view(b, hh * ww, c)
+        for i, blk in enumerate(self.transformer_blocks):
+            h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i])
+        out = self.proj_out(h.view(b, hh, ww, c), residual=x)
+        return out
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin, cout, temb_channels=None, groups=32, eps=1e-5, groups_out=None):
+        super().__init__()
+        self.norm1 = GroupNorm(groups, cin, eps=eps)
+        self.conv1 = Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = Linear(temb_channels, cout) if temb_channels else None
+        self.norm2 = GroupNorm(groups_out or groups, cout, eps=eps)
+        self.conv2 = Conv2d(cout, cout, 3, padding=1)
+        self.conv_shortcut = Conv2d(cin, cout, 1, padding=0) if cin != cout else None
+        self.out_channels = cout
+
+    def forward(self, x, temb_proj=None):
+        """``temb_proj``: this block's [B, Cout] time projection (already
+        computed by the model's batched time-embedding GEMM)."""
+        h = self.norm1(x, silu=True)
+        h = self.conv1(h, bias2d=temb_proj)
+        h = self.norm2(h, silu=True)
+        sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
+        return self.conv2(h, residual=sc)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, channels, padding=1):
+        super().__init__()
+        self.conv = Conv2d(channels, channels, 3, stride=2, padding=padding)
+        self.pad_asym = padding == 0  # VAE encoder: F.pad(0,1,0,1) then conv s2 p0
+
+    def forward(self, x):
+        if self.pad_asym:
+            return self.conv(x, padding=(0, 0, 1, 1))
+        return self.conv(x)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = Conv2d(channels, channels, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(x, up2x=True)
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos=True, shift=0.0,
+                       max_period=10000.0) -> torch.Tensor:
+    """Sinusoidal embedding (diffusers ``Timesteps``); fp32 output [B, dim]."""
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(half, dtype=torch.float32, device=t.device)
+    exponent = exponent / (half - shift)
+    emb = t.float()[:, None] * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin, dim):
+        super().__init__()
+        self.linear_1 = Linear(cin, dim)
+        self.linear_2 = Linear(dim, dim)
+
+    def forward(self, x):
+        return self.linear_2(self.linear_1(x, act="silu"))
+
+
+def init_random_(model: nn.Module, seed: int = 0, std_scale: float = 1.0):
+    """Deterministic random init (no checkpoints offline): N(0, 1/fan_in)
+    weights, zero biases, unit norms.  Keeps activations O(1) through deep
+    stacks so random-weight benchmarks do not overflow bf16."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if p.dim() >= 2:
+                fan_in = p[0].numel()
+                std = std_scale / math.sqrt(fan_in)
+                if name.endswith("embedding.weight") or "embedding" in name and p.dim() == 2 and "linear" not in name:
+                    std = 0.02
+                t = torch.randn(p.shape, generator=g, dtype=torch.float32) * std
+                p.copy_(t.to(p.dtype))
+            elif name.endswith("bias"):
+                p.zero_()
+            else:  # norm weights
+                p.fill_(1.0)
+    return model
+
+
+def init_random_fast_(model: nn.Module, seed: int = 0, std_scale: float = 1.0):
+    """Same distribution as ``init_random_`` but generated on the parameter's
+    device (seconds instead of minutes for 2.6B-parameter SDXL on the GPU)."""
+    dev = next(model.parameters()).device
+    g = torch.Generator(device=dev).manual_seed(seed)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if p.dim() >= 2:
+                fan_in = p[0].numel()
+                std = std_scale / math.sqrt(fan_in)
+                if "embedding" in name and "linear" not in name:
+                    std = 0.02
+                p.copy_((torch.randn(p.shape, generator=g, device=dev, dtype=torch.float32) * std).to(p.dtype))
+            elif name.endswith("bias"):
+                p.zero_()
+            else:
+                p.fill_(1.0)
+    return model

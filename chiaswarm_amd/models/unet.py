@@ -1,0 +1,254 @@
+"""UNet2DConditionModel (SD1.5 / SD2.x / SDXL configs) on NHWC bf16.
+
+Covers the denoiser reached by the reference's txt2img / img2img / inpaint /
+ControlNet / pix2pix / upscaler calls (swarm/diffusion/diffusion_func.py:96,
+swarm/diffusion/upscale.py:22, swarm/video/pix2pix.py:142).  Geometry from the
+public model configs (SURVEY.md §2.3 "Model geometry").
+
+MI355X-specific structure:
+  * all ResNet time projections of a step are ONE batched GEMM
+    (``prepare_self`` concatenates every ``time_emb_proj``), then each block
+    receives its [B, Cout] slice as a per-sample bias fused into conv1's
+    epilogue;
+  * cross-attention K/V of the (fixed) prompt context are computed once per
+    request by ``encode_context`` and re-used for every denoising step (K8);
+  * ControlNet residuals are added where the skip tensors are produced.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Sequence
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import (Conv2d, Downsample2D, GroupNorm, Linear, Prepared, ResnetBlock2D,
+                     TimestepEmbedding, Transformer2D, Upsample2D, timestep_embedding)
+
+
+@dataclasses.dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: Sequence[int] = (320, 640, 1280, 1280)
+    layers_per_block: int = 2
+    down_block_types: Sequence[str] = ("CrossAttnDownBlock2D",) * 3 + ("DownBlock2D",)
+    up_block_types: Sequence[str] = ("UpBlock2D",) + ("CrossAttnUpBlock2D",) * 3
+    num_heads: Sequence[int] | int = (5, 10, 20, 20)  # diffusers "attention_head_dim"
+    cross_attention_dim: int = 1024
+    use_linear_projection: bool = True
+    transformer_layers_per_block: Sequence[int] | int = 1
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-5
+    addition_embed_type: str | None = None  # "text_time" for SDXL
+    addition_time_embed_dim: int = 256
+    projection_class_embeddings_input_dim: int = 2816
+    prediction_type: str = "epsilon"
+    sample_size: int = 64
+    # sd-x2-latent-upscaler / x4 upscaler style extra conditioning
+    num_class_embeds: int | None = None
+    class_embed_type: str | None = None
+
+    def per_block(self, v, n):
+        return list(v) if isinstance(v, (list, tuple)) else [v] * n
+
+
+SD15 = UNetConfig(num_heads=8, cross_attention_dim=768, use_linear_projection=False)
+SD21 = UNetConfig()  # stabilityai/stable-diffusion-2-1-base (512^2, epsilon)
+SD21_V = dataclasses.replace(SD21, prediction_type="v_prediction", sample_size=96)
+SDXL = UNetConfig(
+    block_out_channels=(320, 640, 1280),
+    down_block_types=("DownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D"),
+    up_block_types=("CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "UpBlock2D"),
+    num_heads=(5, 10, 20), transformer_layers_per_block=(1, 2, 10),
+    cross_attention_dim=2048, addition_embed_type="text_time", sample_size=128)
+PIX2PIX = dataclasses.replace(SD15, in_channels=8)
+INPAINT_SD2 = dataclasses.replace(SD21, in_channels=9)
+# tiny config for CPU plumbing tests (same topology, small widths)
+TINY = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
+                  down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
+                  up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"),
+                  num_heads=(2, 2), cross_attention_dim=32, sample_size=8)
+
+CONFIGS = {"sd15": SD15, "sd21": SD21, "sd21-v": SD21_V, "sdxl": SDXL, "pix2pix": PIX2PIX,
+           "sd2-inpaint": INPAINT_SD2, "tiny": TINY}
+
+
+class _Block(nn.Module):
+    def __init__(self, resnets, attentions, sampler_attr, sampler):
+        super().__init__()
+        self.resnets = nn.ModuleList(resnets)
+        self.attentions = nn.ModuleList(attentions) if attentions else None
+        if sampler is not None:
+            setattr(self, sampler_attr, nn.ModuleList([sampler]))
+        else:
+            setattr(self, sampler_attr, None)
+
+
+class UNet2DConditionModel(Prepared):
+    def __init__(self, cfg: UNetConfig = SD21):
+        super().__init__()
+        self.cfg = cfg
+        ch = list(cfg.block_out_channels)
+        nb = len(ch)
+        heads = cfg.per_block(cfg.num_heads, nb)
+        tlayers = cfg.per_block(cfg.transformer_layers_per_block, nb)
+        temb_dim = ch[0] * 4
+        g, eps = cfg.norm_num_groups, cfg.norm_eps
+
+        self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, padding=1)
+        self.time_embedding = TimestepEmbedding(ch[0], temb_dim)
+        if cfg.addition_embed_type == "text_time":
+            self.add_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, temb_dim)
+        if cfg.class_embed_type == "timestep":
+            self.class_embedding = TimestepEmbedding(ch[0], temb_dim)
+
+        def resnet(ci, co):
+            return ResnetBlock2D(ci, co, temb_dim, g, eps)
+
+        def xformer(c, i):
+            return Transformer2D(c, heads[i], cfg.cross_attention_dim, tlayers[i],
+                                 cfg.use_linear_projection, g)
+
+        self.down_blocks = nn.ModuleList()
+        cout = ch[0]
+        for i, btype in enumerate(cfg.down_block_types):
+            cin, cout = cout, ch[i]
+            final = i == nb - 1
+            res = [resnet(cin if j == 0 else cout, cout) for j in range(cfg.layers_per_block)]
+            att = ([xformer(cout, i) for _ in range(cfg.layers_per_block)]
+                   if btype.startswith("CrossAttn") else None)
+            self.down_blocks.append(_Block(res, att, "downsamplers", None if final else Downsample2D(cout)))
+
+        self.mid_block = _Block([resnet(ch[-1], ch[-1]), resnet(ch[-1], ch[-1])],
+                                [xformer(ch[-1], nb - 1)], "upsamplers", None)
+
+        rch = list(reversed(ch))
+        rheads = list(reversed(heads))
+        rtl = list(reversed(tlayers))
+        self.up_blocks = nn.ModuleList()
+        out_c = rch[0]
+        for i, btype in enumerate(cfg.up_block_types):
+            prev_c, out_c = out_c, rch[i]
+            in_c = rch[min(i + 1, nb - 1)]
+            final = i == nb - 1
+            nl = cfg.layers_per_block + 1
+            res = []
+            for j in range(nl):
+                skip = in_c if j == nl - 1 else out_c
+                rin = prev_c if j == 0 else out_c
+                res.append(resnet(rin + skip, out_c))
+            att = None
+            if btype.startswith("CrossAttn"):
+                att = [Transformer2D(out_c, rheads[i], cfg.cross_attention_dim, rtl[i],
+                                     cfg.use_linear_projection, g) for _ in range(nl)]
+            self.up_blocks.append(_Block(res, att, "upsamplers", None if final else Upsample2D(out_c)))
+
+        self.conv_norm_out = GroupNorm(g, ch[0], eps=eps)
+        self.conv_out = Conv2d(ch[0], cfg.out_channels, 3, padding=1)
+
+    # ------------------------------------------------------------------
+    def _resnets(self):
+        out = []
+        for blk in list(self.down_blocks) + [self.mid_block] + list(self.up_blocks):
+            out.extend(blk.resnets)
+        return out
+
+    def prepare_self(self):
+        """Concatenate every ResNet's time_emb_proj into one [sum Cout, Temb] GEMM."""
+        rs = self._resnets()
+        self._temb_w = torch.cat([r.time_emb_proj.weight for r in rs], 0).detach()
+        self._temb_b = torch.cat([r.time_emb_proj.bias for r in rs], 0).detach()
+        self._temb_splits = [r.out_channels for r in rs]
+
+    def _temb_projs(self, temb):
+        w = getattr(self, "_temb_w", None)
+        if w is None or w.device != temb.device or w.dtype != self.conv_in.weight.dtype:
+            self.prepare_self()
+        proj = ops.gemm(ops.silu(temb), self._temb_w, self._temb_b)
+        return list(torch.split(proj, self._temb_splits, dim=-1))
+
+    def cross_attention_modules(self):
+        mods = []
+        for blk in list(self.down_blocks) + [self.mid_block] + list(self.up_blocks):
+            if blk.attentions is not None:
+                for t in blk.attentions:
+                    mods.extend(t.cross_modules())
+        return mods
+
+    @torch.no_grad()
+    def encode_context(self, ctx: torch.Tensor):
+        """Per-request cache of every cross-attention K/V (constant over steps)."""
+        return [m.context_kv(ctx) for m in self.cross_attention_modules()]
+
+    # ------------------------------------------------------------------
+    def time_embed(self, timestep, batch, dtype, added_cond=None, class_labels=None):
+        t = timestep
+        if not torch.is_tensor(t):
+            t = torch.tensor([t], dtype=torch.float32, device=self.conv_in.weight.device)
+        t = t.reshape(-1).float()
+        if t.numel() == 1:
+            t = t.expand(batch)
+        temb = self.time_embedding(timestep_embedding(t, self.cfg.block_out_channels[0]).to(dtype))
+        if self.cfg.addition_embed_type == "text_time":
+            text_embeds = added_cond["text_embeds"]
+            time_ids = added_cond["time_ids"]
+            tid = timestep_embedding(time_ids.reshape(-1), self.cfg.addition_time_embed_dim)
+            tid = tid.reshape(text_embeds.shape[0], -1)
+            add_in = torch.cat([text_embeds.float(), tid], dim=-1).to(dtype)
+            temb = temb + self.add_embedding(add_in)
+        if self.cfg.class_embed_type == "timestep" and class_labels is not None:
+            cl = timestep_embedding(class_labels.reshape(-1).float(), self.cfg.block_out_channels[0])
+            temb = temb + self.class_embedding(cl.to(dtype))
+        return temb
+
+    def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
+                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None):
+        """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout]."""
+        b = sample.shape[0]
+        dtype = self.conv_in.weight.dtype
+        x = sample.to(dtype)
+        temb = self.time_embed(timestep, b, dtype, added_cond, class_labels)
+        tprojs = iter(self._temb_projs(temb))
+        kv_iter = iter(cross_kv) if cross_kv is not None else None
+        ctx = encoder_hidden_states
+
+        def run_attn(t, h):
+            kvs = None
+            if kv_iter is not None:
+                kvs = [next(kv_iter) for _ in t.transformer_blocks]
+            return t(h, ctx=ctx, kvs=kvs)
+
+        h = self.conv_in(x)
+        skips = [h]
+        for blk in self.down_blocks:
+            for j, r in enumerate(blk.resnets):
+                h = r(h, next(tprojs))
+                if blk.attentions is not None:
+                    h = run_attn(blk.attentions[j], h)
+                skips.append(h)
+            if blk.downsamplers is not None:
+                h = blk.downsamplers[0](h)
+                skips.append(h)
+
+        if down_residuals is not None:
+            skips = [s + r.to(s.dtype) for s, r in zip(skips, down_residuals)]
+
+        h = self.mid_block.resnets[0](h, next(tprojs))
+        h = run_attn(self.mid_block.attentions[0], h)
+        h = self.mid_block.resnets[1](h, next(tprojs))
+        if mid_residual is not None:
+            h = h + mid_residual.to(h.dtype)
+
+        for blk in self.up_blocks:
+            for j, r in enumerate(blk.resnets):
+                s = skips.pop()
+                h = r(torch.cat([h, s], dim=-1), next(tprojs))
+                if blk.attentions is not None:
+                    h = run_attn(blk.attentions[j], h)
+            if blk.upsamplers is not None:
+                h = blk.upsamplers[0](h)
+
+        h = self.conv_norm_out(h, silu=True)
+        return self.conv_out(h)

@@ -1,0 +1,271 @@
+"""Op layer: every hot op of the UNet / VAE / text-encoder / RRDB stacks.
+
+Layout conventions (MI355X-first):
+  * image activations are NHWC  ``[B, H, W, C]`` (C contiguous) end to end;
+  * token activations are ``[B, S, C]``;
+  * conv weights are packed ``[Cout, kh, kw, Cin]`` (K-contiguous rows of the
+    implicit GEMM), linear weights ``[N, K]``;
+  * attention q/k/v are ``[B, S, H, D]`` views (D contiguous; any B/S/H strides),
+    so a fused QKV projection output ``[B, S, 3, H, D]`` is consumed in place.
+
+Each op has one plain-PyTorch definition (``_ref_*``), used for CPU tensors and
+in ``reference`` mode, and one gfx950 kernel in libcsk.so (``hip_ops``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .mode import get_mode, ops_mode, set_mode, use_hip  # noqa: F401
+
+GEGLU_BLOCK = 16  # row-interleave granularity of packed GEGLU weights
+
+
+# ----------------------------------------------------------------------------
+# GEMM  (Linear / 1x1 conv)
+# ----------------------------------------------------------------------------
+def pack_geglu(w: torch.Tensor, b: torch.Tensor | None):
+    """[2F, K] (hidden rows then gate rows, diffusers GEGLU order) ->
+    rows interleaved in blocks of 16: h0..h15, g0..g15, h16..h31, ...
+    so one 16-column MFMA output sub-tile pair holds (hidden, gate) for the same
+    output columns in the same lane: the GEGLU epilogue needs no shuffle."""
+    two_f, k = w.shape
+    f = two_f // 2
+    assert f % GEGLU_BLOCK == 0
+    wp = w.view(2, f // GEGLU_BLOCK, GEGLU_BLOCK, k).transpose(0, 1).reshape(two_f, k)
+    bp = None
+    if b is not None:
+        bp = b.view(2, f // GEGLU_BLOCK, GEGLU_BLOCK).transpose(0, 1).reshape(two_f)
+    return wp.contiguous(), (bp.contiguous() if bp is not None else None)
+
+
+def _gelu_f(x):
+    return F.gelu(x)
+
+
+def _cdt(t):
+    """Reference compute dtype: fp32 on CPU; the tensor's own dtype on GPU (so
+    ``reference`` mode on MI355X is the diffusers-style bf16 eager baseline:
+    hipBLASLt GEMMs, MIOpen channels-last convs, SDPA attention)."""
+    return torch.float32 if not t.is_cuda else t.dtype
+
+
+def _ref_gemm(a2, w, bias, residual, act):
+    dt = _cdt(a2)
+    if bias is not None:
+        y = torch.addmm(bias.to(dt), a2.to(dt), w.to(dt).t())
+    else:
+        y = a2.to(dt) @ w.to(dt).t()
+    if act == "geglu":
+        m, n = y.shape
+        y = y.view(m, n // (2 * GEGLU_BLOCK), 2, GEGLU_BLOCK)
+        y = (y[:, :, 0, :] * _gelu_f(y[:, :, 1, :])).reshape(m, n // 2)
+    elif act == "gelu":
+        y = _gelu_f(y)
+    elif act == "silu":
+        y = F.silu(y)
+    elif act == "quick_gelu":
+        y = y * torch.sigmoid(1.702 * y)
+    if residual is not None:
+        y = y + residual.reshape(y.shape).to(dt)
+    return y.to(a2.dtype)
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None):
+    """y[..., N'] = act(a[..., K] @ w[N, K]^T + bias) + residual.
+
+    ``act='geglu'`` expects ``pack_geglu`` weights and returns N' = N/2."""
+    lead = a.shape[:-1]
+    k = a.shape[-1]
+    a2 = a.reshape(-1, k)
+    if use_hip(a):
+        from . import hip_ops
+
+        y = hip_ops.gemm(a2, w, bias, residual, act)
+    else:
+        y = _ref_gemm(a2, w, bias, residual, act)
+    return y.view(*lead, y.shape[-1])
+
+
+# ----------------------------------------------------------------------------
+# Conv2d NHWC (implicit GEMM)
+# ----------------------------------------------------------------------------
+def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, kh, kw] (PyTorch/diffusers) -> [Cout, kh, kw, Cin]."""
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
+def norm_padding(padding):
+    """int p -> (top, left, bottom, right)."""
+    if isinstance(padding, int):
+        return (padding,) * 4
+    assert len(padding) == 4
+    return tuple(int(p) for p in padding)
+
+
+def conv_out_size(h, w, kh, kw, stride, padding, up2x=False):
+    pt, pl, pb, pr = norm_padding(padding)
+    if up2x:
+        h, w = 2 * h, 2 * w
+    return (h + pt + pb - kh) // stride + 1, (w + pl + pr - kw) // stride + 1
+
+
+def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
+    dt = _cdt(x)
+    # NHWC tensor viewed as channels-last NCHW: no copies, MIOpen NHWC kernels
+    xn = x.to(dt).permute(0, 3, 1, 2)
+    if up2x:
+        xn = F.interpolate(xn, scale_factor=2.0, mode="nearest")
+    pt, pl, pb, pr = norm_padding(padding)
+    w = wp.to(dt).permute(0, 3, 1, 2)
+    b = bias.to(dt) if bias is not None else None
+    if pt == pb and pl == pr:
+        y = F.conv2d(xn, w, b, stride=stride, padding=(pt, pl))
+    else:
+        y = F.conv2d(F.pad(xn, (pl, pr, pt, pb)), w, b, stride=stride)
+    y = y.permute(0, 2, 3, 1)
+    if bias2d is not None:
+        y = y + bias2d.to(dt)[:, None, None, :]
+    if residual is not None:
+        y = y + residual.to(dt)
+    return y.to(x.dtype).contiguous()
+
+
+def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None):
+    """NHWC conv.  ``wp``: packed [Cout, kh, kw, Cin].  ``up2x`` fuses a
+    nearest-neighbour x2 upsample into the input addressing; ``bias2d`` [B, Cout]
+    is a per-sample channel bias (ResNet time-embedding add) fused in the
+    epilogue; ``residual`` [B, Ho, Wo, Cout] is added in the epilogue."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d)
+    return _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d)
+
+
+# ----------------------------------------------------------------------------
+# Normalisation
+# ----------------------------------------------------------------------------
+def _ref_group_norm(x, gamma, beta, groups, eps, silu):
+    dt = _cdt(x)
+    c = x.shape[-1]
+    xn = x.to(dt).movedim(-1, 1)  # channels-last view [B, C, ...]
+    y = F.group_norm(xn, groups, gamma.to(dt), beta.to(dt), eps)
+    if silu:
+        y = F.silu(y)
+    return y.movedim(1, -1).to(x.dtype).contiguous()
+
+
+def group_norm(x, gamma, beta, groups=32, eps=1e-5, silu=False):
+    """GroupNorm over a channels-last tensor [B, ..., C] (+ optional fused SiLU)."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.group_norm(x, gamma, beta, groups, eps, silu)
+    return _ref_group_norm(x, gamma, beta, groups, eps, silu)
+
+
+def _ref_layer_norm(x, gamma, beta, eps):
+    dt = _cdt(x)
+    return F.layer_norm(x.to(dt), (x.shape[-1],), gamma.to(dt), beta.to(dt), eps).to(x.dtype)
+
+
+def layer_norm(x, gamma, beta, eps=1e-5):
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.layer_norm(x, gamma, beta, eps)
+    return _ref_layer_norm(x, gamma, beta, eps)
+
+
+# ----------------------------------------------------------------------------
+# Attention
+# ----------------------------------------------------------------------------
+def _ref_attention(q, k, v, scale, causal):
+    # [B,S,H,D] -> [B,H,S,D]
+    if q.is_cuda:
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                           is_causal=causal, scale=scale)
+        return o.transpose(1, 2).contiguous()
+    qt, kt, vt = (t.permute(0, 2, 1, 3).float() for t in (q, k, v))
+    s = (qt @ kt.transpose(-1, -2)) * scale
+    if causal:
+        sq, sk = s.shape[-2], s.shape[-1]
+        mask = torch.ones(sq, sk, dtype=torch.bool, device=s.device).triu(1 + sk - sq)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = p @ vt
+    return o.permute(0, 2, 1, 3).to(q.dtype).contiguous()
+
+
+def attention(q, k, v, scale=None, causal=False):
+    """softmax(q k^T * scale) v for [B, S, H, D] views; returns [B, Sq, H, D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if use_hip(q):
+        from . import hip_ops
+
+        return hip_ops.attention(q, k, v, scale, causal)
+    return _ref_attention(q, k, v, scale, causal)
+
+
+# ----------------------------------------------------------------------------
+# Elementwise
+# ----------------------------------------------------------------------------
+def silu(x):
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.silu(x)
+    return F.silu(x.to(_cdt(x))).to(x.dtype)
+
+
+def add(x, y):
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.add(x, y)
+    return (x.to(_cdt(x)) + y.to(_cdt(x))).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------
+# Sampler step (CFG combine + x0 + linear update) and VAE post-process
+# ----------------------------------------------------------------------------
+def _ref_sched_step(e, x, prev_x0, c, guidance, noise):
+    ef = e.float()
+    if guidance is not None:
+        e_u, e_c = ef.chunk(2)
+        ef = e_u + guidance * (e_c - e_u)
+    x0 = c.p * x + c.q * ef
+    out = c.A * x + c.B * x0
+    if c.C != 0.0 and prev_x0 is not None:
+        out = out + c.C * prev_x0
+    if c.D != 0.0 and noise is not None:
+        out = out + c.D * noise
+    return out, x0
+
+
+def sched_step(e, x, sched, coeffs, guidance=None, noise=None):
+    """Fused CFG + sampler update.  Updates ``sched`` state
+    (prev_x0, step_index) and returns the new fp32 latents."""
+    prev = sched.prev_x0
+    if use_hip(x):
+        from . import hip_ops
+
+        out, x0 = hip_ops.sched_step(e, x, prev, coeffs, guidance, noise)
+    else:
+        out, x0 = _ref_sched_step(e, x, prev, coeffs, guidance, noise)
+    sched.prev_x0 = x0
+    sched.step_index += 1
+    return out
+
+
+def vae_postprocess(img):
+    """NHWC [-1, 1] -> uint8 NHWC (x/2+0.5).clamp(0,1)*255 rounded (K15)."""
+    if use_hip(img):
+        from . import hip_ops
+
+        return hip_ops.vae_postprocess(img)
+    return ((img.float() / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)

@@ -1,0 +1,86 @@
+"""Loader for the in-tree HIP kernel library (``chiaswarm_amd/lib/libcsk.so``).
+
+The kernels live in ``csrc/kernels/*.hip`` and are compiled for gfx950 by
+``chiaswarm_amd/_build.py`` (``hipcc --offload-arch=gfx950 -shared``).  Every
+launcher is an ``extern "C"`` function taking raw device pointers, sizes and a
+``hipStream_t``; we call them through ctypes with torch's *current* stream so
+they are captured by ``torch.cuda.CUDAGraph`` (= hipGraph on ROCm) like any
+other kernel.
+
+Policy (see README "no silent fallback"): on a GPU box the library MUST load;
+if it does not, every GPU op raises.  The torch reference implementations in
+``ops/*`` are used only for CPU tensors (plumbing tests, BASELINE config #1) or
+when a caller explicitly selects ``reference`` mode for A/B numerics.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_LIB = None
+_LOCK = threading.Lock()
+_LOAD_ERR: Exception | None = None
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libcsk.so")
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_int64 = ctypes.c_int64
+
+# name -> argtypes.  Every launcher returns int (hipError_t).
+_SIGS: dict[str, list] = {}
+
+
+def sig(name: str, *argtypes):
+    _SIGS[name] = list(argtypes)
+
+
+def load():
+    """Load libcsk.so (idempotent).  Raises if it is missing or broken."""
+    global _LIB, _LOAD_ERR
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not os.path.exists(LIB_PATH):
+            _LOAD_ERR = FileNotFoundError(
+                f"{LIB_PATH} not built: run `python -m chiaswarm_amd._build`"
+            )
+            raise _LOAD_ERR
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        _LIB = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args):
+    lib = load()
+    fn = getattr(lib, name)
+    err = fn(*args)
+    if err != 0:
+        raise RuntimeError(f"HIP kernel launcher {name} failed with hipError {err}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,138 @@
+"""Result envelope encoding (hive-visible, must match the reference byte-for-
+byte in structure): ARTIFACT = {blob: base64, content_type, thumbnail: base64
+JPEG 100x100 "web_low", sha256_hash: hex sha256 of the blob bytes}.
+
+Reference semantics re-implemented here:
+  * OutputProcessor / make_result / make_text_result:  swarm/output_processor.py:10-70
+    (text artifacts hash the *string*, not the blob: :69 — replicated);
+  * thumbnail:        swarm/output_processor.py:73-79;
+  * error image:      swarm/output_processor.py:82-87;
+  * grid policy 1/2/<=4/<=6/<=9, >9 -> ValueError: swarm/output_processor.py:90-107;
+  * PNG / JPEG(web_high, optimize, progressive) else ValueError: :121-136.
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import io
+import json
+
+from PIL import Image, ImageDraw
+
+THUMB = (100, 100)
+
+
+class OutputProcessor:
+    def __init__(self, output_list, main_content_type):
+        self.outputs: list = []
+        self.other_outputs: dict = {}
+        self.output_list = list(output_list or ["primary"])
+        self.main_content_type = main_content_type
+
+    def add_outputs(self, images):
+        self.outputs.extend(images)
+
+    def add_other_outputs(self, name, images):
+        self.other_outputs[name] = images
+
+    def get_results(self) -> dict:
+        results = {}
+        if "primary" in self.output_list:
+            buf = image_to_buffer(post_process(self.outputs), self.main_content_type)
+            results["primary"] = make_result(buf, buf, self.main_content_type)
+        for key, images in self.other_outputs.items():
+            buf = image_to_buffer(post_process(images), self.main_content_type)
+            results[key] = make_result(buf, buf, self.main_content_type)
+        return results
+
+
+def _b64(b: bytes) -> str:
+    return base64.b64encode(b).decode("UTF-8")
+
+
+def _getvalue(buf) -> bytes:
+    return buf.getvalue() if isinstance(buf, io.BytesIO) else bytes(buf)
+
+
+def make_result(buffer, thumb, content_type) -> dict:
+    if thumb is None:
+        tb = image_to_buffer(image_from_text(content_type, THUMB, 1), "image/jpeg", "web_low")
+    else:
+        tb = make_thumbnail(thumb)
+    data = _getvalue(buffer)
+    return {
+        "blob": _b64(data),
+        "content_type": content_type,
+        "thumbnail": _b64(tb.getvalue()),
+        "sha256_hash": hashlib.sha256(data).hexdigest(),
+    }
+
+
+def make_text_result(string: str) -> dict:
+    tb = image_to_buffer(image_from_text("text/plain", THUMB, 1), "image/jpeg", "web_low")
+    return {
+        "blob": _b64(json.dumps({"caption": string}).encode("utf-8")),
+        "content_type": "application/json",
+        "thumbnail": _b64(tb.getvalue()),
+        "sha256_hash": hashlib.sha256(string.encode()).hexdigest(),
+    }
+
+
+def make_thumbnail(buffer) -> io.BytesIO:
+    if not isinstance(buffer, io.BytesIO):
+        buffer = io.BytesIO(buffer)
+    buffer.seek(0)
+    image = Image.open(buffer).convert("RGB")
+    image.thumbnail(THUMB, Image.Resampling.LANCZOS)
+    return image_to_buffer(image, "image/jpeg", "web_low")
+
+
+def image_from_text(text, size=(512, 512), color=0) -> Image.Image:
+    image = Image.new(mode="RGB", size=size, color=color)
+    ImageDraw.Draw(image).multiline_text((5, 5), str(text))
+    return image
+
+
+def grid_shape(n: int):
+    if n == 1:
+        return 1, 1
+    if n == 2:
+        return 1, 2
+    if n <= 4:
+        return 2, 2
+    if n <= 6:
+        return 2, 3
+    if n <= 9:
+        return 3, 3
+    raise ValueError(f"Too many images ({n}) for post-processing. Maximum supported images: 9")
+
+
+def post_process(images):
+    n = len(images)
+    rows, cols = grid_shape(n)
+    if n == 1:
+        return images[0]
+    return image_grid(images, rows, cols)
+
+
+def image_grid(images, rows, cols) -> Image.Image:
+    w, h = images[0].size
+    grid = Image.new("RGB", size=(cols * w, rows * h))
+    for i, im in enumerate(images[: rows * cols]):
+        r, c = divmod(i, cols)
+        grid.paste(im, box=(c * w, r * h))
+    return grid
+
+
+def image_to_buffer(image, content_type, quality="web_high") -> io.BytesIO:
+    if not content_type.startswith("image"):
+        raise ValueError(f"Unsupported content type: {content_type}")
+    buf = io.BytesIO()
+    if content_type == "image/png":
+        image.save(buf, format="PNG")
+    elif content_type == "image/jpeg":
+        image.save(buf, format="JPEG", quality=quality, optimize=True, progressive=True)
+    else:
+        raise ValueError(f"Invalid image format: {content_type}")
+    buf.seek(0)
+    return buf

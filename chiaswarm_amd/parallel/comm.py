@@ -1,0 +1,146 @@
+"""Intra-node RCCL communication (torch.distributed backend "nccl" == RCCL on
+ROCm) over xGMI.  The reference has no collectives at all (all its
+parallelism is one job per GPU); these are the north-star additions:
+
+  * ``allgather_module``: every rank holds/loads 1/N of a model's bytes and one
+    ``all_gather_into_tensor`` per dtype-bucket assembles the full copy on all
+    GPUs (each GPU reads only 1/N over its own PCIe link; xGMI does the rest);
+  * ``broadcast_module``: rank-0-loads fallback, bucketed;
+  * ``all_gather_tensor``: split-job latent / image assembly.
+
+Buckets are large (default 512 MiB): with 288 GB HBM per GPU there is no
+reason to chunk finely, and fewer, larger collectives keep each xGMI link busy.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+BUCKET_BYTES = 512 << 20
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_distributed(backend: str | None = None, timeout_s: int = 600):
+    """Initialise the process group from torchrun env vars (one rank per GPU)."""
+    rank, local_rank, world = env_rank()
+    if world <= 1:
+        return rank, local_rank, world
+    if dist.is_initialized():
+        return rank, local_rank, world
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", local_rank)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, local_rank, world
+
+
+def is_dist():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def barrier():
+    if is_dist():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def _buckets(tensors, limit=BUCKET_BYTES):
+    """Group tensors by dtype into buckets of <= limit bytes (order preserved)."""
+    by_dtype: dict = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for _, ts in by_dtype.items():
+        cur, size = [], 0
+        for t in ts:
+            nb = t.numel() * t.element_size()
+            if cur and size + nb > limit:
+                yield cur
+                cur, size = [], 0
+            cur.append(t)
+            size += nb
+        if cur:
+            yield cur
+
+
+def _state_tensors(module):
+    return [p.data for p in module.parameters()] + [b for b in module.buffers()]
+
+
+@torch.no_grad()
+def broadcast_module(module: torch.nn.Module, src: int = 0, bucket_bytes=BUCKET_BYTES):
+    if not is_dist():
+        return module
+    for bucket in _buckets(_state_tensors(module), bucket_bytes):
+        flat = torch.cat([t.reshape(-1) for t in bucket])
+        dist.broadcast(flat, src)
+        off = 0
+        for t in bucket:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n
+    return module
+
+
+@torch.no_grad()
+def allgather_module(module: torch.nn.Module, bucket_bytes=BUCKET_BYTES):
+    """Sharded distribution: rank r contributes elements [r*L, (r+1)*L) of each
+    flattened bucket (the part it loaded from host); one all_gather per bucket
+    rebuilds the full bucket on every rank."""
+    if not is_dist():
+        return module
+    world, rank = dist.get_world_size(), dist.get_rank()
+    for bucket in _buckets(_state_tensors(module), bucket_bytes):
+        flat = torch.cat([t.reshape(-1) for t in bucket])
+        n = flat.numel()
+        shard = (n + world - 1) // world
+        padded = torch.zeros(shard * world, dtype=flat.dtype, device=flat.device)
+        padded[:n] = flat
+        mine = padded[rank * shard:(rank + 1) * shard].clone()
+        dist.all_gather_into_tensor(padded, mine)
+        off = 0
+        for t in bucket:
+            k = t.numel()
+            t.copy_(padded[off:off + k].view_as(t))
+            off += k
+    return module
+
+
+def all_gather_tensor(x: torch.Tensor) -> torch.Tensor:
+    """Concatenate equal-shaped per-rank tensors along dim 0 on every rank."""
+    if not is_dist():
+        return x
+    world = dist.get_world_size()
+    out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous())
+    return out
+
+
+def max_over_ranks(value: float) -> float:
+    if not is_dist():
+        return value
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def module_checksum(module: torch.nn.Module) -> float:
+    s = 0.0
+    for t in _state_tensors(module):
+        s += float(t.float().sum().item())
+    return s
