@@ -1,0 +1,95 @@
+"""Build the in-tree HIP kernel library for gfx950.
+
+    python -m chiaswarm_amd._build [--force] [-j N]
+
+Compiles every ``csrc/kernels/*.hip`` with ``hipcc --offload-arch=gfx950 -O3``
+into objects under ``build/`` (content-hash cached) and links them into
+``chiaswarm_amd/lib/libcsk.so``.  No torch headers are involved, so a full
+rebuild takes seconds; the library is loaded with ctypes (``ops/_lib.py``).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "csrc", "kernels")
+BUILD = os.path.join(ROOT, "build", "csk")
+OUT = os.path.join(ROOT, "chiaswarm_amd", "lib", "libcsk.so")
+ARCH = os.environ.get("CSK_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+         "-Wno-unused-result"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _digest(path: str, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    with open(path, "rb") as f:
+        h.update(f.read())
+    for hdr in sorted(glob.glob(os.path.join(SRC, "*.h"))):
+        with open(hdr, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str, force: bool) -> str:
+    name = os.path.splitext(os.path.basename(src))[0]
+    dig = _digest(src, " ".join(FLAGS))
+    obj = os.path.join(BUILD, f"{name}.{dig}.o")
+    if os.path.exists(obj) and not force:
+        return obj
+    cmd = [hipcc(), *FLAGS, "-I", SRC, "-c", src, "-o", obj + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(SRC, "*.hip")))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    key = hashlib.sha256("".join(objs).encode()).hexdigest()[:16]
+    stamp = OUT + ".stamp"
+    if os.path.exists(OUT) and not force and os.path.exists(stamp) and open(stamp).read() == key:
+        os.utime(OUT)
+        if verbose:
+            print(f"[csk] up to date: {OUT}")
+        return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(OUT + ".tmp", OUT)
+    with open(stamp, "w") as f:
+        f.write(key)
+    if verbose:
+        print(f"[csk] built {OUT} from {len(srcs)} sources")
+    return OUT
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args(argv)
+    build(a.force, a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -18,6 +18,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import _lib  # noqa: F401
 from .mode import get_mode, ops_mode, set_mode, use_hip  # noqa: F401
 
 GEGLU_BLOCK = 16  # row-interleave granularity of packed GEGLU weights

@@ -40,6 +40,26 @@ def sig(name: str, *argtypes):
     _SIGS[name] = list(argtypes)
 
 
+def _maybe_rebuild():
+    """Rebuild libcsk.so if any csrc/kernels source is newer than it (a stale
+    library with an old launcher signature would be called with the wrong
+    arguments).  Needs hipcc, which both this image and the GPU boxes have."""
+    src_dir = os.path.join(os.path.dirname(LIB_DIR), "..", "csrc", "kernels")
+    src_dir = os.path.normpath(src_dir)
+    if not os.path.isdir(src_dir) or os.environ.get("CSK_NO_AUTOBUILD"):
+        return
+    srcs = [os.path.join(src_dir, f) for f in os.listdir(src_dir) if f.endswith((".hip", ".h"))]
+    newest = max((os.path.getmtime(s) for s in srcs), default=0.0)
+    if os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+        return
+    try:
+        from .. import _build
+
+        _build.build(verbose=False)
+    except Exception as e:  # surfaced by the existence check / first call
+        print(f"[csk] rebuild failed: {e}")
+
+
 def load():
     """Load libcsk.so (idempotent).  Raises if it is missing or broken."""
     global _LIB, _LOAD_ERR
@@ -48,6 +68,7 @@ def load():
     with _LOCK:
         if _LIB is not None:
             return _LIB
+        _maybe_rebuild()
         if not os.path.exists(LIB_PATH):
             _LOAD_ERR = FileNotFoundError(
                 f"{LIB_PATH} not built: run `python -m chiaswarm_amd._build`"
@@ -74,9 +95,17 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_BOUND: dict = {}
+
+
 def call(name: str, *args):
-    lib = load()
-    fn = getattr(lib, name)
+    fn = _BOUND.get(name)
+    if fn is None:
+        lib = load()
+        fn = getattr(lib, name)
+        fn.argtypes = _SIGS[name]
+        fn.restype = c_int
+        _BOUND[name] = fn
     err = fn(*args)
     if err != 0:
         raise RuntimeError(f"HIP kernel launcher {name} failed with hipError {err}")

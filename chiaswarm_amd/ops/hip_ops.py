@@ -1,2 +1,228 @@
-"""ctypes bindings of the gfx950 kernels in libcsk.so (filled per kernel)."""
+"""ctypes bindings of the gfx950 kernels in libcsk.so.
+
+Every function allocates its output with the torch caching allocator and
+launches on torch's current stream (graph-capture safe: no host syncs, no
+hipMalloc).  Shape/stride preconditions are checked on the host BEFORE launch
+so a bad call raises here instead of faulting the GPU.
+"""
 from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import c_float, c_int, c_int64, c_void_p, sig
+
+ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "geglu": 3, "quick_gelu": 4}
+
+sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p)
+sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p)
+sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_float, c_int, c_void_p)
+sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
+sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
+    c_int, c_float, c_int, c_void_p)
+sig("csk_silu", c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+    c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p)
+sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_softmax_rows", c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
+sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
+
+
+def _bf16(t, name):
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: HIP kernels take bfloat16, got {t.dtype}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _s():
+    return _lib.stream_ptr()
+
+
+def _round8(n):
+    return (n + 7) // 8 * 8
+
+
+def pad_last(x: torch.Tensor, n: int) -> torch.Tensor:
+    """Zero-pad the last (contiguous) dim of a bf16 tensor to n."""
+    c = x.shape[-1]
+    if c == n:
+        return x
+    x = x.contiguous()
+    y = torch.empty(x.shape[:-1] + (n,), dtype=x.dtype, device=x.device)
+    rows = x.numel() // c
+    _lib.call("csk_pad_channels", _p(y), _p(x), rows, c, n, _s())
+    return y
+
+
+# ---------------------------------------------------------------------------
+def gemm(a2, w, bias=None, residual=None, act=None, out=None):
+    _bf16(a2, "gemm.a")
+    _bf16(w, "gemm.w")
+    M, K = a2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"gemm: K mismatch {a2.shape} x {w.shape}")
+    if a2.stride(1) != 1 or a2.stride(0) % 8 != 0 or (a2.data_ptr() % 16):
+        a2 = a2.contiguous()
+    if w.stride(1) != 1 or w.stride(0) % 8 != 0:
+        w = w.contiguous()
+    if K % 8 != 0:
+        kp = _round8(K)
+        a2 = pad_last(a2, kp)
+        w = pad_last(w, kp)
+        K = kp
+    code = ACT[act]
+    n_out = N // 2 if code == 3 else N
+    if out is None:
+        out = torch.empty((M, n_out), dtype=torch.bfloat16, device=a2.device)
+    if residual is not None:
+        residual = residual.reshape(M, n_out)
+        _bf16(residual, "gemm.residual")
+        if not residual.is_contiguous():
+            residual = residual.contiguous()
+    if bias is not None:
+        _bf16(bias, "gemm.bias")
+    _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
+              M, N, K, a2.stride(0), w.stride(0), n_out, 1, code, _s())
+    return out
+
+
+def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
+    from . import conv_out_size, norm_padding
+
+    _bf16(x, "conv.x")
+    _bf16(wp, "conv.w")
+    x = x.contiguous()
+    B, H, W, Cin = x.shape
+    Cout, kh, kw, Cw = wp.shape
+    if Cw != Cin:
+        raise ValueError(f"conv2d: Cin mismatch {x.shape} vs {wp.shape}")
+    if Cin % 8 != 0:
+        cp = _round8(Cin)
+        x = pad_last(x, cp)
+        wp = pad_last(wp.contiguous(), cp)
+        Cin = cp
+    pt, pl, pb, pr = norm_padding(padding)
+    Ho, Wo = conv_out_size(H, W, kh, kw, stride, padding, up2x)
+    y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
+    if residual is not None:
+        residual = residual.contiguous()
+        if residual.shape != y.shape:
+            raise ValueError(f"conv2d residual {tuple(residual.shape)} != {tuple(y.shape)}")
+    if bias2d is not None:
+        bias2d = bias2d.contiguous()
+        if bias2d.shape != (B, Cout):
+            raise ValueError("conv2d bias2d shape")
+    _lib.call("csk_conv2d", _p(y), _p(x), _p(wp.contiguous()), _p(bias), _p(bias2d), _p(residual),
+              B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), _s())
+    return y
+
+
+def group_norm(x, gamma, beta, groups, eps, silu):
+    _bf16(x, "group_norm.x")
+    x = x.contiguous()
+    B, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (B * C)
+    nchunk = max(1, min(P, -(-2048 // B)))
+    chunk = -(-P // nchunk)
+    nchunk = -(-P // chunk)
+    part = torch.empty(B * nchunk * groups * 3, dtype=torch.float32, device=x.device)
+    y = torch.empty_like(x)
+    _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
+              float(eps), int(bool(silu)), _s())
+    return y
+
+
+def layer_norm(x, gamma, beta, eps):
+    _bf16(x, "layer_norm.x")
+    x = x.contiguous()
+    C = x.shape[-1]
+    y = torch.empty_like(x)
+    _lib.call("csk_layer_norm", _p(y), _p(x), _p(gamma), _p(beta), x.numel() // C, C, float(eps), _s())
+    return y
+
+
+def attention(q, k, v, scale, causal=False):
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _bf16(t, "attention." + n)
+        if t.stride(-1) != 1:
+            raise ValueError("attention: last dim must be contiguous")
+    B, Sq, H, D = q.shape
+    Skv = k.shape[1]
+    if D > 256:
+        return _attention_gemm(q, k, v, scale)
+    o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+    st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
+    _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
+              _s())
+    return o
+
+
+def _attention_gemm(q, k, v, scale):
+    """Large head dim (VAE mid-block, d=512): S = Q K^T (MFMA GEMM) ->
+    row softmax kernel -> O = P V (MFMA GEMM against V^T)."""
+    B, Sq, H, D = q.shape
+    Skv = k.shape[1]
+    o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+    for b in range(B):
+        for h in range(H):
+            qb, kb, vb = q[b, :, h], k[b, :, h], v[b, :, h]
+            s = gemm(qb, kb)
+            p = torch.empty_like(s)
+            _lib.call("csk_softmax_rows", _p(p), _p(s), Sq, Skv, float(scale), _s())
+            o[b, :, h] = gemm(p, vb.t().contiguous())
+    return o
+
+
+def silu(x):
+    _bf16(x, "silu")
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    if x.numel() % 8:
+        return torch.nn.functional.silu(x)
+    _lib.call("csk_silu", _p(y), _p(x), x.numel(), _s())
+    return y
+
+
+def add(x, y):
+    _bf16(x, "add")
+    x, y = x.contiguous(), y.contiguous().to(x.dtype)
+    out = torch.empty_like(x)
+    if x.numel() % 8 or x.shape != y.shape:
+        return x + y
+    _lib.call("csk_add", _p(out), _p(x), _p(y), x.numel(), _s())
+    return out
+
+
+def sched_step(e, x, prev_x0, c, guidance, noise):
+    _bf16(e, "sched_step.e")
+    x = x.contiguous()
+    n = x.numel()
+    cfg = guidance is not None
+    if e.numel() != n * (2 if cfg else 1):
+        raise ValueError("sched_step: model output / latent size mismatch")
+    xn = torch.empty_like(x)
+    x0 = torch.empty_like(x)
+    _lib.call("csk_sched_step", _p(xn), _p(x0), _p(e.contiguous()), _p(x),
+              _p(prev_x0) if (prev_x0 is not None and c.C != 0.0) else None,
+              _p(noise) if (noise is not None and c.D != 0.0) else None, n,
+              float(c.p), float(c.q), float(c.A), float(c.B), float(c.C), float(c.D),
+              float(guidance or 0.0), int(cfg), _s())
+    return xn, x0
+
+
+def vae_postprocess(img):
+    _bf16(img, "vae_post")
+    img = img.contiguous()
+    y = torch.empty(img.shape, dtype=torch.uint8, device=img.device)
+    _lib.call("csk_vae_post", _p(y), _p(img), img.numel(), _s())
+    return y

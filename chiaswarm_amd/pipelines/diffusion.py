@@ -1,0 +1,116 @@
+"""Stable-Diffusion-family job callback (reference:
+swarm/diffusion/diffusion_func.py:14-124).
+
+Same contract: ``diffusion_callback(device_identifier, model_name, **kwargs) ->
+(artifacts, pipeline_config)``; kwargs not consumed here are forwarded to the
+pipeline call (the hive drives guidance_scale, negative_prompt, strength,
+num_images_per_prompt, height, width, ...).  Differences by design: models
+come from the resident cache (no per-job reload), no CPU offload / xformers /
+VAE slicing heuristics (288 GB HBM), and the optional x2 latent upscale is
+applied to every image (the reference returned only images[0],
+swarm/diffusion/upscale.py:28-32).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+
+from ..output.processor import OutputProcessor
+from ..runtime.model_cache import cache, find_weights
+from ..schedulers import get_scheduler
+from .sd import StableDiffusion, family_for_model
+
+_DROP = ("supports_xformers", "cross_attention_kwargs", "eta", "callback", "callback_steps", "output_type",
+         "return_dict", "prompt_embeds", "negative_prompt_embeds", "guidance_rescale", "clip_skip")
+
+
+def load_sd(model_name: str, device_identifier: str, revision: str = "main", controlnet_name: str | None = None,
+            controlnet_revision: str = "main") -> StableDiffusion:
+    fam = family_for_model(model_name)
+
+    def make():
+        return StableDiffusion(fam, device=device_identifier, weights_dir=find_weights(model_name, revision),
+                               seed=abs(hash(model_name)) % (1 << 31))
+
+    pipe = cache().get(("sd", model_name, revision, device_identifier), make)
+    pipe.controlnet = None
+    if controlnet_name:
+        from .controlnet import load_controlnet
+
+        pipe.controlnet = load_controlnet(controlnet_name, pipe, device_identifier, controlnet_revision)
+    return pipe
+
+
+def _apply_lora(pipe, lora, scale):
+    from ..models.lora import load_lora
+
+    try:
+        load_lora(pipe.unet, lora, scale)
+    except Exception as e:
+        raise ValueError(f"Could not load lora \n{lora}\nIt might be incompatible with {pipe.family.name}\n{e}") from e
+
+
+def _apply_textual_inversion(pipe, ti, model_name):
+    from ..models.lora import load_textual_inversion
+
+    try:
+        load_textual_inversion(pipe, ti)
+    except Exception as e:
+        raise ValueError(f"Textual inversion\n{ti}\nis incompatible with\n{model_name}\n\n{e}") from e
+
+
+def diffusion_callback(device_identifier, model_name, **kwargs):
+    t0 = time.perf_counter()
+    scheduler_type = kwargs.pop("scheduler_type", "DPMSolverMultistepScheduler")
+    pipeline_type = kwargs.pop("pipeline_type", "DiffusionPipeline")
+    upscale = kwargs.pop("upscale", False)
+    textual_inversion = kwargs.pop("textual_inversion", None)
+    lora = kwargs.pop("lora", None)
+    cross_attention_scale = kwargs.pop("cross_attention_scale", 1.0)
+    revision = kwargs.pop("revision", "main")
+    kwargs.pop("variant", None)
+    for k in _DROP:
+        kwargs.pop(k, None)
+    output_processor = OutputProcessor(kwargs.pop("outputs", ["primary"]), kwargs.pop("content_type", "image/jpeg"))
+
+    controlnet_name = kwargs.pop("controlnet_model_name", None)
+    controlnet_revision = kwargs.pop("controlnet_revision", "main")
+    if kwargs.pop("save_preprocessed_input", False) and kwargs.get("image") is not None:
+        output_processor.add_other_outputs("preprocessed_input", [kwargs.get("image")])
+
+    pipe = load_sd(model_name, device_identifier, revision, controlnet_name, controlnet_revision)
+    if textual_inversion is not None:
+        _apply_textual_inversion(pipe, textual_inversion, model_name)
+    if lora is not None:
+        _apply_lora(pipe, lora, cross_attention_scale)
+
+    sched = get_scheduler(scheduler_type, prediction_type=pipe.family.prediction_type)
+    load_s = time.perf_counter() - t0
+    try:
+        p = pipe(scheduler=sched, **kwargs)
+    finally:
+        if lora is not None:
+            from ..models.lora import unload_lora
+
+            unload_lora(pipe.unet)
+
+    config = dict(pipe.config)
+    config["scheduler"] = ["chiaswarm_amd", sched.name]
+    config["_pipeline_type"] = str(pipeline_type)
+    if any(bool(x) for x in (p.nsfw_content_detected or [])):
+        config["nsfw"] = True
+
+    images = p.images
+    if upscale:
+        from .upscale import upscale_images
+
+        images = upscale_images(images, device_identifier, kwargs.get("prompt", ""), kwargs.get("generator"))
+    output_processor.add_outputs(images)
+    results = output_processor.get_results()
+    if os.environ.get("SDAAS_TIMINGS"):
+        t = dict(p.timings or {})
+        t["load"] = load_s
+        config["timings"] = {k: round(v, 4) for k, v in t.items()}
+    return results, config

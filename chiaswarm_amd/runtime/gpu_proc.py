@@ -1,0 +1,44 @@
+"""One OS process per GPU: the reference ran every GPU as a
+thread of one Python process (swarm/generator.py:13-14, one shared GIL); here
+each GPU gets its own process that owns its HBM-resident model cache, runs jobs
+and encodes results (JPEG/base64/sha256) locally.
+
+This module must not import torch at import time: the child selects its GPU via
+HIP_VISIBLE_DEVICES *before* torch initialises.
+"""
+from __future__ import annotations
+
+import os
+import traceback
+
+
+def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
+    """Child entry point.  inbox: job dicts (None = stop); outbox: (gpu, job_id, result|None, err)."""
+    if gpu_index != "cpu":
+        os.environ["HIP_VISIBLE_DEVICES"] = str(gpu_index)
+        os.environ["CUDA_VISIBLE_DEVICES"] = str(gpu_index)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k, v in (env or {}).items():
+        os.environ[k] = v
+    from ..log_setup import setup_logging
+    from ..settings import load_settings, resolve_path
+    from .device import Device
+    from .generator import synchronous_do_work_function
+
+    settings = load_settings()
+    try:
+        setup_logging(resolve_path(settings.log_filename), settings.log_level, suffix=f"gpu{gpu_index}")
+    except Exception:
+        pass
+    device = Device("cpu" if gpu_index == "cpu" else 0)
+    outbox.put((gpu_index, "__ready__", None, device.descriptor()))
+    while True:
+        job = inbox.get()
+        if job is None:
+            break
+        jid = job.get("id")
+        try:
+            result = synchronous_do_work_function(job, device)
+            outbox.put((gpu_index, jid, result, None))
+        except BaseException as e:  # never let the loop die silently
+            outbox.put((gpu_index, jid, None, f"{e}\n{traceback.format_exc()}"))

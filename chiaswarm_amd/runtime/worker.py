@@ -1,0 +1,241 @@
+"""The worker daemon (reference: swarm/worker.py:34-195).
+
+asyncio supervisor: poll the hive -> bounded work queue (depth = #devices) ->
+one executor per device -> result queue -> POST results.  Poll cadence, queue
+depth, error backoff and hive endpoints are the reference's.
+
+MI355X-first changes:
+  * ``ProcessExecutor``: one OS process per GPU (HIP_VISIBLE_DEVICES=i), so
+    the eight GPUs of a node do not share a GIL and each keeps its own resident
+    models; results are encoded in the GPU's process.
+  * per-GPU watchdog: a crashed / hung child is restarted and its in-flight job
+    is reported as a NON-fatal error (the hive may retry it), SURVEY §5.3.
+  * ``ThreadExecutor`` (reference-style, in-process) for CPU plumbing runs and
+    tests.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import multiprocessing as mp
+import os
+import threading
+import time
+
+from .. import __version__
+from ..hive.client import HiveClient
+from ..settings import load_settings, resolve_path
+
+
+def visible_gpus(settings) -> list:
+    if settings.gpus:
+        return [int(x) for x in str(settings.gpus).split(",") if x.strip() != ""]
+    try:
+        import torch  # counting devices does not initialise HIP on this image
+
+        return list(range(torch.cuda.device_count()))
+    except Exception:
+        return []
+
+
+class ThreadExecutor:
+    def __init__(self, device_id="cpu"):
+        from .device import Device
+
+        self.device = Device(device_id)
+        self.name = self.device.descriptor()
+
+    async def run(self, job):
+        from .generator import do_work
+
+        return await do_work(job, self.device)
+
+    def close(self):
+        pass
+
+
+class ProcessExecutor:
+    def __init__(self, gpu_index, env=None, job_timeout_s: float = 1800.0):
+        self.gpu_index = gpu_index
+        self.env = dict(env or {})
+        self.job_timeout_s = job_timeout_s
+        self.ctx = mp.get_context("spawn")
+        self.name = f"gpu{gpu_index}"
+        self.pending: dict = {}
+        self.loop = None
+        self._start()
+
+    def _start(self):
+        from .gpu_proc import gpu_main
+
+        self.inbox = self.ctx.Queue()
+        self.outbox = self.ctx.Queue()
+        self.proc = self.ctx.Process(target=gpu_main, args=(self.gpu_index, self.inbox, self.outbox, self.env),
+                                     daemon=True, name=f"chiaswarm-gpu{self.gpu_index}")
+        self.proc.start()
+        self.reader = threading.Thread(target=self._read, args=(self.outbox,), daemon=True)
+        self.reader.start()
+
+    def _read(self, outbox):
+        while True:
+            try:
+                item = outbox.get()
+            except (EOFError, OSError):
+                return
+            if item is None:
+                return
+            _, jid, result, err = item
+            if jid == "__ready__":
+                print(f"Started device {err}")
+                continue
+            fut = self.pending.pop(jid, None)
+            if fut is not None and self.loop is not None:
+                self.loop.call_soon_threadsafe(_resolve, fut, (result, err))
+
+    def _restart(self):
+        try:
+            self.proc.kill()
+        except Exception:
+            pass
+        self.proc.join(timeout=10)
+        self._start()
+
+    async def run(self, job):
+        from .generator import _error_result
+
+        self.loop = asyncio.get_running_loop()
+        fut = self.loop.create_future()
+        jid = job.get("id")
+        self.pending[jid] = fut
+        self.inbox.put(job)
+        t0 = time.monotonic()
+        while True:
+            done, _ = await asyncio.wait({fut}, timeout=2.0)
+            if done:
+                result, err = fut.result()
+                if result is not None:
+                    return result
+                return _error_result(jid, RuntimeError(f"worker error: {err}"), job.get("content_type", "image/jpeg"),
+                                     False)
+            if not self.proc.is_alive() or time.monotonic() - t0 > self.job_timeout_s:
+                why = "crashed" if not self.proc.is_alive() else "timed out"
+                logging.error(f"{self.name} {why} on job {jid}; restarting")
+                self.pending.pop(jid, None)
+                self._restart()
+                return _error_result(jid, RuntimeError(f"GPU worker {why}"), job.get("content_type", "image/jpeg"),
+                                     False)
+
+    def close(self):
+        try:
+            self.inbox.put(None)
+            self.proc.join(timeout=10)
+        finally:
+            if self.proc.is_alive():
+                self.proc.kill()
+
+
+def _resolve(fut, value):
+    if not fut.done():
+        fut.set_result(value)
+
+
+class Supervisor:
+    def __init__(self, settings=None, executors=None, hive=None):
+        self.settings = settings or load_settings()
+        self.hive = hive or HiveClient(self.settings)
+        self.executors = executors if executors is not None else self._default_executors()
+        n = max(1, len(self.executors))
+        self.work_queue: asyncio.Queue = asyncio.Queue(maxsize=n)
+        self.result_queue: asyncio.Queue = asyncio.Queue()
+        self.busy = 0
+        self.results_submitted = 0
+        self.stop = asyncio.Event()
+
+    def _default_executors(self):
+        gpus = visible_gpus(self.settings)
+        if not gpus:
+            return [ThreadExecutor("cpu")]
+        return [ProcessExecutor(g) for g in gpus]
+
+    async def device_worker(self, ex):
+        while True:
+            job = await self.work_queue.get()
+            self.busy += 1
+            try:
+                result = await ex.run(job)
+                await self.result_queue.put(result)
+            except Exception as e:
+                logging.exception(e)
+                print(f"device_worker {e}")
+            finally:
+                self.busy -= 1
+                self.work_queue.task_done()
+
+    async def result_worker(self):
+        while True:
+            result = await self.result_queue.get()
+            try:
+                print("Result complete")
+                await self.hive.submit_result(result)
+                self.results_submitted += 1
+            except Exception as e:
+                logging.exception(e)
+                print(f"result_worker {e}")
+            finally:
+                self.result_queue.task_done()
+
+    async def run(self, max_polls: int | None = None):
+        logging.info(f"worker {__version__}")
+        tasks = [asyncio.create_task(self.device_worker(ex)) for ex in self.executors]
+        tasks.append(asyncio.create_task(self.result_worker()))
+        polls = 0
+        try:
+            while not self.stop.is_set():
+                while (self.work_queue.full() or self.busy + self.work_queue.qsize() >= len(self.executors)) \
+                        and not self.stop.is_set():
+                    await asyncio.sleep(0.05 if max_polls else 1)
+                jobs, sleep_s = await self.hive.ask_for_work()
+                for job in jobs:
+                    await self.work_queue.put(job)
+                polls += 1
+                if max_polls is not None and polls >= max_polls:
+                    break
+                try:
+                    await asyncio.wait_for(self.stop.wait(), timeout=sleep_s)
+                except asyncio.TimeoutError:
+                    pass
+            await self.work_queue.join()
+            await self.result_queue.join()
+        finally:
+            for t in tasks:
+                t.cancel()
+
+
+def startup(settings=None, require_gpu=True):
+    from ..log_setup import setup_logging
+
+    s = settings or load_settings()
+    setup_logging(resolve_path(s.log_filename), s.log_level)
+    logging.info(f"Version {__version__}")
+    if require_gpu and not visible_gpus(s) and not os.environ.get("SDAAS_ALLOW_CPU"):
+        raise Exception("No GPU present (set SDAAS_ALLOW_CPU=1 for a CPU plumbing run). Quitting.")
+    return s
+
+
+async def run_worker(max_polls=None):
+    s = startup()
+    sup = Supervisor(s)
+    print(f"Found {len(sup.executors)} devices")
+    try:
+        await sup.run(max_polls=max_polls)
+    finally:
+        for ex in sup.executors:
+            ex.close()
+
+
+def main():
+    asyncio.run(run_worker())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,261 @@
+// Flash-style fused attention forward, bf16 in/out, fp32 softmax (SURVEY K7/K8,
+// K14 causal for CLIP).  O = softmax(Q K^T * scale) V for [B, S, H, D] strided
+// views (D contiguous), so fused QKV projection outputs are consumed in place.
+//
+// CDNA4 structure ("swapped" QK^T, everything lane-local):
+//   * workgroup = 4 waves; each wave owns QT x 16 query rows; KV blocks of 64 keys
+//     are register-staged into double-buffered, XOR-swizzled LDS tiles (one
+//     barrier per block).
+//   * S^T = K Q^T with v_mfma_f32_16x16x32_bf16 (A = K rows from LDS via
+//     ds_read_b128, B = Q fragments held in registers for the whole loop): the
+//     accumulator puts ONE query column on each lane and 4 consecutive keys in
+//     its registers, so the online-softmax row max / sum are in-lane plus two
+//     cross-group shuffles, and the rescale factor is a per-lane scalar.
+//   * O^T = V^T P^T: P^T comes straight from the S^T accumulators (converted to
+//     bf16, no lane movement) by permuting the k order of the PV MFMA; the
+//     matching V^T operand is fetched with ds_read_b64_tr_b16 (gfx950 hardware
+//     transpose read) from the same row-major V tile.
+//   * exp2 with log2(e)*scale folded in; masked keys (tail, causal) -> -inf.
+#include "common.h"
+
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+template <int CPR>
+__device__ __forceinline__ int kv_off(int row, int chunk) {
+  // element offset of 16-byte chunk `chunk` of row `row` in a [64][CPR*8] tile
+  constexpr int MASK = CPR >= 16 ? 15 : CPR - 1;
+  return row * (CPR * 8) + ((chunk ^ (row & MASK)) << 3);
+}
+
+struct AttnArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* o;
+  long long sqb, sqs, sqh;  // element strides of q (b, s, h)
+  long long skb, sks, skh;
+  long long svb, svs, svh;
+  long long sob, sos, soh;
+  int B, H, Sq, Skv, D;
+  float scale_log2;
+  int causal;
+};
+
+template <int DP, int QT>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
+  constexpr int CPR = DP / 8;          // 16B chunks per K/V row
+  constexpr int KB = 64;               // keys per block
+  constexpr int DS = DP / 32;          // k-steps of S = K Q^T over d
+  constexpr int DT = DP / 16;          // O^T d-tiles
+  constexpr int QROWS = QT * 16 * 4;   // query rows per workgroup
+  constexpr int TILE = KB * DP;        // elements per K or V tile
+  constexpr int LPT = KB * CPR / 256;  // 16B chunks per thread per tile
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // K0 V0 K1 V1
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nqb = (a.Sq + QROWS - 1) / QROWS;
+  const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qb * QROWS + wid * QT * 16;
+
+  const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
+  const bf16_t* kp = a.k + b * a.skb + h * a.skh;
+  const bf16_t* vp = a.v + b * a.svb + h * a.svh;
+
+  // Q fragments (B operand): lane holds Q[q0 + qt*16 + fr][ds*32 + 8*fg .. +7]
+  v8s qf[QT][DS];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      const int qi = q0 + qt * 16 + fr, d = ds * 32 + 8 * fg;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qi < a.Sq && d < a.D) v = *reinterpret_cast<const uint4*>(qp + qi * a.sqs + d);
+      qf[qt][ds] = __builtin_bit_cast(v8s, v);
+    }
+
+  v4f oacc[DT][QT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < QT; ++j) oacc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  float mrow[QT], lrow[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
+
+  int kv_end = a.Skv;
+  if (a.causal) {  // keys beyond the last query row of this workgroup are never visible
+    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (a.Skv - a.Sq);
+    kv_end = min(a.Skv, qlast + 1);
+  }
+  const int nkb = (kv_end + KB - 1) / KB;
+
+  uint4 rk[LPT], rv[LPT];
+  auto load_kv = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      const int key = kb * KB + row, d = c * 8;
+      uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (key < a.Skv && d < a.D) {
+        vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
+        vv = *reinterpret_cast<const uint4*>(vp + key * a.svs + d);
+      }
+      rk[i] = vk;
+      rv[i] = vv;
+    }
+  };
+  auto store_kv = [&](int buf) {
+    bf16_t* ks = smem + buf * 2 * TILE;
+    bf16_t* vs = ks + TILE;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
+      *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
+    }
+  };
+
+  if (nkb > 0) {
+    load_kv(0);
+    store_kv(0);
+  }
+  __syncthreads();
+  const float sl2 = a.scale_log2;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) load_kv(kb + 1);
+    const bf16_t* ks = smem + cur * 2 * TILE;
+    const bf16_t* vs = ks + TILE;
+
+    // ---- S^T = K Q^T : 4 key tiles x QT query tiles ----
+    v4f s[4][QT];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, ds * 4 + fg));
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[kt][qt], 0, 0, 0);
+      }
+    }
+    // ---- online softmax (per lane: one query column, 16 keys) ----
+    const int kbase = kb * KB;
+    v8s pf[2][QT];  // P^T fragments for the two 32-key PV k-steps
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      const int qi = q0 + qt * 16 + fr + (a.Skv - a.Sq);
+      float mx = -1e30f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kbase + kt * 16 + 4 * fg + r;
+          float x = s[kt][qt][r] * sl2;
+          if (key >= kv_end || (a.causal && key > qi)) x = -INFINITY;
+          s[kt][qt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrow[qt], mx);
+      const float alpha = exp2f(mrow[qt] - mnew);
+      mrow[qt] = mnew;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[kt][qt][r] - mnew);
+          s[kt][qt][r] = p;
+          ls += p;
+        }
+      lrow[qt] = lrow[qt] * alpha + ls;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
+#pragma unroll
+      for (int kp2 = 0; kp2 < 2; ++kp2) {
+        u32 w0 = pack2(s[2 * kp2][qt][0], s[2 * kp2][qt][1]);
+        u32 w1 = pack2(s[2 * kp2][qt][2], s[2 * kp2][qt][3]);
+        u32 w2 = pack2(s[2 * kp2 + 1][qt][0], s[2 * kp2 + 1][qt][1]);
+        u32 w3 = pack2(s[2 * kp2 + 1][qt][2], s[2 * kp2 + 1][qt][3]);
+        pf[kp2][qt] = __builtin_bit_cast(v8s, make_uint4(w0, w1, w2, w3));
+      }
+    }
+    // ---- O^T += V^T P^T ; V^T fragments via ds_read_b64_tr_b16 ----
+#pragma unroll
+    for (int kp2 = 0; kp2 < 2; ++kp2) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        // group fg reads rows (keys) kp2*32 + 4*fg + {0..3} and kp2*32 + 16 + 4*fg + {0..3},
+        // lane 4q+p of the group addresses row q, columns dt*16 + 4p .. +3
+        const int qq = fr >> 2, pp = fr & 3;
+        const int col = dt * 16 + 4 * pp;
+        const int r0 = kp2 * 32 + 4 * fg + qq, r1 = r0 + 16;
+        const bf16_t* a0 = vs + kv_off<CPR>(r0, col >> 3) + (col & 7);
+        const bf16_t* a1 = vs + kv_off<CPR>(r1, col >> 3) + (col & 7);
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
+        v8s vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          oacc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kp2][qt], oacc[dt][qt], 0, 0, 0);
+      }
+    }
+    if (kb + 1 < nkb) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: reduce l over the 4 lane groups, normalise, store ----
+  bf16_t* op = a.o + b * a.sob + h * a.soh;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float l = lrow[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    const int qi = q0 + qt * 16 + fr;
+    if (qi >= a.Sq) continue;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d = dt * 16 + 4 * fg;
+      if (d >= a.D) continue;
+      uint2 w;
+      w.x = pack2(oacc[dt][qt][0] * inv, oacc[dt][qt][1] * inv);
+      w.y = pack2(oacc[dt][qt][2] * inv, oacc[dt][qt][3] * inv);
+      *reinterpret_cast<uint2*>(op + qi * a.sos + d) = w;
+    }
+  }
+}
+
+template <int DP, int QT>
+static int launch_attn(const AttnArgs& a, hipStream_t s) {
+  constexpr int QROWS = QT * 64;
+  const int nqb = (a.Sq + QROWS - 1) / QROWS;
+  attn_fwd_kernel<DP, QT><<<a.B * a.H * nqb, 256, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
+                          int Sq, int Skv, int D, float scale, int causal, hipStream_t stream) {
+  // strides: q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h) in elements
+  if (D % 8 != 0 || D > 256) return (int)hipErrorInvalidValue;
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
+  a.sqb = strides[0]; a.sqs = strides[1]; a.sqh = strides[2];
+  a.skb = strides[3]; a.sks = strides[4]; a.skh = strides[5];
+  a.svb = strides[6]; a.svs = strides[7]; a.svh = strides[8];
+  a.sob = strides[9]; a.sos = strides[10]; a.soh = strides[11];
+  a.B = B; a.H = H; a.Sq = Sq; a.Skv = Skv; a.D = D;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.causal = causal;
+  if (D <= 64) return launch_attn<64, 2>(a, stream);
+  if (D <= 128) return launch_attn<128, 2>(a, stream);
+  return launch_attn<256, 1>(a, stream);
+}

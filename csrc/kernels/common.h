@@ -1,0 +1,77 @@
+// Shared helpers for the gfx950 (CDNA4, wave64) kernels of chiaswarm_amd.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short bf16_t;  // storage type of bfloat16
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef unsigned int u32;
+
+#define CSK_API extern "C" __attribute__((visibility("default")))
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((u32)x) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ u32 pack2(float lo, float hi) {
+  return (u32)f2bf(lo) | ((u32)f2bf(hi) << 16);
+}
+
+// 8 bf16 <-> 8 floats through a 16-byte vector
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float qgelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Chan et al. parallel combination of (count, mean, M2) partial moments.
+__device__ __forceinline__ void chan_combine(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  float nn = n + nb;
+  if (nn <= 0.f) return;
+  float d = meanb - mean;
+  float r = nb / nn;
+  mean += d * r;
+  m2 += m2b + d * d * n * r;
+  n = nn;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (MI355X: 8 XCDs, blocks
+// dealt round-robin; consecutive remapped ids land on one XCD's L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int NX = 8;
+  if (nwg < NX) return bid;
+  int q = nwg / NX, r = nwg % NX, x = bid % NX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / NX;
+}
+
+#define CSK_CHECK_LAUNCH() return (int)hipGetLastError()

@@ -1,0 +1,179 @@
+// Streaming kernels: SiLU, add, fused sampler step, VAE post-process
+// to uint8 (K15), row softmax (VAE single-head attention), channel padding.
+// All bf16 traffic is 16 bytes per lane (8 elements), grid-strided.
+#include "common.h"
+
+static inline int ew_grid(size_t nvec) {
+  size_t g = (nvec + 255) / 256;
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+__global__ void silu_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(x[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
+    y[i] = pack8(f);
+  }
+}
+
+CSK_API int csk_silu(void* y, const void* x, long long n, hipStream_t stream) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  size_t nv = n / 8;
+  silu_kernel<<<ew_grid(nv), 256, 0, stream>>>((const uint4*)x, (uint4*)y, nv);
+  CSK_CHECK_LAUNCH();
+}
+
+__global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b, uint4* __restrict__ y, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float fa[8], fb[8];
+    unpack8(a[i], fa);
+    unpack8(b[i], fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] += fb[j];
+    y[i] = pack8(fa);
+  }
+}
+
+CSK_API int csk_add(void* y, const void* a, const void* b, long long n, hipStream_t stream) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  size_t nv = n / 8;
+  add_kernel<<<ew_grid(nv), 256, 0, stream>>>((const uint4*)a, (const uint4*)b, (uint4*)y, nv);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
+// Fused sampler step.  e: UNet output bf16 [(cfg?2:1)*n] (uncond half first),
+// x, x0prev, noise: fp32 [n]; writes x_next fp32, x0 fp32.
+//   e_g = e_u + g (e_c - e_u);  x0 = p x + q e_g;
+//   x_next = A x + B x0 + C x0prev + D noise
+// --------------------------------------------------------------------------
+struct StepC {
+  float p, q, A, B, C, D, g;
+  int cfg, has_prev, has_noise;
+};
+
+__global__ void sched_step_kernel(const bf16_t* __restrict__ e, const float* __restrict__ x,
+                                  const float* __restrict__ x0prev, const float* __restrict__ noise,
+                                  float* __restrict__ xn, float* __restrict__ x0o, size_t n4, size_t n, StepC c) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 xv = reinterpret_cast<const float4*>(x)[i];
+    uint2 eu = reinterpret_cast<const uint2*>(e)[i];
+    float ev[4] = {__uint_as_float(eu.x << 16), __uint_as_float(eu.x & 0xffff0000u), __uint_as_float(eu.y << 16),
+                   __uint_as_float(eu.y & 0xffff0000u)};
+    if (c.cfg) {
+      uint2 ec = reinterpret_cast<const uint2*>(e + n)[i];
+      float cv[4] = {__uint_as_float(ec.x << 16), __uint_as_float(ec.x & 0xffff0000u), __uint_as_float(ec.y << 16),
+                     __uint_as_float(ec.y & 0xffff0000u)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ev[j] = ev[j] + c.g * (cv[j] - ev[j]);
+    }
+    float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    float pv[4] = {0, 0, 0, 0}, nz[4] = {0, 0, 0, 0};
+    if (c.has_prev) {
+      float4 t = reinterpret_cast<const float4*>(x0prev)[i];
+      pv[0] = t.x; pv[1] = t.y; pv[2] = t.z; pv[3] = t.w;
+    }
+    if (c.has_noise) {
+      float4 t = reinterpret_cast<const float4*>(noise)[i];
+      nz[0] = t.x; nz[1] = t.y; nz[2] = t.z; nz[3] = t.w;
+    }
+    float o[4], z[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      z[j] = c.p * xs[j] + c.q * ev[j];
+      o[j] = c.A * xs[j] + c.B * z[j] + c.C * pv[j] + c.D * nz[j];
+    }
+    reinterpret_cast<float4*>(xn)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(x0o)[i] = make_float4(z[0], z[1], z[2], z[3]);
+  }
+}
+
+CSK_API int csk_sched_step(void* xn, void* x0o, const void* e, const void* x, const void* x0prev, const void* noise,
+                           long long n, float p, float q, float A, float B, float C, float D, float g, int cfg,
+                           hipStream_t stream) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  StepC c{p, q, A, B, C, D, g, cfg, x0prev != nullptr, noise != nullptr};
+  size_t n4 = n / 4;
+  sched_step_kernel<<<ew_grid(n4 / 2 + 1), 256, 0, stream>>>((const bf16_t*)e, (const float*)x, (const float*)x0prev,
+                                                             (const float*)noise, (float*)xn, (float*)x0o, n4, n, c);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
+// VAE post-process: NHWC bf16 [-1,1], C channels (3) -> uint8 NHWC.
+// --------------------------------------------------------------------------
+__global__ void vae_post_kernel(const bf16_t* __restrict__ x, unsigned char* __restrict__ y, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float v = bf2f(x[i]) * 0.5f + 0.5f;
+    v = fminf(fmaxf(v, 0.f), 1.f);
+    y[i] = (unsigned char)__float2int_rn(v * 255.f);
+  }
+}
+
+CSK_API int csk_vae_post(void* y, const void* x, long long n, hipStream_t stream) {
+  vae_post_kernel<<<ew_grid((size_t)n), 256, 0, stream>>>((const bf16_t*)x, (unsigned char*)y, (size_t)n);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
+// Row softmax with scale: bf16 [rows, n] -> bf16 (fp32 math), one wave per row
+// (used for the d=512 single-head VAE attention via GEMM-softmax-GEMM).
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                           int rows, int n, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * n);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * n);
+  const int nv = n / 8;
+  float m = -INFINITY;
+  for (int v = lane; v < nv; v += 64) {
+    float f[8];
+    unpack8(xr[v], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, f[j] * scale);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+  for (int v = lane; v < nv; v += 64) {
+    float f[8];
+    unpack8(xr[v], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(f[j] * scale - m);
+  }
+  const float inv = 1.0f / wave_sum(s);
+  for (int v = lane; v < nv; v += 64) {
+    float f[8];
+    unpack8(xr[v], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = __expf(f[j] * scale - m) * inv;
+    yr[v] = pack8(f);
+  }
+}
+
+CSK_API int csk_softmax_rows(void* y, const void* x, int rows, int n, float scale, hipStream_t stream) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  softmax_rows_kernel<<<(rows + 3) / 4, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, rows, n, scale);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
+// Channel pad: [R, Cin] -> [R, Cout] (zero fill), for Cin % 8 != 0 convs.
+// --------------------------------------------------------------------------
+__global__ void pad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t rows, int cin, int cout) {
+  size_t n = rows * cout;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    size_t r = i / cout;
+    int c = (int)(i - r * cout);
+    y[i] = c < cin ? x[r * cin + c] : (bf16_t)0;
+  }
+}
+
+CSK_API int csk_pad_channels(void* y, const void* x, long long rows, int cin, int cout, hipStream_t stream) {
+  pad_channels_kernel<<<ew_grid((size_t)rows * cout), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (size_t)rows, cin,
+                                                                         cout);
+  CSK_CHECK_LAUNCH();
+}

@@ -1,0 +1,149 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference of the
+same op (run on the MI355X box: ``pytest -m gpu``)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from chiaswarm_amd import ops
+from chiaswarm_amd.ops import hip_ops
+from chiaswarm_amd.schedulers import StepCoeffs
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(y, ref):
+    y, ref = y.float(), ref.float()
+    return ((y - ref).norm() / (ref.norm() + 1e-12)).item()
+
+
+def rnd(*shape, dev, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape, device=dev) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 320, 320), (77 * 8, 1024, 1024), (8, 1280, 320),
+                                   (4096 * 2, 640, 1280), (130, 48, 40), (33, 4, 16), (512, 2560, 640)])
+@pytest.mark.parametrize("act", [None, "gelu", "silu"])
+def test_gemm(gpu, M, N, K, act):
+    a, w, b = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu)
+    r = rnd(M, N, dev=gpu)
+    y = hip_ops.gemm(a, w, b, r, act)
+    ref = ops._ref_gemm(a.float().cpu(), w.float().cpu(), b.float().cpu(), r.float().cpu(), act)
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
+def test_gemm_strided_a_and_geglu(gpu):
+    M, K, F_ = 300, 320, 1280
+    big = rnd(M, 3 * K, dev=gpu)
+    a = big[:, K:2 * K]  # row stride 3K
+    w, b = rnd(2 * F_, K, dev=gpu, scale=K ** -0.5), rnd(2 * F_, dev=gpu)
+    wp, bp = ops.pack_geglu(w, b)
+    y = hip_ops.gemm(a, wp, bp, None, "geglu")
+    h, g = (a.float() @ w.float().t() + b.float()).chunk(2, dim=-1)
+    ref = h * F.gelu(g)
+    assert y.shape == (M, F_)
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,pad,up", [
+    (2, 16, 16, 320, 320, 3, 1, 1, False), (2, 16, 16, 64, 128, 3, 2, 1, False), (1, 8, 8, 128, 64, 3, 1, 1, True),
+    (2, 9, 7, 32, 32, 3, 1, 1, False), (1, 16, 16, 4, 320, 3, 1, 1, False), (1, 16, 16, 320, 4, 3, 1, 1, False),
+    (1, 16, 16, 64, 64, 3, 2, (0, 0, 1, 1), False), (2, 8, 8, 96, 32, 3, 1, 1, False), (1, 12, 12, 3, 64, 3, 1, 1, False),
+    (2, 32, 32, 960, 640, 3, 1, 1, False)])
+def test_conv2d(gpu, B, H, W, Cin, Cout, k, stride, pad, up):
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wt = rnd(Cout, Cin, k, k, dev=gpu, scale=(Cin * k * k) ** -0.5)
+    wp = ops.pack_conv_weight(wt)
+    bias = rnd(Cout, dev=gpu)
+    Ho, Wo = ops.conv_out_size(H, W, k, k, stride, pad, up)
+    res = rnd(B, Ho, Wo, Cout, dev=gpu)
+    b2 = rnd(B, Cout, dev=gpu)
+    y = hip_ops.conv2d(x, wp, bias, stride, pad, res, up, b2)
+    ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), bias.float().cpu(), stride, pad, res.float().cpu(), up,
+                          b2.float().cpu())
+    assert y.shape == ref.shape
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape,G,silu", [((2, 16, 16, 320), 32, True), ((2, 64, 64, 128), 32, False),
+                                          ((2, 8, 8, 2560), 32, True), ((1, 32, 32, 1920), 32, True),
+                                          ((3, 77, 640), 32, False), ((1, 128, 128, 256), 32, True)])
+def test_group_norm(gpu, shape, G, silu):
+    x = rnd(*shape, dev=gpu, scale=3.0) + 2.0
+    g, b = rnd(shape[-1], dev=gpu), rnd(shape[-1], dev=gpu)
+    y = hip_ops.group_norm(x, g, b, G, 1e-5, silu)
+    ref = ops._ref_group_norm(x.float().cpu(), g.float().cpu(), b.float().cpu(), G, 1e-5, silu)
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("C", [320, 768, 1024, 1280, 2048])
+def test_layer_norm(gpu, C):
+    x = rnd(3, 50, C, dev=gpu, scale=2.0) + 1.0
+    g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
+    y = hip_ops.layer_norm(x, g, b, 1e-5)
+    ref = F.layer_norm(x.float(), (C,), g.float(), b.float(), 1e-5)
+    assert rel_err(y, ref) < 1e-2
+
+
+def _attn_ref(q, k, v, scale, causal):
+    return ops._ref_attention(q.float().cpu(), k.float().cpu(), v.float().cpu(), scale, causal)
+
+
+@pytest.mark.parametrize("B,Sq,Skv,H,D,causal", [(2, 1024, 1024, 5, 64, False), (2, 4096, 77, 5, 64, False),
+                                                  (1, 256, 256, 8, 40, False), (1, 300, 300, 8, 80, False),
+                                                  (1, 64, 64, 8, 160, False), (2, 77, 77, 16, 64, True),
+                                                  (1, 200, 130, 2, 64, False), (1, 77, 77, 12, 64, True)])
+def test_attention(gpu, B, Sq, Skv, H, D, causal):
+    q, k, v = (rnd(B, s, H, D, dev=gpu) for s in (Sq, Skv, Skv))
+    scale = 1 / math.sqrt(D)
+    y = hip_ops.attention(q, k, v, scale, causal)
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, scale, causal)) < 1.5e-2
+
+
+def test_attention_fused_qkv_strides(gpu):
+    B, S, H, D = 2, 333, 10, 64
+    qkv = rnd(B, S, 3, H, D, dev=gpu)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    y = hip_ops.attention(q, k, v, 0.125)
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
+
+
+def test_attention_spike_rescale(gpu):
+    # forces the online-softmax rescale: a huge logit appears in a late KV block
+    B, S, H, D = 1, 128, 1, 64
+    q, k, v = (rnd(B, S, H, D, dev=gpu) for _ in range(3))
+    k[0, 100, 0] = q[0, 5, 0] * 8
+    y = hip_ops.attention(q, k, v, 0.125)
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
+
+
+def test_attention_vae_d512(gpu):
+    q, k, v = (rnd(2, 256, 1, 512, dev=gpu) for _ in range(3))
+    y = hip_ops.attention(q, k, v, 512 ** -0.5)
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 512 ** -0.5, False)) < 1.5e-2
+
+
+def test_elementwise(gpu):
+    x, y = rnd(4, 64, 64, 8, dev=gpu), rnd(4, 64, 64, 8, dev=gpu)
+    assert rel_err(hip_ops.silu(x), F.silu(x.float())) < 1e-2
+    assert rel_err(hip_ops.add(x, y), x.float() + y.float()) < 1e-2
+    img = rnd(2, 32, 32, 3, dev=gpu, scale=0.8)
+    u8 = hip_ops.vae_postprocess(img)
+    ref = ((img.float() / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+    assert (u8.int() - ref.int()).abs().max().item() <= 1
+
+
+@pytest.mark.parametrize("cfg,prev,noise", [(True, True, False), (False, False, True), (True, False, False)])
+def test_sched_step(gpu, cfg, prev, noise):
+    n = 2 * 64 * 64 * 4
+    x = torch.randn(2, 64, 64, 4, device=gpu)
+    e = rnd(2 * (2 if cfg else 1), 64, 64, 4, dev=gpu)
+    x0p = torch.randn_like(x) if prev else None
+    nz = torch.randn_like(x) if noise else None
+    c = StepCoeffs(1.3, -0.7, 0.9, 0.2, 0.05 if prev else 0.0, 0.3 if noise else 0.0)
+    g = 7.5 if cfg else None
+    out, x0 = hip_ops.sched_step(e, x, x0p, c, g, nz)
+    ro, rx0 = ops._ref_sched_step(e, x, x0p, c, g, nz)
+    assert rel_err(out, ro) < 1e-5 and rel_err(x0, rx0) < 1e-5
+    assert n == x.numel()
