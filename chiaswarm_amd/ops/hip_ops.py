@@ -11,15 +11,16 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, tuning
 from ._lib import c_float, c_int, c_int64, c_void_p, sig
 
 ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "geglu": 3, "quick_gelu": 4}
 
 sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p)
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p)
 sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p)
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_void_p, c_void_p)
 sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
     c_float, c_int, c_void_p)
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
@@ -91,8 +92,15 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None):
             residual = residual.contiguous()
     if bias is not None:
         _bf16(bias, "gemm.bias")
-    _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
-              M, N, K, a2.stride(0), w.stride(0), n_out, 1, code, _s())
+    lda, ldb = a2.stride(0), w.stride(0)
+
+    def run(tile, split):
+        ws = torch.empty(split * M * N, dtype=torch.float32, device=a2.device) if split > 1 else None
+        _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
+                  M, N, K, lda, ldb, n_out, 1, code, tile, split, _p(ws), _s())
+
+    tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
+    run(tile, split)
     return out
 
 
@@ -122,8 +130,17 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
         bias2d = bias2d.contiguous()
         if bias2d.shape != (B, Cout):
             raise ValueError("conv2d bias2d shape")
-    _lib.call("csk_conv2d", _p(y), _p(x), _p(wp.contiguous()), _p(bias), _p(bias2d), _p(residual),
-              B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), _s())
+    wp = wp.contiguous()
+    M, K = B * Ho * Wo, kh * kw * Cin
+
+    def run(tile, split):
+        ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
+        _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
+                  B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), tile, split, _p(ws), _s())
+
+    key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:{kh}:{stride}:{int(bool(up2x))}"
+    tile, split = tuning.choose(key, M, Cout, K, run)
+    run(tile, split)
     return y
 
 
@@ -132,10 +149,11 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     x = x.contiguous()
     B, C = x.shape[0], x.shape[-1]
     P = x.numel() // (B * C)
-    nchunk = max(1, min(P, -(-2048 // B)))
+    # ~1024 workgroups over the whole tensor, >= 32 pixels per chunk
+    nchunk = max(1, min(-(-1024 // B), -(-P // 32)))
     chunk = -(-P // nchunk)
     nchunk = -(-P // chunk)
-    part = torch.empty(B * nchunk * groups * 3, dtype=torch.float32, device=x.device)
+    part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     y = torch.empty_like(x)
     _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
               float(eps), int(bool(silu)), _s())

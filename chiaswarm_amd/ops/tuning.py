@@ -1,0 +1,114 @@
+"""Per-shape kernel configuration table (the ``cudnn.benchmark`` analogue the
+reference turned on at swarm/worker.py:180; SURVEY §5.4 "tuned-kernel table on
+disk").
+
+For every GEMM / implicit-GEMM conv shape we pick (tile, ksplit):
+  tile   1:128x128  2:128x64  3:64x128  4:64x64  5:128x32  6:128x64(4x1 waves)
+  ksplit split-K factor (fp32 partials + reduce kernel) for small-M/large-K
+         shapes (UNet 16x16 / 8x8 levels) that would otherwise not fill 256 CUs.
+
+Lookup order: in-memory -> user table ($SDAAS_ROOT/csk_tune.json) -> shipped
+table (chiaswarm_amd/lib/tune_gfx950.json, measured on MI355X) -> heuristic.
+With CSK_AUTOTUNE=1 a miss is measured on the spot (outside graph capture)
+with hip events over every candidate and the winner is recorded.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+
+import torch
+
+SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "tune_gfx950.json")
+_TABLE: dict | None = None
+_LOCK = threading.Lock()
+TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64)}
+
+
+def _user_path():
+    root = os.environ.get("SDAAS_ROOT") or os.path.expanduser("~/.sdaas")
+    return os.path.join(root, "csk_tune.json")
+
+
+def table() -> dict:
+    global _TABLE
+    if _TABLE is None:
+        t = {}
+        for p in (SHIPPED, _user_path()):
+            try:
+                with open(p) as f:
+                    t.update(json.load(f))
+            except (FileNotFoundError, json.JSONDecodeError):
+                pass
+        _TABLE = t
+    return _TABLE
+
+
+def save_user():
+    p = _user_path()
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    with open(p, "w") as f:
+        json.dump(table(), f, indent=0, sort_keys=True)
+
+
+def heuristic(M, N, K) -> tuple[int, int]:
+    tiles128 = -(-M // 128) * -(-N // 128)
+    if tiles128 >= 512:
+        return 1, 1
+    tiles64 = -(-M // 64) * -(-N // 64)
+    if tiles64 >= 512 or K < 1024:
+        return 4, 1
+    split = 1
+    while tiles64 * split < 512 and K // 64 >= 4 * split * 2 and split < 8:
+        split *= 2
+    return 4, split
+
+
+def candidates(M, N, K):
+    out = []
+    for tile, (bm, bn) in TILES.items():
+        if tile == 5 and N > 32:
+            continue
+        if tile in (2, 6) and N > 1280:
+            continue
+        ntiles = -(-M // bm) * -(-N // bn)
+        for split in (1, 2, 4, 8):
+            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split):
+                continue
+            out.append((tile, split))
+    return out
+
+
+def _time(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def choose(key: str, M: int, N: int, K: int, runner) -> tuple[int, int]:
+    """runner(tile, ksplit) launches the kernel once (used only when tuning)."""
+    t = table()
+    hit = t.get(key)
+    if hit is not None:
+        return int(hit[0]), int(hit[1])
+    if os.environ.get("CSK_AUTOTUNE") == "1" and not torch.cuda.is_current_stream_capturing():
+        with _LOCK:
+            best, best_ms = None, float("inf")
+            for tile, split in candidates(M, N, K):
+                try:
+                    ms = _time(lambda: runner(tile, split))
+                except RuntimeError:
+                    continue
+                if ms < best_ms:
+                    best, best_ms = (tile, split), ms
+            if best is not None:
+                t[key] = [best[0], best[1], round(best_ms * 1000, 2)]
+                return best
+    return heuristic(M, N, K)

@@ -258,7 +258,7 @@ class StableDiffusion:
 
         if image is not None and not isinstance(image, list):
             image = [image]
-        if image is not None and (height is None or width is None) and self.controlnet is None:
+        if image is not None and (height is None or width is None):
             width, height = image[0].size
         height = height or self.family.default_size
         width = width or self.family.default_size

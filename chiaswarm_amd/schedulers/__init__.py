@@ -54,7 +54,8 @@ class Scheduler:
 
     name = "base"
     order = 1
-    space = "vp"  # "vp": sample lives in x_t = a x0 + s eps; "k": x = x0 + sigma eps
+    space = "vp"
+    karras_full_range = False  # DPM-Solver: Karras over the whole training sigma range  # "vp": sample lives in x_t = a x0 + s eps; "k": x = x0 + sigma eps
 
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
                  beta_schedule="scaled_linear", prediction_type="epsilon", use_karras_sigmas=True,
@@ -85,7 +86,10 @@ class Scheduler:
         ts = np.linspace(0, self.T - 1, n + 1).round()[::-1][:-1].copy()
         sig = np.interp(ts, np.arange(self.T), self.train_sigmas)
         if self.use_karras:
-            sig = karras_sigmas(sig[-1], sig[0], n)
+            if self.karras_full_range:
+                sig = karras_sigmas(self.train_sigmas[0], self.train_sigmas[-1], n)
+            else:
+                sig = karras_sigmas(sig[-1], sig[0], n)
             ts = np.array([round(self.sigma_to_t(s)) for s in sig], dtype=np.float64)
         return ts, sig
 
@@ -175,6 +179,7 @@ class DPMSolverMultistepScheduler(Scheduler):
 
     name = "DPMSolverMultistepScheduler"
     order = 2
+    karras_full_range = True
 
     def __init__(self, solver_order=2, lower_order_final=True, **kw):
         super().__init__(**kw)

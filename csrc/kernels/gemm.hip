@@ -38,6 +38,8 @@ struct GemmArgs {
   const bf16_t* bias2d;  // [B][N] or null (row m uses b = m / rows_per_b)
   const bf16_t* res;     // [M][ldc] or null
   int M, N, K, lda, ldb, ldc, rows_per_b, act;
+  float* ws;   // split-K fp32 partials [ksplit][M][N] (null: no split)
+  int kchunk;  // K elements per split (multiple of BK)
   // conv geometry
   int H, Wd, Cin, Ho, Wo, kh, kw, stride, pt, pl, up2x;
 };
@@ -64,6 +66,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   const int M = args.M, N = args.N, K = args.K;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int split = blockIdx.y;
+  const int kbeg = split * args.kchunk;
+  const int kend = args.ws ? min(K, kbeg + args.kchunk) : K;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 
   // ---- per-thread load bookkeeping (each thread's 16B chunk column is fixed) ----
@@ -100,18 +105,22 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     b_ok[i] = n < N;
     b_ptr[i] = args.W + (size_t)(b_ok[i] ? n : 0) * args.ldb + lc * 8;
   }
-  // conv K-position state for this thread's chunk: k = kt*64 + lc*8 -> (tap, ci)
-  int c_ci = lc * 8, c_ky = 0, c_kx = 0;
+  // conv K-position state for this thread's chunk: k = kbeg + kt*64 + lc*8 -> (tap, ci)
+  int c_ci = 0, c_ky = 0, c_kx = 0;
   if constexpr (CONV) {
-    while (c_ci >= args.Cin) { c_ci -= args.Cin; if (++c_kx == args.kw) { c_kx = 0; ++c_ky; } }
+    const int k0 = kbeg + lc * 8;
+    const int tap = k0 / args.Cin;
+    c_ci = k0 - tap * args.Cin;
+    c_ky = tap / args.kw;
+    c_kx = tap - c_ky * args.kw;
   }
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
 
   uint4 ra[CA], rb[CB];
   auto load_tiles = [&](int kt) {
-    const int k = kt * BK + lc * 8;
-    const bool kin = k < K;
+    const int k = kbeg + kt * BK + lc * 8;
+    const bool kin = k < kend;
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -122,14 +131,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
           v = *reinterpret_cast<const uint4*>(args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.Cin + c_ci);
         }
       } else {
-        if (kin && a_ok[i]) v = *reinterpret_cast<const uint4*>(a_ptr[i] + (size_t)kt * BK);
+        if (kin && a_ok[i]) v = *reinterpret_cast<const uint4*>(a_ptr[i] + (size_t)kbeg + (size_t)kt * BK);
       }
       ra[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (kin && b_ok[i]) v = *reinterpret_cast<const uint4*>(b_ptr[i] + (size_t)kt * BK);
+      if (kin && b_ok[i]) v = *reinterpret_cast<const uint4*>(b_ptr[i] + (size_t)kbeg + (size_t)kt * BK);
       rb[i] = v;
     }
     if constexpr (CONV) {  // advance (tap, ci) by 64 channels
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
+  const int nk = (kend - kbeg + BK - 1) / BK;
   load_tiles(0);
   store_tiles(0);
   __syncthreads();
@@ -181,6 +190,21 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   }
 
   // ---- epilogue ----
+  if (args.ws) {  // split-K: raw fp32 partials, epilogue applied by the reduce kernel
+    float* wp = args.ws + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+          if (m < M && n < N) wp[(size_t)m * N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC_S]
   const int act = args.act;
   if (act == ACT_GEGLU) {
@@ -264,38 +288,87 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV>
-static int launch(const GemmArgs& a, hipStream_t s) {
+static int launch(const GemmArgs& a, int ksplit, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  gemm_kernel<BM, BN, WM, WN, CONV><<<tiles, 256, 0, s>>>(a);
+  gemm_kernel<BM, BN, WM, WN, CONV><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 
+// split-K reduce: out = epilogue(sum_s ws[s]) (bias, bias2d, act, residual)
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C, const bf16_t* __restrict__ bias,
+                                     const bf16_t* __restrict__ bias2d, const bf16_t* __restrict__ res, int M, int N,
+                                     int ldc, int rows_per_b, int act, int ksplit) {
+  const size_t total = (size_t)M * N;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / N), n = (int)(i - (size_t)m * N);
+    float v = 0.f;
+    for (int sidx = 0; sidx < ksplit; ++sidx) v += ws[(size_t)sidx * total + i];
+    if (bias) v += bf2f(bias[n]);
+    if (bias2d) v += bf2f(bias2d[(size_t)(m / rows_per_b) * N + n]);
+    if (act == ACT_GELU) v = gelu_f(v);
+    else if (act == ACT_SILU) v = silu_f(v);
+    else if (act == ACT_QGELU) v = qgelu_f(v);
+    if (res) v += bf2f(res[(size_t)m * ldc + n]);
+    C[(size_t)m * ldc + n] = f2bf(v);
+  }
+}
+
 template <bool CONV>
-static int dispatch(const GemmArgs& a, hipStream_t s) {
-  // tile choice: wide tiles for big problems, narrow-N tiles for Cout <= 64
-  // (RRDB growth convs, conv_out), small tiles when there are too few tiles
-  // to fill 256 CUs.
-  const long long t128 = (long long)((a.M + 127) / 128) * ((a.N + 127) / 128);
-  if (a.N <= 32) return launch<128, 32, 4, 1, CONV>(a, s);
-  if (a.N <= 64) return launch<128, 64, 4, 1, CONV>(a, s);
-  if (t128 >= 512 || a.act == ACT_GEGLU) return launch<128, 128, 2, 2, CONV>(a, s);
-  return launch<64, 64, 2, 2, CONV>(a, s);
+static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
+  if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
+  if (ksplit > 1) {
+    if (!a.ws) return (int)hipErrorInvalidValue;
+    const int nk = (a.K + BK - 1) / BK;
+    a.kchunk = ((nk + ksplit - 1) / ksplit) * BK;
+    ksplit = (a.K + a.kchunk - 1) / a.kchunk;
+  } else {
+    a.ws = nullptr;
+    a.kchunk = a.K;
+    ksplit = 1;
+  }
+  if (tile == 0) {  // heuristic: wide tiles for big problems, narrow-N tiles for Cout <= 64
+    const long long t128 = (long long)((a.M + 127) / 128) * ((a.N + 127) / 128);
+    if (a.N <= 32) tile = 5;
+    else if (a.N <= 64) tile = 6;
+    else if (t128 >= 512 || a.act == ACT_GEGLU) tile = 1;
+    else tile = 4;
+  }
+  if (a.act == ACT_GEGLU && tile != 1 && tile != 3) tile = 1;  // needs >= 32 cols per wave
+  int err;
+  switch (tile) {
+    case 1: err = launch<128, 128, 2, 2, CONV>(a, ksplit, s); break;
+    case 2: err = launch<128, 64, 2, 2, CONV>(a, ksplit, s); break;
+    case 3: err = launch<64, 128, 2, 2, CONV>(a, ksplit, s); break;
+    case 4: err = launch<64, 64, 2, 2, CONV>(a, ksplit, s); break;
+    case 5: err = launch<128, 32, 4, 1, CONV>(a, ksplit, s); break;
+    case 6: err = launch<128, 64, 4, 1, CONV>(a, ksplit, s); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (err || ksplit == 1) return err;
+  const size_t total = (size_t)a.M * a.N;
+  int grid = (int)((total + 255) / 256);
+  if (grid > 8192) grid = 8192;
+  splitk_reduce_kernel<<<grid, 256, 0, s>>>(a.ws, a.C, a.bias, a.bias2d, a.res, a.M, a.N, a.ldc, a.rows_per_b, a.act,
+                                             ksplit);
+  return (int)hipGetLastError();
 }
 
 CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
-                     int M, int N, int K, int lda, int ldb, int ldc, int rows_per_b, int act, hipStream_t stream) {
+                     int M, int N, int K, int lda, int ldb, int ldc, int rows_per_b, int act, int tile, int ksplit,
+                     void* ws, hipStream_t stream) {
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (act == ACT_GEGLU && N % 32 != 0)) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.bias2d = (const bf16_t*)bias2d; a.res = (const bf16_t*)res;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.rows_per_b = rows_per_b > 0 ? rows_per_b : 1; a.act = act;
+  a.ws = (float*)ws;
   if (M == 0 || N == 0) return 0;
-  return dispatch<false>(a, stream);
+  return dispatch<false>(a, tile, ksplit, stream);
 }
 
 CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
                        int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
-                       int up2x, hipStream_t stream) {
+                       int up2x, int tile, int ksplit, void* ws, hipStream_t stream) {
   if (Cin % 8 != 0) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.W = (const bf16_t*)Wp; a.C = (bf16_t*)Y;
@@ -304,6 +377,7 @@ CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias,
   a.act = ACT_NONE;
   a.H = H; a.Wd = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.kh = kh; a.kw = kw; a.stride = stride; a.pt = pt; a.pl = pl;
   a.up2x = up2x;
+  a.ws = (float*)ws;
   if (a.M == 0) return 0;
-  return dispatch<true>(a, stream);
+  return dispatch<true>(a, tile, ksplit, stream);
 }

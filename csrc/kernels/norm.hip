@@ -15,91 +15,84 @@
 #define GN_THREADS 256
 #define GN_MAXC 4096
 
-// partial layout: part[((b * nchunk + chunk) * G + g) * 3 + {0:n, 1:mean, 2:M2}]
+// Thread layout shared by the stats and apply kernels: thread = (cv, r); cv is
+// the 8-channel vector column the thread owns for the whole chunk (so its
+// per-channel constants live in registers), r its pixel row; R = 256 / NVT rows
+// advance together.  C > 2048 (NV > 256) gives each thread two columns
+// (cv, cv + NVT).
+struct GnLayout {
+  int NV, NVT, TPV, R, cv, r;
+  __device__ GnLayout(int C, int tid) {
+    NV = C >> 3;
+    TPV = NV > GN_THREADS ? 2 : 1;
+    NVT = (NV + TPV - 1) / TPV;
+    R = GN_THREADS / NVT;
+    cv = tid % NVT;
+    r = tid / NVT;
+  }
+};
+
+// part[((b * nchunk + chunk) * G + g) * 3 + {n, mean, M2}]
 __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
                                                               int P, int C, int G, int chunk, int nchunk) {
   __shared__ float red[2][GN_MAXC];
-  const int b = blockIdx.y, ck = blockIdx.x;
-  const int NV = C >> 3;
-  const int tid = threadIdx.x;
-  const int p0 = ck * chunk;
-  const int p1 = min(P, p0 + chunk);
+  const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
+  const GnLayout L(C, tid);
+  const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
   const bf16_t* xb = x + (size_t)b * P * C;
-  // vector slots handled by this thread: cv = tid, tid+256 (C <= 4096 -> NV <= 512)
-  const int R = NV >= GN_THREADS ? 1 : GN_THREADS / NV;  // pixel rows per pass
+  for (int i = tid; i < C; i += GN_THREADS) { red[0][i] = 0.f; red[1][i] = 0.f; }
   float s[2][8], ss[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[u][j] = ss[u][j] = 0.f;
-  if (NV < GN_THREADS) {
-    const int cv = tid % NV, r = tid / NV;
-    if (r < R) {
-      for (int p = p0 + r; p < p1; p += R) {
-        uint4 v = *reinterpret_cast<const uint4*>(xb + (size_t)p * C + cv * 8);
-        float f[8];
-        unpack8(v, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { s[0][j] += f[j]; ss[0][j] += f[j] * f[j]; }
-      }
-    }
-  } else {
-    for (int p = p0; p < p1; ++p) {
+  if (L.r < L.R) {
+    for (int p = p0 + L.r; p < p1; p += L.R) {
+      const bf16_t* row = xb + (size_t)p * C;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        int cv = tid + u * GN_THREADS;
-        if (cv < NV) {
-          uint4 v = *reinterpret_cast<const uint4*>(xb + (size_t)p * C + cv * 8);
+        const int v = L.cv + u * L.NVT;
+        if (u < L.TPV && v < L.NV) {
           float f[8];
-          unpack8(v, f);
+          unpack8(*reinterpret_cast<const uint4*>(row + v * 8), f);
 #pragma unroll
           for (int j = 0; j < 8; ++j) { s[u][j] += f[j]; ss[u][j] += f[j] * f[j]; }
         }
       }
     }
   }
-  // reduce over rows -> per-channel sums in LDS
-  const int Cg = C / G;
-  for (int i = tid; i < C; i += GN_THREADS) { red[0][i] = 0.f; red[1][i] = 0.f; }
   __syncthreads();
-  if (NV < GN_THREADS) {
-    const int cv = tid % NV, r = tid / NV;
-    if (r < R) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&red[0][cv * 8 + j], s[0][j]); atomicAdd(&red[1][cv * 8 + j], ss[0][j]); }
-    }
-  } else {
+  if (L.r < L.R) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      int cv = tid + u * GN_THREADS;
-      if (cv < NV) {
+      const int v = L.cv + u * L.NVT;
+      if (u < L.TPV && v < L.NV) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { red[0][cv * 8 + j] = s[u][j]; red[1][cv * 8 + j] = ss[u][j]; }
+        for (int j = 0; j < 8; ++j) {
+          atomicAdd(&red[0][v * 8 + j], s[u][j]);
+          atomicAdd(&red[1][v * 8 + j], ss[u][j]);
+        }
       }
     }
   }
   __syncthreads();
+  const int Cg = C / G;
   for (int g = tid; g < G; g += GN_THREADS) {
-    const int c0 = g * Cg;
     float sm = 0.f, sq = 0.f;
-    for (int c = c0; c < c0 + Cg; ++c) { sm += red[0][c]; sq += red[1][c]; }
-    float n = (float)(p1 - p0) * (float)Cg;
-    float mean = n > 0.f ? sm / n : 0.f;
-    float m2 = fmaxf(sq - sm * mean, 0.f);
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { sm += red[0][c]; sq += red[1][c]; }
+    const float n = (float)(p1 - p0) * (float)Cg;
+    const float mean = n > 0.f ? sm / n : 0.f;
     float* o = part + (((size_t)b * nchunk + ck) * G + g) * 3;
-    o[0] = n; o[1] = mean; o[2] = m2;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = fmaxf(sq - sm * mean, 0.f);
   }
 }
 
-__global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                              const float* __restrict__ part,
-                                                              const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
-                                                              int P, int C, int G, int chunk, int nchunk, float eps, int silu) {
-  __shared__ float sa[GN_MAXC], sb[GN_MAXC];
-  __shared__ float smean[128], srstd[128];
-  const int b = blockIdx.y, ck = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // 1) merge chunk partials per group (one wave per group)
+// stat[(b * G + g) * 2 + {mean, rstd}]: merge chunk partials (Chan), one wave per group.
+__global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stat,
+                                                                 int G, int nchunk, float eps) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int g = wid; g < G; g += GN_THREADS / 64) {
     float n = 0.f, mean = 0.f, m2 = 0.f;
     for (int c = lane; c < nchunk; c += 64) {
@@ -108,51 +101,71 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
+      const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
       chan_combine(n, mean, m2, n2, me2, q2);
     }
     if (lane == 0) {
-      smean[g] = mean;
-      srstd[g] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+      stat[(b * G + g) * 2] = mean;
+      stat[(b * G + g) * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
     }
-  }
-  __syncthreads();
-  const int Cg = C / G;
-  for (int c = tid; c < C; c += GN_THREADS) {
-    int g = c / Cg;
-    float a = bf2f(gamma[c]) * srstd[g];
-    sa[c] = a;
-    sb[c] = bf2f(beta[c]) - smean[g] * a;
-  }
-  __syncthreads();
-  // 2) stream the chunk
-  const int NV = C >> 3;
-  const size_t base = ((size_t)b * P + (size_t)ck * chunk) * NV;
-  const int p1 = min(P, (ck + 1) * chunk);
-  const size_t nvec = (size_t)(p1 - ck * chunk) * NV;
-  const uint4* xin = reinterpret_cast<const uint4*>(x) + base;
-  uint4* yo = reinterpret_cast<uint4*>(y) + base;
-  for (size_t i = tid; i < nvec; i += GN_THREADS) {
-    int cv = (int)(i % NV);
-    float f[8];
-    unpack8(xin[i], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sa[cv * 8 + j] + sb[cv * 8 + j];
-      f[j] = silu ? silu_f(v) : v;
-    }
-    yo[i] = pack8(f);
   }
 }
 
+__global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                              const float* __restrict__ stat,
+                                                              const bf16_t* __restrict__ gamma,
+                                                              const bf16_t* __restrict__ beta, int P, int C, int G,
+                                                              int chunk, int silu) {
+  const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
+  const GnLayout L(C, tid);
+  if (L.r >= L.R) return;
+  const int Cg = C / G;
+  float sa[2][8], sb[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int v = L.cv + u * L.NVT;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = min(v * 8 + j, C - 1);
+      const int g = c / Cg;
+      const float mean = stat[(b * G + g) * 2], rstd = stat[(b * G + g) * 2 + 1];
+      const float a = bf2f(gamma[c]) * rstd;
+      sa[u][j] = a;
+      sb[u][j] = bf2f(beta[c]) - mean * a;
+    }
+  }
+  const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
+  const size_t boff = (size_t)b * P * C;
+  for (int p = p0 + L.r; p < p1; p += L.R) {
+    const size_t roff = boff + (size_t)p * C;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int v = L.cv + u * L.NVT;
+      if (u < L.TPV && v < L.NV) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + roff + v * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = f[j] * sa[u][j] + sb[u][j];
+          f[j] = silu ? silu_f(t) : t;
+        }
+        *reinterpret_cast<uint4*>(y + roff + v * 8) = pack8(f);
+      }
+    }
+  }
+}
+
+// part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
 CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma, const void* beta, int B, int P, int C,
                            int G, int chunk, int nchunk, float eps, int silu, hipStream_t stream) {
-  if (C % 8 != 0 || C > GN_MAXC || G > 128 || C % G != 0) return (int)hipErrorInvalidValue;
+  if (C % 8 != 0 || C > GN_MAXC || C % G != 0) return (int)hipErrorInvalidValue;
+  float* pt = (float*)part;
+  float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
-  gn_stats_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (float*)part, P, C, G, chunk, nchunk);
-  gn_apply_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float*)part,
-                                                   (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G, chunk, nchunk,
-                                                   eps, silu);
+  gn_stats_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
+  gn_finalize_kernel<<<B, GN_THREADS, 0, stream>>>(pt, st, G, nchunk, eps);
+  gn_apply_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
+                                                   (const bf16_t*)beta, P, C, G, chunk, silu);
   CSK_CHECK_LAUNCH();
 }
 

@@ -33,6 +33,32 @@ def test_gemm(gpu, M, N, K, act):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("split", [1, 3])
+def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, N, K = 200, 96, 640
+    a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=gpu)
+    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, 1, 2, tile, split, _p(ws), _s())
+    ref = ops._ref_gemm(a.float().cpu(), w.float().cpu(), b.float().cpu(), r.float().cpu(), "silu")
+    assert rel_err(out.cpu(), ref) < 1e-2
+    # implicit-GEMM conv, K split across taps
+    B, H, W, Cin, Cout = 2, 10, 12, 96, 48
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    b2 = rnd(B, Cout, dev=gpu)
+    y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=gpu)
+    ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=gpu)
+    _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, _p(b2), None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1, H, W, 0,
+              tile, split, _p(ws), _s())
+    ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), None, 1, 1, None, False, b2.float().cpu())
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
 def test_gemm_strided_a_and_geglu(gpu):
     M, K, F_ = 300, 320, 1280
     big = rnd(M, 3 * K, dev=gpu)

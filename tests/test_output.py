@@ -1,0 +1,79 @@
+"""Golden result-envelope tests (reference swarm/output_processor.py)."""
+import base64
+import hashlib
+import io
+import json
+
+import pytest
+from PIL import Image
+
+from chiaswarm_amd.output import processor as op
+
+
+def img(c=(10, 20, 30), size=(64, 48)):
+    return Image.new("RGB", size, c)
+
+
+@pytest.mark.parametrize("n,grid", [(1, (1, 1)), (2, (1, 2)), (3, (2, 2)), (4, (2, 2)), (5, (2, 3)), (6, (2, 3)),
+                                    (7, (3, 3)), (9, (3, 3))])
+def test_grid_policy(n, grid):
+    out = op.post_process([img((i * 20, 0, 0)) for i in range(n)])
+    rows, cols = grid
+    assert out.size == (64 * cols, 48 * rows)
+
+
+def test_too_many_images():
+    with pytest.raises(ValueError):
+        op.post_process([img()] * 10)
+
+
+def test_grid_row_major_order():
+    ims = [img((255, 0, 0)), img((0, 255, 0)), img((0, 0, 255))]
+    g = op.post_process(ims)
+    assert g.getpixel((10, 10)) == (255, 0, 0)
+    assert g.getpixel((64 + 10, 10)) == (0, 255, 0)
+    assert g.getpixel((10, 48 + 10)) == (0, 0, 255)
+    assert g.getpixel((64 + 10, 48 + 10)) == (0, 0, 0)
+
+
+@pytest.mark.parametrize("ct,fmt", [("image/jpeg", "JPEG"), ("image/png", "PNG")])
+def test_envelope(ct, fmt):
+    p = op.OutputProcessor(["primary"], ct)
+    p.add_outputs([img(), img()])
+    res = p.get_results()
+    a = res["primary"]
+    assert set(a) == {"blob", "content_type", "thumbnail", "sha256_hash"}
+    blob = base64.b64decode(a["blob"])
+    assert a["sha256_hash"] == hashlib.sha256(blob).hexdigest()
+    assert Image.open(io.BytesIO(blob)).format == fmt
+    th = Image.open(io.BytesIO(base64.b64decode(a["thumbnail"])))
+    assert th.format == "JPEG" and max(th.size) <= 100
+    assert a["content_type"] == ct
+
+
+def test_other_outputs_and_unknown_names():
+    p = op.OutputProcessor(["primary", "inference_image_strip"], "image/jpeg")
+    p.add_outputs([img()])
+    p.add_other_outputs("preprocessed_input", [img((1, 2, 3))])
+    res = p.get_results()
+    assert set(res) == {"primary", "preprocessed_input"}
+
+
+def test_text_result_hashes_string_not_blob():
+    r = op.make_text_result("a caption")
+    assert r["content_type"] == "application/json"
+    assert json.loads(base64.b64decode(r["blob"])) == {"caption": "a caption"}
+    assert r["sha256_hash"] == hashlib.sha256(b"a caption").hexdigest()
+
+
+def test_audio_thumbnail_is_text_tile():
+    r = op.make_result(io.BytesIO(b"ID3fakeaudio"), None, "audio/mpeg")
+    th = Image.open(io.BytesIO(base64.b64decode(r["thumbnail"])))
+    assert th.size == (100, 100)
+
+
+def test_bad_content_type():
+    with pytest.raises(ValueError):
+        op.image_to_buffer(img(), "image/gif")
+    with pytest.raises(ValueError):
+        op.image_to_buffer(img(), "video/mp4")

@@ -1,0 +1,96 @@
+"""SD-family pipeline plumbing on CPU fp32 (tiny configs + BASELINE config #1)."""
+import base64
+import io
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from chiaswarm_amd.pipelines.sd import StableDiffusion, family_for_model
+from chiaswarm_amd.runtime.device import Device
+from chiaswarm_amd.runtime.generator import synchronous_do_work_function
+from chiaswarm_amd.schedulers import get_scheduler
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    return StableDiffusion("tiny", "cpu", seed=1)
+
+
+def gen(s=0):
+    return torch.Generator().manual_seed(s)
+
+
+def test_family_mapping():
+    assert family_for_model("stabilityai/stable-diffusion-2-1-base") == "sd21"
+    assert family_for_model("stabilityai/stable-diffusion-2-1") == "sd21-v"
+    assert family_for_model("runwayml/stable-diffusion-v1-5") == "sd15"
+    assert family_for_model("stabilityai/stable-diffusion-xl-base-1.0") == "sdxl"
+    assert family_for_model("timbrooks/instruct-pix2pix") == "pix2pix"
+
+
+@pytest.mark.parametrize("sched", ["DPMSolverMultistepScheduler", "EulerAncestralDiscreteScheduler",
+                                   "DDIMScheduler", "HeunDiscreteScheduler", "LMSDiscreteScheduler"])
+def test_txt2img_schedulers(tiny, sched):
+    out = tiny(prompt="x", num_inference_steps=3, height=64, width=64, generator=gen(),
+               scheduler=get_scheduler(sched))
+    assert out.images[0].size == (64, 64) and torch.isfinite(out.latents).all()
+
+
+def test_seed_reproducible_and_negative_prompt(tiny):
+    a = tiny(prompt="x", num_inference_steps=3, height=64, width=64, generator=gen(5)).latents
+    b = tiny(prompt="x", num_inference_steps=3, height=64, width=64, generator=gen(5)).latents
+    c = tiny(prompt="x", negative_prompt="blurry", num_inference_steps=3, height=64, width=64,
+             generator=gen(5)).latents
+    assert torch.equal(a, b) and not torch.equal(a, c)
+
+
+def test_img2img_strength(tiny):
+    img = Image.fromarray((np.random.default_rng(0).random((64, 64, 3)) * 255).astype(np.uint8))
+    out = tiny(prompt="x", image=img, strength=0.5, num_inference_steps=4, generator=gen())
+    assert out.images[0].size == (64, 64)
+
+
+def test_inpaint_legacy(tiny):
+    img = Image.new("RGB", (64, 64), (120, 30, 30))
+    mask = Image.new("L", (64, 64), 0)
+    mask.paste(255, (16, 16, 48, 48))
+    out = tiny(prompt="x", image=img, mask_image=mask, strength=1.0, num_inference_steps=3, generator=gen())
+    assert out.images[0].size == (64, 64)
+
+
+def test_controlnet_tiny(tiny):
+    from chiaswarm_amd.pipelines.controlnet import load_controlnet
+
+    tiny.controlnet = load_controlnet("tiny/controlnet", tiny, "cpu")
+    try:
+        cond = Image.new("RGB", (64, 64), (255, 255, 255))
+        out = tiny(prompt="x", image=cond, num_inference_steps=2, generator=gen(),
+                   controlnet_conditioning_scale=0.7)
+        assert out.images[0].size == (64, 64)
+    finally:
+        tiny.controlnet = None
+
+
+def test_canny_matches_known_edges():
+    from chiaswarm_amd.controlnet.preprocess import canny_np, image_to_canny
+
+    a = np.zeros((32, 32), np.uint8)
+    a[:, 16:] = 255
+    e = canny_np(a, 100, 200)
+    cols = np.nonzero(e.any(axis=0))[0]
+    assert set(cols.tolist()) <= {15, 16} and e[5:27].any()
+    im = image_to_canny(Image.fromarray(np.stack([a] * 3, -1)))
+    assert im.mode == "RGB" and im.size == (32, 32)
+
+
+def test_baseline_config1_sd21_cpu():
+    """BASELINE config #1: SD2.1 txt2img 64x64, 4 steps, batch 1, CPU fp32 via the generator."""
+    r = synchronous_do_work_function({"id": "c1", "model_name": "stabilityai/stable-diffusion-2-1-base",
+                                      "prompt": "spoons", "num_inference_steps": 4, "height": 64, "width": 64,
+                                      "seed": 1}, Device("cpu"))
+    assert "error" not in r["pipeline_config"], r["pipeline_config"]
+    assert r["pipeline_config"]["family"] == "sd21" and r["pipeline_config"]["seed"] == 1
+    im = Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"])))
+    assert im.size == (64, 64)

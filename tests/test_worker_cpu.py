@@ -1,0 +1,143 @@
+"""Worker plumbing on CPU: error classification, device wrapper, the full
+supervisor loop against a fake hive with injected faults,
+and BASELINE config #1 (txt2img through the real router/device/encoder)."""
+import asyncio
+import base64
+import io
+
+import pytest
+from PIL import Image
+
+from chiaswarm_amd import __version__
+from chiaswarm_amd.hive.client import POLL_ERROR, POLL_FOUND, POLL_IDLE, HiveClient
+from chiaswarm_amd.runtime.device import Device
+from chiaswarm_amd.runtime.generator import synchronous_do_work_function
+from chiaswarm_amd.runtime.worker import Supervisor, ThreadExecutor
+from chiaswarm_amd.settings import Settings
+from tests.fakehive import FakeHive
+
+TINY = {"model_name": "tiny/sd", "prompt": "a red fox", "num_inference_steps": 3, "height": 64, "width": 64}
+
+
+@pytest.fixture(autouse=True)
+def sdaas_root(tmp_path, monkeypatch):
+    monkeypatch.setenv("SDAAS_ROOT", str(tmp_path))
+
+
+def test_success_envelope():
+    r = synchronous_do_work_function({"id": "j1", **TINY, "seed": 42}, Device("cpu"))
+    assert r["id"] == "j1" and r["worker_version"] == __version__
+    assert r["nsfw"] is False and "fatal_error" not in r
+    assert r["pipeline_config"]["seed"] == 42
+    img = Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"])))
+    assert img.size == (64, 64) and img.format == "JPEG"
+
+
+def test_seed_determinism_and_grid():
+    job = {"id": "j", **TINY, "seed": 7, "num_images_per_prompt": 2, "content_type": "image/png"}
+    a = synchronous_do_work_function(dict(job), Device("cpu"))
+    b = synchronous_do_work_function(dict(job), Device("cpu"))
+    assert a["artifacts"]["primary"]["sha256_hash"] == b["artifacts"]["primary"]["sha256_hash"]
+    img = Image.open(io.BytesIO(base64.b64decode(a["artifacts"]["primary"]["blob"])))
+    assert img.size == (128, 64) and img.format == "PNG"
+
+
+def test_fatal_on_bad_arguments():
+    r = synchronous_do_work_function({"id": "j2", "model_name": "m", "height": 4096, "width": 64}, Device("cpu"))
+    assert r["fatal_error"] is True and "max image size" in r["pipeline_config"]["error"]
+    assert r["artifacts"]["primary"]["content_type"] == "image/jpeg"
+
+
+def test_fatal_on_value_error_text_artifact():
+    job = {"id": "j3", **TINY, "lora": "/nonexistent/lora.safetensors", "content_type": "audio/mpeg"}
+    r = synchronous_do_work_function(job, Device("cpu"))
+    assert r["fatal_error"] is True
+    assert r["artifacts"]["primary"]["content_type"] == "application/json"
+
+
+def test_nonfatal_on_runtime_error(monkeypatch):
+    from chiaswarm_amd.pipelines import diffusion
+
+    def boom(*a, **k):
+        raise RuntimeError("out of memory")
+
+    monkeypatch.setattr(diffusion, "diffusion_callback", boom)
+    r = synchronous_do_work_function({"id": "j4", **TINY}, Device("cpu"))
+    assert "fatal_error" not in r and r["pipeline_config"]["error"] == "out of memory"
+
+
+def test_device_busy():
+    d = Device("cpu")
+    d.mutex.acquire()
+    with pytest.raises(Exception, match="busy"):
+        d(lambda *a, **k: ({}, {}), model_name="m")
+
+
+def _settings(hive):
+    s = Settings()
+    s.sdaas_uri = hive.base
+    s.sdaas_token = "tok"
+    s.worker_name = "w1"
+    return s
+
+
+def test_hive_client_cadence_and_faults():
+    hive = FakeHive(jobs=[{"id": "a", **TINY}], faults=[None, None, 400, 500]).start()
+    try:
+        c = HiveClient(_settings(hive))
+        jobs, sl = asyncio.run(c.ask_for_work())
+        assert [j["id"] for j in jobs] == ["a"] and sl == POLL_FOUND
+        assert asyncio.run(c.ask_for_work()) == ([], POLL_IDLE)
+        assert asyncio.run(c.ask_for_work())[1] == POLL_ERROR  # 400 bad worker
+        assert asyncio.run(c.ask_for_work())[1] == POLL_ERROR  # 500
+        assert hive.auth[0] == "Bearer tok"
+        assert hive.poll_params[0] == {"worker_version": __version__, "worker_name": "w1"}
+    finally:
+        hive.stop()
+
+
+def test_submit_retry_with_backoff():
+    hive = FakeHive().start()
+    hive.result_faults = [503, 503]
+    try:
+        c = HiveClient(_settings(hive), submit_retries=3, retry_base_s=0.01)
+        out = asyncio.run(c.submit_result({"id": "r1", "artifacts": {}}))
+        assert out == {"ok": True, "id": "r1"} and len(hive.results) == 1
+    finally:
+        hive.stop()
+
+
+def test_supervisor_end_to_end():
+    jobs = [{"id": f"job{i}", **TINY, "seed": i} for i in range(3)]
+    jobs.append({"id": "bad", "model_name": "m", "height": 9999, "width": 9})
+    hive = FakeHive(jobs=jobs).start()
+    try:
+        async def main():
+            sup = Supervisor(_settings(hive), executors=[ThreadExecutor("cpu")])
+            await sup.run(max_polls=3)
+            return sup
+
+        sup = asyncio.run(main())
+        ids = sorted(r["id"] for r in hive.results)
+        assert ids == ["bad", "job0", "job1", "job2"]
+        bad = [r for r in hive.results if r["id"] == "bad"][0]
+        assert bad["fatal_error"] is True
+        assert sup.results_submitted == 4
+    finally:
+        hive.stop()
+
+
+def test_stitch_workflow():
+    hive = FakeHive().start()
+    try:
+        urls = [hive.add_image(f"r{i}.png", size=(200, 100 + 40 * i), color=(50 * i, 80, 90)) for i in range(5)]
+        job = {"id": "s", "model_name": "stitch", "workflow": "stitch",
+               "jobs": [{"resultUri": u, "fileName": f"f{i}.png", "model_name": f"m{i}"} for i, u in enumerate(urls)]}
+        r = synchronous_do_work_function(job, Device("cpu"))
+        img = Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"])))
+        assert img.size == (144 * 3, 144 * 3)
+        m = r["pipeline_config"]["image_map"]
+        assert len(m) == 5 and m[3]["coords"] == "0,144,144,288" and m[4]["alt"] == "m4"
+        assert m[0]["filename"] == "f0.png"
+    finally:
+        hive.stop()
