@@ -113,7 +113,7 @@ def conv_out_size(h, w, kh, kw, stride, padding, up2x=False):
     return (h + pt + pb - kh) // stride + 1, (w + pl + pr - kw) // stride + 1
 
 
-def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
+def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0):
     dt = _cdt(x)
     # NHWC tensor viewed as channels-last NCHW: no copies, MIOpen NHWC kernels
     xn = x.to(dt).permute(0, 3, 1, 2)
@@ -129,21 +129,44 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
     y = y.permute(0, 2, 3, 1)
     if bias2d is not None:
         y = y + bias2d.to(dt)[:, None, None, :]
+    if act == "lrelu":
+        y = F.leaky_relu(y, 0.2)
+    elif act == "silu":
+        y = F.silu(y)
+    elif act == "gelu":
+        y = F.gelu(y)
+    if out_scale != 1.0:
+        y = y * out_scale
     if residual is not None:
         y = y + residual.to(dt)
     return y.to(x.dtype).contiguous()
 
 
-def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None):
+def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None, act=None,
+           out_scale=1.0, out=None):
     """NHWC conv.  ``wp``: packed [Cout, kh, kw, Cin].  ``up2x`` fuses a
     nearest-neighbour x2 upsample into the input addressing; ``bias2d`` [B, Cout]
     is a per-sample channel bias (ResNet time-embedding add) fused in the
-    epilogue; ``residual`` [B, Ho, Wo, Cout] is added in the epilogue."""
+    epilogue; y = act(conv + bias + bias2d) * out_scale + residual.  ``x``,
+    ``residual`` and ``out`` may be channel slices of wider NHWC buffers."""
     if use_hip(x):
         from . import hip_ops
 
-        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d)
-    return _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d)
+        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out)
+    y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def axpby(x, y, a, b):
+    """a*x + b*y."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.axpby(x, y, a, b)
+    return (a * x.to(_cdt(x)) + b * y.to(_cdt(x))).to(x.dtype)
 
 
 # ----------------------------------------------------------------------------

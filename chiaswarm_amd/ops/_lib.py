@@ -79,6 +79,11 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
+        if hasattr(lib, "csk_init"):
+            lib.csk_init.restype = c_int
+            err = lib.csk_init()  # zero page for LDS-DMA padding (allocated outside any graph capture)
+            if err != 0:
+                raise RuntimeError(f"csk_init failed with hipError {err}")
         _LIB = lib
         return lib
 

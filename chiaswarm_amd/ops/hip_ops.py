@@ -17,10 +17,12 @@ from ._lib import c_float, c_int, c_int64, c_void_p, sig
 ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "geglu": 3, "quick_gelu": 4}
 
 sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p)
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p)
 sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_int, c_int, c_void_p, c_void_p)
+    c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p)
+sig("csk_axpby", c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p)
+ACT["lrelu"] = 5
 sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
     c_float, c_int, c_void_p)
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
@@ -97,51 +99,87 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None):
     def run(tile, split):
         ws = torch.empty(split * M * N, dtype=torch.float32, device=a2.device) if split > 1 else None
         _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
-                  M, N, K, lda, ldb, n_out, 1, code, tile, split, _p(ws), _s())
+                  M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
     run(tile, split)
     return out
 
 
-def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d):
+def _pix_stride(t):
+    """Pixel stride of an NHWC tensor / channel-slice view (None if not NHWC-strided)."""
+    B, H, W, C = t.shape
+    s = t.stride()
+    if s[3] != 1:
+        return None
+    ps = s[2]
+    if (W > 1 and s[2] != ps) or (H > 1 and s[1] != W * ps) or (B > 1 and s[0] != H * W * ps):
+        return None
+    return ps
+
+
+def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None):
+    """NHWC conv.  ``x``, ``residual`` and ``out`` may be channel-slice views of
+    wider NHWC buffers (last dim contiguous): the kernel takes their pixel
+    strides, so dense/concat blocks need no copies."""
     from . import conv_out_size, norm_padding
 
     _bf16(x, "conv.x")
     _bf16(wp, "conv.w")
-    x = x.contiguous()
     B, H, W, Cin = x.shape
+    xs = _pix_stride(x)
+    if xs is None or xs % 8 != 0 or Cin % 8 != 0 or x.data_ptr() % 16:
+        x = x.contiguous()
+        xs = Cin
     Cout, kh, kw, Cw = wp.shape
     if Cw != Cin:
-        raise ValueError(f"conv2d: Cin mismatch {x.shape} vs {wp.shape}")
+        raise ValueError(f"conv2d: Cin mismatch {tuple(x.shape)} vs {tuple(wp.shape)}")
     if Cin % 8 != 0:
         cp = _round8(Cin)
         x = pad_last(x, cp)
         wp = pad_last(wp.contiguous(), cp)
-        Cin = cp
+        Cin = xs = cp
+    wp = wp.contiguous()
     pt, pl, pb, pr = norm_padding(padding)
     Ho, Wo = conv_out_size(H, W, kh, kw, stride, padding, up2x)
-    y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
+    ys = _pix_stride(out)
+    if out.shape != (B, Ho, Wo, Cout) or ys is None:
+        raise ValueError(f"conv2d out {tuple(out.shape)} / strides unsupported")
+    rs = 0
     if residual is not None:
-        residual = residual.contiguous()
-        if residual.shape != y.shape:
-            raise ValueError(f"conv2d residual {tuple(residual.shape)} != {tuple(y.shape)}")
+        if residual.shape != out.shape:
+            raise ValueError(f"conv2d residual {tuple(residual.shape)} != {tuple(out.shape)}")
+        rs = _pix_stride(residual)
+        if rs is None:
+            residual = residual.contiguous()
+            rs = Cout
     if bias2d is not None:
         bias2d = bias2d.contiguous()
         if bias2d.shape != (B, Cout):
             raise ValueError("conv2d bias2d shape")
-    wp = wp.contiguous()
     M, K = B * Ho * Wo, kh * kw * Cin
+    code = ACT[act]
 
     def run(tile, split):
         ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
-        _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
-                  B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), tile, split, _p(ws), _s())
+        _lib.call("csk_conv2d", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
+                  B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
+                  float(out_scale), tile, split, _p(ws), _s())
 
     key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:{kh}:{stride}:{int(bool(up2x))}"
     tile, split = tuning.choose(key, M, Cout, K, run)
     run(tile, split)
-    return y
+    return out
+
+
+def axpby(x, y, a, b, out=None):
+    """out = a*x + b*y (bf16, contiguous)."""
+    x, y = x.contiguous(), y.contiguous()
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("csk_axpby", _p(out), _p(x), _p(y), x.numel(), float(a), float(b), _s())
+    return out
 
 
 def group_norm(x, gamma, beta, groups, eps, silu):

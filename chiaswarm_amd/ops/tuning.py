@@ -23,7 +23,9 @@ import torch
 SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "tune_gfx950.json")
 _TABLE: dict | None = None
 _LOCK = threading.Lock()
-TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64)}
+TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64),
+         # LDS-DMA multi-stage variants (gemm_glds.hip)
+         11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64)}
 
 
 def _user_path():
@@ -35,7 +37,7 @@ def table() -> dict:
     global _TABLE
     if _TABLE is None:
         t = {}
-        for p in (SHIPPED, _user_path()):
+        for p in (() if os.environ.get("CSK_RETUNE") == "1" else (SHIPPED, _user_path())):
             try:
                 with open(p) as f:
                     t.update(json.load(f))
@@ -68,9 +70,9 @@ def heuristic(M, N, K) -> tuple[int, int]:
 def candidates(M, N, K):
     out = []
     for tile, (bm, bn) in TILES.items():
-        if tile == 5 and N > 32:
+        if tile in (5, 16) and N > 32:
             continue
-        if tile in (2, 6) and N > 1280:
+        if tile in (2, 6, 12, 17) and N > 1280:
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8):

@@ -161,6 +161,28 @@ CSK_API int csk_softmax_rows(void* y, const void* x, int rows, int n, float scal
 }
 
 // --------------------------------------------------------------------------
+// y = a*x + b*z  (RRDB residual scaling, ControlNet residual scale)
+// --------------------------------------------------------------------------
+__global__ void axpby_kernel(const uint4* __restrict__ x, const uint4* __restrict__ z, uint4* __restrict__ y, size_t nvec,
+                             float a, float b) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float fx[8], fz[8];
+    unpack8(x[i], fx);
+    unpack8(z[i], fz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fx[j] = a * fx[j] + b * fz[j];
+    y[i] = pack8(fx);
+  }
+}
+
+CSK_API int csk_axpby(void* y, const void* x, const void* z, long long n, float a, float b, hipStream_t stream) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  size_t nv = n / 8;
+  axpby_kernel<<<ew_grid(nv), 256, 0, stream>>>((const uint4*)x, (const uint4*)z, (uint4*)y, nv, a, b);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
 // Channel pad: [R, Cin] -> [R, Cout] (zero fill), for Cin % 8 != 0 convs.
 // --------------------------------------------------------------------------
 __global__ void pad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t rows, int cin, int cout) {

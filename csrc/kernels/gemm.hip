@@ -26,27 +26,7 @@
 //
 // Workgroup -> tile mapping is XCD-aware (common.h xcd_remap): consecutive
 // tiles of one A row-panel land on one XCD's L2.
-#include "common.h"
-
-enum { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GEGLU = 3, ACT_QGELU = 4 };
-
-struct GemmArgs {
-  const bf16_t* A;  // GEMM: [M][lda];  CONV: NHWC input [B][H][W][Cin]
-  const bf16_t* W;  // [N][K]
-  bf16_t* C;        // [M][ldc]
-  const bf16_t* bias;    // [N] or null
-  const bf16_t* bias2d;  // [B][N] or null (row m uses b = m / rows_per_b)
-  const bf16_t* res;     // [M][ldc] or null
-  int M, N, K, lda, ldb, ldc, rows_per_b, act;
-  float* ws;   // split-K fp32 partials [ksplit][M][N] (null: no split)
-  int kchunk;  // K elements per split (multiple of BK)
-  // conv geometry
-  int H, Wd, Cin, Ho, Wo, kh, kw, stride, pt, pl, up2x;
-};
-
-#define BK 64
-
-__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+#include "gemm_common.h"
 
 template <int BM, int BN, int WM, int WN, bool CONV>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
@@ -128,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
         const int ih = a_ihb[i] + c_ky, iw = a_iwb[i] + c_kx;
         if (kin && a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win) {
           const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
-          v = *reinterpret_cast<const uint4*>(args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.Cin + c_ci);
+          v = *reinterpret_cast<const uint4*>(args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + c_ci);
         }
       } else {
         if (kin && a_ok[i]) v = *reinterpret_cast<const uint4*>(a_ptr[i] + (size_t)kbeg + (size_t)kt * BK);
@@ -189,102 +169,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  if (args.ws) {  // split-K: raw fp32 partials, epilogue applied by the reduce kernel
-    float* wp = args.ws + (size_t)split * M * N;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + fr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-          if (m < M && n < N) wp[(size_t)m * N + n] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC_S]
-  const int act = args.act;
-  if (act == ACT_GEGLU) {
-    // packed columns: even 16-tiles = hidden, odd = gate (same output column in the same lane)
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; j += 2) {
-        const int nh = n0 + wn * WTN + j * 16 + fr;
-        const float bh = (args.bias && nh < N) ? bf2f(args.bias[nh]) : 0.f;
-        const float bg = (args.bias && nh + 16 < N) ? bf2f(args.bias[nh + 16]) : 0.f;
-        const int oc = (wn * WTN + j * 16) / 2 + fr;  // column within the half-width output tile
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WTM + i * 16 + fq * 4 + r;
-          const float h = acc[i][j][r] + bh, g = acc[i][j + 1][r] + bg;
-          cs[row * LDC_S + oc] = h * gelu_f(g);
-        }
-      }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          cs[(wm * WTM + i * 16 + fq * 4 + r) * LDC_S + wn * WTN + j * 16 + fr] = acc[i][j][r];
-  }
-  __syncthreads();
-  const int outN = act == ACT_GEGLU ? N / 2 : N;
-  const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
-  const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
-  const int vpr = BNo / 8;  // 16-byte vectors per tile row
-  for (int v = tid; v < BM * vpr; v += 256) {
-    const int row = v / vpr, cv = v - row * vpr;
-    const int m = m0 + row, n = on0 + cv * 8;
-    if (m >= M || n >= outN) continue;
-    float f[8];
-    const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
-    const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
-    f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
-    const bool full = n + 8 <= outN;
-    if (act != ACT_GEGLU) {
-      if (args.bias) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(args.bias[n + j]) : 0.f;
-      }
-      if (args.bias2d) {
-        const bf16_t* b2 = args.bias2d + (size_t)(m / args.rows_per_b) * N;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(b2[n + j]) : 0.f;
-      }
-      if (act == ACT_GELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-      } else if (act == ACT_SILU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
-      } else if (act == ACT_QGELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = qgelu_f(f[j]);
-      }
-    }
-    bf16_t* cp = args.C + (size_t)m * args.ldc + n;
-    if (full && ((((size_t)cp) & 15) == 0)) {
-      if (args.res) {
-        float rf[8];
-        unpack8(*reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldc + n), rf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += rf[j];
-      }
-      *reinterpret_cast<uint4*>(cp) = pack8(f);
-    } else {
-      for (int j = 0; j < 8 && n + j < outN; ++j) {
-        float o = f[j];
-        if (args.res) o += bf2f(args.res[(size_t)m * args.ldc + n + j]);
-        cp[j] = f2bf(o);
-      }
-    }
-  }
+  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split);
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV>
@@ -295,22 +180,31 @@ static int launch(const GemmArgs& a, int ksplit, hipStream_t s) {
 }
 
 // split-K reduce: out = epilogue(sum_s ws[s]) (bias, bias2d, act, residual)
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C, const bf16_t* __restrict__ bias,
-                                     const bf16_t* __restrict__ bias2d, const bf16_t* __restrict__ res, int M, int N,
-                                     int ldc, int rows_per_b, int act, int ksplit) {
+__global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
+  const int M = a.M, N = a.N;
   const size_t total = (size_t)M * N;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / N), n = (int)(i - (size_t)m * N);
     float v = 0.f;
-    for (int sidx = 0; sidx < ksplit; ++sidx) v += ws[(size_t)sidx * total + i];
-    if (bias) v += bf2f(bias[n]);
-    if (bias2d) v += bf2f(bias2d[(size_t)(m / rows_per_b) * N + n]);
-    if (act == ACT_GELU) v = gelu_f(v);
-    else if (act == ACT_SILU) v = silu_f(v);
-    else if (act == ACT_QGELU) v = qgelu_f(v);
-    if (res) v += bf2f(res[(size_t)m * ldc + n]);
-    C[(size_t)m * ldc + n] = f2bf(v);
+    for (int sidx = 0; sidx < ksplit; ++sidx) v += a.ws[(size_t)sidx * total + i];
+    if (a.bias) v += bf2f(a.bias[n]);
+    if (a.bias2d) v += bf2f(a.bias2d[(size_t)(m / a.rows_per_b) * N + n]);
+    if (a.act == ACT_GELU) v = gelu_f(v);
+    else if (a.act == ACT_SILU) v = silu_f(v);
+    else if (a.act == ACT_QGELU) v = qgelu_f(v);
+    else if (a.act == ACT_LRELU) v = v > 0.f ? v : 0.2f * v;
+    v *= a.out_scale;
+    if (a.res) v += bf2f(a.res[(size_t)m * a.ldr + n]);
+    a.C[(size_t)m * a.ldc + n] = f2bf(v);
   }
+}
+
+static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
+  const size_t total = (size_t)a.M * a.N;
+  int grid = (int)((total + 255) / 256);
+  if (grid > 8192) grid = 8192;
+  splitk_reduce_kernel<<<grid, 256, 0, s>>>(a, ksplit);
+  return (int)hipGetLastError();
 }
 
 template <bool CONV>
@@ -333,48 +227,54 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else if (t128 >= 512 || a.act == ACT_GEGLU) tile = 1;
     else tile = 4;
   }
-  if (a.act == ACT_GEGLU && tile != 1 && tile != 3) tile = 1;  // needs >= 32 cols per wave
   int err;
-  switch (tile) {
-    case 1: err = launch<128, 128, 2, 2, CONV>(a, ksplit, s); break;
-    case 2: err = launch<128, 64, 2, 2, CONV>(a, ksplit, s); break;
-    case 3: err = launch<64, 128, 2, 2, CONV>(a, ksplit, s); break;
-    case 4: err = launch<64, 64, 2, 2, CONV>(a, ksplit, s); break;
-    case 5: err = launch<128, 32, 4, 1, CONV>(a, ksplit, s); break;
-    case 6: err = launch<128, 64, 4, 1, CONV>(a, ksplit, s); break;
-    default: return (int)hipErrorInvalidValue;
+  if (tile >= 11) {
+    err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
+  } else {
+    if (a.act == ACT_GEGLU && tile != 1 && tile != 3) tile = 1;  // needs >= 32 cols per wave
+    switch (tile) {
+      case 1: err = launch<128, 128, 2, 2, CONV>(a, ksplit, s); break;
+      case 2: err = launch<128, 64, 2, 2, CONV>(a, ksplit, s); break;
+      case 3: err = launch<64, 128, 2, 2, CONV>(a, ksplit, s); break;
+      case 4: err = launch<64, 64, 2, 2, CONV>(a, ksplit, s); break;
+      case 5: err = launch<128, 32, 4, 1, CONV>(a, ksplit, s); break;
+      case 6: err = launch<128, 64, 4, 1, CONV>(a, ksplit, s); break;
+      default: return (int)hipErrorInvalidValue;
+    }
   }
   if (err || ksplit == 1) return err;
-  const size_t total = (size_t)a.M * a.N;
-  int grid = (int)((total + 255) / 256);
-  if (grid > 8192) grid = 8192;
-  splitk_reduce_kernel<<<grid, 256, 0, s>>>(a.ws, a.C, a.bias, a.bias2d, a.res, a.M, a.N, a.ldc, a.rows_per_b, a.act,
-                                             ksplit);
-  return (int)hipGetLastError();
+  return splitk_reduce(a, ksplit, s);
 }
 
+// y[M, ldc] = act(A[M, lda] . W[N, ldb]^T + bias + bias2d) * out_scale + res[M, ldr]
 CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
-                     int M, int N, int K, int lda, int ldb, int ldc, int rows_per_b, int act, int tile, int ksplit,
-                     void* ws, hipStream_t stream) {
+                     int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
+                     int tile, int ksplit, void* ws, hipStream_t stream) {
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (act == ACT_GEGLU && N % 32 != 0)) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.bias2d = (const bf16_t*)bias2d; a.res = (const bf16_t*)res;
-  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.rows_per_b = rows_per_b > 0 ? rows_per_b : 1; a.act = act;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr > 0 ? ldr : ldc;
+  a.rows_per_b = rows_per_b > 0 ? rows_per_b : 1; a.act = act; a.out_scale = out_scale;
   a.ws = (float*)ws;
   if (M == 0 || N == 0) return 0;
   return dispatch<false>(a, tile, ksplit, stream);
 }
 
+// NHWC conv; xs / ys / rs: pixel strides (elements) of input / output / residual
+// buffers (>= channel counts: lets dense blocks read and write channel slices of
+// one concat buffer without copies).
 CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
                        int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
-                       int up2x, int tile, int ksplit, void* ws, hipStream_t stream) {
-  if (Cin % 8 != 0) return (int)hipErrorInvalidValue;
+                       int up2x, int xs, int ys, int rs, int act, float out_scale, int tile, int ksplit, void* ws,
+                       hipStream_t stream) {
+  if (Cin % 8 != 0 || xs % 8 != 0 || xs < Cin) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.W = (const bf16_t*)Wp; a.C = (bf16_t*)Y;
   a.bias = (const bf16_t*)bias; a.bias2d = (const bf16_t*)bias2d; a.res = (const bf16_t*)res;
-  a.M = B * Ho * Wo; a.N = Cout; a.K = kh * kw * Cin; a.lda = 0; a.ldb = kh * kw * Cin; a.ldc = Cout; a.rows_per_b = Ho * Wo;
-  a.act = ACT_NONE;
+  a.M = B * Ho * Wo; a.N = Cout; a.K = kh * kw * Cin; a.lda = xs; a.ldb = kh * kw * Cin; a.ldc = ys;
+  a.ldr = rs > 0 ? rs : ys; a.rows_per_b = Ho * Wo;
+  a.act = act; a.out_scale = out_scale;
   a.H = H; a.Wd = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.kh = kh; a.kw = kw; a.stride = stride; a.pt = pt; a.pl = pl;
   a.up2x = up2x;
   a.ws = (float*)ws;

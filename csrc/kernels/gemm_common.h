@@ -1,0 +1,146 @@
+// Shared pieces of the MFMA GEMM / implicit-GEMM conv kernels (gemm.hip:
+// register-staged pipeline; gemm_glds.hip: LDS-DMA multi-stage pipeline).
+#pragma once
+#include "common.h"
+
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GEGLU = 3, ACT_QGELU = 4, ACT_LRELU = 5 };
+
+struct GemmArgs {
+  const bf16_t* A;  // GEMM: [M][lda];  CONV: NHWC input [B][H][W][Cin]
+  const bf16_t* W;  // [N][ldb] (K-contiguous rows)
+  bf16_t* C;        // [M][ldc]
+  const bf16_t* bias;    // [N] or null
+  const bf16_t* bias2d;  // [B][N] or null (row m uses b = m / rows_per_b)
+  const bf16_t* res;     // [M][ldc] or null
+  const bf16_t* zero;    // >= 16 zero bytes in global memory (LDS-DMA source for padding)
+  int M, N, K, lda, ldb, ldc, rows_per_b, act;  // CONV: lda = input pixel stride (>= Cin)
+  int ldr;          // residual row stride
+  float out_scale;  // y = act(acc + bias + bias2d) * out_scale + residual
+  float* ws;   // split-K fp32 partials [ksplit][M][N] (null: no split)
+  int kchunk;  // K elements per split (multiple of BK)
+  // conv geometry
+  int H, Wd, Cin, Ho, Wo, kh, kw, stride, pt, pl, up2x;
+};
+
+#define BK 64
+
+// element offset of 16-byte chunk `chunk` (0..7) of row `row` in a [rows][64] bf16
+// tile; chunk XOR (row & 7) makes the ds_read_b128 fragment reads conflict-free.
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+
+// Epilogue: accumulators -> fp32 LDS tile -> coalesced row pass applying bias,
+// bias2d, activation / GEGLU gating and residual; or raw split-K partials.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
+                                              bf16_t* smem, int m0, int n0, int split) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MT = WTM / 16, NT = WTN / 16;
+  constexpr int LDC_S = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = args.M, N = args.N;
+  if (args.ws) {  // split-K: raw fp32 partials, epilogue applied by the reduce kernel
+    float* wp = args.ws + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+          if (m < M && n < N) wp[(size_t)m * N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC_S]
+  const int act = args.act;
+  if (act == ACT_GEGLU) {
+    // packed columns: even 16-tiles = hidden, odd = gate (same output column in the same lane)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; j += 2) {
+        const int nh = n0 + wn * WTN + j * 16 + fr;
+        const float bh = (args.bias && nh < N) ? bf2f(args.bias[nh]) : 0.f;
+        const float bg = (args.bias && nh + 16 < N) ? bf2f(args.bias[nh + 16]) : 0.f;
+        const int oc = (wn * WTN + j * 16) / 2 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + fq * 4 + r;
+          cs[row * LDC_S + oc] = (acc[i][j][r] + bh) * gelu_f(acc[i][j + 1][r] + bg);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * WTM + i * 16 + fq * 4 + r) * LDC_S + wn * WTN + j * 16 + fr] = acc[i][j][r];
+  }
+  __syncthreads();
+  const int outN = act == ACT_GEGLU ? N / 2 : N;
+  const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
+  const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
+  const int vpr = BNo / 8;
+  for (int v = tid; v < BM * vpr; v += 256) {
+    const int row = v / vpr, cv = v - row * vpr;
+    const int m = m0 + row, n = on0 + cv * 8;
+    if (m >= M || n >= outN) continue;
+    float f[8];
+    const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
+    const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
+    f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
+    const bool full = n + 8 <= outN;
+    if (act != ACT_GEGLU) {
+      if (args.bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(args.bias[n + j]) : 0.f;
+      }
+      if (args.bias2d) {
+        const bf16_t* b2 = args.bias2d + (size_t)(m / args.rows_per_b) * N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(b2[n + j]) : 0.f;
+      }
+      if (act == ACT_GELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+      } else if (act == ACT_SILU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
+      } else if (act == ACT_QGELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = qgelu_f(f[j]);
+      } else if (act == ACT_LRELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : 0.2f * f[j];
+      }
+    }
+    if (args.out_scale != 1.0f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= args.out_scale;
+    }
+    bf16_t* cp = args.C + (size_t)m * args.ldc + n;
+    if (full && ((((size_t)cp) & 15) == 0)) {
+      if (args.res) {
+        float rf[8];
+        unpack8(*reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n), rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += rf[j];
+      }
+      *reinterpret_cast<uint4*>(cp) = pack8(f);
+    } else {
+      for (int j = 0; j < 8 && n + j < outN; ++j) {
+        float o = f[j];
+        if (args.res) o += bf2f(args.res[(size_t)m * args.ldr + n + j]);
+        cp[j] = f2bf(o);
+      }
+    }
+  }
+}
+
+int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);

@@ -1,0 +1,207 @@
+// LDS-DMA (global_load_lds, 16 B/lane) multi-stage MFMA GEMM / implicit-GEMM conv.
+//
+// Same math, operand layouts, swizzled LDS image and epilogue as gemm.hip, but
+// the global->LDS staging is done by the LDS-DMA engine:
+//   * no staging VGPRs and no ds_write instructions; the per-lane SOURCE
+//     address carries the XOR swizzle (LDS destination is lane-linear: lane L
+//     of a wave-instruction lands at base + 16 L, i.e. row L/8, slot L%8, so
+//     it fetches chunk (L%8) ^ (L/8) of its row -> the same image as swz());
+//   * conv padding / out-of-range rows read a 16-byte zero block in global
+//     memory (DMA cannot zero-fill);
+//   * S-stage ring (S = 2..4): stage kt+S-1 is issued right after the barrier
+//     of step kt, so S-2 K-steps of loads stay in flight across every barrier;
+//     the wait is a COUNTED `s_waitcnt vmcnt((S-2) * loads_per_stage)` and the
+//     barrier is a raw s_barrier (never __syncthreads, whose vmcnt(0) would
+//     drain the ring) — cdna_hip_programming.md §5 "Pipelining across barriers".
+#include "gemm_common.h"
+
+static bf16_t* g_zero = nullptr;
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int S, bool CONV>
+__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MT = WTM / 16, NT = WTN / 16;
+  constexpr int IA = BM / 32, IB = BN / 32;  // LDS-DMA instructions per wave per stage (8 rows each)
+  constexpr int LPG = IA + IB;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int SMEM_MAIN = S * STAGE;
+  constexpr int SMEM_EPI = BM * (BN + 4) * 2;
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int M = args.M, N = args.N, K = args.K;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int split = blockIdx.y;
+  const int kbeg = split * args.kchunk;
+  const int kend = args.ws ? min(K, kbeg + args.kchunk) : K;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int lrow = lane >> 3;                 // row within the 8-row DMA group
+  const int lchunk = (lane & 7) ^ lrow;       // source chunk for this lane's LDS slot
+  const bf16_t* zero = args.zero;
+
+  // ---- per-lane source bookkeeping ----
+  const bf16_t* a_ptr[IA];
+  bool a_ok[IA];
+  int a_ihb[IA], a_iwb[IA];
+  size_t a_bbase[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int m = m0 + (wid * IA + i) * 8 + lrow;
+    a_ok[i] = m < M;
+    if constexpr (CONV) {
+      const int mm = a_ok[i] ? m : 0;
+      const int hw = args.Ho * args.Wo;
+      const int b = mm / hw, r = mm - b * hw;
+      const int oh = r / args.Wo, ow = r - oh * args.Wo;
+      a_ihb[i] = oh * args.stride - args.pt;
+      a_iwb[i] = ow * args.stride - args.pl;
+      a_bbase[i] = (size_t)b * args.H * args.Wd;
+      a_ptr[i] = nullptr;
+    } else {
+      a_ptr[i] = args.A + (size_t)(a_ok[i] ? m : 0) * args.lda + kbeg + lchunk * 8;
+      a_ihb[i] = a_iwb[i] = 0;
+      a_bbase[i] = 0;
+    }
+  }
+  const bf16_t* b_ptr[IB];
+  bool b_ok[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int n = n0 + (wid * IB + i) * 8 + lrow;
+    b_ok[i] = n < N;
+    b_ptr[i] = args.W + (size_t)(b_ok[i] ? n : 0) * args.ldb + kbeg + lchunk * 8;
+  }
+  int c_ci = 0, c_ky = 0, c_kx = 0;
+  if constexpr (CONV) {
+    const int k0 = kbeg + lchunk * 8;
+    const int tap = k0 / args.Cin;
+    c_ci = k0 - tap * args.Cin;
+    c_ky = tap / args.kw;
+    c_kx = tap - c_ky * args.kw;
+  }
+  const int Hin = args.up2x ? 2 * args.H : args.H;
+  const int Win = args.up2x ? 2 * args.Wd : args.Wd;
+
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  auto issue = [&](int kt, int buf) {
+    bf16_t* as = smem + buf * STAGE;
+    bf16_t* bs = as + BM * BK;
+    const int k = kbeg + kt * BK + lchunk * 8;
+    const bool kin = k < kend;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const bf16_t* src = zero;
+      if constexpr (CONV) {
+        const int ih = a_ihb[i] + c_ky, iw = a_iwb[i] + c_kx;
+        if (kin && a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win) {
+          const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
+          src = args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + c_ci;
+        }
+      } else {
+        if (kin && a_ok[i]) src = a_ptr[i] + (size_t)kt * BK;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const bf16_t* src = (kin && b_ok[i]) ? b_ptr[i] + (size_t)kt * BK : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(bs + (wid * IB + i) * 8 * BK), 16, 0, 0);
+    }
+    if constexpr (CONV) {
+      c_ci += BK;
+      while (c_ci >= args.Cin) { c_ci -= args.Cin; if (++c_kx == args.kw) { c_kx = 0; ++c_ky; } }
+    }
+  };
+
+  v4f acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed once at most min(S-2, nk-1-kt) younger stages are in flight
+    const int younger = min(S - 2, nk - 1 - kt);
+    if constexpr (S >= 4) {
+      if (younger >= 2) vmcnt_wait<2 * LPG>();
+      else if (younger == 1) vmcnt_wait<LPG>();
+      else vmcnt_wait<0>();
+    } else if constexpr (S == 3) {
+      if (younger >= 1) vmcnt_wait<LPG>();
+      else vmcnt_wait<0>();
+    } else {
+      vmcnt_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+    const bf16_t* as = smem + (kt % S) * STAGE;
+    const bf16_t* bs = as + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v8s af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[i] = *reinterpret_cast<const v8s*>(as + swz(wm * WTM + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split);
+}
+
+template <int BM, int BN, int WM, int WN, int S>
+static int launch_glds(const GemmArgs& a, int ksplit, bool conv, hipStream_t s) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  if (conv)
+    gemm_glds_kernel<BM, BN, WM, WN, S, true><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
+  else
+    gemm_glds_kernel<BM, BN, WM, WN, S, false><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+CSK_API int csk_init() {
+  if (g_zero) return 0;
+  hipError_t e = hipMalloc(&g_zero, 4096);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(g_zero, 0, 4096);
+}
+
+int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hipStream_t s) {
+  if (!g_zero) return (int)hipErrorNotInitialized;
+  GemmArgs a = a0;
+  a.zero = g_zero;
+  if (a.act == ACT_GEGLU && !(tile == 11 || tile == 13 || tile == 15)) tile = 11;
+  switch (tile) {
+    case 11: return launch_glds<128, 128, 2, 2, 2>(a, ksplit, conv, s);
+    case 12: return launch_glds<128, 64, 4, 1, 3>(a, ksplit, conv, s);
+    case 13: return launch_glds<64, 128, 2, 2, 3>(a, ksplit, conv, s);
+    case 14: return launch_glds<64, 64, 2, 2, 4>(a, ksplit, conv, s);
+    case 15: return launch_glds<128, 128, 2, 2, 3>(a, ksplit, conv, s);
+    case 16: return launch_glds<128, 32, 4, 1, 4>(a, ksplit, conv, s);
+    case 17: return launch_glds<128, 64, 2, 2, 3>(a, ksplit, conv, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
