@@ -67,6 +67,12 @@ def format_args(job: dict):
         return _cb("video", "model_video_callback"), args
     if workflow == "txt2vid":
         return format_txt2vid_args(args)
+    if workflow == "upscale" or "esrgan" in args["model_name"].lower():
+        # extension: Real-ESRGAN x4 (not in the reference; roadmap README.md:34)
+        if "start_image_uri" in args:
+            args["image"] = get_image(args.pop("start_image_uri"), None)
+        args.pop("parameters", None)
+        return _cb("esrgan", "esrgan_callback"), args
     if args["model_name"].startswith("DeepFloyd/"):
         return _cb("deepfloyd", "diffusion_if_callback"), args
     return format_stable_diffusion_args(args)

@@ -56,17 +56,24 @@ class Conv2d(nn.Conv2d, Prepared):
             self.prepare()
         return self.wp
 
-    def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None):  # type: ignore[override]
+    def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None, act=None, out_scale=1.0,
+                out=None):  # type: ignore[override]
         kh, kw = self.kernel_size
-        if kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x:
+        if (kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x and act is None and out_scale == 1.0
+                and out is None and x.is_contiguous()):
             w2 = self.weight.view(self.out_channels, self.in_channels)
             y = ops.gemm(x, w2, self.bias, residual=residual)
             if bias2d is not None:
                 y = y + bias2d[:, None, None, :].to(y.dtype)
             return y
-        pad = self.padding[0] if padding is None else padding
+        if padding is None:
+            ph, pw = self.padding
+            pad = ph if ph == pw else (ph, pw, ph, pw)
+        else:
+            pad = padding
         return ops.conv2d(x, self._wp(), self.bias, self.stride[0], pad, residual=residual,
-                          up2x=up2x, bias2d=bias2d)
+                          up2x=up2x, bias2d=bias2d, act=act, out_scale=out_scale, out=out,
+                          dilation=max(self.dilation))
 
 
 class GroupNorm(nn.GroupNorm):
@@ -129,8 +136,8 @@ class Attention(Prepared):
         h, d = self.heads, self.dim_head
         if self.is_cross:
             q = self.to_q(x).view(b, s, h, d)
-            if kv is None:
-                kv = self.context_kv(ctx)
+            if kv is None:  # no context given: attend to itself (diffusers attn2 semantics)
+                kv = self.context_kv(ctx if ctx is not None else x)
             k, v = kv[:, :, 0], kv[:, :, 1]
         else:
             qkv = ops.gemm(x, self.w_qkv, self.b_qkv).view(b, s, 3, h, d)

@@ -49,6 +49,7 @@ class UNetConfig:
     # sd-x2-latent-upscaler / x4 upscaler style extra conditioning
     num_class_embeds: int | None = None
     class_embed_type: str | None = None
+    class_embeddings_concat: bool = False
 
     def per_block(self, v, n):
         return list(v) if isinstance(v, (list, tuple)) else [v] * n
@@ -96,6 +97,7 @@ class UNet2DConditionModel(Prepared):
         tlayers = cfg.per_block(cfg.transformer_layers_per_block, nb)
         temb_dim = ch[0] * 4
         g, eps = cfg.norm_num_groups, cfg.norm_eps
+        xdims = cfg.per_block(cfg.cross_attention_dim, nb)
 
         self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, padding=1)
         self.time_embedding = TimestepEmbedding(ch[0], temb_dim)
@@ -103,13 +105,15 @@ class UNet2DConditionModel(Prepared):
             self.add_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, temb_dim)
         if cfg.class_embed_type == "timestep":
             self.class_embedding = TimestepEmbedding(ch[0], temb_dim)
+        elif cfg.class_embed_type == "simple_projection":  # AudioLDM: CLAP embedding -> temb
+            self.class_embedding = Linear(cfg.projection_class_embeddings_input_dim, temb_dim)
+        rtemb = temb_dim * (2 if cfg.class_embeddings_concat else 1)
 
         def resnet(ci, co):
-            return ResnetBlock2D(ci, co, temb_dim, g, eps)
+            return ResnetBlock2D(ci, co, rtemb, g, eps)
 
         def xformer(c, i):
-            return Transformer2D(c, heads[i], cfg.cross_attention_dim, tlayers[i],
-                                 cfg.use_linear_projection, g)
+            return Transformer2D(c, heads[i], xdims[i], tlayers[i], cfg.use_linear_projection, g)
 
         self.down_blocks = nn.ModuleList()
         cout = ch[0]
@@ -127,6 +131,7 @@ class UNet2DConditionModel(Prepared):
         rch = list(reversed(ch))
         rheads = list(reversed(heads))
         rtl = list(reversed(tlayers))
+        rxd = list(reversed(xdims))
         self.up_blocks = nn.ModuleList()
         out_c = rch[0]
         for i, btype in enumerate(cfg.up_block_types):
@@ -141,7 +146,7 @@ class UNet2DConditionModel(Prepared):
                 res.append(resnet(rin + skip, out_c))
             att = None
             if btype.startswith("CrossAttn"):
-                att = [Transformer2D(out_c, rheads[i], cfg.cross_attention_dim, rtl[i],
+                att = [Transformer2D(out_c, rheads[i], rxd[i], rtl[i],
                                      cfg.use_linear_projection, g) for _ in range(nl)]
             self.up_blocks.append(_Block(res, att, "upsamplers", None if final else Upsample2D(out_c)))
 
@@ -201,6 +206,9 @@ class UNet2DConditionModel(Prepared):
         if self.cfg.class_embed_type == "timestep" and class_labels is not None:
             cl = timestep_embedding(class_labels.reshape(-1).float(), self.cfg.block_out_channels[0])
             temb = temb + self.class_embedding(cl.to(dtype))
+        elif self.cfg.class_embed_type == "simple_projection" and class_labels is not None:
+            cemb = self.class_embedding(class_labels.to(dtype))
+            temb = torch.cat([temb, cemb], -1) if self.cfg.class_embeddings_concat else temb + cemb
         return temb
 
     def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,

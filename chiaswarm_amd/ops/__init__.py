@@ -106,14 +106,15 @@ def norm_padding(padding):
     return tuple(int(p) for p in padding)
 
 
-def conv_out_size(h, w, kh, kw, stride, padding, up2x=False):
+def conv_out_size(h, w, kh, kw, stride, padding, up2x=False, dilation=1):
     pt, pl, pb, pr = norm_padding(padding)
     if up2x:
         h, w = 2 * h, 2 * w
-    return (h + pt + pb - kh) // stride + 1, (w + pl + pr - kw) // stride + 1
+    return ((h + pt + pb - dilation * (kh - 1) - 1) // stride + 1,
+            (w + pl + pr - dilation * (kw - 1) - 1) // stride + 1)
 
 
-def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0):
+def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, dilation=1):
     dt = _cdt(x)
     # NHWC tensor viewed as channels-last NCHW: no copies, MIOpen NHWC kernels
     xn = x.to(dt).permute(0, 3, 1, 2)
@@ -123,9 +124,9 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, 
     w = wp.to(dt).permute(0, 3, 1, 2)
     b = bias.to(dt) if bias is not None else None
     if pt == pb and pl == pr:
-        y = F.conv2d(xn, w, b, stride=stride, padding=(pt, pl))
+        y = F.conv2d(xn, w, b, stride=stride, padding=(pt, pl), dilation=dilation)
     else:
-        y = F.conv2d(F.pad(xn, (pl, pr, pt, pb)), w, b, stride=stride)
+        y = F.conv2d(F.pad(xn, (pl, pr, pt, pb)), w, b, stride=stride, dilation=dilation)
     y = y.permute(0, 2, 3, 1)
     if bias2d is not None:
         y = y + bias2d.to(dt)[:, None, None, :]
@@ -143,7 +144,7 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, 
 
 
 def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None, act=None,
-           out_scale=1.0, out=None):
+           out_scale=1.0, out=None, dilation=1):
     """NHWC conv.  ``wp``: packed [Cout, kh, kw, Cin].  ``up2x`` fuses a
     nearest-neighbour x2 upsample into the input addressing; ``bias2d`` [B, Cout]
     is a per-sample channel bias (ResNet time-embedding add) fused in the
@@ -152,12 +153,22 @@ def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bia
     if use_hip(x):
         from . import hip_ops
 
-        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out)
-    y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale)
+        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation)
+    y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, dilation)
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+def axpby_nhwc(x, z, a, b, out):
+    """out = a*x + b*z on NHWC (possibly channel-slice) views; in place allowed."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.axpby_nhwc(x, z, a, b, out)
+    out.copy_((a * x.to(_cdt(x)) + b * z.to(_cdt(x))).to(out.dtype))
+    return out
 
 
 def axpby(x, y, a, b):

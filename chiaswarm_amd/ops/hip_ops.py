@@ -20,7 +20,7 @@ sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p)
 sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p)
+    c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p)
 sig("csk_axpby", c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p)
 ACT["lrelu"] = 5
 sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -118,7 +118,7 @@ def _pix_stride(t):
     return ps
 
 
-def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None):
+def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None, dilation=1):
     """NHWC conv.  ``x``, ``residual`` and ``out`` may be channel-slice views of
     wider NHWC buffers (last dim contiguous): the kernel takes their pixel
     strides, so dense/concat blocks need no copies."""
@@ -141,7 +141,7 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
         Cin = xs = cp
     wp = wp.contiguous()
     pt, pl, pb, pr = norm_padding(padding)
-    Ho, Wo = conv_out_size(H, W, kh, kw, stride, padding, up2x)
+    Ho, Wo = conv_out_size(H, W, kh, kw, stride, padding, up2x, dilation)
     if out is None:
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
     ys = _pix_stride(out)
@@ -166,11 +166,26 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
         ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
         _lib.call("csk_conv2d", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
                   B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
-                  float(out_scale), tile, split, _p(ws), _s())
+                  float(out_scale), int(dilation), tile, split, _p(ws), _s())
 
     key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:{kh}:{stride}:{int(bool(up2x))}"
+    if kh != kw or dilation != 1:
+        key += f":{kw}:{dilation}"
     tile, split = tuning.choose(key, M, Cout, K, run)
     run(tile, split)
+    return out
+
+
+sig("csk_axpby_nhwc", c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_float, c_float, c_void_p)
+
+
+def axpby_nhwc(x, z, a, b, out):
+    """out = a*x + b*z on NHWC channel-slice views (in place allowed)."""
+    xs, zs, ys = _pix_stride(x), _pix_stride(z), _pix_stride(out)
+    if None in (xs, zs, ys) or x.shape != z.shape or x.shape != out.shape:
+        raise ValueError("axpby_nhwc: operands must be same-shape NHWC views")
+    B, H, W, C = x.shape
+    _lib.call("csk_axpby_nhwc", _p(out), ys, _p(x), xs, _p(z), zs, B * H * W, C, float(a), float(b), _s())
     return out
 
 

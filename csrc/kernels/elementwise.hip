@@ -182,6 +182,32 @@ CSK_API int csk_axpby(void* y, const void* x, const void* z, long long n, float 
   CSK_CHECK_LAUNCH();
 }
 
+// Strided NHWC form: y[p, c] = a*x[p, c] + b*z[p, c] over P pixels x C channels,
+// each operand with its own pixel stride (channel slices of wider buffers).
+__global__ void axpby_nhwc_kernel(bf16_t* __restrict__ y, int ys, const bf16_t* __restrict__ x, int xs,
+                                  const bf16_t* __restrict__ z, int zs, size_t P, int C, float a, float b) {
+  const int nv = C >> 3;
+  const size_t total = P * nv;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = i / nv;
+    const int c = (int)(i - p * nv) * 8;
+    float fx[8], fz[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + p * xs + c), fx);
+    unpack8(*reinterpret_cast<const uint4*>(z + p * zs + c), fz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fx[j] = a * fx[j] + b * fz[j];
+    *reinterpret_cast<uint4*>(y + p * ys + c) = pack8(fx);
+  }
+}
+
+CSK_API int csk_axpby_nhwc(void* y, int ys, const void* x, int xs, const void* z, int zs, long long P, int C, float a,
+                           float b, hipStream_t stream) {
+  if (C % 8 || ys % 8 || xs % 8 || zs % 8) return (int)hipErrorInvalidValue;
+  axpby_nhwc_kernel<<<ew_grid((size_t)P * (C / 8)), 256, 0, stream>>>((bf16_t*)y, ys, (const bf16_t*)x, xs,
+                                                                       (const bf16_t*)z, zs, (size_t)P, C, a, b);
+  CSK_CHECK_LAUNCH();
+}
+
 // --------------------------------------------------------------------------
 // Channel pad: [R, Cin] -> [R, Cout] (zero fill), for Cin % 8 != 0 convs.
 // --------------------------------------------------------------------------

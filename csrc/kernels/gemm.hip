@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     for (int i = 0; i < CA; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if constexpr (CONV) {
-        const int ih = a_ihb[i] + c_ky, iw = a_iwb[i] + c_kx;
+        const int ih = a_ihb[i] + c_ky * args.dil, iw = a_iwb[i] + c_kx * args.dil;
         if (kin && a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win) {
           const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
           v = *reinterpret_cast<const uint4*>(args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + c_ci);
@@ -266,8 +266,8 @@ CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, co
 // one concat buffer without copies).
 CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
                        int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
-                       int up2x, int xs, int ys, int rs, int act, float out_scale, int tile, int ksplit, void* ws,
-                       hipStream_t stream) {
+                       int up2x, int xs, int ys, int rs, int act, float out_scale, int dil, int tile, int ksplit,
+                       void* ws, hipStream_t stream) {
   if (Cin % 8 != 0 || xs % 8 != 0 || xs < Cin) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.W = (const bf16_t*)Wp; a.C = (bf16_t*)Y;
@@ -277,6 +277,7 @@ CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias,
   a.act = act; a.out_scale = out_scale;
   a.H = H; a.Wd = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.kh = kh; a.kw = kw; a.stride = stride; a.pt = pt; a.pl = pl;
   a.up2x = up2x;
+  a.dil = dil > 0 ? dil : 1;
   a.ws = (float*)ws;
   if (a.M == 0) return 0;
   return dispatch<true>(a, tile, ksplit, stream);

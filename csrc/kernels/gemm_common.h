@@ -20,6 +20,7 @@ struct GemmArgs {
   int kchunk;  // K elements per split (multiple of BK)
   // conv geometry
   int H, Wd, Cin, Ho, Wo, kh, kw, stride, pt, pl, up2x;
+  int dil;  // dilation (both spatial dims)
 };
 
 #define BK 64

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
     for (int i = 0; i < IA; ++i) {
       const bf16_t* src = zero;
       if constexpr (CONV) {
-        const int ih = a_ihb[i] + c_ky, iw = a_iwb[i] + c_kx;
+        const int ih = a_ihb[i] + c_ky * args.dil, iw = a_iwb[i] + c_kx * args.dil;
         if (kin && a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win) {
           const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
           src = args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + c_ci;

@@ -43,7 +43,8 @@ def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     ws = torch.empty(split * M * N, dtype=torch.float32, device=gpu)
-    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, 1, 2, tile, split, _p(ws), _s())
+    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, tile, split,
+              _p(ws), _s())
     ref = ops._ref_gemm(a.float().cpu(), w.float().cpu(), b.float().cpu(), r.float().cpu(), "silu")
     assert rel_err(out.cpu(), ref) < 1e-2
     # implicit-GEMM conv, K split across taps
@@ -54,7 +55,7 @@ def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=gpu)
     ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=gpu)
     _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, _p(b2), None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1, H, W, 0,
-              tile, split, _p(ws), _s())
+              Cin, Cout, 0, 0, 1.0, 1, tile, split, _p(ws), _s())
     ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), None, 1, 1, None, False, b2.float().cpu())
     assert rel_err(y.cpu(), ref) < 1e-2
 
