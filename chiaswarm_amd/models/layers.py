@@ -76,6 +76,42 @@ class Conv2d(nn.Conv2d, Prepared):
                           dilation=max(self.dilation))
 
 
+class Conv1d(nn.Conv1d, Prepared):
+    """1-D conv on token-layout [B, T, C] tensors (state dict = nn.Conv1d);
+    runs the implicit-GEMM conv kernel on the [B, 1, T, C] view with a (1, k)
+    packed kernel.  Only stride 1 (HiFi-GAN / EnCodec decoder convs)."""
+
+    def prepare(self):
+        self.wp = self.weight.detach().permute(0, 2, 1).unsqueeze(1).contiguous()  # [Cout, 1, k, Cin]
+
+    def _wp(self):
+        wp = getattr(self, "wp", None)
+        if wp is None or wp.device != self.weight.device or wp.dtype != self.weight.dtype:
+            self.prepare()
+        return self.wp
+
+    def forward(self, x, act=None, residual=None, out_scale=1.0, out=None, padding=None):  # type: ignore[override]
+        assert self.stride == (1,), "Conv1d: stride 1 only"
+        p = self.padding[0] if padding is None else padding
+        return ops.conv1d(x, self._wp(), self.bias, padding=p, dilation=self.dilation[0], act=act,
+                          residual=residual, out_scale=out_scale, out=out)
+
+
+class ConvTranspose1d(nn.ConvTranspose1d, Prepared):
+    """Transposed 1-D conv on [B, T, C] as ``stride`` polyphase convolutions
+    (``ops.pack_conv_transpose1d``): no zero-insertion."""
+
+    def prepare(self):
+        self.phases = ops.pack_conv_transpose1d(self.weight.detach(), self.stride[0], self.padding[0])
+
+    def forward(self, x, act=None):  # type: ignore[override]
+        ph = getattr(self, "phases", None)
+        if ph is None or (ph[0][0] is not None and (ph[0][0].device != self.weight.device
+                                                    or ph[0][0].dtype != self.weight.dtype)):
+            self.prepare()
+        return ops.conv_transpose1d(x, self.weight, self.bias, self.stride[0], self.padding[0], self.phases, act)
+
+
 class GroupNorm(nn.GroupNorm):
     def forward(self, x, silu=False):  # type: ignore[override]
         return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu=silu)

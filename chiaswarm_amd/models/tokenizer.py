@@ -119,3 +119,71 @@ class CLIPTokenizer:
             ids = ids + [pad] * (self.max_length - len(ids))
             out.append(ids)
         return torch.tensor(out, dtype=torch.long)
+
+
+class ByteBPETokenizer(CLIPTokenizer):
+    """GPT-2 / RoBERTa byte-level BPE (``vocab.json`` + ``merges.txt``): the
+    CLAP text tower of AudioLDM (RobertaTokenizer).  No lower-casing, no
+    ``</w>`` suffix, spaces folded into the following token ("Ġ").  Hash
+    fallback without vocabulary files, like ``CLIPTokenizer``."""
+
+    def __init__(self, model_dir: str | None = None, max_length: int = 77, vocab_size: int = 50265,
+                 bos: int = 0, eos: int = 2, pad: int = 1):
+        super().__init__(model_dir, max_length, pad_with_eos=False, vocab_size=vocab_size)
+        self._bos, self._eos, self.pad = bos, eos, pad
+        import regex
+
+        self._pat = regex.compile(r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+""")
+
+    @property
+    def bos(self):
+        return self._bos
+
+    @property
+    def eos(self):
+        return self._eos
+
+    def _bpe(self, token: str) -> list[str]:
+        if token in self.cache:
+            return self.cache[token].split(" ")
+        word = tuple(token)
+        while len(word) > 1:
+            pairs = {(word[i], word[i + 1]) for i in range(len(word) - 1)}
+            best = min(pairs, key=lambda p: self.bpe_ranks.get(p, float("inf")))
+            if best not in self.bpe_ranks:
+                break
+            first, second = best
+            new, i = [], 0
+            while i < len(word):
+                if i < len(word) - 1 and word[i] == first and word[i + 1] == second:
+                    new.append(first + second)
+                    i += 2
+                else:
+                    new.append(word[i])
+                    i += 1
+            word = tuple(new)
+        self.cache[token] = " ".join(word)
+        return list(word)
+
+    def encode_plain(self, text: str) -> list[int]:
+        ids: list[int] = []
+        for tok in self._pat.findall(text):
+            if self.encoder is not None:
+                t = "".join(self.byte_encoder[b] for b in tok.encode("utf-8"))
+                ids.extend(self.encoder[p] for p in self._bpe(t) if p in self.encoder)
+            else:
+                h = int.from_bytes(hashlib.blake2b(tok.encode(), digest_size=8).digest(), "little")
+                ids.append(h % (self.vocab_size - 4) + 4)
+        return ids
+
+    def __call__(self, texts: list[str] | str, pad: bool = False) -> list[list[int]]:  # type: ignore[override]
+        """Unpadded id lists ([bos] ids [eos]); attention needs no padding mask."""
+        if isinstance(texts, str):
+            texts = [texts]
+        out = []
+        for t in texts:
+            ids = [self.bos] + self.encode(t)[: self.max_length - 2] + [self.eos]
+            if pad:
+                ids = ids + [self.pad] * (self.max_length - len(ids))
+            out.append(ids)
+        return out

@@ -72,6 +72,39 @@ TINY = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
                   up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"),
                   num_heads=(2, 2), cross_attention_dim=32, sample_size=8)
 
+# AudioLDM (cvssp/audioldm-*): 8-channel mel latents, CLAP embedding as a
+# concatenated class embedding, attention blocks whose "cross" attention runs on
+# the hidden states themselves (no text sequence)
+AUDIOLDM = UNetConfig(
+    in_channels=8, out_channels=8, block_out_channels=(128, 256, 384, 640),
+    down_block_types=("DownBlock2D",) + ("CrossAttnDownBlock2D",) * 3,
+    up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
+    num_heads=8, cross_attention_dim=(128, 256, 384, 640), use_linear_projection=False,
+    class_embed_type="simple_projection", projection_class_embeddings_input_dim=512,
+    class_embeddings_concat=True, sample_size=128)
+TINY_AUDIOLDM = UNetConfig(
+    in_channels=8, out_channels=8, block_out_channels=(32, 64), layers_per_block=1,
+    down_block_types=("DownBlock2D", "CrossAttnDownBlock2D"), up_block_types=("CrossAttnUpBlock2D", "UpBlock2D"),
+    num_heads=2, cross_attention_dim=(32, 64), class_embed_type="simple_projection",
+    projection_class_embeddings_input_dim=32, class_embeddings_concat=True, sample_size=8)
+
+# stabilityai/stable-diffusion-x4-upscaler: 4 latent + 3 low-res RGB channels,
+# noise level as a class embedding, OpenCLIP-H context
+X4_UPSCALER = UNetConfig(
+    in_channels=7, out_channels=4, block_out_channels=(256, 512, 512, 1024),
+    down_block_types=("DownBlock2D",) + ("CrossAttnDownBlock2D",) * 3,
+    up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
+    num_heads=8, cross_attention_dim=1024, num_class_embeds=1000, sample_size=128)
+# stabilityai/sd-x2-latent-upscaler (geometry approximated with standard blocks:
+# 4 noisy + 4 low-res latent channels, CLIP-L context)
+LATENT_X2 = UNetConfig(
+    in_channels=8, out_channels=4, block_out_channels=(128, 256, 512, 512),
+    down_block_types=("DownBlock2D",) + ("CrossAttnDownBlock2D",) * 3,
+    up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
+    num_heads=(2, 4, 8, 8), cross_attention_dim=768, use_linear_projection=False, sample_size=64)
+TINY_X4 = dataclasses.replace(TINY, in_channels=7, num_class_embeds=1000)
+TINY_X2 = dataclasses.replace(TINY, in_channels=8)
+
 CONFIGS = {"sd15": SD15, "sd21": SD21, "sd21-v": SD21_V, "sdxl": SDXL, "pix2pix": PIX2PIX,
            "sd2-inpaint": INPAINT_SD2, "tiny": TINY}
 
@@ -107,6 +140,8 @@ class UNet2DConditionModel(Prepared):
             self.class_embedding = TimestepEmbedding(ch[0], temb_dim)
         elif cfg.class_embed_type == "simple_projection":  # AudioLDM: CLAP embedding -> temb
             self.class_embedding = Linear(cfg.projection_class_embeddings_input_dim, temb_dim)
+        elif cfg.num_class_embeds is not None:  # x4 upscaler: noise level as a class id
+            self.class_embedding = nn.Embedding(cfg.num_class_embeds, temb_dim)
         rtemb = temb_dim * (2 if cfg.class_embeddings_concat else 1)
 
         def resnet(ci, co):
@@ -209,6 +244,8 @@ class UNet2DConditionModel(Prepared):
         elif self.cfg.class_embed_type == "simple_projection" and class_labels is not None:
             cemb = self.class_embedding(class_labels.to(dtype))
             temb = torch.cat([temb, cemb], -1) if self.cfg.class_embeddings_concat else temb + cemb
+        elif self.cfg.num_class_embeds is not None and class_labels is not None:
+            temb = temb + self.class_embedding(class_labels.reshape(-1).long()).to(dtype).expand_as(temb)
         return temb
 
     def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,

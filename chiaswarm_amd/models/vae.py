@@ -30,6 +30,11 @@ class VAEConfig:
 SD_VAE = VAEConfig()
 SDXL_VAE = dataclasses.replace(SD_VAE, scaling_factor=0.13025)
 TINY_VAE = VAEConfig(block_out_channels=(32, 32, 32, 32), layers_per_block=1)
+# AudioLDM mel-spectrogram VAE: 1 channel in/out, 8 latent channels, f=4
+AUDIOLDM_VAE = VAEConfig(in_channels=1, out_channels=1, latent_channels=8, block_out_channels=(128, 256, 512),
+                         scaling_factor=0.9227914)
+TINY_AUDIO_VAE = VAEConfig(in_channels=1, out_channels=1, latent_channels=8, block_out_channels=(32, 32, 32),
+                           layers_per_block=1, scaling_factor=0.9227914)
 
 
 class _MidBlock(nn.Module):

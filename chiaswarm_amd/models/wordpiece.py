@@ -12,7 +12,8 @@ import zlib
 
 
 class WordPiece:
-    def __init__(self, model_dir: str | None = None, vocab_size: int = 30524):
+    def __init__(self, model_dir: str | None = None, vocab_size: int = 30524, lower: bool = True):
+        self.lower = lower
         self.vocab: dict[str, int] = {}
         self.inv: dict[int, str] = {}
         self.vocab_size = vocab_size
@@ -29,7 +30,7 @@ class WordPiece:
         return lo + zlib.crc32(word.encode()) % max(1, self.vocab_size - lo - 4)
 
     def encode(self, text: str) -> list[int]:
-        words = re.findall(r"\w+|[^\w\s]", text.lower())
+        words = re.findall(r"\w+|[^\w\s]", text.lower() if self.lower else text)
         if not self.vocab:
             return [self._synthetic(w) for w in words]
         ids = []

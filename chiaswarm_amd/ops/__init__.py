@@ -46,6 +46,19 @@ def _gelu_f(x):
     return F.gelu(x)
 
 
+_ACT_REF = {
+    None: lambda y: y, "none": lambda y: y, "gelu": F.gelu, "silu": F.silu,
+    "quick_gelu": lambda y: y * torch.sigmoid(1.702 * y), "lrelu": lambda y: F.leaky_relu(y, 0.2),
+    "lrelu0.1": lambda y: F.leaky_relu(y, 0.1), "lrelu0.01": lambda y: F.leaky_relu(y, 0.01),
+    "tanh": torch.tanh, "relu": F.relu, "elu": F.elu, "gelu_tanh": lambda y: F.gelu(y, approximate="tanh"),
+}
+
+
+def apply_act(y, act):
+    """Reference pointwise activation (codes shared with the GEMM/conv epilogue)."""
+    return _ACT_REF[act](y)
+
+
 def _cdt(t):
     """Reference compute dtype: fp32 on CPU; the tensor's own dtype on GPU (so
     ``reference`` mode on MI355X is the diffusers-style bf16 eager baseline:
@@ -63,12 +76,8 @@ def _ref_gemm(a2, w, bias, residual, act):
         m, n = y.shape
         y = y.view(m, n // (2 * GEGLU_BLOCK), 2, GEGLU_BLOCK)
         y = (y[:, :, 0, :] * _gelu_f(y[:, :, 1, :])).reshape(m, n // 2)
-    elif act == "gelu":
-        y = _gelu_f(y)
-    elif act == "silu":
-        y = F.silu(y)
-    elif act == "quick_gelu":
-        y = y * torch.sigmoid(1.702 * y)
+    else:
+        y = apply_act(y, act)
     if residual is not None:
         y = y + residual.reshape(y.shape).to(dt)
     return y.to(a2.dtype)
@@ -123,19 +132,14 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, 
     pt, pl, pb, pr = norm_padding(padding)
     w = wp.to(dt).permute(0, 3, 1, 2)
     b = bias.to(dt) if bias is not None else None
-    if pt == pb and pl == pr:
+    if pt == pb and pl == pr and min(pt, pl) >= 0:
         y = F.conv2d(xn, w, b, stride=stride, padding=(pt, pl), dilation=dilation)
     else:
         y = F.conv2d(F.pad(xn, (pl, pr, pt, pb)), w, b, stride=stride, dilation=dilation)
     y = y.permute(0, 2, 3, 1)
     if bias2d is not None:
         y = y + bias2d.to(dt)[:, None, None, :]
-    if act == "lrelu":
-        y = F.leaky_relu(y, 0.2)
-    elif act == "silu":
-        y = F.silu(y)
-    elif act == "gelu":
-        y = F.gelu(y)
+    y = apply_act(y, act)
     if out_scale != 1.0:
         y = y * out_scale
     if residual is not None:
@@ -161,14 +165,110 @@ def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bia
     return y
 
 
-def axpby_nhwc(x, z, a, b, out):
-    """out = a*x + b*z on NHWC (possibly channel-slice) views; in place allowed."""
+# ----------------------------------------------------------------------------
+# 1-D convolutions on token-layout tensors [B, T, C] (HiFi-GAN / EnCodec)
+# ----------------------------------------------------------------------------
+def conv1d(x, wp, bias=None, padding=0, dilation=1, act=None, residual=None, out_scale=1.0, out=None):
+    """x [B, T, Cin], packed wp [Cout, 1, k, Cin] -> [B, T', Cout]: the 2-D
+    implicit-GEMM conv on the [B, 1, T, C] view.  ``padding`` int or (left, right)."""
+    pl, pr = (padding, padding) if isinstance(padding, int) else padding
+    x4 = x.unsqueeze(1)
+    r4 = residual.unsqueeze(1) if residual is not None else None
+    o4 = out.unsqueeze(1) if out is not None else None
+    y = conv2d(x4, wp, bias, 1, (0, pl, 0, pr), residual=r4, act=act, out_scale=out_scale, out=o4,
+               dilation=dilation)
+    return y.squeeze(1)
+
+
+def pack_conv_transpose1d(w: torch.Tensor, stride: int, padding: int):
+    """Polyphase decomposition of ConvTranspose1d weight [Cin, Cout, k].
+
+    Output sample o = t*s + r only meets taps j = j0 + m*s with
+    j0 = (r + p) mod s, reading input t + q - m (q = (r + p) div s).  Each phase
+    r is therefore an ordinary correlation with nt = ceil((k - j0)/s) taps and
+    left padding nt - 1 - q, written straight into the interleaved output via
+    its pixel stride: no zero-insertion, s-fold fewer MACs than the upsample +
+    conv formulation.  Returns [(wp_r [Cout, 1, nt, Cin] or None, pl_r)] * s."""
+    cin, cout, k = w.shape
+    s, p = int(stride), int(padding)
+    phases = []
+    for r in range(s):
+        j0, q = (r + p) % s, (r + p) // s
+        nt = max(0, -(-(k - j0) // s))
+        if nt == 0:
+            phases.append((None, 0))
+            continue
+        taps = [j0 + (nt - 1 - u) * s for u in range(nt)]
+        wr = w[:, :, taps]  # [Cin, Cout, nt]
+        phases.append((wr.permute(1, 2, 0).unsqueeze(1).contiguous(), nt - 1 - q))
+    return phases
+
+
+def conv_transpose1d(x, w, bias, stride, padding, phases=None, act=None):
+    """x [B, L, Cin] -> [B, (L-1)*s - 2p + k, Cout] (PyTorch ConvTranspose1d
+    semantics, weight [Cin, Cout, k]).  ``act`` is applied to the output."""
+    b, L, _ = x.shape
+    cout, k = w.shape[1], w.shape[2]
+    s = int(stride)
+    lout = (L - 1) * s - 2 * padding + k
+    if not use_hip(x):
+        dt = _cdt(x)
+        y = F.conv_transpose1d(x.to(dt).transpose(1, 2), w.to(dt), bias.to(dt) if bias is not None else None,
+                               stride=s, padding=padding)
+        return apply_act(y.transpose(1, 2), act).to(x.dtype).contiguous()
+    if phases is None:
+        phases = pack_conv_transpose1d(w, s, padding)
+    return _conv_transpose1d_polyphase(x, phases, bias, s, lout, cout, act)
+
+
+def _conv_transpose1d_polyphase(x, phases, bias, s, lout, cout, act=None):
+    """Device-agnostic polyphase evaluation (the HIP path; CPU-testable)."""
+    b, L, _ = x.shape
+    tmax = -(-lout // s)
+    buf = torch.empty(b, tmax * s, cout, dtype=x.dtype, device=x.device)
+    view = buf.view(b, tmax, s, cout)
+    for r, (wp, pl) in enumerate(phases):
+        tr = -(-(lout - r) // s)
+        if tr <= 0:
+            continue
+        o = view[:, :tr, r, :]
+        if wp is None:
+            o.copy_((bias if bias is not None else torch.zeros(cout, device=x.device)).to(x.dtype).expand_as(o))
+            if act is not None:
+                o.copy_(apply_act(o.float(), act).to(o.dtype))
+            continue
+        nt = wp.shape[2]
+        pr = tr - L - pl + nt - 1  # makes the conv's output length exactly tr
+        if b > 1 and tr != tmax:  # short phase: batch stride != rows * pixel stride -> per sample
+            for i in range(b):
+                conv1d(x[i:i + 1], wp, bias, padding=(pl, pr), act=act, out=o[i:i + 1])
+        else:
+            conv1d(x, wp, bias, padding=(pl, pr), act=act, out=o)
+    return buf[:, :lout] if tmax * s != lout else buf
+
+
+def axpby_nhwc(x, z, a, b, out=None, act=None):
+    """out = act(a*x + b*z) on NHWC (possibly channel-slice) views; in place
+    allowed; ``z`` may be None (then out = act(a*x))."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
     if use_hip(x):
         from . import hip_ops
 
-        return hip_ops.axpby_nhwc(x, z, a, b, out)
-    out.copy_((a * x.to(_cdt(x)) + b * z.to(_cdt(x))).to(out.dtype))
+        if x.dim() == 3:  # token layout [B, T, C] -> [B, 1, T, C] views
+            hip_ops.axpby_nhwc(x.unsqueeze(1), z.unsqueeze(1) if z is not None else None, a, b, out.unsqueeze(1), act)
+            return out
+        return hip_ops.axpby_nhwc(x, z, a, b, out, act)
+    y = a * x.to(_cdt(x))
+    if z is not None:
+        y = y + b * z.to(_cdt(x))
+    out.copy_(apply_act(y, act).to(out.dtype))
     return out
+
+
+def act(x, kind, out=None):
+    """Standalone pointwise activation on an NHWC view."""
+    return axpby_nhwc(x, None, 1.0, 0.0, out, kind)
 
 
 def axpby(x, y, a, b):
@@ -187,14 +287,20 @@ def _ref_group_norm(x, gamma, beta, groups, eps, silu):
     dt = _cdt(x)
     c = x.shape[-1]
     xn = x.to(dt).movedim(-1, 1)  # channels-last view [B, C, ...]
-    y = F.group_norm(xn, groups, gamma.to(dt), beta.to(dt), eps)
+    if gamma.dim() == 2:  # per-sample affine [B, C] (scale-shift time conditioning)
+        y = F.group_norm(xn, groups, None, None, eps)
+        shp = (gamma.shape[0], c) + (1,) * (xn.dim() - 2)
+        y = y * gamma.to(dt).view(shp) + beta.to(dt).view(shp)
+    else:
+        y = F.group_norm(xn, groups, gamma.to(dt), beta.to(dt), eps)
     if silu:
         y = F.silu(y)
     return y.movedim(1, -1).to(x.dtype).contiguous()
 
 
 def group_norm(x, gamma, beta, groups=32, eps=1e-5, silu=False):
-    """GroupNorm over a channels-last tensor [B, ..., C] (+ optional fused SiLU)."""
+    """GroupNorm over a channels-last tensor [B, ..., C] (+ optional fused SiLU).
+    ``gamma``/``beta`` are [C], or [B, C] for a per-sample affine."""
     if use_hip(x):
         from . import hip_ops
 
@@ -204,7 +310,8 @@ def group_norm(x, gamma, beta, groups=32, eps=1e-5, silu=False):
 
 def _ref_layer_norm(x, gamma, beta, eps):
     dt = _cdt(x)
-    return F.layer_norm(x.to(dt), (x.shape[-1],), gamma.to(dt), beta.to(dt), eps).to(x.dtype)
+    return F.layer_norm(x.to(dt), (x.shape[-1],), gamma.to(dt), beta.to(dt) if beta is not None else None,
+                        eps).to(x.dtype)
 
 
 def layer_norm(x, gamma, beta, eps=1e-5):

@@ -22,9 +22,9 @@ sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
     c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p)
 sig("csk_axpby", c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p)
-ACT["lrelu"] = 5
+ACT.update({"lrelu": 5, "lrelu0.1": 6, "tanh": 7, "relu": 8, "lrelu0.01": 9, "elu": 10, "gelu_tanh": 11})
 sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_float, c_int, c_void_p)
+    c_float, c_int, c_int, c_void_p)
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p)
@@ -176,16 +176,21 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     return out
 
 
-sig("csk_axpby_nhwc", c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_float, c_float, c_void_p)
+sig("csk_axpby_nhwc", c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_float, c_float, c_int,
+    c_void_p)
 
 
-def axpby_nhwc(x, z, a, b, out):
-    """out = a*x + b*z on NHWC channel-slice views (in place allowed)."""
-    xs, zs, ys = _pix_stride(x), _pix_stride(z), _pix_stride(out)
-    if None in (xs, zs, ys) or x.shape != z.shape or x.shape != out.shape:
+def axpby_nhwc(x, z, a, b, out, act=None):
+    """out = act(a*x + b*z) on NHWC channel-slice views (in place allowed; z may be None)."""
+    xs, ys = _pix_stride(x), _pix_stride(out)
+    zs = _pix_stride(z) if z is not None else 0
+    if None in (xs, zs, ys) or (z is not None and x.shape != z.shape) or x.shape != out.shape:
         raise ValueError("axpby_nhwc: operands must be same-shape NHWC views")
-    B, H, W, C = x.shape
-    _lib.call("csk_axpby_nhwc", _p(out), ys, _p(x), xs, _p(z), zs, B * H * W, C, float(a), float(b), _s())
+    C = x.shape[-1]
+    P = x.numel() // C
+    if C % 8 or xs % 8 or ys % 8 or zs % 8:
+        raise ValueError("axpby_nhwc: channels / pixel strides must be multiples of 8")
+    _lib.call("csk_axpby_nhwc", _p(out), ys, _p(x), xs, _p(z), zs, P, C, float(a), float(b), ACT[act], _s())
     return out
 
 
@@ -202,14 +207,21 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     x = x.contiguous()
     B, C = x.shape[0], x.shape[-1]
     P = x.numel() // (B * C)
-    # ~1024 workgroups over the whole tensor, >= 32 pixels per chunk
-    nchunk = max(1, min(-(-1024 // B), -(-P // 32)))
+    # ~2048 workgroups over the whole tensor; a chunk is at least one pass of
+    # the workgroup's pixel rows (R = 256 threads / (C/8 vector columns))
+    rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
+    nchunk = max(1, min(-(-2048 // B), -(-P // rows)))
     chunk = -(-P // nchunk)
     nchunk = -(-P // chunk)
+    bstride = 0
+    if gamma.dim() == 2:
+        if gamma.shape != (B, C) or beta.shape != (B, C):
+            raise ValueError("group_norm: per-sample affine must be [B, C]")
+        gamma, beta, bstride = gamma.contiguous(), beta.contiguous(), C
     part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     y = torch.empty_like(x)
     _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
-              float(eps), int(bool(silu)), _s())
+              float(eps), int(bool(silu)), bstride, _s())
     return y
 
 

@@ -39,6 +39,9 @@ class StepCoeffs:
 def _betas(n=1000, start=0.00085, end=0.012, schedule="scaled_linear"):
     if schedule == "scaled_linear":
         return np.linspace(start ** 0.5, end ** 0.5, n, dtype=np.float64) ** 2
+    if schedule == "squaredcos_cap_v2":  # DeepFloyd IF / improved-DDPM cosine schedule
+        f = lambda t: math.cos((t + 0.008) / 1.008 * math.pi / 2) ** 2  # noqa: E731
+        return np.array([min(1 - f((i + 1) / n) / f(i / n), 0.999) for i in range(n)], dtype=np.float64)
     return np.linspace(start, end, n, dtype=np.float64)
 
 

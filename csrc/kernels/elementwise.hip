@@ -2,6 +2,7 @@
 // to uint8 (K15), row softmax (VAE single-head attention), channel padding.
 // All bf16 traffic is 16 bytes per lane (8 elements), grid-strided.
 #include "common.h"
+#include "gemm_common.h"  // apply_act
 
 static inline int ew_grid(size_t nvec) {
   size_t g = (nvec + 255) / 256;
@@ -182,10 +183,12 @@ CSK_API int csk_axpby(void* y, const void* x, const void* z, long long n, float 
   CSK_CHECK_LAUNCH();
 }
 
-// Strided NHWC form: y[p, c] = a*x[p, c] + b*z[p, c] over P pixels x C channels,
-// each operand with its own pixel stride (channel slices of wider buffers).
+// Strided NHWC form: y[p, c] = act(a*x[p, c] + b*z[p, c]) over P pixels x C
+// channels, each operand with its own pixel stride (channel slices of wider
+// buffers); z may be null.  Also the standalone activation op (HiFi-GAN
+// pre-activations, multi-receptive-field averaging).
 __global__ void axpby_nhwc_kernel(bf16_t* __restrict__ y, int ys, const bf16_t* __restrict__ x, int xs,
-                                  const bf16_t* __restrict__ z, int zs, size_t P, int C, float a, float b) {
+                                  const bf16_t* __restrict__ z, int zs, size_t P, int C, float a, float b, int act) {
   const int nv = C >> 3;
   const size_t total = P * nv;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -193,18 +196,25 @@ __global__ void axpby_nhwc_kernel(bf16_t* __restrict__ y, int ys, const bf16_t* 
     const int c = (int)(i - p * nv) * 8;
     float fx[8], fz[8];
     unpack8(*reinterpret_cast<const uint4*>(x + p * xs + c), fx);
-    unpack8(*reinterpret_cast<const uint4*>(z + p * zs + c), fz);
+    if (z) {
+      unpack8(*reinterpret_cast<const uint4*>(z + p * zs + c), fz);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fx[j] = a * fx[j] + b * fz[j];
+      for (int j = 0; j < 8; ++j) fx[j] = a * fx[j] + b * fz[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fx[j] *= a;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fx[j] = apply_act(act, fx[j]);
     *reinterpret_cast<uint4*>(y + p * ys + c) = pack8(fx);
   }
 }
 
 CSK_API int csk_axpby_nhwc(void* y, int ys, const void* x, int xs, const void* z, int zs, long long P, int C, float a,
-                           float b, hipStream_t stream) {
-  if (C % 8 || ys % 8 || xs % 8 || zs % 8) return (int)hipErrorInvalidValue;
+                           float b, int act, hipStream_t stream) {
+  if (C % 8 || ys % 8 || xs % 8 || zs % 8 || act == ACT_GEGLU) return (int)hipErrorInvalidValue;
   axpby_nhwc_kernel<<<ew_grid((size_t)P * (C / 8)), 256, 0, stream>>>((bf16_t*)y, ys, (const bf16_t*)x, xs,
-                                                                       (const bf16_t*)z, zs, (size_t)P, C, a, b);
+                                                                       (const bf16_t*)z, zs, (size_t)P, C, a, b, act);
   CSK_CHECK_LAUNCH();
 }
 

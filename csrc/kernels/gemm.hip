@@ -189,10 +189,7 @@ __global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
     for (int sidx = 0; sidx < ksplit; ++sidx) v += a.ws[(size_t)sidx * total + i];
     if (a.bias) v += bf2f(a.bias[n]);
     if (a.bias2d) v += bf2f(a.bias2d[(size_t)(m / a.rows_per_b) * N + n]);
-    if (a.act == ACT_GELU) v = gelu_f(v);
-    else if (a.act == ACT_SILU) v = silu_f(v);
-    else if (a.act == ACT_QGELU) v = qgelu_f(v);
-    else if (a.act == ACT_LRELU) v = v > 0.f ? v : 0.2f * v;
+    v = apply_act(a.act, v);
     v *= a.out_scale;
     if (a.res) v += bf2f(a.res[(size_t)m * a.ldr + n]);
     a.C[(size_t)m * a.ldc + n] = f2bf(v);

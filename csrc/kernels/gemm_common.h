@@ -3,7 +3,33 @@
 #pragma once
 #include "common.h"
 
-enum { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GEGLU = 3, ACT_QGELU = 4, ACT_LRELU = 5 };
+enum {
+  ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GEGLU = 3, ACT_QGELU = 4,
+  ACT_LRELU = 5,       // leaky relu 0.2 (ESRGAN)
+  ACT_LRELU_01 = 6,    // leaky relu 0.1 (HiFi-GAN)
+  ACT_TANH = 7,
+  ACT_RELU = 8,
+  ACT_LRELU_001 = 9,   // leaky relu 0.01 (torch default)
+  ACT_ELU = 10,        // EnCodec
+  ACT_GELU_TANH = 11,  // T5 "gelu_new"
+};
+
+// pointwise epilogue activation (every act except GEGLU, which pairs columns)
+__device__ __forceinline__ float apply_act(int act, float v) {
+  switch (act) {
+    case ACT_GELU: return gelu_f(v);
+    case ACT_SILU: return silu_f(v);
+    case ACT_QGELU: return qgelu_f(v);
+    case ACT_LRELU: return v > 0.f ? v : 0.2f * v;
+    case ACT_LRELU_01: return v > 0.f ? v : 0.1f * v;
+    case ACT_TANH: return tanhf(v);
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_LRELU_001: return v > 0.f ? v : 0.01f * v;
+    case ACT_ELU: return v > 0.f ? v : expm1f(v);
+    case ACT_GELU_TANH: return 0.5f * v * (1.f + tanhf(0.7978845608028654f * (v + 0.044715f * v * v * v)));
+    default: return v;
+  }
+}
 
 struct GemmArgs {
   const bf16_t* A;  // GEMM: [M][lda];  CONV: NHWC input [B][H][W][Cin]
@@ -107,18 +133,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(b2[n + j]) : 0.f;
       }
-      if (act == ACT_GELU) {
+      if (act != ACT_NONE) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-      } else if (act == ACT_SILU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
-      } else if (act == ACT_QGELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = qgelu_f(f[j]);
-      } else if (act == ACT_LRELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : 0.2f * f[j];
+        for (int j = 0; j < 8; ++j) f[j] = apply_act(act, f[j]);
       }
     }
     if (args.out_scale != 1.0f) {

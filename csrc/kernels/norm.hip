@@ -89,25 +89,27 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
   }
 }
 
-// stat[(b * G + g) * 2 + {mean, rstd}]: merge chunk partials (Chan), one wave per group.
+// stat[(b * G + g) * 2 + {mean, rstd}]: merge chunk partials (Chan); one wave
+// per (b, g) so the merge is spread over B*G/4 workgroups instead of B.
 __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stat,
-                                                                 int G, int nchunk, float eps) {
-  const int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int g = wid; g < G; g += GN_THREADS / 64) {
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int c = lane; c < nchunk; c += 64) {
-      const float* pp = part + (((size_t)b * nchunk + c) * G + g) * 3;
-      chan_combine(n, mean, m2, pp[0], pp[1], pp[2]);
-    }
+                                                                 int B, int G, int nchunk, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int bg = blockIdx.x * (GN_THREADS / 64) + (threadIdx.x >> 6);
+  if (bg >= B * G) return;
+  const int b = bg / G, g = bg - b * G;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int c = lane; c < nchunk; c += 64) {
+    const float* pp = part + (((size_t)b * nchunk + c) * G + g) * 3;
+    chan_combine(n, mean, m2, pp[0], pp[1], pp[2]);
+  }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
-      chan_combine(n, mean, m2, n2, me2, q2);
-    }
-    if (lane == 0) {
-      stat[(b * G + g) * 2] = mean;
-      stat[(b * G + g) * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
-    }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
+    chan_combine(n, mean, m2, n2, me2, q2);
+  }
+  if (lane == 0) {
+    stat[bg * 2] = mean;
+    stat[bg * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
   }
 }
 
@@ -115,8 +117,10 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
                                                               const float* __restrict__ stat,
                                                               const bf16_t* __restrict__ gamma,
                                                               const bf16_t* __restrict__ beta, int P, int C, int G,
-                                                              int chunk, int silu) {
+                                                              int chunk, int silu, int affine_bstride) {
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
+  gamma += (size_t)b * affine_bstride;  // per-sample affine ([B, C]) when affine_bstride == C
+  beta += (size_t)b * affine_bstride;
   const GnLayout L(C, tid);
   if (L.r >= L.R) return;
   const int Cg = C / G;
@@ -157,15 +161,17 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
 
 // part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
 CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma, const void* beta, int B, int P, int C,
-                           int G, int chunk, int nchunk, float eps, int silu, hipStream_t stream) {
+                           int G, int chunk, int nchunk, float eps, int silu, int affine_bstride,
+                           hipStream_t stream) {
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0) return (int)hipErrorInvalidValue;
   float* pt = (float*)part;
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
   gn_stats_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
-  gn_finalize_kernel<<<B, GN_THREADS, 0, stream>>>(pt, st, G, nchunk, eps);
+  gn_finalize_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(pt, st, B, G,
+                                                                                                  nchunk, eps);
   gn_apply_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
-                                                   (const bf16_t*)beta, P, C, G, chunk, silu);
+                                                   (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride);
   CSK_CHECK_LAUNCH();
 }
 
@@ -213,7 +219,12 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const bf16_t* __restric
     if (cv < NV) {
       float gg[8], bb[8], o[8];
       unpack8(reinterpret_cast<const uint4*>(gamma)[cv], gg);
-      unpack8(reinterpret_cast<const uint4*>(beta)[cv], bb);
+      if (beta) {
+        unpack8(reinterpret_cast<const uint4*>(beta)[cv], bb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (f[u][j] - mean) * rstd * gg[j] + bb[j];
       yr[cv] = pack8(o);
