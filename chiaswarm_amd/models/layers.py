@@ -14,6 +14,7 @@ import math
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import ops
 
@@ -308,8 +309,15 @@ class Upsample2D(nn.Module):
         super().__init__()
         self.conv = Conv2d(channels, channels, 3, padding=1)
 
-    def forward(self, x):
-        return self.conv(x, up2x=True)
+    def forward(self, x, size=None):
+        """Nearest x2 fused into the conv's input addressing; an explicit
+        ``size`` that is not exactly 2x (odd skip sizes, e.g. AudioLDM's mel
+        latents — diffusers' ``forward_upsample_size``) interpolates first."""
+        b, h, w, c = x.shape
+        if size is None or (int(size[0]), int(size[1])) == (2 * h, 2 * w):
+            return self.conv(x, up2x=True)
+        xi = F.interpolate(x.permute(0, 3, 1, 2), size=(int(size[0]), int(size[1])), mode="nearest")
+        return self.conv(xi.permute(0, 2, 3, 1).contiguous())
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos=True, shift=0.0,

@@ -293,7 +293,7 @@ class UNet2DConditionModel(Prepared):
                 if blk.attentions is not None:
                     h = run_attn(blk.attentions[j], h)
             if blk.upsamplers is not None:
-                h = blk.upsamplers[0](h)
+                h = blk.upsamplers[0](h, size=skips[-1].shape[1:3] if skips else None)
 
         h = self.conv_norm_out(h, silu=True)
         return self.conv_out(h)

@@ -87,7 +87,8 @@ class HifiGan(nn.Module):
 
     @torch.no_grad()
     def forward(self, mel: torch.Tensor) -> torch.Tensor:
-        """mel [B, T, model_in_dim] -> waveform [B, T * hop] (fp32)."""
+        """mel [B, T, model_in_dim] -> waveform [B, ~T * hop] (fp32; the transposed convs
+        add a few tail samples, trimmed by the caller)."""
         dt = self.conv_pre.weight.dtype
         x = mel.float()
         if self.cfg.normalize_before:

@@ -207,12 +207,13 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     x = x.contiguous()
     B, C = x.shape[0], x.shape[-1]
     P = x.numel() // (B * C)
-    # ~2048 workgroups over the whole tensor; a chunk is at least one pass of
-    # the workgroup's pixel rows (R = 256 threads / (C/8 vector columns))
+    # a chunk gives every thread >= 4 independent row loads (the kernels' unroll;
+    # R = 256 threads / (C/8 vector columns) rows per pass), with <= ~2048
+    # workgroups over the whole tensor
     rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
-    nchunk = max(1, min(-(-2048 // B), -(-P // rows)))
-    chunk = -(-P // nchunk)
+    chunk = max(4 * rows, -(-P * B // 2048))
     nchunk = -(-P // chunk)
+    chunk = -(-P // nchunk)
     bstride = 0
     if gamma.dim() == 2:
         if gamma.shape != (B, C) or beta.shape != (B, C):

@@ -277,3 +277,135 @@ def read_video_frames(path: str, max_frames: int = 100, max_fps: float = 30.0, h
         return frames, min(max_fps, 1000.0 / dur)
     except Exception as e:
         raise ValueError(f"cannot decode video input without ffmpeg ({e})") from e
+
+
+# ----------------------------------------------------------------------------
+# decoding our own I_PCM MP4s (no ffmpeg needed) + frame / clip helpers
+# ----------------------------------------------------------------------------
+def _unescape(nal: bytes) -> bytes:
+    return nal.replace(b"\x00\x00\x03", b"\x00\x00")
+
+
+class _BitReader:
+    def __init__(self, data: bytes):
+        self.d, self.p = data, 0
+
+    def u(self, n: int) -> int:
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | ((self.d[self.p >> 3] >> (7 - (self.p & 7))) & 1)
+            self.p += 1
+        return v
+
+    def ue(self) -> int:
+        z = 0
+        while self.u(1) == 0:
+            z += 1
+        return (1 << z) - 1 + self.u(z)
+
+    def se(self) -> int:
+        k = self.ue()
+        return (k + 1) // 2 if k & 1 else -(k // 2)
+
+
+def _find_box(data: bytes, tag: bytes, start=0, end=None):
+    end = len(data) if end is None else end
+    i = start
+    while i + 8 <= end:
+        size = struct.unpack(">I", data[i:i + 4])[0]
+        if data[i + 4:i + 8] == tag:
+            return i, size
+        if size < 8:
+            return None
+        i += size
+    return None
+
+
+def decode_ipcm_mp4(data: bytes) -> list[np.ndarray]:
+    """Decode an MP4 written by ``frames_to_mp4_ipcm`` (all-I_PCM H.264) back to
+    RGB frames.  Raises ValueError for any other stream."""
+    k = data.find(b"avc1", max(0, data.find(b"stsd")))  # the sample entry, not the ftyp brand
+    md = _find_box(data, b"mdat")
+    if k < 0 or md is None:
+        raise ValueError("not an avc1 mp4")
+    w, h = struct.unpack(">HH", data[k + 4 + 24:k + 4 + 28])
+    W16, H16 = (w + 15) // 16 * 16, (h + 15) // 16 * 16
+    wm, hm = W16 // 16, H16 // 16
+    i, end = md[0] + 8, md[0] + md[1]
+    frames = []
+    while i + 4 <= end:
+        n = struct.unpack(">I", data[i:i + 4])[0]
+        nal = data[i + 4:i + 4 + n]
+        i += 4 + n
+        if not nal or nal[0] & 0x1F != 5:
+            continue
+        rb = _unescape(nal[1:])
+        br = _BitReader(rb)
+        br.ue(); br.ue(); br.ue(); br.u(4); br.ue(); br.u(1); br.u(1); br.se()  # noqa: E702
+        if br.ue() != 1:
+            raise ValueError("unsupported slice header")
+        if br.ue() != 25:
+            raise ValueError("not an I_PCM stream")
+        pos = (br.p + 7) >> 3
+        nmb = wm * hm
+        buf = np.frombuffer(rb, np.uint8)
+        mbs = np.empty((nmb, 384), np.uint8)
+        for m in range(nmb):
+            if m:
+                pos += 2  # ue(25) + alignment of the next I_PCM macroblock
+            mbs[m] = buf[pos:pos + 384]
+            pos += 384
+        y = mbs[:, :256].reshape(hm, wm, 16, 16).transpose(0, 2, 1, 3).reshape(H16, W16).astype(np.float32)
+        cb = mbs[:, 256:320].reshape(hm, wm, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
+        cr = mbs[:, 320:].reshape(hm, wm, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
+        cb = cb.astype(np.float32).repeat(2, 0).repeat(2, 1) - 128.0
+        cr = cr.astype(np.float32).repeat(2, 0).repeat(2, 1) - 128.0
+        yy = (y - 16.0) * (255.0 / 219.0)
+        r = yy + 1.402 * cr * (255.0 / 224.0)
+        g = yy - (0.344136 * cb + 0.714136 * cr) * (255.0 / 224.0)
+        b = yy + 1.772 * cb * (255.0 / 224.0)
+        rgb = np.clip(np.rint(np.stack([r, g, b], -1)), 0, 255).astype(np.uint8)
+        frames.append(rgb[:h, :w])
+    return frames
+
+
+def get_frame(video_path: str, frame_index: int = 0):
+    """JPEG ``BytesIO`` of one frame of a video, or None (reference:
+    swarm/toolbox/video_helpers.py:6-25, used for video thumbnails)."""
+    import io
+
+    from PIL import Image
+
+    try:
+        frame = None
+        if have_ffmpeg():
+            r = subprocess.run(["ffmpeg", "-hide_banner", "-loglevel", "error", "-i", video_path, "-vf",
+                                f"select=eq(n\\,{int(frame_index)})", "-vframes", "1", "-f", "image2pipe",
+                                "-vcodec", "png", "pipe:1"], capture_output=True)
+            if r.returncode == 0 and r.stdout:
+                frame = Image.open(io.BytesIO(r.stdout)).convert("RGB")
+        if frame is None:
+            with open(video_path, "rb") as f:
+                data = f.read()
+            try:
+                frames = decode_ipcm_mp4(data)
+                frame = Image.fromarray(frames[min(int(frame_index), len(frames) - 1)])
+            except ValueError:
+                frames, _ = read_video_frames(video_path, max_frames=int(frame_index) + 1)
+                frame = frames[min(int(frame_index), len(frames) - 1)]
+        buf = io.BytesIO()
+        frame.save(buf, format="JPEG")
+        buf.seek(0)
+        return buf
+    except Exception as e:  # the reference prints and returns None
+        print(e)
+        return None
+
+
+def make_video(images, duration_seconds: float, content_type: str = "video/webm") -> tuple[bytes, str]:
+    """Clip of PIL images / HWC arrays spread over ``duration_seconds``
+    (reference: swarm/diffusion/video_maker.py:7-21, dead code there)."""
+    frames = np.stack([np.asarray(im.convert("RGB") if hasattr(im, "convert") else im, dtype=np.uint8)
+                       for im in images])
+    fps = max(1, int(round(len(frames) / max(duration_seconds, 1e-3))))
+    return frames_to_video(frames, fps, content_type)

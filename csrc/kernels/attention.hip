@@ -52,7 +52,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   constexpr int LPT = KB * CPR / 256;  // 16B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // K0 V0 K1 V1
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int fr = lane & 15, fg = lane >> 4;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
   const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;

@@ -28,7 +28,7 @@
 // tiles of one A row-panel land on one XCD's L2.
 #include "gemm_common.h"
 
-template <int BM, int BN, int WM, int WN, bool CONV>
+template <int BM, int BN, int WM, int WN, bool CONV, bool FAST>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
@@ -41,7 +41,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   bf16_t* As = smem;                 // [2][BM*BK]
   bf16_t* Bs = smem + 2 * BM * BK;   // [2][BN*BK]
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int wm = wid / WN, wn = wid % WN;
   const int M = args.M, N = args.N, K = args.K;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
@@ -97,8 +98,58 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
 
+  // FAST staging (see gemm_glds.hip): uniform tap, running per-row pointers,
+  // invalid rows / padding read the zero page -> no per-step address math.
+  const bf16_t* fa[CA];
+  const bf16_t* fb[CB];
+  int f_ky = 0, f_kx = 0, f_c = 0;
+  auto set_rows = [&]() {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int ih = a_ihb[i] + f_ky * args.dil, iw = a_iwb[i] + f_kx * args.dil;
+      const bool v = a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win;
+      const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
+      fa[i] = v ? args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + lc * 8 : args.zero + lc * 8;
+    }
+  };
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < CB; ++i) fb[i] = b_ok[i] ? b_ptr[i] + kbeg : args.zero + lc * 8;
+    if constexpr (CONV) {
+      const int tap = kbeg / args.Cin;
+      f_c = kbeg - tap * args.Cin;
+      f_ky = tap / args.kw;
+      f_kx = tap - f_ky * args.kw;
+      set_rows();
+    } else {
+#pragma unroll
+      for (int i = 0; i < CA; ++i) fa[i] = a_ok[i] ? a_ptr[i] + kbeg : args.zero + lc * 8;
+    }
+  }
+
   uint4 ra[CA], rb[CB];
   auto load_tiles = [&](int kt) {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < CA; ++i) ra[i] = *reinterpret_cast<const uint4*>(CONV ? fa[i] + f_c : fa[i]);
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
+        rb[i] = *reinterpret_cast<const uint4*>(fb[i]);
+        fb[i] += BK;
+      }
+      if constexpr (CONV) {
+        f_c += BK;
+        if (f_c == args.Cin) {
+          f_c = 0;
+          if (++f_kx == args.kw) { f_kx = 0; ++f_ky; }
+          set_rows();
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) fa[i] += BK;
+      }
+      return;
+    }
     const int k = kbeg + kt * BK + lc * 8;
     const bool kin = k < kend;
 #pragma unroll
@@ -175,7 +226,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 template <int BM, int BN, int WM, int WN, bool CONV>
 static int launch(const GemmArgs& a, int ksplit, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  gemm_kernel<BM, BN, WM, WN, CONV><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
+  const int span = ksplit > 1 ? a.kchunk : a.K;
+  const bool fast = a.zero && (CONV ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
+                    (size_t)(span + 2 * BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes() &&
+                    (!CONV || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes());
+  if (fast)
+    gemm_kernel<BM, BN, WM, WN, CONV, true><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
+  else
+    gemm_kernel<BM, BN, WM, WN, CONV, false><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -206,6 +264,7 @@ static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
 
 template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
+  a.zero = csk_zero_ptr();
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;

@@ -51,6 +51,11 @@ struct GemmArgs {
 
 #define BK 64
 
+// zero page owned by gemm_glds.hip (allocated by csk_init): LDS-DMA padding
+// source and the FAST staging paths' pointer target for invalid rows / taps
+const bf16_t* csk_zero_ptr();
+int csk_zero_bytes();
+
 // element offset of 16-byte chunk `chunk` (0..7) of row `row` in a [rows][64] bf16
 // tile; chunk XOR (row & 7) makes the ds_read_b128 fragment reads conflict-free.
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
@@ -63,7 +68,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int LDC_S = BN + 4;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int wm = wid / WN, wn = wid % WN;
   const int fr = lane & 15, fq = lane >> 4;
   const int M = args.M, N = args.N;

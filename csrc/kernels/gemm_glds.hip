@@ -13,16 +13,25 @@
 //     the wait is a COUNTED `s_waitcnt vmcnt((S-2) * loads_per_stage)` and the
 //     barrier is a raw s_barrier (never __syncthreads, whose vmcnt(0) would
 //     drain the ring) — cdna_hip_programming.md §5 "Pipelining across barriers".
+//   * FAST staging (Cin % 64 == 0 for convs, K % 64 == 0 for GEMMs — every UNet /
+//     VAE layer): a K-step never straddles a conv tap, so the tap is wave-uniform
+//     (SGPRs) and each lane keeps one source pointer per DMA row, recomputed only
+//     when the tap changes (every Cin/64 K-steps).  A K-step then costs one 64-bit
+//     pointer add per DMA instruction instead of the full im2col address + bounds
+//     logic (the PMC run measured ~6 VALU per MFMA on the generic path).  Invalid
+//     rows / padding taps point into a 128 KB zero page, large enough that the
+//     running channel offset never leaves it, so no per-step select is needed.
 #include "gemm_common.h"
 
 static bf16_t* g_zero = nullptr;
+#define ZERO_BYTES (128 * 1024)
 
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int S, bool CONV>
+template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST>
 __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
@@ -34,7 +43,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int wm = wid / WN, wn = wid % WN;
   const int M = args.M, N = args.N, K = args.K;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
@@ -94,9 +104,62 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
 
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
+
+  // ---- FAST path state: per-row running source pointers, uniform tap / channel offset ----
+  const bf16_t* fa[IA];
+  const bf16_t* fb[IB];
+  int f_ky = 0, f_kx = 0, f_c = 0;
+  auto set_rows = [&]() {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int ih = a_ihb[i] + f_ky * args.dil, iw = a_iwb[i] + f_kx * args.dil;
+      const bool v = a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win;
+      const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
+      fa[i] = v ? args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + lchunk * 8 : zero + lchunk * 8;
+    }
+  };
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < IB; ++i) fb[i] = b_ok[i] ? b_ptr[i] : zero + lchunk * 8;
+    if constexpr (CONV) {
+      const int tap = kbeg / args.Cin;
+      f_c = kbeg - tap * args.Cin;
+      f_ky = tap / args.kw;
+      f_kx = tap - f_ky * args.kw;
+      set_rows();
+    } else {
+#pragma unroll
+      for (int i = 0; i < IA; ++i) fa[i] = a_ok[i] ? a_ptr[i] : zero + lchunk * 8;
+    }
+  }
+
   auto issue = [&](int kt, int buf) {
     bf16_t* as = smem + buf * STAGE;
     bf16_t* bs = as + BM * BK;
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        __builtin_amdgcn_global_load_lds((gptr_t)fb[i], (lptr_t)(bs + (wid * IB + i) * 8 * BK), 16, 0, 0);
+        fb[i] += BK;
+      }
+      if constexpr (CONV) {
+        f_c += BK;
+        if (f_c == args.Cin) {
+          f_c = 0;
+          if (++f_kx == args.kw) { f_kx = 0; ++f_ky; }
+          set_rows();
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < IA; ++i) fa[i] += BK;
+      }
+      return;
+    }
     const int k = kbeg + kt * BK + lchunk * 8;
     const bool kin = k < kend;
 #pragma unroll
@@ -175,18 +238,31 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
 template <int BM, int BN, int WM, int WN, int S>
 static int launch_glds(const GemmArgs& a, int ksplit, bool conv, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  if (conv)
-    gemm_glds_kernel<BM, BN, WM, WN, S, true><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
-  else
-    gemm_glds_kernel<BM, BN, WM, WN, S, false><<<dim3(tiles, ksplit), 256, 0, s>>>(a);
+  // FAST staging: K-steps never straddle a tap / the K tail, and every running
+  // offset stays inside the zero page
+  const int span = ksplit > 1 ? a.kchunk : a.K;
+  const bool fast = (conv ? (a.Cin % BK == 0) : (a.K % BK == 0)) && a.K % BK == 0 &&
+                    (size_t)(span + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
+                    (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
+  dim3 grid(tiles, ksplit);
+  if (conv) {
+    if (fast) gemm_glds_kernel<BM, BN, WM, WN, S, true, true><<<grid, 256, 0, s>>>(a);
+    else gemm_glds_kernel<BM, BN, WM, WN, S, true, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (fast) gemm_glds_kernel<BM, BN, WM, WN, S, false, true><<<grid, 256, 0, s>>>(a);
+    else gemm_glds_kernel<BM, BN, WM, WN, S, false, false><<<grid, 256, 0, s>>>(a);
+  }
   return (int)hipGetLastError();
 }
 
+const bf16_t* csk_zero_ptr() { return g_zero; }
+int csk_zero_bytes() { return ZERO_BYTES; }
+
 CSK_API int csk_init() {
   if (g_zero) return 0;
-  hipError_t e = hipMalloc(&g_zero, 4096);
+  hipError_t e = hipMalloc(&g_zero, ZERO_BYTES);
   if (e != hipSuccess) return (int)e;
-  return (int)hipMemset(g_zero, 0, 4096);
+  return (int)hipMemset(g_zero, 0, ZERO_BYTES);
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hipStream_t s) {

@@ -33,30 +33,44 @@ struct GnLayout {
 };
 
 // part[((b * nchunk + chunk) * G + g) * 3 + {n, mean, M2}]
+// The pixel loop issues GN_UNROLL independent 16-byte loads before accumulating
+// (a chunk is only a few rows per thread, so a dependent load->add chain would
+// leave the kernel latency-bound at ~1 TB/s); LDS is sized to C (dynamic), not
+// GN_MAXC, so more workgroups fit per CU.
+#define GN_UNROLL 4
 __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
                                                               int P, int C, int G, int chunk, int nchunk) {
-  __shared__ float red[2][GN_MAXC];
+  extern __shared__ float red[];  // [2][C]
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
   const GnLayout L(C, tid);
   const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
   const bf16_t* xb = x + (size_t)b * P * C;
-  for (int i = tid; i < C; i += GN_THREADS) { red[0][i] = 0.f; red[1][i] = 0.f; }
+  for (int i = tid; i < 2 * C; i += GN_THREADS) red[i] = 0.f;
   float s[2][8], ss[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[u][j] = ss[u][j] = 0.f;
   if (L.r < L.R) {
-    for (int p = p0 + L.r; p < p1; p += L.R) {
-      const bf16_t* row = xb + (size_t)p * C;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int v = L.cv + u * L.NVT;
-        if (u < L.TPV && v < L.NV) {
-          float f[8];
-          unpack8(*reinterpret_cast<const uint4*>(row + v * 8), f);
+    for (int u = 0; u < 2; ++u) {
+      const int v = L.cv + u * L.NVT;
+      if (u < L.TPV && v < L.NV) {
+        for (int p = p0 + L.r; p < p1; p += GN_UNROLL * L.R) {
+          // unconditional loads from clamped rows (a select around each load would
+          // make hipcc wait vmcnt(0) per element); out-of-chunk rows are masked
+          uint4 q[GN_UNROLL];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s[u][j] += f[j]; ss[u][j] += f[j] * f[j]; }
+          for (int w = 0; w < GN_UNROLL; ++w)
+            q[w] = *reinterpret_cast<const uint4*>(xb + (size_t)min(p + w * L.R, p1 - 1) * C + v * 8);
+#pragma unroll
+          for (int w = 0; w < GN_UNROLL; ++w) {
+            const float mk = (p + w * L.R < p1) ? 1.f : 0.f;
+            float f[8];
+            unpack8(q[w], f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { const float t = f[j] * mk; s[u][j] += t; ss[u][j] += t * t; }
+          }
         }
       }
     }
@@ -69,8 +83,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
       if (u < L.TPV && v < L.NV) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          atomicAdd(&red[0][v * 8 + j], s[u][j]);
-          atomicAdd(&red[1][v * 8 + j], ss[u][j]);
+          atomicAdd(&red[v * 8 + j], s[u][j]);
+          atomicAdd(&red[C + v * 8 + j], ss[u][j]);
         }
       }
     }
@@ -79,7 +93,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
   const int Cg = C / G;
   for (int g = tid; g < G; g += GN_THREADS) {
     float sm = 0.f, sq = 0.f;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { sm += red[0][c]; sq += red[1][c]; }
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { sm += red[c]; sq += red[C + c]; }
     const float n = (float)(p1 - p0) * (float)Cg;
     const float mean = n > 0.f ? sm / n : 0.f;
     float* o = part + (((size_t)b * nchunk + ck) * G + g) * 3;
@@ -140,20 +154,29 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
   }
   const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
   const size_t boff = (size_t)b * P * C;
-  for (int p = p0 + L.r; p < p1; p += L.R) {
-    const size_t roff = boff + (size_t)p * C;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int v = L.cv + u * L.NVT;
-      if (u < L.TPV && v < L.NV) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + roff + v * 8), f);
+  for (int u = 0; u < 2; ++u) {
+    const int v = L.cv + u * L.NVT;
+    if (u < L.TPV && v < L.NV) {
+      for (int p = p0 + L.r; p < p1; p += GN_UNROLL * L.R) {
+        uint4 q[GN_UNROLL];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = f[j] * sa[u][j] + sb[u][j];
-          f[j] = silu ? silu_f(t) : t;
+        for (int w = 0; w < GN_UNROLL; ++w)
+          q[w] = *reinterpret_cast<const uint4*>(x + boff + (size_t)min(p + w * L.R, p1 - 1) * C + v * 8);
+#pragma unroll
+        for (int w = 0; w < GN_UNROLL; ++w) {
+          const int pp = p + w * L.R;
+          if (pp < p1) {
+            float f[8];
+            unpack8(q[w], f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float t = f[j] * sa[u][j] + sb[u][j];
+              f[j] = silu ? silu_f(t) : t;
+            }
+            *reinterpret_cast<uint4*>(y + boff + (size_t)pp * C + v * 8) = pack8(f);
+          }
         }
-        *reinterpret_cast<uint4*>(y + roff + v * 8) = pack8(f);
       }
     }
   }
@@ -167,7 +190,7 @@ CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma
   float* pt = (float*)part;
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
-  gn_stats_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
+  gn_stats_kernel<<<grid, GN_THREADS, 2 * C * sizeof(float), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
   gn_finalize_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(pt, st, B, G,
                                                                                                   nchunk, eps);
   gn_apply_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,

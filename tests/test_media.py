@@ -71,3 +71,47 @@ def test_frames_to_video_fallback():
     frames = np.zeros((2, 32, 32, 3), np.uint8)
     data, ct = media.frames_to_video(frames, 8, "video/mp4")
     assert ct == "video/mp4" and data[4:8] == b"ftyp"
+
+
+def test_ipcm_decoder_roundtrip_and_get_frame(tmp_path):
+    import numpy as np
+
+    from chiaswarm_amd.output import media
+
+    fr = np.zeros((3, 40, 56, 3), np.uint8)
+    fr[0] = (200, 30, 30)
+    fr[1] = (30, 200, 30)
+    fr[2, :, :28] = (30, 30, 200)
+    data = media.frames_to_mp4_ipcm(fr, 8)
+    dec = media.decode_ipcm_mp4(data)
+    assert len(dec) == 3 and dec[0].shape == (40, 56, 3)
+    # flat colours survive the BT.601 limited-range round trip within rounding
+    assert np.abs(dec[0].astype(int) - fr[0].astype(int)).max() <= 3
+    assert np.abs(dec[1].astype(int) - fr[1].astype(int)).max() <= 3
+    p = tmp_path / "clip.mp4"
+    p.write_bytes(data)
+    from PIL import Image
+
+    jpg = media.get_frame(str(p), 1)
+    im = Image.open(jpg)
+    assert im.size == (56, 40)
+    assert media.get_frame(str(tmp_path / "missing.mp4")) is None
+    blob, ct = media.make_video([fr[0], fr[1]], 0.25)
+    assert ct in ("video/webm", "video/mp4") and len(blob) > 100
+
+
+def test_type_helpers_and_device_pool():
+    from chiaswarm_amd.runtime import device_pool
+    from chiaswarm_amd.runtime.device import Device
+    from chiaswarm_amd.utils import get_type, has_method
+
+    assert get_type("chiaswarm_amd.schedulers", "EulerDiscreteScheduler").__name__ == "EulerDiscreteScheduler"
+    assert has_method([], "append") and not has_method([], "nope")
+    d = Device("cpu")
+    device_pool.add_device_to_pool(d)
+    assert device_pool.get_available_gpu_count() == 1
+    assert device_pool.remove_device_from_pool() is d
+    import pytest
+
+    with pytest.raises(RuntimeError):
+        device_pool.remove_device_from_pool()

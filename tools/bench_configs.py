@@ -5,6 +5,8 @@
   controlnet ControlNet-canny on SD1.5 512x512 (config #4)
   esrgan    Real-ESRGAN x4 512 -> 2048 (config #5)
   sd21-b1   SD2.1 512x512 50 steps batch 1 (latency)
+  audioldm  AudioLDM-S 10 s clip, 25 steps (txt2audio default)
+  bark      Bark (large) ~ one sentence
 
     python tools/bench_configs.py --only sdxl,esrgan [--impl hip|reference]
 Prints one JSON line per config (images/s, p50 latency ms).
@@ -93,6 +95,23 @@ def main():
         lat = timed(run, a.reps)
         emit("controlnet-canny-sd15-512-30step", 1, lat)
         del p
+    if "audioldm" in todo:
+        from chiaswarm_amd.pipelines.audio import AudioLDM
+
+        p = AudioLDM(str(dev))
+        g = torch.Generator(device=dev)
+        lat = timed(lambda: p(prompt="rain on a tin roof", num_inference_steps=25, audio_length_in_s=10.0,
+                              generator=g.manual_seed(0)), a.reps)
+        emit("audioldm-10s-25step", 1, lat, {"phases_ms": {k: round(v * 1000, 1) for k, v in p.timings.items()}})
+        del p
+    if "bark" in todo:
+        from chiaswarm_amd.models.bark import Bark
+
+        bk = Bark(str(dev), size="large")
+        lat = timed(lambda: bk.generate_audio("Hello, this is a test of the speech model.", seed=0,
+                                              max_semantic_tokens=256), a.reps, warm=0)
+        emit("bark-large-256-semantic-tokens", 1, lat)
+        del bk
     if "esrgan" in todo:
         from chiaswarm_amd.pipelines.esrgan import load_esrgan, upscale_x4
 
