@@ -58,12 +58,13 @@ class Conv2d(nn.Conv2d, Prepared):
         return self.wp
 
     def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None, act=None, out_scale=1.0,
-                out=None):  # type: ignore[override]
+                out=None, gn_stats=False):  # type: ignore[override]
         kh, kw = self.kernel_size
         if (kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x and act is None and out_scale == 1.0
                 and out is None and x.is_contiguous()):
             w2 = self.weight.view(self.out_channels, self.in_channels)
-            y = ops.gemm(x, w2, self.bias, residual=residual)
+            gr = x.shape[1] * x.shape[2] if (gn_stats and bias2d is None and x.dim() == 4) else 0
+            y = ops.gemm(x, w2, self.bias, residual=residual, gn_rows=gr)
             if bias2d is not None:
                 y = y + bias2d[:, None, None, :].to(y.dtype)
             return y
@@ -74,7 +75,7 @@ class Conv2d(nn.Conv2d, Prepared):
             pad = padding
         return ops.conv2d(x, self._wp(), self.bias, self.stride[0], pad, residual=residual,
                           up2x=up2x, bias2d=bias2d, act=act, out_scale=out_scale, out=out,
-                          dilation=max(self.dilation))
+                          dilation=max(self.dilation), gn_stats=gn_stats)
 
 
 class Conv1d(nn.Conv1d, Prepared):
@@ -267,8 +268,10 @@ class Transformer2D(nn.Module):
         h = self.proj_in(h).view(b, hh * ww, c)
         for i, blk in enumerate(self.transformer_blocks):
             h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i])
-        out = self.proj_out(h.view(b, hh, ww, c), residual=x)
-        return out
+        if isinstance(self.proj_out, Linear):
+            return ops.gemm(h.view(b, hh, ww, c), self.proj_out.weight, self.proj_out.bias, residual=x,
+                            gn_rows=hh * ww)
+        return self.proj_out(h.view(b, hh, ww, c), residual=x, gn_stats=True)
 
 
 class ResnetBlock2D(nn.Module):
@@ -286,10 +289,10 @@ class ResnetBlock2D(nn.Module):
         """``temb_proj``: this block's [B, Cout] time projection (already
         computed by the model's batched time-embedding GEMM)."""
         h = self.norm1(x, silu=True)
-        h = self.conv1(h, bias2d=temb_proj)
+        h = self.conv1(h, bias2d=temb_proj, gn_stats=True)  # norm2's statistics from conv1's epilogue
         h = self.norm2(h, silu=True)
         sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
-        return self.conv2(h, residual=sc)
+        return self.conv2(h, residual=sc, gn_stats=True)  # block output usually feeds the next GroupNorm
 
 
 class Downsample2D(nn.Module):
@@ -300,8 +303,8 @@ class Downsample2D(nn.Module):
 
     def forward(self, x):
         if self.pad_asym:
-            return self.conv(x, padding=(0, 0, 1, 1))
-        return self.conv(x)
+            return self.conv(x, padding=(0, 0, 1, 1), gn_stats=True)
+        return self.conv(x, gn_stats=True)
 
 
 class Upsample2D(nn.Module):
@@ -315,9 +318,9 @@ class Upsample2D(nn.Module):
         latents — diffusers' ``forward_upsample_size``) interpolates first."""
         b, h, w, c = x.shape
         if size is None or (int(size[0]), int(size[1])) == (2 * h, 2 * w):
-            return self.conv(x, up2x=True)
+            return self.conv(x, up2x=True, gn_stats=True)
         xi = F.interpolate(x.permute(0, 3, 1, 2), size=(int(size[0]), int(size[1])), mode="nearest")
-        return self.conv(xi.permute(0, 2, 3, 1).contiguous())
+        return self.conv(xi.permute(0, 2, 3, 1).contiguous(), gn_stats=True)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos=True, shift=0.0,

@@ -289,7 +289,7 @@ class UNet2DConditionModel(Prepared):
         for blk in self.up_blocks:
             for j, r in enumerate(blk.resnets):
                 s = skips.pop()
-                h = r(torch.cat([h, s], dim=-1), next(tprojs))
+                h = r(ops.cat_channels(h, s), next(tprojs))
                 if blk.attentions is not None:
                     h = run_attn(blk.attentions[j], h)
             if blk.upsamplers is not None:

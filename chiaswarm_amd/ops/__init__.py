@@ -83,20 +83,40 @@ def _ref_gemm(a2, w, bias, residual, act):
     return y.to(a2.dtype)
 
 
-def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None):
+def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, gn_rows=0):
     """y[..., N'] = act(a[..., K] @ w[N, K]^T + bias) + residual.
 
-    ``act='geglu'`` expects ``pack_geglu`` weights and returns N' = N/2."""
+    ``act='geglu'`` expects ``pack_geglu`` weights and returns N' = N/2.
+    ``gn_rows`` > 0 asks the HIP epilogue for the GroupNorm statistics of the
+    output (``gn_rows`` rows per sample) for the GroupNorm that consumes it."""
     lead = a.shape[:-1]
     k = a.shape[-1]
     a2 = a.reshape(-1, k)
     if use_hip(a):
         from . import hip_ops
 
-        y = hip_ops.gemm(a2, w, bias, residual, act)
+        y = hip_ops.gemm(a2, w, bias, residual, act, gn_rows=gn_rows)
     else:
         y = _ref_gemm(a2, w, bias, residual, act)
-    return y.view(*lead, y.shape[-1])
+    out = y.view(*lead, y.shape[-1])
+    st = getattr(y, "_csk_gn", None)
+    if st is not None:
+        out._csk_gn = st
+    return out
+
+
+def cat_channels(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """torch.cat on the channel (last) dim that keeps fused GroupNorm
+    statistics: they are per (row tile, channel), so the concatenated tensor's
+    statistics are the two parts side by side (UNet skip connections)."""
+    y = torch.cat([a, b], dim=-1)
+    sa, sb = getattr(a, "_csk_gn", None), getattr(b, "_csk_gn", None)
+    if sa is not None and sb is not None and sa[1] == sb[1]:
+        ca, cb = a.shape[-1], b.shape[-1]
+        nseg = sa[0].numel() // (2 * ca)
+        if nseg * 2 * cb == sb[0].numel():
+            y._csk_gn = (torch.cat([sa[0].view(nseg, ca, 2), sb[0].view(nseg, cb, 2)], 1).view(-1), sa[1])
+    return y
 
 
 # ----------------------------------------------------------------------------
@@ -148,16 +168,19 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, 
 
 
 def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None, act=None,
-           out_scale=1.0, out=None, dilation=1):
+           out_scale=1.0, out=None, dilation=1, gn_stats=False):
     """NHWC conv.  ``wp``: packed [Cout, kh, kw, Cin].  ``up2x`` fuses a
     nearest-neighbour x2 upsample into the input addressing; ``bias2d`` [B, Cout]
     is a per-sample channel bias (ResNet time-embedding add) fused in the
     epilogue; y = act(conv + bias + bias2d) * out_scale + residual.  ``x``,
-    ``residual`` and ``out`` may be channel slices of wider NHWC buffers."""
+    ``residual`` and ``out`` may be channel slices of wider NHWC buffers.
+    ``gn_stats``: the HIP epilogue also emits the GroupNorm statistics of the
+    output (consumed by ``group_norm`` of that tensor; skips its stats pass)."""
     if use_hip(x):
         from . import hip_ops
 
-        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation)
+        return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation,
+                              gn_stats)
     y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, dilation)
     if out is not None:
         out.copy_(y)

@@ -8,6 +8,7 @@ so a bad call raises here instead of faulting the GPU.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -17,17 +18,35 @@ from ._lib import c_float, c_int, c_int64, c_void_p, sig
 ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "geglu": 3, "quick_gelu": 4}
 
 sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p)
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p, c_void_p)
 sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p)
+    c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
+sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+    c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
+
+
+# ---------------------------------------------------------------------------
+# GroupNorm statistics fused into producer epilogues
+# ---------------------------------------------------------------------------
+def _gn_seg(tile, split, rows_per_b, M, code):
+    """Row-tile height usable for fused GN statistics, or 0."""
+    bm = tuning.TILES.get(tile, (0, 0))[0]
+    if split != 1 or code == 3 or bm == 0 or rows_per_b <= 0 or rows_per_b % bm or M % bm:
+        return 0
+    return bm
+
+
+def _gn_part(M, N, seg, device):
+    return torch.empty((M // seg) * N * 2, dtype=torch.float32, device=device)
 sig("csk_axpby", c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p)
 ACT.update({"lrelu": 5, "lrelu0.1": 6, "tanh": 7, "relu": 8, "lrelu0.01": 9, "elu": 10, "gelu_tanh": 11})
 sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
     c_float, c_int, c_int, c_void_p)
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
+ATTN_VARIANT = int(os.environ.get("CSK_ATTN", "0"))  # 0 auto, 1 plain, 2 pipelined (D <= 64)
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
-    c_int, c_float, c_int, c_void_p)
+    c_int, c_float, c_int, c_int, c_void_p)
 sig("csk_silu", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
@@ -67,7 +86,9 @@ def pad_last(x: torch.Tensor, n: int) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
-def gemm(a2, w, bias=None, residual=None, act=None, out=None):
+def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0):
+    """``gn_rows`` > 0: also produce GroupNorm statistics of the output for a
+    consumer GN (rows per sample = gn_rows), attached as ``out._csk_gn``."""
     _bf16(a2, "gemm.a")
     _bf16(w, "gemm.w")
     M, K = a2.shape
@@ -96,13 +117,17 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None):
         _bf16(bias, "gemm.bias")
     lda, ldb = a2.stride(0), w.stride(0)
 
-    def run(tile, split):
+    def run(tile, split, part=None):
         ws = torch.empty(split * M * N, dtype=torch.float32, device=a2.device) if split > 1 else None
         _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
-                  M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, tile, split, _p(ws), _s())
+                  M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
-    run(tile, split)
+    seg = _gn_seg(tile, split, gn_rows, M, code) if gn_rows and out.is_contiguous() else 0
+    part = _gn_part(M, N, seg, a2.device) if seg else None
+    run(tile, split, part)
+    if part is not None:
+        out._csk_gn = (part, seg)
     return out
 
 
@@ -118,7 +143,8 @@ def _pix_stride(t):
     return ps
 
 
-def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None, dilation=1):
+def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None, dilation=1,
+           gn_stats=False):
     """NHWC conv.  ``x``, ``residual`` and ``out`` may be channel-slice views of
     wider NHWC buffers (last dim contiguous): the kernel takes their pixel
     strides, so dense/concat blocks need no copies."""
@@ -162,17 +188,21 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     M, K = B * Ho * Wo, kh * kw * Cin
     code = ACT[act]
 
-    def run(tile, split):
+    def run(tile, split, part=None):
         ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
         _lib.call("csk_conv2d", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
                   B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
-                  float(out_scale), int(dilation), tile, split, _p(ws), _s())
+                  float(out_scale), int(dilation), _p(part), tile, split, _p(ws), _s())
 
     key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:{kh}:{stride}:{int(bool(up2x))}"
     if kh != kw or dilation != 1:
         key += f":{kw}:{dilation}"
     tile, split = tuning.choose(key, M, Cout, K, run)
-    run(tile, split)
+    seg = _gn_seg(tile, split, Ho * Wo, M, code) if gn_stats and ys == Cout else 0
+    part = _gn_part(M, Cout, seg, x.device) if seg else None
+    run(tile, split, part)
+    if part is not None:
+        out._csk_gn = (part, seg)
     return out
 
 
@@ -219,8 +249,16 @@ def group_norm(x, gamma, beta, groups, eps, silu):
         if gamma.shape != (B, C) or beta.shape != (B, C):
             raise ValueError("group_norm: per-sample affine must be [B, C]")
         gamma, beta, bstride = gamma.contiguous(), beta.contiguous(), C
-    part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     y = torch.empty_like(x)
+    fused = getattr(x, "_csk_gn", None)
+    if fused is not None:
+        fpart, seg = fused
+        if P % seg == 0 and fpart.numel() == (B * P // seg) * C * 2:
+            stat = torch.empty(B * groups * 2, dtype=torch.float32, device=x.device)
+            _lib.call("csk_group_norm_part", _p(y), _p(x), _p(fpart), seg, _p(stat), _p(gamma), _p(beta), B, P, C,
+                      groups, chunk, nchunk, float(eps), int(bool(silu)), bstride, _s())
+            return y
+    part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
               float(eps), int(bool(silu)), bstride, _s())
     return y
@@ -247,7 +285,7 @@ def attention(q, k, v, scale, causal=False):
     o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
     st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
-              _s())
+              ATTN_VARIANT, _s())
     return o
 
 

@@ -158,6 +158,12 @@ class StableDiffusion:
         # (orig_h, orig_w, crop_top, crop_left, target_h, target_w)
         return torch.tensor([[h, w, 0, 0, h, w]] * b, dtype=torch.float32, device=device)
 
+    def _phase_sync(self):
+        """Phase timings are device time: sync at phase boundaries (a ~10 us
+        bubble per job; the decode needs the denoised latents anyway)."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
     # ------------------------------------------------------------------
     def _unet_eval(self, x_in, t, cross_kv, added, ctl):
         key = (x_in.shape, added is not None, ctl is not None, len(cross_kv))
@@ -274,6 +280,7 @@ class StableDiffusion:
         if added is not None:
             nrep = ctx.shape[0] // b
             added["time_ids"] = self._time_ids(nrep * b, height, width, self.device)
+        self._phase_sync()
         timings["text_encode"] = time.perf_counter() - t0
 
         sched.set_timesteps(num_inference_steps)
@@ -324,6 +331,7 @@ class StableDiffusion:
         x = self.denoise(x, sched, cross_kv, guidance_scale, added, generator,
                          image_latents=image_latents, image_guidance=img_guid,
                          mask=mask_t, init_latents=init_latents, noise=noise, controlnet_fn=controlnet_fn)
+        self._phase_sync()
         timings["denoise"] = time.perf_counter() - t1
         if output_type == "latent":
             return PipelineOutput([], [False] * b, x, timings)

@@ -241,6 +241,205 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   }
 }
 
+// Software-pipelined variant (D <= 64, 3 LDS K/V buffers, one barrier per
+// block): S for block kb+1 is issued on the matrix cores BEFORE the online
+// softmax of block kb, so the exp/max/sum VALU work of one block overlaps the
+// QK^T MFMAs of the next inside a single wave (cdna_hip_programming.md T15
+// "compute[cur] || finish[prev]"); block kb+2 is register-staged meanwhile and
+// written to the buffer freed two blocks ago, so no second barrier is needed.
+template <int QT>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a) {
+  constexpr int DP = 64;
+  constexpr int CPR = DP / 8;
+  constexpr int KB = 64;
+  constexpr int DS = DP / 32;
+  constexpr int DT = DP / 16;
+  constexpr int QROWS = QT * 16 * 4;
+  constexpr int TILE = KB * DP;
+  constexpr int LPT = KB * CPR / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * 2 * TILE];  // (K, V) x 3
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nqb = (a.Sq + QROWS - 1) / QROWS;
+  const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qb * QROWS + wid * QT * 16;
+  const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
+  const bf16_t* kp = a.k + b * a.skb + h * a.skh;
+  const bf16_t* vp = a.v + b * a.svb + h * a.svh;
+
+  v8s qf[QT][DS];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      const int qi = q0 + qt * 16 + fr, d = ds * 32 + 8 * fg;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qi < a.Sq && d < a.D) v = *reinterpret_cast<const uint4*>(qp + qi * a.sqs + d);
+      qf[qt][ds] = __builtin_bit_cast(v8s, v);
+    }
+  v4f oacc[DT][QT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < QT; ++j) oacc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  float mrow[QT], lrow[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
+
+  int kv_end = a.Skv;
+  if (a.causal) {
+    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (a.Skv - a.Sq);
+    kv_end = min(a.Skv, qlast + 1);
+  }
+  const int nkb = (kv_end + KB - 1) / KB;
+
+  uint4 rk[LPT], rv[LPT];
+  auto load_kv = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      const int key = min(kb * KB + row, a.Skv - 1), d = c * 8;  // clamped rows are masked later
+      uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (d < a.D) {
+        vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
+        vv = *reinterpret_cast<const uint4*>(vp + key * a.svs + d);
+      }
+      rk[i] = vk;
+      rv[i] = vv;
+    }
+  };
+  auto store_kv = [&](int buf) {
+    bf16_t* ks = smem + buf * 2 * TILE;
+    bf16_t* vs = ks + TILE;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
+      *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
+    }
+  };
+  auto qk = [&](int buf, v4f (&s)[4][QT]) {
+    const bf16_t* ks = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, ds * 4 + fg));
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[kt][qt], 0, 0, 0);
+      }
+  };
+
+  if (nkb > 0) { load_kv(0); store_kv(0); }
+  if (nkb > 1) { load_kv(1); store_kv(1); }
+  __syncthreads();
+  const float sl2 = a.scale_log2;
+  v4f s_cur[4][QT], s_nxt[4][QT];
+  if (nkb > 0) qk(0, s_cur);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb % 3;
+    if (kb + 2 < nkb) load_kv(kb + 2);
+    if (kb + 1 < nkb) qk((kb + 1) % 3, s_nxt);  // matrix cores busy while the softmax below runs
+
+    const int kbase = kb * KB;
+    const bool masked = a.causal || (kbase + KB > kv_end);
+    v8s pf[2][QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      if (masked) {
+        const int qi = q0 + qt * 16 + fr + (a.Skv - a.Sq);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kbase + kt * 16 + 4 * fg + r;
+            if (key >= kv_end || (a.causal && key > qi)) s_cur[kt][qt][r] = -INFINITY;
+          }
+      }
+      float mx = -1e30f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s_cur[kt][qt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrow[qt], mx * sl2);
+      const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
+      mrow[qt] = mnew;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s_cur[kt][qt][r], sl2, -mnew));
+          s_cur[kt][qt][r] = p;
+          ls += p;
+        }
+      lrow[qt] = lrow[qt] * alpha + ls;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
+#pragma unroll
+      for (int kp2 = 0; kp2 < 2; ++kp2) {
+        u32 w0 = pack2(s_cur[2 * kp2][qt][0], s_cur[2 * kp2][qt][1]);
+        u32 w1 = pack2(s_cur[2 * kp2][qt][2], s_cur[2 * kp2][qt][3]);
+        u32 w2 = pack2(s_cur[2 * kp2 + 1][qt][0], s_cur[2 * kp2 + 1][qt][1]);
+        u32 w3 = pack2(s_cur[2 * kp2 + 1][qt][2], s_cur[2 * kp2 + 1][qt][3]);
+        pf[kp2][qt] = __builtin_bit_cast(v8s, make_uint4(w0, w1, w2, w3));
+      }
+    }
+    const bf16_t* vs = smem + cur * 2 * TILE + TILE;
+#pragma unroll
+    for (int kp2 = 0; kp2 < 2; ++kp2)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int qq = fr >> 2, pp = fr & 3;
+        const int col = dt * 16 + 4 * pp;
+        const int r0 = kp2 * 32 + 4 * fg + qq, r1 = r0 + 16;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r0, col >> 3) + (col & 7)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r1, col >> 3) + (col & 7)));
+        v8s vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          oacc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kp2][qt], oacc[dt][qt], 0, 0, 0);
+      }
+    // block kb+2 -> the buffer that held block kb-1 (last read before the previous barrier)
+    if (kb + 2 < nkb) store_kv((kb + 2) % 3);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s_cur[kt][qt] = s_nxt[kt][qt];
+  }
+
+  bf16_t* op = a.o + b * a.sob + h * a.soh;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float l = lrow[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    const int qi = q0 + qt * 16 + fr;
+    if (qi >= a.Sq) continue;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d = dt * 16 + 4 * fg;
+      if (d >= a.D) continue;
+      uint2 w;
+      w.x = pack2(oacc[dt][qt][0] * inv, oacc[dt][qt][1] * inv);
+      w.y = pack2(oacc[dt][qt][2] * inv, oacc[dt][qt][3] * inv);
+      *reinterpret_cast<uint2*>(op + qi * a.sos + d) = w;
+    }
+  }
+}
+
 template <int DP, int QT>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
   constexpr int QROWS = QT * 64;
@@ -249,8 +448,9 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64)
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
-                          int Sq, int Skv, int D, float scale, int causal, hipStream_t stream) {
+                          int Sq, int Skv, int D, float scale, int causal, int variant, hipStream_t stream) {
   // strides: q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h) in elements
   if (D % 8 != 0 || D > 256) return (int)hipErrorInvalidValue;
   AttnArgs a;
@@ -264,7 +464,14 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   a.causal = causal;
   const long long wg4 = (long long)B * H * ((Sq + 255) / 256);
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
-  if (D <= 64) return launch_attn<64, 2>(a, stream);
+  if (D <= 64) {
+    if (variant == 2 || (variant == 0 && Skv > 128)) {
+      const int nqb = (Sq + 127) / 128;
+      attn_fwd_pipe_kernel<2><<<B * H * nqb, 256, 0, stream>>>(a);
+      return (int)hipGetLastError();
+    }
+    return launch_attn<64, 2>(a, stream);
+  }
   if (D <= 128) return launch_attn<128, 2>(a, stream);
   return launch_attn<256, 1>(a, stream);
 }

@@ -227,7 +227,11 @@ template <int BM, int BN, int WM, int WN, bool CONV>
 static int launch(const GemmArgs& a, int ksplit, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int span = ksplit > 1 ? a.kchunk : a.K;
-  const bool fast = a.zero && (CONV ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
+  // FAST staging measured SLOWER on this register-staged pipeline (127 -> 309 us on
+  // the 64x64x320 conv: the running-pointer loads lose their overlap with the
+  // MFMAs); it stays on for the LDS-DMA kernels only (gemm_glds.hip, 512 -> 732 TF/s).
+  constexpr bool kFastRegStaged = false;
+  const bool fast = kFastRegStaged && a.zero && (CONV ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
                     (size_t)(span + 2 * BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes() &&
                     (!CONV || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes());
   if (fast)
@@ -266,6 +270,7 @@ template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
+  if (a.gn_part && (ksplit > 1 || a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;
     const int nk = (a.K + BK - 1) / BK;
@@ -305,7 +310,7 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
 // y[M, ldc] = act(A[M, lda] . W[N, ldb]^T + bias + bias2d) * out_scale + res[M, ldr]
 CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
                      int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
-                     int tile, int ksplit, void* ws, hipStream_t stream) {
+                     void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (act == ACT_GEGLU && N % 32 != 0)) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
@@ -313,6 +318,7 @@ CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, co
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr > 0 ? ldr : ldc;
   a.rows_per_b = rows_per_b > 0 ? rows_per_b : 1; a.act = act; a.out_scale = out_scale;
   a.ws = (float*)ws;
+  a.gn_part = (float*)gn_part;
   if (M == 0 || N == 0) return 0;
   return dispatch<false>(a, tile, ksplit, stream);
 }
@@ -322,8 +328,8 @@ CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, co
 // one concat buffer without copies).
 CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
                        int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
-                       int up2x, int xs, int ys, int rs, int act, float out_scale, int dil, int tile, int ksplit,
-                       void* ws, hipStream_t stream) {
+                       int up2x, int xs, int ys, int rs, int act, float out_scale, int dil, void* gn_part, int tile,
+                       int ksplit, void* ws, hipStream_t stream) {
   if (Cin % 8 != 0 || xs % 8 != 0 || xs < Cin) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.W = (const bf16_t*)Wp; a.C = (bf16_t*)Y;
@@ -335,6 +341,7 @@ CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias,
   a.up2x = up2x;
   a.dil = dil > 0 ? dil : 1;
   a.ws = (float*)ws;
+  a.gn_part = (float*)gn_part;
   if (a.M == 0) return 0;
   return dispatch<true>(a, tile, ksplit, stream);
 }

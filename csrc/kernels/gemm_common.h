@@ -47,6 +47,10 @@ struct GemmArgs {
   // conv geometry
   int H, Wd, Cin, Ho, Wo, kh, kw, stride, pt, pl, up2x;
   int dil;  // dilation (both spatial dims)
+  // fused GroupNorm statistics of the OUTPUT (null: off): per (row tile, column)
+  // (mean, M2) over the tile's BM rows; requires rows_per_batch % BM == 0, no
+  // split-K, no GEGLU.  gn_part[((m0 / BM) * N + n) * 2 + {0, 1}]
+  float* gn_part;
 };
 
 #define BK 64
@@ -149,6 +153,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       for (int j = 0; j < 8; ++j) f[j] *= args.out_scale;
     }
     bf16_t* cp = args.C + (size_t)m * args.ldc + n;
+    float* crow = cs + row * LDC_S + cv * 8;  // final values back into LDS for the GN statistics
     if (full && ((((size_t)cp) & 15) == 0)) {
       if (args.res) {
         float rf[8];
@@ -157,12 +162,35 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         for (int j = 0; j < 8; ++j) f[j] += rf[j];
       }
       *reinterpret_cast<uint4*>(cp) = pack8(f);
+      if (args.gn_part) {
+        *reinterpret_cast<float4*>(crow) = make_float4(f[0], f[1], f[2], f[3]);
+        *reinterpret_cast<float4*>(crow + 4) = make_float4(f[4], f[5], f[6], f[7]);
+      }
     } else {
       for (int j = 0; j < 8 && n + j < outN; ++j) {
         float o = f[j];
         if (args.res) o += bf2f(args.res[(size_t)m * args.ldr + n + j]);
         cp[j] = f2bf(o);
+        crow[j] = o;
       }
+    }
+  }
+  if (args.gn_part) {
+    // column pass: (mean, M2) of each output channel over this tile's rows
+    // (two-pass in LDS: exact, no E[x^2]-E[x]^2 cancellation)
+    __syncthreads();
+    const int rows = min(BM, M - m0);
+    for (int c = tid; c < BN; c += 256) {
+      const int n = n0 + c;
+      if (n >= N || rows <= 0) continue;
+      float sm = 0.f;
+      for (int r = 0; r < rows; ++r) sm += cs[r * LDC_S + c];
+      const float mean = sm / (float)rows;
+      float m2 = 0.f;
+      for (int r = 0; r < rows; ++r) { const float d = cs[r * LDC_S + c] - mean; m2 += d * d; }
+      float* o = args.gn_part + ((size_t)(m0 / BM) * N + n) * 2;
+      o[0] = mean;
+      o[1] = m2;
     }
   }
 }

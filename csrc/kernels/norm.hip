@@ -182,6 +182,49 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
   }
 }
 
+// GroupNorm from statistics fused into the producing GEMM/conv epilogue
+// (GemmArgs::gn_part: per (row tile of seg_rows rows, channel) (mean, M2)):
+// merge them per (b, g) — one wave each — then the usual apply pass.  The
+// stats pass over the tensor disappears.
+__global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const float* __restrict__ part,
+                                                                      float* __restrict__ stat, int B, int C, int G,
+                                                                      int nseg, int seg_rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int bg = blockIdx.x * (GN_THREADS / 64) + (threadIdx.x >> 6);
+  if (bg >= B * G) return;
+  const int b = bg / G, g = bg - b * G, Cg = C / G;
+  const int ne = nseg * Cg;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int e = lane; e < ne; e += 64) {
+    const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
+    const float* pp = part + ((size_t)sg * C + c) * 2;
+    chan_combine(n, mean, m2, (float)seg_rows, pp[0], pp[1]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
+    chan_combine(n, mean, m2, n2, me2, q2);
+  }
+  if (lane == 0) {
+    stat[bg * 2] = mean;
+    stat[bg * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+  }
+}
+
+// stat: B*G*2 floats of workspace
+CSK_API int csk_group_norm_part(void* y, const void* x, const void* part, int seg_rows, void* stat, const void* gamma,
+                                const void* beta, int B, int P, int C, int G, int chunk, int nchunk, float eps,
+                                int silu, int affine_bstride, hipStream_t stream) {
+  if (C % 8 != 0 || C > GN_MAXC || C % G != 0 || seg_rows <= 0 || P % seg_rows != 0) return (int)hipErrorInvalidValue;
+  float* st = (float*)stat;
+  gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
+      (const float*)part, st, B, C, G, P / seg_rows, seg_rows, eps);
+  gn_apply_kernel<<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
+                                                              (const bf16_t*)beta, P, C, G, chunk, silu,
+                                                              affine_bstride);
+  CSK_CHECK_LAUNCH();
+}
+
 // part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
 CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma, const void* beta, int B, int P, int C,
                            int G, int chunk, int nchunk, float eps, int silu, int affine_bstride,

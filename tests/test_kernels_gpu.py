@@ -43,7 +43,7 @@ def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     ws = torch.empty(split * M * N, dtype=torch.float32, device=gpu)
-    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, tile, split,
+    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, None, tile, split,
               _p(ws), _s())
     ref = ops._ref_gemm(a.float().cpu(), w.float().cpu(), b.float().cpu(), r.float().cpu(), "silu")
     assert rel_err(out.cpu(), ref) < 1e-2
@@ -55,7 +55,7 @@ def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=gpu)
     ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=gpu)
     _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, _p(b2), None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1, H, W, 0,
-              Cin, Cout, 0, 0, 1.0, 1, tile, split, _p(ws), _s())
+              Cin, Cout, 0, 0, 1.0, 1, None, tile, split, _p(ws), _s())
     ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), None, 1, 1, None, False, b2.float().cpu())
     assert rel_err(y.cpu(), ref) < 1e-2
 
@@ -128,6 +128,20 @@ def test_attention(gpu, B, Sq, Skv, H, D, causal):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, scale, causal)) < 1.5e-2
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("B,Sq,Skv,H,D,causal", [(2, 1024, 1024, 5, 64, False), (1, 300, 517, 3, 64, False),
+                                                  (1, 333, 333, 2, 40, True), (2, 4096, 77, 5, 64, False)])
+def test_attention_variants(gpu, variant, B, Sq, Skv, H, D, causal):
+    q, k, v = (rnd(B, s, H, D, dev=gpu) for s in (Sq, Skv, Skv))
+    old = hip_ops.ATTN_VARIANT
+    hip_ops.ATTN_VARIANT = variant
+    try:
+        y = hip_ops.attention(q, k, v, 1 / math.sqrt(D), causal)
+    finally:
+        hip_ops.ATTN_VARIANT = old
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 1 / math.sqrt(D), causal)) < 1.5e-2
+
+
 def test_attention_fused_qkv_strides(gpu):
     B, S, H, D = 2, 333, 10, 64
     qkv = rnd(B, S, 3, H, D, dev=gpu)
@@ -174,3 +188,41 @@ def test_sched_step(gpu, cfg, prev, noise):
     ro, rx0 = ops._ref_sched_step(e, x, x0p, c, g, nz)
     assert rel_err(out, ro) < 1e-5 and rel_err(x0, rx0) < 1e-5
     assert n == x.numel()
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 17])
+def test_fused_group_norm_stats(gpu, tile):
+    """GroupNorm fed by conv-epilogue statistics == GroupNorm with its own stats pass."""
+    from chiaswarm_amd.ops import tuning
+
+    B, H, W, Cin, Cout = 2, 16, 16, 64, 320
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    res = rnd(B, H, W, Cout, dev=gpu) + 1.0
+    g, b = rnd(Cout, dev=gpu), rnd(Cout, dev=gpu)
+    key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:3:1:0"
+    t = tuning.table()
+    old = t.get(key)
+    t[key] = [tile, 1, 0.0]
+    try:
+        y = hip_ops.conv2d(x, wp, None, 1, 1, res, False, None, gn_stats=True)
+    finally:
+        if old is None:
+            t.pop(key, None)
+        else:
+            t[key] = old
+    assert getattr(y, "_csk_gn", None) is not None
+    fused = hip_ops.group_norm(y, g, b, 32, 1e-5, True)
+    plain = hip_ops.group_norm(y.clone(), g, b, 32, 1e-5, True)
+    ref = ops._ref_group_norm(y.float().cpu(), g.float().cpu(), b.float().cpu(), 32, 1e-5, True)
+    assert rel_err(fused.cpu(), ref) < 1e-2
+    assert rel_err(fused, plain) < 1e-2
+    # channel concat keeps the statistics (UNet skip connections)
+    y2 = hip_ops.conv2d(x, wp, None, 1, 1, None, False, None, gn_stats=True)
+    cat = ops.cat_channels(y, y2)
+    if getattr(y2, "_csk_gn", (None, -1))[1] == y._csk_gn[1]:
+        assert getattr(cat, "_csk_gn", None) is not None
+    g2, b2 = rnd(2 * Cout, dev=gpu), rnd(2 * Cout, dev=gpu)
+    yc = hip_ops.group_norm(cat, g2, b2, 32, 1e-5, False)
+    refc = ops._ref_group_norm(cat.float().cpu(), g2.float().cpu(), b2.float().cpu(), 32, 1e-5, False)
+    assert rel_err(yc.cpu(), refc) < 1e-2

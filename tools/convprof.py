@@ -30,7 +30,7 @@ def main():
     for tile in [int(t) for t in a.tiles.split(",")]:
         def run():
             _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Ci, Co, 3, 3, 1, 1, 1, H, W, 0,
-                      Ci, Co, 0, 0, 1.0, 1, tile, 1, None, _s())
+                      Ci, Co, 0, 0, 1.0, 1, None, tile, 1, None, _s())
         for _ in range(3):
             run()
         torch.cuda.synchronize()

@@ -41,6 +41,18 @@ def r(*s, scale=1.0):
     return (torch.randn(*s, device="cuda") * scale).bfloat16()
 
 
+def _attn_variant(q, k, v, var):
+    from chiaswarm_amd.ops import hip_ops
+
+    if not ops.use_hip(q):
+        return ops.attention(q, k, v)
+    old, hip_ops.ATTN_VARIANT = hip_ops.ATTN_VARIANT, var
+    try:
+        return ops.attention(q, k, v)
+    finally:
+        hip_ops.ATTN_VARIANT = old
+
+
 def cases():
     B = 8
     out = []
@@ -71,6 +83,9 @@ def cases():
         q, k, v = r(B, S, Hh, D), r(B, Skv, Hh, D), r(B, Skv, Hh, D)
         out.append((f"attn B{B} S{S} Skv{Skv} H{Hh} D{D}", 4 * B * Hh * S * Skv * D,
                     lambda q=q, k=k, v=v: ops.attention(q, k, v)))
+        for var in (1, 2):
+            out.append((f"attn B{B} S{S} Skv{Skv} H{Hh} D{D} variant{var}", 4 * B * Hh * S * Skv * D,
+                        lambda q=q, k=k, v=v, var=var: _attn_variant(q, k, v, var)))
     q, k, v = r(4, 4096, 1, 512), r(4, 4096, 1, 512), r(4, 4096, 1, 512)
     out.append(("vae attn B4 S4096 D512", 4 * 4 * 4096 * 4096 * 512, lambda: ops.attention(q, k, v)))
     # norms
