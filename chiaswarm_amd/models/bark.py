@@ -78,6 +78,16 @@ class _Attn(nn.Module):
         self.att_proj = Linear(c.n_embd, 3 * c.n_embd, bias=c.bias)
         self.out_proj = Linear(c.n_embd, c.n_embd, bias=c.bias)
 
+    def decode(self, x, residual, cache, pos_t, len_t):
+        """One-token step with device-side position / length (graph-capturable)."""
+        b = x.shape[0]
+        qkv = self.att_proj(x).view(b, 1, 3, self.nh, self.dh)
+        kc, vc = cache
+        kc.index_copy_(1, pos_t, qkv[:, :, 1])
+        vc.index_copy_(1, pos_t, qkv[:, :, 2])
+        o = ops.attention(qkv[:, :, 0], kc, vc, 1.0 / math.sqrt(self.dh), kv_len=len_t)
+        return self.out_proj(o.reshape(b, 1, -1), residual=residual)
+
     def forward(self, x, residual, causal, cache=None, pos=0):
         b, s, _ = x.shape
         qkv = self.att_proj(x).view(b, s, 3, self.nh, self.dh)
@@ -109,6 +119,10 @@ class _Block(nn.Module):
         x = self.attn(self.layernorm_1(x), x, causal, cache, pos)
         return self.mlp.out_proj(self.mlp.in_proj(self.layernorm_2(x), act="gelu"), residual=x)
 
+    def decode(self, x, cache, pos_t, len_t):
+        x = self.attn.decode(self.layernorm_1(x), x, cache, pos_t, len_t)
+        return self.mlp.out_proj(self.mlp.in_proj(self.layernorm_2(x), act="gelu"), residual=x)
+
 
 class BarkCausalGPT(nn.Module):
     """Semantic / coarse GPT (HF ``BarkCausalModel`` parameter names)."""
@@ -124,11 +138,49 @@ class BarkCausalGPT(nn.Module):
         self.cache = None
 
     def new_cache(self, batch=1):
+        """(Re)use the persistent per-layer KV buffers (allocated once, so a
+        captured decode graph stays valid across generations)."""
         c = self.cfg
         p = self.lm_head.weight
         shape = (batch, c.block_size, c.n_head, c.n_embd // c.n_head)
-        self.cache = [(torch.empty(shape, device=p.device, dtype=p.dtype),
-                       torch.empty(shape, device=p.device, dtype=p.dtype)) for _ in range(c.n_layer)]
+        kv = getattr(self, "_kv", None)
+        if kv is None or kv[0][0].shape != shape or kv[0][0].device != p.device or kv[0][0].dtype != p.dtype:
+            self._kv = [(torch.empty(shape, device=p.device, dtype=p.dtype),
+                         torch.empty(shape, device=p.device, dtype=p.dtype)) for _ in range(c.n_layer)]
+            self._graph = None
+        self.cache = self._kv
+
+    @torch.no_grad()
+    def _decode_fn(self, ids, pos_t, len_t):
+        x = self.input_embeds_layer(ids) + self.position_embeds_layer.weight.index_select(0, pos_t)[None]
+        x = x.to(self.lm_head.weight.dtype)
+        for i, layer in enumerate(self.layers):
+            x = layer.decode(x, self.cache[i], pos_t, len_t)
+        return self.lm_head(self.layernorm_final(x[:, -1])).float()
+
+    @torch.no_grad()
+    def decode_step(self, token: int, pos: int):
+        """Logits after appending ``token`` at position ``pos`` of the KV cache.
+        On the GPU the whole step (every layer) replays from one hipGraph."""
+        dev = self.lm_head.weight.device
+        st = getattr(self, "_dstate", None)
+        if st is None or st[0].device != dev:
+            st = (torch.zeros(1, 1, dtype=torch.long, device=dev), torch.zeros(1, dtype=torch.long, device=dev),
+                  torch.zeros(1, dtype=torch.int32, device=dev))
+            self._dstate = st
+        ids, pos_t, len_t = st
+        ids.fill_(int(token))
+        pos_t.fill_(int(pos))
+        len_t.fill_(int(pos) + 1)
+        from ..pipelines.graphs import CapturedCall, graphs_enabled
+
+        if not graphs_enabled(dev):
+            return self._decode_fn(ids, pos_t, len_t)
+        g = getattr(self, "_graph", None)
+        if g is None:
+            g = CapturedCall(self._decode_fn, ids=ids, pos_t=pos_t, len_t=len_t)
+            self._graph = g
+        return g.run(ids=ids, pos_t=pos_t, len_t=len_t)
 
     @torch.no_grad()
     def forward(self, ids=None, embeds=None, pos=0, last_only=True):
@@ -378,9 +430,8 @@ class Bark:
             if nxt == SEMANTIC_VOCAB or float(probs[-1]) >= min_eos_p:
                 break
             out.append(nxt)
-            logits = m(torch.tensor([[nxt]], device=dev), pos=pos)[0]
+            logits = m.decode_step(nxt, pos)[0]
             pos += 1
-        m.cache = None
         return np.array(out, dtype=np.int64)
 
     # -- stage 2 -----------------------------------------------------------
@@ -409,9 +460,8 @@ class Bark:
                 nxt = _sample(logits[lo:lo + CODEBOOK_SIZE], temp, gen) + lo
                 coarse.append(nxt)
                 n_step += 1
-                logits = m(torch.tensor([[nxt]], device=dev), pos=pos)[0]
+                logits = m.decode_step(nxt, pos)[0]
                 pos += 1
-        m.cache = None
         arr = np.array(coarse, dtype=np.int64).reshape(-1, N_COARSE).T - SEMANTIC_VOCAB
         for n in range(1, N_COARSE):
             arr[n] -= n * CODEBOOK_SIZE

@@ -365,14 +365,19 @@ def _ref_attention(q, k, v, scale, causal):
     return o.permute(0, 2, 1, 3).to(q.dtype).contiguous()
 
 
-def attention(q, k, v, scale=None, causal=False):
-    """softmax(q k^T * scale) v for [B, S, H, D] views; returns [B, Sq, H, D]."""
+def attention(q, k, v, scale=None, causal=False, kv_len=None):
+    """softmax(q k^T * scale) v for [B, S, H, D] views; returns [B, Sq, H, D].
+    ``kv_len`` (int32 device tensor [1]): only the first kv_len keys are used;
+    read on the device by the HIP kernel (hipGraph-capturable decode step)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     if use_hip(q):
         from . import hip_ops
 
-        return hip_ops.attention(q, k, v, scale, causal)
+        return hip_ops.attention(q, k, v, scale, causal, kv_len)
+    if kv_len is not None:
+        n = int(kv_len.reshape(-1)[0].item())
+        k, v = k[:, :n], v[:, :n]
     return _ref_attention(q, k, v, scale, causal)
 
 

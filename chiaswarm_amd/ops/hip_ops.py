@@ -46,7 +46,7 @@ sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 ATTN_VARIANT = int(os.environ.get("CSK_ATTN", "0"))  # 0 auto, 1 plain, 2 pipelined (D <= 64)
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
-    c_int, c_float, c_int, c_int, c_void_p)
+    c_int, c_float, c_int, c_int, c_void_p, c_void_p)
 sig("csk_silu", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
@@ -273,7 +273,9 @@ def layer_norm(x, gamma, beta, eps):
     return y
 
 
-def attention(q, k, v, scale, causal=False):
+def attention(q, k, v, scale, causal=False, kv_len=None):
+    """``kv_len``: optional int32 device tensor [1] = number of valid keys
+    (<= k.shape[1]), read by the kernel (graph-capturable KV-cache decode)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _bf16(t, "attention." + n)
         if t.stride(-1) != 1:
@@ -284,8 +286,10 @@ def attention(q, k, v, scale, causal=False):
         return _attention_gemm(q, k, v, scale)
     o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
     st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
+    if kv_len is not None and (kv_len.dtype != torch.int32 or not kv_len.is_cuda):
+        raise TypeError("attention: kv_len must be an int32 device tensor")
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
-              ATTN_VARIANT, _s())
+              ATTN_VARIANT, _p(kv_len), _s())
     return o
 
 

@@ -39,6 +39,8 @@ struct AttnArgs {
   int B, H, Sq, Skv, D;
   float scale_log2;
   int causal;
+  const int* kv_len;  // optional device-side key count (<= Skv): lets a fixed-shape
+                      // KV-cache decode step be captured once in a hipGraph
 };
 
 template <int DP, int QT>
@@ -55,6 +57,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int fr = lane & 15, fg = lane >> 4;
+  const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
   const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
   const int b = bh / a.H, h = bh % a.H;
@@ -85,10 +88,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
 
-  int kv_end = a.Skv;
+  int kv_end = Skv;
   if (a.causal) {  // keys beyond the last query row of this workgroup are never visible
-    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (a.Skv - a.Sq);
-    kv_end = min(a.Skv, qlast + 1);
+    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (Skv - a.Sq);
+    kv_end = min(Skv, qlast + 1);
   }
   const int nkb = (kv_end + KB - 1) / KB;
 
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
       const int key = kb * KB + row, d = c * 8;
       uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (key < a.Skv && d < a.D) {
+      if (key < Skv && d < a.D) {
         vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
         vv = *reinterpret_cast<const uint4*>(vp + key * a.svs + d);
       }
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       if (masked) {
-        const int qi = q0 + qt * 16 + fr + (a.Skv - a.Sq);
+        const int qi = q0 + qt * 16 + fr + (Skv - a.Sq);
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
+  const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
   const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
   const int b = bh / a.H, h = bh % a.H;
@@ -289,10 +293,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
 
-  int kv_end = a.Skv;
+  int kv_end = Skv;
   if (a.causal) {
-    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (a.Skv - a.Sq);
-    kv_end = min(a.Skv, qlast + 1);
+    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (Skv - a.Sq);
+    kv_end = min(Skv, qlast + 1);
   }
   const int nkb = (kv_end + KB - 1) / KB;
 
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
-      const int key = min(kb * KB + row, a.Skv - 1), d = c * 8;  // clamped rows are masked later
+      const int key = min(kb * KB + row, Skv - 1), d = c * 8;  // clamped rows are masked later
       uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (d < a.D) {
         vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       if (masked) {
-        const int qi = q0 + qt * 16 + fr + (a.Skv - a.Sq);
+        const int qi = q0 + qt * 16 + fr + (Skv - a.Sq);
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -450,7 +454,8 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
 
 // variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64)
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
-                          int Sq, int Skv, int D, float scale, int causal, int variant, hipStream_t stream) {
+                          int Sq, int Skv, int D, float scale, int causal, int variant, const void* kv_len,
+                          hipStream_t stream) {
   // strides: q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h) in elements
   if (D % 8 != 0 || D > 256) return (int)hipErrorInvalidValue;
   AttnArgs a;
@@ -462,6 +467,7 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   a.B = B; a.H = H; a.Sq = Sq; a.Skv = Skv; a.D = D;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.causal = causal;
+  a.kv_len = (const int*)kv_len;
   const long long wg4 = (long long)B * H * ((Sq + 255) / 256);
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {

@@ -8,4 +8,4 @@ timeout -k 10 300 python tools/opbench.py --out gpurun_out/opbench10.json > gpur
 timeout -k 10 600 python bench.py > gpurun_out/bench10.log 2>&1 || exit $?
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof10 -o bench -- python bench.py --steps 1 --warmup 1 > gpurun_out/prof10.log 2>&1 || exit $?
-timeout -k 10 600 python tools/bench_configs.py --only sdxl,esrgan,controlnet > gpurun_out/configs10.log 2>&1
+timeout -k 10 600 python tools/bench_configs.py --only sdxl,esrgan,controlnet,bark,audioldm > gpurun_out/configs10.log 2>&1

@@ -31,6 +31,18 @@ def test_kv_cache_decode_matches_full_forward():
         assert torch.allclose(step[0], full[0, i], atol=1e-4), i
 
 
+def test_decode_step_matches_full_forward():
+    m = _gpt()
+    ids = torch.randint(0, 1000, (1, 10))
+    m.cache = None
+    full = m(ids, last_only=False)
+    m.new_cache()
+    m(ids[:, :4], pos=0)
+    for i in range(4, 10):
+        step = m.decode_step(int(ids[0, i]), i)
+        assert torch.allclose(step[0], full[0, i], atol=1e-4), i
+
+
 def test_fine_model_shapes():
     _, _, fc = bk.bark_configs("tiny")
     m = bk.BarkFineGPT(fc).eval()

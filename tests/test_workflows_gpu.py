@@ -130,6 +130,12 @@ def test_bark_gpt_cache_parity(gpu):
     m(ids[:, :39], pos=0)
     step = m(ids[:, 39:40], pos=39)
     assert rel_err(step[0], full[0, 39]) < 3e-2
+    # hipGraph-replayed decode step (device-side position / kv length)
+    m.new_cache()
+    m(ids[:, :30], pos=0)
+    for i in range(30, 40):
+        g = m.decode_step(int(ids[0, i]), i)
+        assert rel_err(g[0], full[0, i]) < 3e-2, i
     with ops.ops_mode("reference"):
         m.cache = None
         ref = m(ids, last_only=False)
