@@ -114,3 +114,47 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
         t["load"] = load_s
         config["timings"] = {k: round(v, 4) for k, v in t.items()}
     return results, config
+
+
+def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dict]]:
+    """Several compatible txt2img jobs (``runtime.batcher``) as ONE denoising
+    batch.  ``jobs``: routed kwargs, each with its own ``generator``.  Each
+    job's initial noise comes from its own generator, so deterministic samplers
+    reproduce the job's solo images exactly.  Returns (artifacts, config) per job."""
+    import torch
+
+    k0 = jobs[0]
+    model_name = k0["model_name"]
+    pipe = load_sd(model_name, device_identifier, k0.get("revision", "main"))
+    sched_type = k0.get("scheduler_type", "DPMSolverMultistepScheduler")
+    sched = get_scheduler(sched_type, prediction_type=pipe.family.prediction_type)
+    steps = int(k0.get("num_inference_steps", 30))
+    sched.set_timesteps(steps)
+    height = int(k0.get("height") or pipe.family.default_size) // 8 * 8
+    width = int(k0.get("width") or pipe.family.default_size) // 8 * 8
+    prompts, negs, lat, counts = [], [], [], []
+    for kw in jobs:
+        n = max(1, int(kw.get("num_images_per_prompt", 1) or 1))
+        counts.append(n)
+        prompts += [kw.get("prompt", "")] * n
+        negs += [kw.get("negative_prompt") or ""] * n
+        noise = torch.randn((n, 4, height // 8, width // 8), generator=kw["generator"], device=pipe.device,
+                            dtype=torch.float32)
+        lat.append(noise.permute(0, 2, 3, 1) * sched.init_noise_sigma)
+    p = pipe(prompt=prompts, negative_prompt=negs, num_inference_steps=steps,
+             guidance_scale=float(k0.get("guidance_scale", 7.5)), height=height, width=width,
+             latents=torch.cat(lat, 0).contiguous(), scheduler=sched, generator=k0["generator"])
+    outs, i = [], 0
+    for kw, n in zip(jobs, counts):
+        op = OutputProcessor(kw.get("outputs", ["primary"]), kw.get("content_type", "image/jpeg"))
+        op.add_outputs(p.images[i:i + n])
+        cfg = dict(pipe.config)
+        cfg["scheduler"] = ["chiaswarm_amd", sched.name]
+        cfg["_pipeline_type"] = str(kw.get("pipeline_type", "DiffusionPipeline"))
+        if any(bool(x) for x in (p.nsfw_content_detected or [])[i:i + n]):
+            cfg["nsfw"] = True
+        if os.environ.get("SDAAS_TIMINGS"):
+            cfg["timings"] = {k: round(v, 4) for k, v in (p.timings or {}).items()}
+        outs.append((op.get_results(), cfg))
+        i += n
+    return outs

@@ -62,3 +62,28 @@ class Device:
             return artifacts, pipeline_config
         finally:
             self.mutex.release()
+
+    def run_batch(self, func, kwargs_list):
+        """Batched variant (runtime.batcher): every job gets its own seeded
+        generator; ``func(identifier, kwargs_list) -> [(artifacts, config)]``."""
+        import torch
+
+        if not self.mutex.acquire(False):
+            raise Exception("busy")
+        try:
+            jobs, seeds = [], []
+            for kw in kwargs_list:
+                kw = dict(kw)
+                seed = kw.pop("seed", None)
+                if seed is None:
+                    seed = random.SystemRandom().randrange(0, 2 ** 63 - 1)
+                seed = int(seed)
+                seeds.append(seed)
+                kw["generator"] = torch.Generator(device=self.identifier()).manual_seed(seed)
+                jobs.append(kw)
+            outs = func(self.identifier(), jobs)
+            for (_, cfg), seed in zip(outs, seeds):
+                cfg["seed"] = seed
+            return outs
+        finally:
+            self.mutex.release()

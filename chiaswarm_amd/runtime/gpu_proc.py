@@ -36,6 +36,16 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         job = inbox.get()
         if job is None:
             break
+        if isinstance(job, list):  # a coalesced batch (runtime.batcher)
+            from .batcher import run_jobs
+
+            try:
+                for res in run_jobs(job, device, max(1, settings.max_batch)):
+                    outbox.put((gpu_index, res["id"], res, None))
+            except BaseException as e:
+                for j in job:
+                    outbox.put((gpu_index, j.get("id"), None, f"{e}\n{traceback.format_exc()}"))
+            continue
         jid = job.get("id")
         try:
             result = synchronous_do_work_function(job, device)

@@ -50,6 +50,12 @@ class ThreadExecutor:
 
         return await do_work(job, self.device)
 
+    async def run_batch(self, jobs, max_images=8):
+        from .batcher import run_jobs
+
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(None, run_jobs, jobs, self.device, max_images)
+
     def close(self):
         pass
 
@@ -125,6 +131,44 @@ class ProcessExecutor:
                 return _error_result(jid, RuntimeError(f"GPU worker {why}"), job.get("content_type", "image/jpeg"),
                                      False)
 
+    async def run_batch(self, jobs, max_images=8):
+        """Send compatible jobs as one list; the child coalesces them."""
+        from .generator import _error_result
+
+        self.loop = asyncio.get_running_loop()
+        futs = {}
+        for j in jobs:
+            fut = self.loop.create_future()
+            self.pending[j.get("id")] = fut
+            futs[j.get("id")] = fut
+        self.inbox.put(list(jobs))
+        t0 = time.monotonic()
+        while True:
+            done, _ = await asyncio.wait(set(futs.values()), timeout=2.0)
+            if len(done) == len(futs):
+                break
+            if not self.proc.is_alive() or time.monotonic() - t0 > self.job_timeout_s * len(jobs):
+                why = "crashed" if not self.proc.is_alive() else "timed out"
+                logging.error(f"{self.name} {why} on a batch of {len(jobs)}; restarting")
+                for jid in futs:
+                    self.pending.pop(jid, None)
+                self._restart()
+                break
+        out = []
+        for j in jobs:
+            fut = futs[j.get("id")]
+            if fut.done():
+                result, err = fut.result()
+                if result is not None:
+                    out.append(result)
+                    continue
+                out.append(_error_result(j.get("id"), RuntimeError(f"worker error: {err}"),
+                                         j.get("content_type", "image/jpeg"), False))
+            else:
+                out.append(_error_result(j.get("id"), RuntimeError("GPU worker failed"),
+                                         j.get("content_type", "image/jpeg"), False))
+        return out
+
     def close(self):
         try:
             self.inbox.put(None)
@@ -132,6 +176,20 @@ class ProcessExecutor:
         finally:
             if self.proc.is_alive():
                 self.proc.kill()
+
+
+def _raw_key(job):
+    """Batch-compatibility key of a raw hive job (None: run alone)."""
+    if job.get("workflow") not in (None, "txt2img") or job.get("start_image_uri") or job.get("mask_image_uri"):
+        return None
+    p = job.get("parameters") or {}
+    if any(p.get(k) for k in ("controlnet", "lora", "textual_inversion", "upscale")):
+        return None
+    if str(job.get("model_name", "")).startswith("DeepFloyd/"):
+        return None
+    return (job.get("model_name"), job.get("height"), job.get("width"), job.get("num_inference_steps"),
+            job.get("guidance_scale"), p.get("scheduler_type"), p.get("pipeline_type"), job.get("content_type"),
+            job.get("revision"))
 
 
 def _resolve(fut, value):
@@ -145,7 +203,10 @@ class Supervisor:
         self.hive = hive or HiveClient(self.settings)
         self.executors = executors if executors is not None else self._default_executors()
         n = max(1, len(self.executors))
-        self.work_queue: asyncio.Queue = asyncio.Queue(maxsize=n)
+        # batching: each device may hold up to max_batch queued jobs (max_batch <= 1:
+        # the reference's queue depth of one job per device)
+        self.batch_jobs = max(1, int(getattr(self.settings, "max_batch", 1) or 1))
+        self.work_queue: asyncio.Queue = asyncio.Queue(maxsize=n * self.batch_jobs)
         self.result_queue: asyncio.Queue = asyncio.Queue()
         self.busy = 0
         self.results_submitted = 0
@@ -157,18 +218,41 @@ class Supervisor:
             return [ThreadExecutor("cpu")]
         return [ProcessExecutor(g) for g in gpus]
 
+    def _drain_compatible(self, first) -> list:
+        """Take queued jobs that can share ``first``'s UNet batch (cheap raw-job
+        check; runtime.batcher re-validates after routing)."""
+        batch = [first]
+        if self.batch_jobs <= 1 or not hasattr(self.executors[0], "run_batch"):
+            return batch
+        keep = []
+        while not self.work_queue.empty() and len(batch) < self.batch_jobs:
+            j = self.work_queue.get_nowait()
+            if _raw_key(j) is not None and _raw_key(j) == _raw_key(first):
+                batch.append(j)
+            else:
+                keep.append(j)
+            self.work_queue.task_done()
+        for j in keep:
+            self.work_queue.put_nowait(j)
+        return batch
+
     async def device_worker(self, ex):
         while True:
             job = await self.work_queue.get()
-            self.busy += 1
+            batch = self._drain_compatible(job)
+            self.busy += len(batch)
             try:
-                result = await ex.run(job)
-                await self.result_queue.put(result)
+                if len(batch) == 1:
+                    results = [await ex.run(job)]
+                else:
+                    results = await ex.run_batch(batch, max(1, int(self.settings.max_batch)))
+                for result in results:
+                    await self.result_queue.put(result)
             except Exception as e:
                 logging.exception(e)
                 print(f"device_worker {e}")
             finally:
-                self.busy -= 1
+                self.busy -= len(batch)
                 self.work_queue.task_done()
 
     async def result_worker(self):
@@ -191,7 +275,8 @@ class Supervisor:
         polls = 0
         try:
             while not self.stop.is_set():
-                while (self.work_queue.full() or self.busy + self.work_queue.qsize() >= len(self.executors)) \
+                while (self.work_queue.full() or
+                       self.busy + self.work_queue.qsize() >= len(self.executors) * self.batch_jobs) \
                         and not self.stop.is_set():
                     await asyncio.sleep(0.05 if max_polls else 1)
                 jobs, sleep_s = await self.hive.ask_for_work()

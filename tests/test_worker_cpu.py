@@ -141,3 +141,45 @@ def test_stitch_workflow():
         assert m[0]["filename"] == "f0.png"
     finally:
         hive.stop()
+
+
+def test_batched_jobs_match_solo_results():
+    """Coalesced txt2img jobs (runtime.batcher) return the images each job gets alone."""
+    from chiaswarm_amd.runtime.batcher import run_jobs
+
+    jobs = [{"id": f"b{i}", **TINY, "seed": 100 + i, "num_images_per_prompt": 1 + (i % 2),
+             "prompt": f"fox {i}"} for i in range(3)]
+    jobs.append({"id": "solo", **TINY, "seed": 5, "height": 128})  # different size: not coalesced
+    jobs.append({"id": "bad", "model_name": "m", "height": 9999, "width": 9})
+    dev = Device("cpu")
+    batched = run_jobs([dict(j) for j in jobs], dev, max_images=8)
+    assert [r["id"] for r in batched] == [j["id"] for j in jobs]
+    assert batched[0]["pipeline_config"].get("batched_with") == 3
+    assert batched[-1]["fatal_error"] is True
+    for j, r in zip(jobs[:4], batched[:4]):
+        solo = synchronous_do_work_function(dict(j), dev)
+        assert r["pipeline_config"]["seed"] == solo["pipeline_config"]["seed"]
+        a = Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"]))).convert("RGB")
+        b = Image.open(io.BytesIO(base64.b64decode(solo["artifacts"]["primary"]["blob"]))).convert("RGB")
+        assert a.size == b.size
+        import numpy as np
+
+        assert np.abs(np.asarray(a, np.int16) - np.asarray(b, np.int16)).max() <= 2  # JPEG re-encode noise only
+
+
+def test_supervisor_coalesces_queued_jobs():
+    jobs = [{"id": f"q{i}", **TINY, "seed": i} for i in range(4)]
+    hive = FakeHive(jobs=jobs).start()
+    try:
+        async def main():
+            s = _settings(hive)
+            s.max_batch = 4
+            sup = Supervisor(s, executors=[ThreadExecutor("cpu")])
+            await sup.run(max_polls=2)
+            return sup
+
+        asyncio.run(main())
+        assert sorted(r["id"] for r in hive.results) == [f"q{i}" for i in range(4)]
+        assert any(r["pipeline_config"].get("batched_with", 1) > 1 for r in hive.results)
+    finally:
+        hive.stop()
