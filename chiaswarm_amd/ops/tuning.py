@@ -25,7 +25,9 @@ _TABLE: dict | None = None
 _LOCK = threading.Lock()
 TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64),
          # LDS-DMA multi-stage variants (gemm_glds.hip)
-         11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64)}
+         11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64),
+         # persistent continuous-ring LDS-DMA variants (K % 64 == 0, no split-K)
+         21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64)}
 
 
 def _user_path():
@@ -77,11 +79,13 @@ def candidates(M, N, K):
     for tile, (bm, bn) in TILES.items():
         if tile in (5, 16) and N > 32:
             continue
-        if tile in (2, 6, 12, 17) and N > 1280:
+        if tile in (2, 6, 12, 17, 22, 24) and N > 1280:
+            continue
+        if tile >= 21 and K % 64:
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8):
-            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split):
+            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split or tile >= 21):
                 continue
             out.append((tile, split))
     return out

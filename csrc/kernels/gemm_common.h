@@ -66,7 +66,19 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 
 // Epilogue: accumulators -> fp32 LDS tile -> coalesced row pass applying bias,
 // bias2d, activation / GEGLU gating and residual; or raw split-K partials.
-template <int BM, int BN, int WM, int WN>
+// RAW: raw s_barrier + lgkmcnt(0) instead of __syncthreads (whose vmcnt(0) would
+// drain LDS-DMA loads a persistent kernel keeps in flight across the epilogue)
+template <bool RAW>
+__device__ __forceinline__ void epi_barrier() {
+  if constexpr (RAW) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool RAW = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                               bf16_t* smem, int m0, int n0, int split) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -119,7 +131,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         for (int r = 0; r < 4; ++r)
           cs[(wm * WTM + i * 16 + fq * 4 + r) * LDC_S + wn * WTN + j * 16 + fr] = acc[i][j][r];
   }
-  __syncthreads();
+  epi_barrier<RAW>();
   const int outN = act == ACT_GEGLU ? N / 2 : N;
   const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
@@ -178,7 +190,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   if (args.gn_part) {
     // column pass: (mean, M2) of each output channel over this tile's rows
     // (two-pass in LDS: exact, no E[x^2]-E[x]^2 cancellation)
-    __syncthreads();
+    epi_barrier<RAW>();
     const int rows = min(BM, M - m0);
     for (int c = tid; c < BN; c += 256) {
       const int n = n0 + c;

@@ -33,7 +33,7 @@ def test_gemm(gpu, M, N, K, act):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 21, 22, 23, 24])
 @pytest.mark.parametrize("split", [1, 3])
 def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     from chiaswarm_amd.ops import _lib
@@ -190,7 +190,30 @@ def test_sched_step(gpu, cfg, prev, noise):
     assert n == x.numel()
 
 
-@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 17])
+@pytest.mark.parametrize("tile", [21, 22, 23, 24])
+def test_persistent_tiles_many_tiles_per_workgroup(gpu, tile):
+    """Persistent continuous-ring kernels with more tiles than workgroups (GEMM and conv)."""
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, N, K = 32768, 320, 320
+    a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, None, tile, 1,
+              None, _s())
+    ref = ops._ref_gemm(a.float(), w.float(), b.float(), r.float(), "silu")
+    assert rel_err(out, ref) < 1e-2
+    B, H, W, Cin, Cout = 8, 64, 64, 128, 192
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=gpu)
+    _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1, H, W, 0,
+              Cin, Cout, 0, 0, 1.0, 1, None, tile, 1, None, _s())
+    refc = ops._ref_conv2d(x.float(), wp.float(), None, 1, 1, None, False, None)
+    assert rel_err(y, refc) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 17, 21, 23])
 def test_fused_group_norm_stats(gpu, tile):
     """GroupNorm fed by conv-epilogue statistics == GroupNorm with its own stats pass."""
     from chiaswarm_amd.ops import tuning
