@@ -127,17 +127,56 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __
   }
 }
 
+// MODE 0: `stat` holds final (mean, rstd) per (b, g) (a finalize kernel ran).
+// MODE 1: `stat` is the stats kernel's chunk partials [b][nent][g][3];
+// MODE 2: `stat` is epilogue partials [seg][c][2] (nent = segments per sample,
+//         seg_rows rows each).  MODES 1/2 merge them in the prologue (Chan),
+// which removes the finalize launch when there are few entries per group.
+template <int MODE>
 __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                               const float* __restrict__ stat,
                                                               const bf16_t* __restrict__ gamma,
                                                               const bf16_t* __restrict__ beta, int P, int C, int G,
-                                                              int chunk, int silu, int affine_bstride) {
+                                                              int chunk, int silu, int affine_bstride, int nent,
+                                                              int seg_rows, float eps) {
+  __shared__ float gst[2 * 64];
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
   gamma += (size_t)b * affine_bstride;  // per-sample affine ([B, C]) when affine_bstride == C
   beta += (size_t)b * affine_bstride;
+  const int Cg = C / G;
+  if constexpr (MODE != 0) {
+    // tpg threads (a power of two) merge one group's entries, then shuffle-merge
+    int tpg = 1;
+    while (tpg * 2 * G <= GN_THREADS && tpg < 64) tpg *= 2;
+    const int g = tid / tpg, sub = tid % tpg;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    if (g < G) {
+      if constexpr (MODE == 1) {
+        for (int e = sub; e < nent; e += tpg) {
+          const float* pp = stat + (((size_t)b * nent + e) * G + g) * 3;
+          chan_combine(n, mean, m2, pp[0], pp[1], pp[2]);
+        }
+      } else {
+        const int ne = nent * Cg;
+        for (int e = sub; e < ne; e += tpg) {
+          const int sg = b * nent + e / Cg, c = g * Cg + e % Cg;
+          const float* pp = stat + ((size_t)sg * C + c) * 2;
+          chan_combine(n, mean, m2, (float)seg_rows, pp[0], pp[1]);
+        }
+      }
+    }
+    for (int o = 1; o < tpg; o <<= 1) {
+      const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
+      chan_combine(n, mean, m2, n2, me2, q2);
+    }
+    if (g < G && sub == 0) {
+      gst[2 * g] = mean;
+      gst[2 * g + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+    }
+    __syncthreads();
+  }
   const GnLayout L(C, tid);
   if (L.r >= L.R) return;
-  const int Cg = C / G;
   float sa[2][8], sb[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -146,7 +185,14 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
     for (int j = 0; j < 8; ++j) {
       const int c = min(v * 8 + j, C - 1);
       const int g = c / Cg;
-      const float mean = stat[(b * G + g) * 2], rstd = stat[(b * G + g) * 2 + 1];
+      float mean, rstd;
+      if constexpr (MODE == 0) {
+        mean = stat[(b * G + g) * 2];
+        rstd = stat[(b * G + g) * 2 + 1];
+      } else {
+        mean = gst[2 * g];
+        rstd = gst[2 * g + 1];
+      }
       const float a = bf2f(gamma[c]) * rstd;
       sa[u][j] = a;
       sb[u][j] = bf2f(beta[c]) - mean * a;
@@ -217,11 +263,18 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* part, int se
                                 int silu, int affine_bstride, hipStream_t stream) {
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0 || seg_rows <= 0 || P % seg_rows != 0) return (int)hipErrorInvalidValue;
   float* st = (float*)stat;
+  const int nseg = P / seg_rows;
+  if (G <= 64 && nseg * (C / G) <= 512) {  // few entries per group: merge in the apply prologue
+    gn_apply_kernel<2><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>(
+        (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G, chunk,
+        silu, affine_bstride, nseg, seg_rows, eps);
+    CSK_CHECK_LAUNCH();
+  }
   gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
-      (const float*)part, st, B, C, G, P / seg_rows, seg_rows, eps);
-  gn_apply_kernel<<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
-                                                              (const bf16_t*)beta, P, C, G, chunk, silu,
-                                                              affine_bstride);
+      (const float*)part, st, B, C, G, nseg, seg_rows, eps);
+  gn_apply_kernel<0><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st,
+                                                                 (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G,
+                                                                 chunk, silu, affine_bstride, 0, 0, eps);
   CSK_CHECK_LAUNCH();
 }
 
@@ -234,10 +287,17 @@ CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
   gn_stats_kernel<<<grid, GN_THREADS, 2 * C * sizeof(float), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
+  if (G <= 64 && nchunk <= 512) {  // merge the chunk partials in the apply prologue (no finalize launch)
+    gn_apply_kernel<1><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, pt, (const bf16_t*)gamma,
+                                                        (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride,
+                                                        nchunk, 0, eps);
+    CSK_CHECK_LAUNCH();
+  }
   gn_finalize_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(pt, st, B, G,
                                                                                                   nchunk, eps);
-  gn_apply_kernel<<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
-                                                   (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride);
+  gn_apply_kernel<0><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
+                                                      (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride, 0,
+                                                      0, eps);
   CSK_CHECK_LAUNCH();
 }
 
