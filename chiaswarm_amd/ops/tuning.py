@@ -26,6 +26,7 @@ _LOCK = threading.Lock()
 TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64),
          # LDS-DMA multi-stage variants (gemm_glds.hip)
          11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64),
+         18: (64, 64), 19: (128, 64), 20: (64, 128),
          # persistent continuous-ring LDS-DMA variants (K % 64 == 0, no split-K)
          21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64)}
 
@@ -79,7 +80,7 @@ def candidates(M, N, K):
     for tile, (bm, bn) in TILES.items():
         if tile in (5, 16) and N > 32:
             continue
-        if tile in (2, 6, 12, 17, 22, 24) and N > 1280:
+        if tile in (2, 6, 12, 17, 19, 22, 24) and N > 1280:
             continue
         if tile >= 21 and K % 64:
             continue

@@ -490,6 +490,11 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     case 15: return launch_glds<128, 128, 2, 2, 3>(a, ksplit, conv, s);
     case 16: return launch_glds<128, 32, 4, 1, 4>(a, ksplit, conv, s);
     case 17: return launch_glds<128, 64, 2, 2, 3>(a, ksplit, conv, s);
+    // small-LDS 2-stage variants: 3-5 workgroups per CU, for short-K (K = 320..640)
+    // GEMMs that are bound by memory latency rather than by the MFMA pipe
+    case 18: return launch_glds<64, 64, 2, 2, 2>(a, ksplit, conv, s);
+    case 19: return launch_glds<128, 64, 4, 1, 2>(a, ksplit, conv, s);
+    case 20: return launch_glds<64, 128, 2, 2, 2>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }
 }

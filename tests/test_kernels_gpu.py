@@ -33,7 +33,7 @@ def test_gemm(gpu, M, N, K, act):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 21, 22, 23, 24])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
 @pytest.mark.parametrize("split", [1, 3])
 def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     from chiaswarm_amd.ops import _lib
