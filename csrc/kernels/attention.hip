@@ -346,12 +346,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   if (nkb > 1) { load_kv(1); store_kv(1); }
   __syncthreads();
   const float sl2 = a.scale_log2;
-  v4f s_cur[4][QT], s_nxt[4][QT];
-  if (nkb > 0) qk(0, s_cur);
-  for (int kb = 0; kb < nkb; ++kb) {
+  v4f s_a[4][QT], s_b[4][QT];
+  // one pipelined block: softmax + PV of block kb (scores in sc) while the QK^T
+  // of block kb+1 fills sn.  Called alternately with (s_a, s_b) / (s_b, s_a) so
+  // the score registers are never copied.
+  auto block = [&](int kb, v4f (&sc)[4][QT], v4f (&sn)[4][QT]) {
     const int cur = kb % 3;
     if (kb + 2 < nkb) load_kv(kb + 2);
-    if (kb + 1 < nkb) qk((kb + 1) % 3, s_nxt);  // matrix cores busy while the softmax below runs
+    if (kb + 1 < nkb) qk((kb + 1) % 3, sn);  // matrix cores busy while the softmax below runs
 
     const int kbase = kb * KB;
     const bool masked = a.causal || (kbase + KB > kv_end);
@@ -365,37 +367,44 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = kbase + kt * 16 + 4 * fg + r;
-            if (key >= kv_end || (a.causal && key > qi)) s_cur[kt][qt][r] = -INFINITY;
+            if (key >= kv_end || (a.causal && key > qi)) sc[kt][qt][r] = -INFINITY;
           }
       }
       float mx = -1e30f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s_cur[kt][qt][r]);
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][qt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(mrow[qt], mx * sl2);
-      const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
-      mrow[qt] = mnew;
+      // lazy rescale (cdna_hip_programming.md T13): keep the reference max unless
+      // the block max exceeds it by > 2^8; p stays <= 256, exact after the final 1/l
+      const float mb = mx * sl2;
+      if (mb > mrow[qt] + 8.f) {
+        const float mnew = fmaxf(mrow[qt], mb);
+        const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
+        mrow[qt] = mnew;
+        lrow[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
+      }
+      const float mref = mrow[qt];
       float ls = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s_cur[kt][qt][r], sl2, -mnew));
-          s_cur[kt][qt][r] = p;
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][qt][r], sl2, -mref));
+          sc[kt][qt][r] = p;
           ls += p;
         }
-      lrow[qt] = lrow[qt] * alpha + ls;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
+      lrow[qt] += ls;
 #pragma unroll
       for (int kp2 = 0; kp2 < 2; ++kp2) {
-        u32 w0 = pack2(s_cur[2 * kp2][qt][0], s_cur[2 * kp2][qt][1]);
-        u32 w1 = pack2(s_cur[2 * kp2][qt][2], s_cur[2 * kp2][qt][3]);
-        u32 w2 = pack2(s_cur[2 * kp2 + 1][qt][0], s_cur[2 * kp2 + 1][qt][1]);
-        u32 w3 = pack2(s_cur[2 * kp2 + 1][qt][2], s_cur[2 * kp2 + 1][qt][3]);
+        u32 w0 = pack2(sc[2 * kp2][qt][0], sc[2 * kp2][qt][1]);
+        u32 w1 = pack2(sc[2 * kp2][qt][2], sc[2 * kp2][qt][3]);
+        u32 w2 = pack2(sc[2 * kp2 + 1][qt][0], sc[2 * kp2 + 1][qt][1]);
+        u32 w3 = pack2(sc[2 * kp2 + 1][qt][2], sc[2 * kp2 + 1][qt][3]);
         pf[kp2][qt] = __builtin_bit_cast(v8s, make_uint4(w0, w1, w2, w3));
       }
     }
@@ -417,10 +426,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     // block kb+2 -> the buffer that held block kb-1 (last read before the previous barrier)
     if (kb + 2 < nkb) store_kv((kb + 2) % 3);
     __syncthreads();
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < QT; ++qt) s_cur[kt][qt] = s_nxt[kt][qt];
+  };
+  if (nkb > 0) qk(0, s_a);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    block(kb, s_a, s_b);
+    if (kb + 1 < nkb) block(kb + 1, s_b, s_a);
   }
 
   bf16_t* op = a.o + b * a.sob + h * a.soh;

@@ -78,6 +78,38 @@ __device__ __forceinline__ void epi_barrier() {
   }
 }
 
+__device__ __forceinline__ void add8(float (&f)[8], const bf16_t* p, bool vec, int valid) {
+  if (vec) {
+    float g[8];
+    unpack8(*reinterpret_cast<const uint4*>(p), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += g[j];
+  } else {
+    for (int j = 0; j < 8 && j < valid; ++j) f[j] += bf2f(p[j]);
+  }
+}
+
+__device__ __forceinline__ void act8(int act, float (&f)[8]) {
+#define CSK_ACT8(CODE)                                     \
+  case CODE:                                               \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) f[j] = apply_act(CODE, f[j]); \
+    break;
+  switch (act) {
+    CSK_ACT8(ACT_GELU)
+    CSK_ACT8(ACT_SILU)
+    CSK_ACT8(ACT_QGELU)
+    CSK_ACT8(ACT_LRELU)
+    CSK_ACT8(ACT_LRELU_01)
+    CSK_ACT8(ACT_TANH)
+    CSK_ACT8(ACT_RELU)
+    CSK_ACT8(ACT_LRELU_001)
+    CSK_ACT8(ACT_ELU)
+    CSK_ACT8(ACT_GELU_TANH)
+    default: break;
+  }
+#undef CSK_ACT8
+}
+
 template <int BM, int BN, int WM, int WN, bool RAW = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                               bf16_t* smem, int m0, int n0, int split) {
@@ -146,19 +178,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
     const bool full = n + 8 <= outN;
     if (act != ACT_GEGLU) {
-      if (args.bias) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(args.bias[n + j]) : 0.f;
-      }
-      if (args.bias2d) {
-        const bf16_t* b2 = args.bias2d + (size_t)(m / args.rows_per_b) * N;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += (n + j < outN) ? bf2f(b2[n + j]) : 0.f;
-      }
-      if (act != ACT_NONE) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = apply_act(act, f[j]);
-      }
+      // bias / bias2d: one 16-byte load for a full, aligned group of 8 columns
+      // (per-element guarded loads otherwise) — keeps the epilogue branch-free
+      // in the common case, which matters for short-K GEMMs (K = 320)
+      if (args.bias) add8(f, args.bias + n, full && (N % 8 == 0), outN - n);
+      if (args.bias2d) add8(f, args.bias2d + (size_t)(m / args.rows_per_b) * N + n, full && (N % 8 == 0), outN - n);
+      act8(act, f);  // one uniform switch per 8 values, not per value
     }
     if (args.out_scale != 1.0f) {
 #pragma unroll
