@@ -35,6 +35,15 @@ def load_sd(model_name: str, device_identifier: str, revision: str = "main", con
                                seed=abs(hash(model_name)) % (1 << 31))
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)
+    if not hasattr(pipe, "_safety_probed"):
+        # the NSFW checker runs when its weights are available locally (a random
+        # tower would be meaningless); SDAAS_SAFETY=0 disables it
+        pipe._safety_probed = True
+        sw = find_weights("CompVis/stable-diffusion-safety-checker")
+        if sw and os.environ.get("SDAAS_SAFETY", "1") != "0":
+            from ..models.safety import load_safety_checker
+
+            pipe.safety_checker = load_safety_checker(device_identifier, sw)
     pipe.controlnet = None
     if controlnet_name:
         from .controlnet import load_controlnet

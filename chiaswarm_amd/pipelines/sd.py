@@ -227,11 +227,11 @@ class StableDiffusion:
         return x
 
     @torch.no_grad()
-    def decode(self, latents) -> torch.Tensor:
-        """NHWC fp32 latents -> uint8 NHWC images on the host."""
+    def decode(self, latents, to_host=True) -> torch.Tensor:
+        """NHWC fp32 latents -> uint8 NHWC images (on the host unless to_host=False)."""
         z = latents / self.vae.cfg.scaling_factor
-        img = self.vae.decode(z)
-        return ops.vae_postprocess(img).cpu()
+        img = ops.vae_postprocess(self.vae.decode(z))
+        return img.cpu() if to_host else img
 
     @torch.no_grad()
     def encode_image(self, images: list[Image.Image], h, w, generator=None, sample=True):
@@ -336,12 +336,13 @@ class StableDiffusion:
         if output_type == "latent":
             return PipelineOutput([], [False] * b, x, timings)
         t2 = time.perf_counter()
-        imgs = self.decode(x)
+        imgs = self.decode(x, to_host=False)
+        nsfw = [False] * b
+        if self.safety_checker is not None:  # on the device, before the D2H copy
+            nsfw, imgs = self.safety_checker(imgs)
+        imgs = imgs.cpu()
         timings["decode"] = time.perf_counter() - t2
         pil = [Image.fromarray(a.numpy()) for a in imgs] if output_type == "pil" else imgs
-        nsfw = [False] * b
-        if self.safety_checker is not None:
-            nsfw = self.safety_checker(imgs)
         return PipelineOutput(pil, nsfw, x, timings)
 
 
