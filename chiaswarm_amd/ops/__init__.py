@@ -382,6 +382,20 @@ def attention(q, k, v, scale=None, causal=False, kv_len=None):
 
 
 # ----------------------------------------------------------------------------
+# Image preprocessing
+# ----------------------------------------------------------------------------
+def canny(gray: torch.Tensor, low: float = 100.0, high: float = 200.0) -> torch.Tensor:
+    """Canny edges of a uint8 [H, W] image (0/255), cv2 semantics."""
+    if use_hip(gray):
+        from . import hip_ops
+
+        return hip_ops.canny(gray, low, high)
+    from ..controlnet.preprocess import canny_np
+
+    return torch.from_numpy(canny_np(gray.cpu().numpy(), float(low), float(high))).to(gray.device)
+
+
+# ----------------------------------------------------------------------------
 # Elementwise
 # ----------------------------------------------------------------------------
 def silu(x):

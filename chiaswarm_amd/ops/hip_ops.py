@@ -48,6 +48,7 @@ ATTN_VARIANT = int(os.environ.get("CSK_ATTN", "0"))  # 0 auto, 1 plain, 2 pipeli
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_int, c_void_p, c_void_p)
 sig("csk_silu", c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_canny", c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_void_p)
 sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
     c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p)
@@ -352,3 +353,15 @@ def vae_postprocess(img):
     y = torch.empty(img.shape, dtype=torch.uint8, device=img.device)
     _lib.call("csk_vae_post", _p(y), _p(img), img.numel(), _s())
     return y
+
+
+def canny(gray, low, high):
+    """uint8 [H, W] device image -> uint8 0/255 edge map (csrc/kernels/canny.hip)."""
+    if gray.dtype != torch.uint8 or gray.dim() != 2:
+        raise TypeError("canny: uint8 [H, W] expected")
+    gray = gray.contiguous()
+    H, W = gray.shape
+    out = torch.empty_like(gray)
+    ws = torch.empty(H * W * 6 + 64, dtype=torch.uint8, device=gray.device)
+    _lib.call("csk_canny", _p(out), _p(gray), H, W, float(low), float(high), _p(ws), _s())
+    return out

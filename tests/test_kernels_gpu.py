@@ -249,3 +249,19 @@ def test_fused_group_norm_stats(gpu, tile):
     yc = hip_ops.group_norm(cat, g2, b2, 32, 1e-5, False)
     refc = ops._ref_group_norm(cat.float().cpu(), g2.float().cpu(), b2.float().cpu(), 32, 1e-5, False)
     assert rel_err(yc.cpu(), refc) < 1e-2
+
+
+@pytest.mark.parametrize("size", [(512, 512), (97, 131)])
+def test_canny_matches_numpy(gpu, size):
+    import numpy as np
+
+    from chiaswarm_amd.controlnet.preprocess import canny_np
+
+    rng = np.random.default_rng(0)
+    H, W = size
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = (127 + 100 * np.sin(xx / 9.0) * np.cos(yy / 13.0) + rng.normal(0, 8, (H, W))).clip(0, 255).astype(np.uint8)
+    ref = canny_np(img, 100.0, 200.0)
+    got = hip_ops.canny(torch.from_numpy(img).to(gpu), 100.0, 200.0).cpu().numpy()
+    # direction quantisation at exact 22.5-degree boundaries may differ (f32 atan2 vs f64)
+    assert (got != ref).mean() < 2e-3
