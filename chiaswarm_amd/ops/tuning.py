@@ -58,21 +58,28 @@ def save_user():
 
 
 def heuristic(M, N, K) -> tuple[int, int]:
-    """Untuned shapes: LDS-DMA tiles (the FAST staging path makes them the
-    fastest family on gfx950: 64x64x320 conv 732 TF/s with tile 11 vs 195 with
-    the register-staged 128x128), split-K only when the grid cannot fill 256 CUs."""
+    """Untuned shapes, from the MI355X sweeps (tools/gemmprof.py, the tuned
+    table): LDS-DMA tiles everywhere; short K (<= 1280, latency/bandwidth
+    bound) prefers the small-LDS 2-stage tiles (3-5 workgroups per CU), long K
+    (3x3 convs) the 128x128 tile; split-K only when the grid cannot fill 256 CUs."""
     if N <= 32:
         return 16, 1
     tiles128 = -(-M // 128) * -(-N // 128)
-    if tiles128 >= 384:
-        return (11 if N > 64 else 12), 1
+    tiles12864 = -(-M // 128) * -(-N // 64)
     tiles64 = -(-M // 64) * -(-N // 64)
-    if tiles64 >= 384 or K < 1024:
+    if K <= 1280:
+        if N <= 1280 and tiles12864 >= 256:
+            return 19, 1
+        if tiles64 >= 256:
+            return 18, 1
+    elif tiles128 >= 384:
+        return 11, 1
+    elif tiles64 >= 384:
         return 14, 1
     split = 1
     while tiles64 * split < 384 and K // 64 >= 4 * split * 2 and split < 8:
         split *= 2
-    return 14, split
+    return 18, split
 
 
 def candidates(M, N, K):
