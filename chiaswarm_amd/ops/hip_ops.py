@@ -362,6 +362,7 @@ def canny(gray, low, high):
     gray = gray.contiguous()
     H, W = gray.shape
     out = torch.empty_like(gray)
-    ws = torch.empty(H * W * 6 + 64, dtype=torch.uint8, device=gray.device)
+    a4, a1 = -(-(H * W * 4) // 256) * 256, -(-(H * W) // 256) * 256
+    ws = torch.empty(256 + a4 + 2 * a1, dtype=torch.uint8, device=gray.device)  # torch: 256 B-aligned
     _lib.call("csk_canny", _p(out), _p(gray), H, W, float(low), float(high), _p(ws), _s())
     return out

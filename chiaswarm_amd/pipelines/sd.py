@@ -381,9 +381,15 @@ class _UNetGraph:
     def run(self, x_in, t, cross_kv, added, ctl):
         self.x.copy_(x_in)
         self.t.fill_(float(t))
-        for dst, src in zip(self.kv, cross_kv):
-            if dst.data_ptr() != src.data_ptr():
-                dst.copy_(src)
+        # per-request cross-attention K/V: copied into the graph's static buffers
+        # once per request (the same tensors come back every step)
+        key = tuple(id(k) for k in cross_kv)
+        if key != getattr(self, "_kv_src", None):
+            for dst, src in zip(self.kv, cross_kv):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src)
+            self._kv_src = key
+            self._kv_refs = list(cross_kv)  # keep them alive so ids stay unique
         if added:
             for k, v in added.items():
                 self.added[k].copy_(v)

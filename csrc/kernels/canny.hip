@@ -105,14 +105,17 @@ __global__ void canny_out_kernel(const unsigned char* __restrict__ lab, unsigned
   if (i < n) out[i] = lab[i] == 2 ? 255 : 0;
 }
 
-// ws: >= H*W*6 + 16 bytes of device workspace; flag_host: pinned or pageable int
+// ws: >= canny_ws_bytes(H, W) of 256-byte aligned device workspace
 CSK_API int csk_canny(void* out, const void* gray, int H, int W, float low, float high, void* ws,
                       hipStream_t stream) {
+  // workspace layout (every region 256-byte aligned): [changed flag][mag f32][dir u8][label u8]
   char* w = (char*)ws;
-  float* mag = (float*)w;
-  unsigned char* dir = (unsigned char*)(w + (size_t)H * W * 4);
-  unsigned char* lab = dir + (size_t)H * W;
-  int* changed = (int*)(lab + (((size_t)H * W + 15) & ~(size_t)15));
+  if (((size_t)w) & 255) return (int)hipErrorInvalidValue;
+  const size_t hw = (size_t)H * W, a4 = (hw * 4 + 255) & ~(size_t)255, a1 = (hw + 255) & ~(size_t)255;
+  int* changed = (int*)w;
+  float* mag = (float*)(w + 256);
+  unsigned char* dir = (unsigned char*)(w + 256 + a4);
+  unsigned char* lab = dir + a1;
   dim3 b2(16, 16), g2((W + 15) / 16, (H + 15) / 16);
   canny_grad_kernel<<<g2, b2, 0, stream>>>((const unsigned char*)gray, mag, dir, H, W);
   canny_nms_kernel<<<g2, b2, 0, stream>>>(mag, dir, lab, H, W, low, high);
