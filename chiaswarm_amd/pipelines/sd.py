@@ -134,14 +134,12 @@ class StableDiffusion:
         self.use_graphs = self.device.type == "cuda"
 
     # ------------------------------------------------------------------
-    @torch.no_grad()
-    def encode_prompt(self, prompts: list[str], negatives: list[str], cfg: bool):
-        """Returns (context [2B or B, 77, D], added_cond or None)."""
-        texts = (negatives + prompts) if cfg else prompts
+    def _text_fn(self, ids, with_kv=True):
+        """Device part of prompt encoding: every text encoder (+ the UNet's
+        per-request cross-attention K/V); captured as one hipGraph per batch."""
         hs, pooled = [], None
-        for tok, te in zip(self.tokenizers, self.text_encoders):
-            ids = tok(texts).to(self.device)
-            last, penult, pool, proj = te(ids)
+        for i, te in enumerate(self.text_encoders):
+            last, penult, pool, proj = te(ids[i])
             if self.family.name == "sdxl":
                 hs.append(penult)
                 if proj is not None:
@@ -149,9 +147,29 @@ class StableDiffusion:
             else:
                 hs.append(last)
         ctx = torch.cat(hs, dim=-1) if len(hs) > 1 else hs[0]
-        added = None
-        if self.family.name == "sdxl":
-            added = {"text_embeds": pooled}
+        kv = tuple(self.unet.encode_context(ctx)) if with_kv else ()
+        return ctx, pooled, kv
+
+    @torch.no_grad()
+    def encode(self, prompts: list[str], negatives: list[str], cfg: bool, with_kv=True):
+        """(context, added_cond or None, cross-attention K/V tuple)."""
+        texts = (negatives + prompts) if cfg else prompts
+        ids = tuple(tok(texts).to(self.device) for tok in self.tokenizers)
+        if self.use_graphs and with_kv:
+            if not hasattr(self, "_text_graphs"):
+                from .graphs import GraphCache
+
+                self._text_graphs = GraphCache(self._text_fn)
+            ctx, pooled, kv = self._text_graphs(self.device, ids=ids)
+        else:
+            ctx, pooled, kv = self._text_fn(ids, with_kv)
+        added = {"text_embeds": pooled} if self.family.name == "sdxl" else None
+        return ctx, added, kv
+
+    @torch.no_grad()
+    def encode_prompt(self, prompts: list[str], negatives: list[str], cfg: bool):
+        """Returns (context [2B or B, 77, D], added_cond or None)."""
+        ctx, added, _ = self.encode(prompts, negatives, cfg, with_kv=False)
         return ctx, added
 
     def _time_ids(self, b, h, w, device):
@@ -166,16 +184,17 @@ class StableDiffusion:
 
     # ------------------------------------------------------------------
     def _unet_eval(self, x_in, t, cross_kv, added, ctl):
-        key = (x_in.shape, added is not None, ctl is not None, len(cross_kv))
+        share = bool(getattr(self, "_kv_static", False))
+        key = (x_in.shape, added is not None, ctl is not None, len(cross_kv), share)
         if (not self.use_graphs or ops.get_mode() != "hip" or not ops._lib.available()
                 or self.device.type != "cuda"):
             return self.unet(x_in, torch.tensor([t], device=x_in.device, dtype=torch.float32),
                              cross_kv=cross_kv, added_cond=added, **(ctl or {}))
         g = self._graphs.get(key)
         if g is None:
-            g = _UNetGraph(self.unet, x_in, cross_kv, added, ctl)
+            g = _UNetGraph(self.unet, x_in, cross_kv, added, ctl, share_kv=share)
             self._graphs[key] = g
-        return g.run(x_in, t, cross_kv, added, ctl)
+        return g.run(x_in, t, cross_kv, added, ctl, req=getattr(self, "_req", None))
 
     @torch.no_grad()
     def denoise(self, latents, sched: Scheduler, cross_kv, guidance, added=None, generator=None,
@@ -271,12 +290,20 @@ class StableDiffusion:
         height, width = (height // 8) * 8, (width // 8) * 8
         lh, lw = height // 8, width // 8
 
-        ctx, added = self.encode_prompt(prompts, negs, cfg)
         if is_pix2pix:
+            ctx, added = self.encode_prompt(prompts, negs, cfg)
             # [cond, cond (image-only guidance), uncond]
             ctx_c, ctx_u = ctx[b:], ctx[:b]
             ctx = torch.cat([ctx_c, ctx_u, ctx_u], 0)
-        cross_kv = self.unet.encode_context(ctx)
+            cross_kv = self.unet.encode_context(ctx)
+        else:
+            # text encoders + cross-attention K/V in one hipGraph replay on the GPU
+            ctx, added, cross_kv = self.encode(prompts, negs, cfg)
+            cross_kv = list(cross_kv)
+        # K/V are the text graph's static outputs (rewritten in place per request)
+        self._kv_static = (not is_pix2pix) and self.use_graphs and hasattr(self, "_text_graphs") and \
+            ops.get_mode() == "hip" and ops._lib.available()
+        self._req = getattr(self, "_req", 0) + 1
         if added is not None:
             nrep = ctx.shape[0] // b
             added["time_ids"] = self._time_ids(nrep * b, height, width, self.device)
@@ -357,11 +384,13 @@ class _UNetGraph:
     """hipGraph of one UNet forward at a fixed (batch, H, W): static input
     buffers are refreshed by ``copy_`` before each replay."""
 
-    def __init__(self, unet, x_in, cross_kv, added, ctl, warmup=2):
+    def __init__(self, unet, x_in, cross_kv, added, ctl, warmup=2, share_kv=False):
         self.unet = unet
         self.x = x_in.clone()
         self.t = torch.zeros(1, device=x_in.device, dtype=torch.float32)
-        self.kv = [k.clone() for k in cross_kv]
+        # share_kv: the K/V are another graph's static outputs -> capture them directly
+        self.kv = list(cross_kv) if share_kv else [k.clone() for k in cross_kv]
+        self._kv_req = None
         self.added = {k: v.clone() for k, v in added.items()} if added else None
         self.ctl = ({"down_residuals": [r.clone() for r in ctl["down_residuals"]],
                      "mid_residual": ctl["mid_residual"].clone()} if ctl else None)
@@ -378,18 +407,17 @@ class _UNetGraph:
     def _fwd(self):
         return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, **(self.ctl or {}))
 
-    def run(self, x_in, t, cross_kv, added, ctl):
+    def run(self, x_in, t, cross_kv, added, ctl, req=None):
         self.x.copy_(x_in)
         self.t.fill_(float(t))
         # per-request cross-attention K/V: copied into the graph's static buffers
-        # once per request (the same tensors come back every step)
-        key = tuple(id(k) for k in cross_kv)
-        if key != getattr(self, "_kv_src", None):
+        # once per request (a no-op when they ARE the text-encoder graph's static
+        # outputs, which that graph rewrites in place for every request)
+        if req != self._kv_req:
             for dst, src in zip(self.kv, cross_kv):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src)
-            self._kv_src = key
-            self._kv_refs = list(cross_kv)  # keep them alive so ids stay unique
+            self._kv_req = req
         if added:
             for k, v in added.items():
                 self.added[k].copy_(v)

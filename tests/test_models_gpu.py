@@ -66,3 +66,24 @@ def test_pipeline_txt2img_hip_graphs(gpu):
     assert len(out.images) == 2 and out.images[0].size == (256, 256)
     assert torch.isfinite(out.latents).all()
     assert len(p._graphs) == 1  # the UNet step ran from a captured hipGraph
+
+
+@torch.no_grad()
+def test_graph_requests_match_eager_across_prompts(gpu):
+    """Text-encoder + UNet hipGraphs share the per-request K/V buffers: a second
+    request with a different prompt must not reuse the first request's K/V."""
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    p = StableDiffusion("sd21", device=gpu, seed=5)
+    runs = {}
+    for use_graphs in (True, False):
+        p.use_graphs = use_graphs
+        for prompt in ("a cat", "a red sports car"):
+            g = torch.Generator(device=gpu).manual_seed(3)
+            runs[(use_graphs, prompt)] = p(prompt=prompt, num_inference_steps=3, height=256, width=256,
+                                           generator=g).latents.float()
+    for prompt in ("a cat", "a red sports car"):
+        a, b = runs[(True, prompt)], runs[(False, prompt)]
+        assert ((a - b).norm() / b.norm()).item() < 2e-2, prompt
+    c, d = runs[(True, "a cat")], runs[(True, "a red sports car")]
+    assert ((c - d).norm() / d.norm()).item() > 1e-2  # different prompts -> different latents

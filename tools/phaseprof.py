@@ -38,5 +38,43 @@ def main():
               f"encode_prompt {tall:.2f} ms", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def jobs():
+    """The bench's job loop with and without the overlapped result-encoding thread."""
+    import concurrent.futures as cf
+
+    from chiaswarm_amd.output.processor import OutputProcessor
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+    from chiaswarm_amd.schedulers import get_scheduler
+
+    ops._lib.load()
+    dev = torch.device("cuda", 0)
+    p = StableDiffusion("sd21", device=dev, seed=0)
+    pool = cf.ThreadPoolExecutor(max_workers=2)
+    for overlap in (False, True, False, True):
+        fut = None
+        for i in range(3):
+            g = torch.Generator(device=dev).manual_seed(i)
+            out = p(prompt="a fox", negative_prompt="blurry", num_inference_steps=50, num_images_per_prompt=4,
+                    height=512, width=512, generator=g, scheduler=get_scheduler("DPMSolverMultistepScheduler"))
+
+            def enc(images=out.images):
+                op = OutputProcessor(["primary"], "image/jpeg")
+                op.add_outputs(images)
+                return op.get_results()
+
+            if overlap:
+                fut = pool.submit(enc)
+            else:
+                enc()
+            print(f"overlap={overlap} job {i}: " + " ".join(f"{k} {v * 1000:.1f}" for k, v in out.timings.items()),
+                  flush=True)
+        if fut:
+            fut.result()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "jobs":
+    jobs()
