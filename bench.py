@@ -9,8 +9,8 @@
 One "step" = one complete txt2img job per GPU: prompt encoding (OpenCLIP-H,
 CFG batch), 50 DPM-Solver++(2M) Karras denoising steps of the full SD2.1 UNet
 (865.9M params) on the CFG batch of 8 latents 64x64, VAE decode 512x512, uint8
-D2H, and JPEG/base64/sha256 result-envelope encoding (overlapped with the next
-job on a host thread, joined before the clock stops).  Data-parallel over GPUs
+D2H, and JPEG/base64/sha256 result-envelope encoding (in encoder processes,
+overlapped with the next job, joined before the clock stops).  Data-parallel over GPUs
 (one process per GPU, weak scaling: 4 images per GPU per step); weights are
 random-init on every rank and distributed with a sharded RCCL all_gather
 (outside the timed region); each rank's final latents are all-gathered to
@@ -23,7 +23,6 @@ GEMMs, MIOpen channels-last convs, SDPA) = the diffusers-style eager baseline
 from __future__ import annotations
 
 import argparse
-import concurrent.futures as cf
 import json
 import os
 import statistics
@@ -54,8 +53,11 @@ def parse():
 
 def main():
     args = parse()
+    # result encoders are separate processes, started before this process touches the GPU
+    from chiaswarm_amd.output.encoder import EncoderPool
+
+    pool = EncoderPool()
     from chiaswarm_amd import ops
-    from chiaswarm_amd.output.processor import OutputProcessor
     from chiaswarm_amd.parallel import comm
     from chiaswarm_amd.pipelines.sd import StableDiffusion
     from chiaswarm_amd.schedulers import get_scheduler
@@ -79,7 +81,6 @@ def main():
         comm.allgather_module(m)
     load_s = time.perf_counter() - t_load
 
-    pool = cf.ThreadPoolExecutor(max_workers=2)
     prompts = ["a photograph of an astronaut riding a horse", "a watercolor fox in a snowy forest",
                "a cyberpunk city street at night, neon", "a bowl of ramen, studio lighting"]
 
@@ -89,15 +90,12 @@ def main():
         out = pipe(prompt=prompts[i % len(prompts)], negative_prompt="blurry, low quality",
                    num_inference_steps=args.denoise_steps, guidance_scale=args.guidance,
                    num_images_per_prompt=args.batch, height=args.res, width=args.res,
-                   generator=g, scheduler=sched)
+                   generator=g, scheduler=sched, output_type="uint8")
         gathered = comm.all_gather_tensor(out.latents.contiguous())  # split-job assembly over xGMI
 
-        def encode(images=out.images):
-            op = OutputProcessor(["primary"], "image/jpeg")
-            op.add_outputs(images)
-            return op.get_results()
-
-        return pool.submit(encode), out.timings, gathered.shape
+        # JPEG/base64/sha256 envelope encoding in the encoder processes, overlapped
+        # with the next job (joined before the clock stops)
+        return pool.submit(list(out.images.numpy()), "image/jpeg"), out.timings, gathered.shape
 
     futs = []
     for i in range(args.warmup):

@@ -239,10 +239,11 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     B, C = x.shape[0], x.shape[-1]
     P = x.numel() // (B * C)
     # a chunk gives every thread >= 4 independent row loads (the kernels' unroll;
-    # R = 256 threads / (C/8 vector columns) rows per pass), with <= ~2048
-    # workgroups over the whole tensor
+    # R = 256 threads / (C/8 vector columns) rows per pass), with <= ~1024
+    # workgroups over the whole tensor (each apply workgroup re-merges the
+    # statistics partials in its prologue: fewer, longer workgroups amortise it)
     rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
-    chunk = max(4 * rows, -(-P * B // 2048))
+    chunk = max(4 * rows, -(-P * B // 1024))
     nchunk = -(-P // chunk)
     chunk = -(-P // nchunk)
     bstride = 0

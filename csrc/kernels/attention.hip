@@ -250,13 +250,24 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
 // QK^T MFMAs of the next inside a single wave (cdna_hip_programming.md T15
 // "compute[cur] || finish[prev]"); block kb+2 is register-staged meanwhile and
 // written to the buffer freed two blocks ago, so no second barrier is needed.
-template <int QT>
+//
+// The softmax is VALU-issue bound at D = 64 (one exp per 64 MACs), so two
+// options move per-score work elsewhere:
+//   PRE  : Q is pre-scaled by scale*log2(e) and the QK^T chain starts from the
+//          accumulator value -m (the running max when the block was issued,
+//          one shared C operand per query tile): p = exp2(s) directly, no
+//          per-score FMA.  A rescale between issue and use (rare: lazy max,
+//          T13) is corrected by one wave-uniform subtract pass.
+//   ONES : the row sum l rides on the PV MFMAs as an extra all-ones V^T tile
+//          (4 MFMAs per block instead of 32 adds + 2 shuffles per query tile).
+template <int QT, bool PRE, bool ONES>
 __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a) {
   constexpr int DP = 64;
   constexpr int CPR = DP / 8;
   constexpr int KB = 64;
   constexpr int DS = DP / 32;
   constexpr int DT = DP / 16;
+  constexpr int DTO = DT + (ONES ? 1 : 0);
   constexpr int QROWS = QT * 16 * 4;
   constexpr int TILE = KB * DP;
   constexpr int LPT = KB * CPR / 256;
@@ -273,6 +284,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
   const bf16_t* kp = a.k + b * a.skb + h * a.skh;
   const bf16_t* vp = a.v + b * a.svb + h * a.svh;
+  const float sl2 = a.scale_log2;
 
   v8s qf[QT][DS];
 #pragma unroll
@@ -282,16 +294,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       const int qi = q0 + qt * 16 + fr, d = ds * 32 + 8 * fg;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (qi < a.Sq && d < a.D) v = *reinterpret_cast<const uint4*>(qp + qi * a.sqs + d);
+      if constexpr (PRE) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= sl2;
+        v = pack8(f);
+      }
       qf[qt][ds] = __builtin_bit_cast(v8s, v);
     }
-  v4f oacc[DT][QT];
+  v4f oacc[DTO][QT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i)
+  for (int i = 0; i < DTO; ++i)
 #pragma unroll
     for (int j = 0; j < QT; ++j) oacc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   float mrow[QT], lrow[QT];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
+  const short one_bf = 0x3f80;
+  const v8s ones = {one_bf, one_bf, one_bf, one_bf, one_bf, one_bf, one_bf, one_bf};
 
   int kv_end = Skv;
   if (a.causal) {
@@ -325,14 +346,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
     }
   };
-  auto qk = [&](int buf, v4f (&s)[4][QT]) {
+  // mu[qt]: the offset the block's scores were issued with (PRE), else 0
+  auto qk = [&](int buf, v4f (&s)[4][QT], float (&mu)[QT]) {
     const bf16_t* ks = smem + buf * 2 * TILE;
+    v4f cinit[QT];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int qt = 0; qt < QT; ++qt) {
+      mu[qt] = (PRE && mrow[qt] > -1e29f) ? mrow[qt] : 0.f;
+      cinit[qt] = v4f{-mu[qt], -mu[qt], -mu[qt], -mu[qt]};
+    }
 #pragma unroll
-      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < 4; ++kt) {
+      const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, fg));
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds)
+      for (int qt = 0; qt < QT; ++qt)
+        s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][0], cinit[qt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ds = 1; ds < DS; ++ds)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, ds * 4 + fg));
@@ -345,15 +376,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   if (nkb > 0) { load_kv(0); store_kv(0); }
   if (nkb > 1) { load_kv(1); store_kv(1); }
   __syncthreads();
-  const float sl2 = a.scale_log2;
   v4f s_a[4][QT], s_b[4][QT];
+  float mu_a[QT], mu_b[QT];
   // one pipelined block: softmax + PV of block kb (scores in sc) while the QK^T
   // of block kb+1 fills sn.  Called alternately with (s_a, s_b) / (s_b, s_a) so
   // the score registers are never copied.
-  auto block = [&](int kb, v4f (&sc)[4][QT], v4f (&sn)[4][QT]) {
+  auto block = [&](int kb, v4f (&sc)[4][QT], float (&muc)[QT], v4f (&sn)[4][QT], float (&mun)[QT]) {
     const int cur = kb % 3;
     if (kb + 2 < nkb) load_kv(kb + 2);
-    if (kb + 1 < nkb) qk((kb + 1) % 3, sn);  // matrix cores busy while the softmax below runs
+    if (kb + 1 < nkb) qk((kb + 1) % 3, sn, mun);  // matrix cores busy while the softmax below runs
 
     const int kbase = kb * KB;
     const bool masked = a.causal || (kbase + KB > kv_end);
@@ -374,31 +405,48 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][qt][r]);
+        for (int r = 0; r < 4; r += 2) mx = fmaxf(mx, fmaxf(sc[kt][qt][r], sc[kt][qt][r + 1]));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       // lazy rescale (cdna_hip_programming.md T13): keep the reference max unless
       // the block max exceeds it by > 2^8; p stays <= 256, exact after the final 1/l
-      const float mb = mx * sl2;
+      const float mb = PRE ? mx + muc[qt] : mx * sl2;  // block max in log2 units
       if (mb > mrow[qt] + 8.f) {
         const float mnew = fmaxf(mrow[qt], mb);
         const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
         mrow[qt] = mnew;
         lrow[qt] *= alpha;
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
+        for (int dt = 0; dt < DTO; ++dt) oacc[dt][qt] *= alpha;
       }
-      const float mref = mrow[qt];
-      float ls = 0.f;
+      if constexpr (PRE) {
+        const float shift = mrow[qt] - muc[qt];  // 0 unless the max moved since issue
+        if (__any(shift != 0.f)) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+          for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][qt][r], sl2, -mref));
-          sc[kt][qt][r] = p;
-          ls += p;
+            for (int r = 0; r < 4; ++r) sc[kt][qt][r] -= shift;
         }
-      lrow[qt] += ls;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[kt][qt][r] = __builtin_amdgcn_exp2f(sc[kt][qt][r]);
+      } else {
+        const float mref = mrow[qt];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sc[kt][qt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][qt][r], sl2, -mref));
+      }
+      if constexpr (!ONES) {
+        float ls = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ls += sc[kt][qt][r];
+        lrow[qt] += ls;
+      }
 #pragma unroll
       for (int kp2 = 0; kp2 < 2; ++kp2) {
         u32 w0 = pack2(sc[2 * kp2][qt][0], sc[2 * kp2][qt][1]);
@@ -410,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     }
     const bf16_t* vs = smem + cur * 2 * TILE + TILE;
 #pragma unroll
-    for (int kp2 = 0; kp2 < 2; ++kp2)
+    for (int kp2 = 0; kp2 < 2; ++kp2) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int qq = fr >> 2, pp = fr & 3;
@@ -423,22 +471,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
         for (int qt = 0; qt < QT; ++qt)
           oacc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kp2][qt], oacc[dt][qt], 0, 0, 0);
       }
+      if constexpr (ONES) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          oacc[DT][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[kp2][qt], oacc[DT][qt], 0, 0, 0);
+      }
+    }
     // block kb+2 -> the buffer that held block kb-1 (last read before the previous barrier)
     if (kb + 2 < nkb) store_kv((kb + 2) % 3);
     __syncthreads();
   };
-  if (nkb > 0) qk(0, s_a);
+  if (nkb > 0) qk(0, s_a, mu_a);
   for (int kb = 0; kb < nkb; kb += 2) {
-    block(kb, s_a, s_b);
-    if (kb + 1 < nkb) block(kb + 1, s_b, s_a);
+    block(kb, s_a, mu_a, s_b, mu_b);
+    if (kb + 1 < nkb) block(kb + 1, s_b, mu_b, s_a, mu_a);
   }
 
   bf16_t* op = a.o + b * a.sob + h * a.soh;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    float l = lrow[qt];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l;
+    if constexpr (ONES) {
+      l = oacc[DT][qt][0];  // every row of the ones tile holds this query's sum over all keys
+    } else {
+      l = lrow[qt];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const float inv = l > 0.f ? 1.0f / l : 0.f;
     const int qi = q0 + qt * 16 + fr;
     if (qi >= a.Sq) continue;
@@ -462,7 +521,8 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64)
+// variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64),
+// 3 = pipelined + PRE, 4 = pipelined + ONES, 5 = pipelined + PRE + ONES
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
                           int Sq, int Skv, int D, float scale, int causal, int variant, const void* kv_len,
                           hipStream_t stream) {
@@ -481,9 +541,16 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   const long long wg4 = (long long)B * H * ((Sq + 255) / 256);
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
-    if (variant == 2 || (variant == 0 && Skv > 128)) {
+    if (variant >= 2 || (variant == 0 && Skv > 128)) {
+      if (variant == 0) variant = 3;  // PRE: 0.283 vs 0.318 ms at B8 S4096 H5 (profiles/opbench_attn_r1e.json)
       const int nqb = (Sq + 127) / 128;
-      attn_fwd_pipe_kernel<2><<<B * H * nqb, 256, 0, stream>>>(a);
+      const dim3 grid(B * H * nqb);
+      switch (variant) {
+        case 2: attn_fwd_pipe_kernel<2, false, false><<<grid, 256, 0, stream>>>(a); break;
+        case 3: attn_fwd_pipe_kernel<2, true, false><<<grid, 256, 0, stream>>>(a); break;
+        case 4: attn_fwd_pipe_kernel<2, false, true><<<grid, 256, 0, stream>>>(a); break;
+        default: attn_fwd_pipe_kernel<2, true, true><<<grid, 256, 0, stream>>>(a); break;
+      }
       return (int)hipGetLastError();
     }
     return launch_attn<64, 2>(a, stream);

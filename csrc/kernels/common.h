@@ -19,8 +19,15 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+typedef float csk_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 csk_b2 __attribute__((ext_vector_type(2)));
+
+// ONE v_cvt_pk_bf16_f32 (RNE) for both halves; packing two scalar conversions
+// costs 4 VALU (2 cvt + shift + or), which the attention softmax and every
+// epilogue / normalisation store paid per output pair.
 __device__ __forceinline__ u32 pack2(float lo, float hi) {
-  return (u32)f2bf(lo) | ((u32)f2bf(hi) << 16);
+  const csk_f2 v = {lo, hi};
+  return __builtin_bit_cast(u32, __builtin_convertvector(v, csk_b2));
 }
 
 // 8 bf16 <-> 8 floats through a 16-byte vector

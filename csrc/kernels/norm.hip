@@ -38,14 +38,18 @@ struct GnLayout {
 // leave the kernel latency-bound at ~1 TB/s); LDS is sized to C (dynamic), not
 // GN_MAXC, so more workgroups fit per CU.
 #define GN_UNROLL 4
+// dynamic LDS of gn_stats_kernel: R rows x 2 x C floats (<= 32 KB)
+static inline size_t gn_stats_lds(int C) {
+  const int NV = C >> 3, TPV = NV > GN_THREADS ? 2 : 1, NVT = (NV + TPV - 1) / TPV;
+  return (size_t)(GN_THREADS / NVT) * 2 * C * sizeof(float);
+}
 __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
                                                               int P, int C, int G, int chunk, int nchunk) {
-  extern __shared__ float red[];  // [2][C]
+  extern __shared__ float red[];  // [R][2][C]: per-row partials, reduced in a fixed order (deterministic)
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
   const GnLayout L(C, tid);
   const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
   const bf16_t* xb = x + (size_t)b * P * C;
-  for (int i = tid; i < 2 * C; i += GN_THREADS) red[i] = 0.f;
   float s[2][8], ss[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -75,19 +79,32 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
       }
     }
   }
-  __syncthreads();
+  // every (row r, vector column v) slot has exactly one owner thread: plain
+  // stores, then a fixed-order sum over rows (LDS float atomics made the
+  // statistics, and so whole denoising runs, vary run to run)
   if (L.r < L.R) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int v = L.cv + u * L.NVT;
       if (u < L.TPV && v < L.NV) {
+        float* rs = red + (size_t)L.r * 2 * C + v * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          atomicAdd(&red[v * 8 + j], s[u][j]);
-          atomicAdd(&red[C + v * 8 + j], ss[u][j]);
+          rs[j] = s[u][j];
+          rs[C + j] = ss[u][j];
         }
       }
     }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += GN_THREADS) {
+    float a = red[c], q = red[C + c];
+    for (int rr = 1; rr < L.R; ++rr) {
+      a += red[(size_t)rr * 2 * C + c];
+      q += red[(size_t)rr * 2 * C + C + c];
+    }
+    red[c] = a;
+    red[C + c] = q;
   }
   __syncthreads();
   const int Cg = C / G;
@@ -103,27 +120,58 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
   }
 }
 
+// Group moments from per-entry partials (count n_i, mean m_i, M2_i), merged by
+// `tpg` consecutive lanes (a power of two <= 64):
+//   mean = sum(n_i m_i) / N,   M2 = sum(M2_i) + sum(n_i (m_i - mean)^2)
+// Two passes of independent loads + FMAs and a butterfly per pass: the
+// sequential Chan chain (a division per entry, each step waiting on the last)
+// made the merge the slowest part of a GroupNorm over a few hundred partials.
+template <class Get>
+__device__ __forceinline__ void group_moments(const Get& get, int ne, int sub, int tpg, float& mean, float& rstd,
+                                              float eps) {
+  float sn = 0.f, sm = 0.f;
+#pragma unroll 4
+  for (int e = sub; e < ne; e += tpg) {
+    float n, m, q;
+    get(e, n, m, q);
+    sn += n;
+    sm = __builtin_fmaf(n, m, sm);
+  }
+  for (int o = 1; o < tpg; o <<= 1) {
+    sn += __shfl_xor(sn, o, 64);
+    sm += __shfl_xor(sm, o, 64);
+  }
+  mean = sn > 0.f ? sm / sn : 0.f;
+  float sq = 0.f;
+#pragma unroll 4
+  for (int e = sub; e < ne; e += tpg) {
+    float n, m, q;
+    get(e, n, m, q);
+    const float d = m - mean;
+    sq += __builtin_fmaf(n * d, d, q);
+  }
+  for (int o = 1; o < tpg; o <<= 1) sq += __shfl_xor(sq, o, 64);
+  rstd = rsqrtf(sq / fmaxf(sn, 1.f) + eps);
+}
+
 // stat[(b * G + g) * 2 + {mean, rstd}]: merge chunk partials (Chan); one wave
 // per (b, g) so the merge is spread over B*G/4 workgroups instead of B.
 __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stat,
                                                                  int B, int G, int nchunk, float eps) {
   const int lane = threadIdx.x & 63;
   const int bg = blockIdx.x * (GN_THREADS / 64) + (threadIdx.x >> 6);
-  if (bg >= B * G) return;
+  if (bg >= B * G) return;  // whole waves leave together (one (b, g) per wave)
   const int b = bg / G, g = bg - b * G;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int c = lane; c < nchunk; c += 64) {
-    const float* pp = part + (((size_t)b * nchunk + c) * G + g) * 3;
-    chan_combine(n, mean, m2, pp[0], pp[1], pp[2]);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
-    chan_combine(n, mean, m2, n2, me2, q2);
-  }
+  float mean, rstd;
+  group_moments(
+      [&](int c, float& n, float& m, float& q) {
+        const float* pp = part + (((size_t)b * nchunk + c) * G + g) * 3;
+        n = pp[0]; m = pp[1]; q = pp[2];
+      },
+      nchunk, lane, 64, mean, rstd, eps);
   if (lane == 0) {
     stat[bg * 2] = mean;
-    stat[bg * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+    stat[bg * 2 + 1] = rstd;
   }
 }
 
@@ -149,29 +197,27 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
     int tpg = 1;
     while (tpg * 2 * G <= GN_THREADS && tpg < 64) tpg *= 2;
     const int g = tid / tpg, sub = tid % tpg;
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    if (g < G) {
-      if constexpr (MODE == 1) {
-        for (int e = sub; e < nent; e += tpg) {
-          const float* pp = stat + (((size_t)b * nent + e) * G + g) * 3;
-          chan_combine(n, mean, m2, pp[0], pp[1], pp[2]);
-        }
-      } else {
-        const int ne = nent * Cg;
-        for (int e = sub; e < ne; e += tpg) {
-          const int sg = b * nent + e / Cg, c = g * Cg + e % Cg;
-          const float* pp = stat + ((size_t)sg * C + c) * 2;
-          chan_combine(n, mean, m2, (float)seg_rows, pp[0], pp[1]);
-        }
-      }
-    }
-    for (int o = 1; o < tpg; o <<= 1) {
-      const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
-      chan_combine(n, mean, m2, n2, me2, q2);
+    float mean, rstd;
+    if constexpr (MODE == 1) {
+      group_moments(
+          [&](int e, float& n, float& m, float& q) {
+            const float* pp = stat + (((size_t)b * nent + e) * G + g) * 3;
+            n = pp[0]; m = pp[1]; q = pp[2];
+          },
+          g < G ? nent : 0, sub, tpg, mean, rstd, eps);
+    } else {
+      const float fn = (float)seg_rows;
+      group_moments(
+          [&](int e, float& n, float& m, float& q) {
+            const int sg = b * nent + e / Cg, c = g * Cg + e % Cg;
+            const float2 mq = *reinterpret_cast<const float2*>(stat + ((size_t)sg * C + c) * 2);
+            n = fn; m = mq.x; q = mq.y;
+          },
+          g < G ? nent * Cg : 0, sub, tpg, mean, rstd, eps);
     }
     if (g < G && sub == 0) {
       gst[2 * g] = mean;
-      gst[2 * g + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+      gst[2 * g + 1] = rstd;
     }
     __syncthreads();
   }
@@ -239,21 +285,18 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
   const int bg = blockIdx.x * (GN_THREADS / 64) + (threadIdx.x >> 6);
   if (bg >= B * G) return;
   const int b = bg / G, g = bg - b * G, Cg = C / G;
-  const int ne = nseg * Cg;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int e = lane; e < ne; e += 64) {
-    const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
-    const float* pp = part + ((size_t)sg * C + c) * 2;
-    chan_combine(n, mean, m2, (float)seg_rows, pp[0], pp[1]);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float n2 = __shfl_xor(n, o, 64), me2 = __shfl_xor(mean, o, 64), q2 = __shfl_xor(m2, o, 64);
-    chan_combine(n, mean, m2, n2, me2, q2);
-  }
+  const float fn = (float)seg_rows;
+  float mean, rstd;
+  group_moments(
+      [&](int e, float& n, float& m, float& q) {
+        const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
+        const float2 mq = *reinterpret_cast<const float2*>(part + ((size_t)sg * C + c) * 2);
+        n = fn; m = mq.x; q = mq.y;
+      },
+      nseg * Cg, lane, 64, mean, rstd, eps);
   if (lane == 0) {
     stat[bg * 2] = mean;
-    stat[bg * 2 + 1] = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+    stat[bg * 2 + 1] = rstd;
   }
 }
 
@@ -286,7 +329,7 @@ CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma
   float* pt = (float*)part;
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
-  gn_stats_kernel<<<grid, GN_THREADS, 2 * C * sizeof(float), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
+  gn_stats_kernel<<<grid, GN_THREADS, gn_stats_lds(C), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
   if (G <= 64 && nchunk <= 512) {  // merge the chunk partials in the apply prologue (no finalize launch)
     gn_apply_kernel<1><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, pt, (const bf16_t*)gamma,
                                                         (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride,

@@ -128,7 +128,7 @@ def test_attention(gpu, B, Sq, Skv, H, D, causal):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, scale, causal)) < 1.5e-2
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("B,Sq,Skv,H,D,causal", [(2, 1024, 1024, 5, 64, False), (1, 300, 517, 3, 64, False),
                                                   (1, 333, 333, 2, 40, True), (2, 4096, 77, 5, 64, False)])
 def test_attention_variants(gpu, variant, B, Sq, Skv, H, D, causal):
@@ -150,12 +150,42 @@ def test_attention_fused_qkv_strides(gpu):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
-def test_attention_spike_rescale(gpu):
-    # forces the online-softmax rescale: a huge logit appears in a late KV block
-    B, S, H, D = 1, 128, 1, 64
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_attention_spike_rescale(gpu, variant):
+    # forces the online-softmax rescale: growing logits appear in later KV blocks,
+    # including consecutive blocks (the pipelined kernels issue block kb+1's
+    # scores before block kb's rescale decision)
+    B, S, H, D = 1, 512, 2, 64
     q, k, v = (rnd(B, S, H, D, dev=gpu) for _ in range(3))
     k[0, 100, 0] = q[0, 5, 0] * 8
-    y = hip_ops.attention(q, k, v, 0.125)
+    k[0, 130, 0] = q[0, 5, 0] * 12
+    k[0, 200, 1] = q[0, 70, 1] * 10
+    k[0, 333, 1] = q[0, 70, 1] * 16
+    old = hip_ops.ATTN_VARIANT
+    hip_ops.ATTN_VARIANT = variant
+    try:
+        y = hip_ops.attention(q, k, v, 0.125)
+    finally:
+        hip_ops.ATTN_VARIANT = old
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
+
+
+@pytest.mark.parametrize("variant", [2, 3, 5])
+def test_attention_far_negative_logits(gpu, variant):
+    # every score far below 0 (softmax is shift-invariant): the running-max offset
+    # must follow the logits down, not start from 0
+    B, S, H, D = 1, 300, 1, 64
+    u = torch.nn.functional.normalize(torch.randn(D, device=gpu), dim=0)
+    q = (u * 40 + 0.3 * torch.randn(B, S, H, D, device=gpu)).bfloat16()
+    k = (-u * 40 + 0.3 * torch.randn(B, S, H, D, device=gpu)).bfloat16()
+    v = rnd(B, S, H, D, dev=gpu)
+    old = hip_ops.ATTN_VARIANT
+    hip_ops.ATTN_VARIANT = variant
+    try:
+        y = hip_ops.attention(q, k, v, 0.125)
+    finally:
+        hip_ops.ATTN_VARIANT = old
+    assert torch.isfinite(y.float()).all()
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
