@@ -39,8 +39,8 @@ def prepare_model(model: nn.Module) -> nn.Module:
 class Linear(nn.Linear, Prepared):
     """nn.Linear whose forward runs the MFMA GEMM (fused bias/act/residual)."""
 
-    def forward(self, x, residual=None, act=None):  # type: ignore[override]
-        return ops.gemm(x, self.weight, self.bias, residual=residual, act=act)
+    def forward(self, x, residual=None, act=None, row_stats=False):  # type: ignore[override]
+        return ops.gemm(x, self.weight, self.bias, residual=residual, act=act, row_stats=row_stats)
 
 
 class Conv2d(nn.Conv2d, Prepared):
@@ -58,13 +58,13 @@ class Conv2d(nn.Conv2d, Prepared):
         return self.wp
 
     def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None, act=None, out_scale=1.0,
-                out=None, gn_stats=False):  # type: ignore[override]
+                out=None, gn_stats=False, row_stats=False):  # type: ignore[override]
         kh, kw = self.kernel_size
         if (kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x and act is None and out_scale == 1.0
                 and out is None and x.is_contiguous()):
             w2 = self.weight.view(self.out_channels, self.in_channels)
             gr = x.shape[1] * x.shape[2] if (gn_stats and bias2d is None and x.dim() == 4) else 0
-            y = ops.gemm(x, w2, self.bias, residual=residual, gn_rows=gr)
+            y = ops.gemm(x, w2, self.bias, residual=residual, gn_rows=gr, row_stats=row_stats and bias2d is None)
             if bias2d is not None:
                 y = y + bias2d[:, None, None, :].to(y.dtype)
             return y
@@ -170,18 +170,27 @@ class Attention(Prepared):
     def forward(self, x, ctx=None, kv=None, residual=None, causal=False):
         """x: [B, S, C].  ``residual`` is added in the out-projection epilogue."""
         self._ensure()
-        b, s, _ = x.shape
-        h, d = self.heads, self.dim_head
         if self.is_cross:
-            q = self.to_q(x).view(b, s, h, d)
-            if kv is None:  # no context given: attend to itself (diffusers attn2 semantics)
-                kv = self.context_kv(ctx if ctx is not None else x)
-            k, v = kv[:, :, 0], kv[:, :, 1]
-        else:
-            qkv = ops.gemm(x, self.w_qkv, self.b_qkv).view(b, s, 3, h, d)
-            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        o = ops.attention(q, k, v, self.scale, causal=causal)
-        return self.to_out[0](o.reshape(b, s, h * d), residual=residual)
+            return self.attend_q(self.to_q(x), kv, ctx if ctx is not None else x, residual)
+        return self.attend_qkv(ops.gemm(x, self.w_qkv, self.b_qkv), residual, causal=causal)
+
+    def attend_qkv(self, qkv, residual=None, causal=False, row_stats=False):
+        """Self-attention from the fused QKV projection [B, S, 3*H*D]."""
+        b, s, _ = qkv.shape
+        h, d = self.heads, self.dim_head
+        qkv = qkv.view(b, s, 3, h, d)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], self.scale, causal=causal)
+        return self.to_out[0](o.reshape(b, s, h * d), residual=residual, row_stats=row_stats)
+
+    def attend_q(self, q, kv, ctx, residual=None, row_stats=False):
+        """Cross-attention from the query projection [B, S, H*D]; ``kv`` per-request
+        K/V ([B, Skv, 2, H, D]) or None (computed from ``ctx``)."""
+        b, s, _ = q.shape
+        h, d = self.heads, self.dim_head
+        if kv is None:  # no context given: attend to itself (diffusers attn2 semantics)
+            kv = self.context_kv(ctx)
+        o = ops.attention(q.view(b, s, h, d), kv[:, :, 0], kv[:, :, 1], self.scale)
+        return self.to_out[0](o.reshape(b, s, h * d), residual=residual, row_stats=row_stats)
 
 
 class SpatialSelfAttention(Attention):
@@ -206,10 +215,13 @@ class GEGLU(Prepared):
         self.wp, self.bp = ops.pack_geglu(self.proj.weight.detach(),
                                           self.proj.bias.detach() if self.proj.bias is not None else None)
 
-    def forward(self, x):
+    def ensure(self):
         wp = getattr(self, "wp", None)
         if wp is None or wp.device != self.proj.weight.device or wp.dtype != self.proj.weight.dtype:
             self.prepare()
+
+    def forward(self, x):
+        self.ensure()
         return ops.gemm(x, self.wp, self.bp, act="geglu")
 
 
@@ -235,11 +247,43 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = LayerNorm(dim)
         self.ff = FeedForward(dim)
 
-    def forward(self, x, ctx=None, kv=None):
-        x = self.attn1(self.norm1(x), residual=x)
-        x = self.attn2(self.norm2(x), ctx=ctx, kv=kv, residual=x)
-        x = self.ff(self.norm3(x), residual=x)
-        return x
+    def _fold(self, name, w, b, norm):
+        """gamma/beta-folded copy of a projection that consumes ``norm`` (cached;
+        refolded when the weights change, e.g. a LoRA merge)."""
+        key = (w.data_ptr(), w._version, norm.weight.data_ptr(), norm.weight._version, w.dtype, w.device)
+        folds = self.__dict__.setdefault("_ln_folds", {})
+        f = folds.get(name)
+        if f is None or f[0] != key:
+            f = (key, ops.fold_layer_norm(w.detach(), None if b is None else b.detach(), norm.weight.detach(),
+                                          None if norm.bias is None else norm.bias.detach()))
+            folds[name] = f
+        return f[1]
+
+    def forward(self, x, ctx=None, kv=None, row_stats=None):
+        """On the HIP path every LayerNorm runs inside the GEMM that consumes it
+        (``ops.layer_norm_gemm``): each producer GEMM (proj_in, the attention
+        out-projections, the FF down-projection) emits per-row statistics of its
+        output, so the three LN kernels per block disappear.  ``row_stats``: emit
+        them for whatever consumes this block's output (default: on HIP)."""
+        hip = ops.row_stats_wanted(x)
+        if row_stats is None:
+            row_stats = hip
+        a1, a2, ff = self.attn1, self.attn2, self.ff
+        a1._ensure()
+        fus = ops.ln_fusable(x)
+        qkv = ops.layer_norm_gemm(x, self.norm1, a1.w_qkv, a1.b_qkv,
+                                  self._fold("qkv", a1.w_qkv, a1.b_qkv, self.norm1) if fus else None)
+        x = a1.attend_qkv(qkv, residual=x, row_stats=hip)
+        fus = ops.ln_fusable(x)
+        q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
+                                self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None)
+        x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
+        g = ff.net[0]
+        g.ensure()
+        fus = ops.ln_fusable(x)
+        hdn = ops.layer_norm_gemm(x, self.norm3, g.wp, g.bp, self._fold("ff", g.wp, g.bp, self.norm3) if fus else None,
+                                  act="geglu")
+        return ff.net[2](hdn, residual=x, row_stats=row_stats)
 
 
 class Transformer2D(nn.Module):
@@ -265,9 +309,15 @@ class Transformer2D(nn.Module):
     def forward(self, x, ctx=None, kvs=None):
         b, hh, ww, c = x.shape
         h = self.norm(x)
-        h = self.proj_in(h).view(b, hh * ww, c)
+        hip = ops.row_stats_wanted(x)
+        h = self.proj_in(h, row_stats=hip)  # row statistics feed block 0's fused LayerNorm
+        rows = getattr(h, "_csk_rows", None)
+        h = h.view(b, hh * ww, c)
+        if rows is not None:
+            h._csk_rows = rows
+        nb = len(self.transformer_blocks)
         for i, blk in enumerate(self.transformer_blocks):
-            h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i])
+            h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb)
         if isinstance(self.proj_out, Linear):
             return ops.gemm(h.view(b, hh, ww, c), self.proj_out.weight, self.proj_out.bias, residual=x,
                             gn_rows=hh * ww)

@@ -228,9 +228,14 @@ class UNet2DConditionModel(Prepared):
         if not torch.is_tensor(t):
             t = torch.tensor([t], dtype=torch.float32, device=self.conv_in.weight.device)
         t = t.reshape(-1).float()
-        if t.numel() == 1:
-            t = t.expand(batch)
-        temb = self.time_embedding(timestep_embedding(t, self.cfg.block_out_channels[0]).to(dtype))
+        if ops.use_hip(t) and dtype == torch.bfloat16:
+            from ..ops import hip_ops  # one kernel instead of ~12 small torch ops per step
+
+            emb = hip_ops.timestep_embedding(t, batch, self.cfg.block_out_channels[0])
+        else:
+            emb = timestep_embedding(t.expand(batch) if t.numel() == 1 else t,
+                                     self.cfg.block_out_channels[0]).to(dtype)
+        temb = self.time_embedding(emb)
         if self.cfg.addition_embed_type == "text_time":
             text_embeds = added_cond["text_embeds"]
             time_ids = added_cond["time_ids"]

@@ -80,7 +80,7 @@ class _TemporalBlock(BasicTransformerBlock):
 
         self.attn2 = Attention(dim, heads, dim_head)
 
-    def forward(self, x, ctx=None, kv=None):
+    def forward(self, x, ctx=None, kv=None, row_stats=None):
         x = self.attn1(self.norm1(x), residual=x)
         x = self.attn2(self.norm2(x), residual=x)
         return self.ff(self.norm3(x), residual=x)

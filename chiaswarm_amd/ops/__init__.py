@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -83,26 +85,77 @@ def _ref_gemm(a2, w, bias, residual, act):
     return y.to(a2.dtype)
 
 
-def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, gn_rows=0):
+def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, gn_rows=0, row_stats=False):
     """y[..., N'] = act(a[..., K] @ w[N, K]^T + bias) + residual.
 
     ``act='geglu'`` expects ``pack_geglu`` weights and returns N' = N/2.
     ``gn_rows`` > 0 asks the HIP epilogue for the GroupNorm statistics of the
-    output (``gn_rows`` rows per sample) for the GroupNorm that consumes it."""
+    output (``gn_rows`` rows per sample) for the GroupNorm that consumes it;
+    ``row_stats`` for the per-row statistics a consumer's fused LayerNorm
+    (``layer_norm_gemm``) reads."""
     lead = a.shape[:-1]
     k = a.shape[-1]
     a2 = a.reshape(-1, k)
     if use_hip(a):
         from . import hip_ops
 
-        y = hip_ops.gemm(a2, w, bias, residual, act, gn_rows=gn_rows)
+        y = hip_ops.gemm(a2, w, bias, residual, act, gn_rows=gn_rows, row_stats=row_stats)
     else:
         y = _ref_gemm(a2, w, bias, residual, act)
     out = y.view(*lead, y.shape[-1])
-    st = getattr(y, "_csk_gn", None)
-    if st is not None:
-        out._csk_gn = st
+    for attr in ("_csk_gn", "_csk_rows"):
+        st = getattr(y, attr, None)
+        if st is not None:
+            setattr(out, attr, st)
     return out
+
+
+def fold_layer_norm(w: torch.Tensor, bias, gamma: torch.Tensor, beta):
+    """LayerNorm(x) @ w^T + bias == rstd * (x @ w'^T - mean * colsum) + bias'
+    with w' = w * gamma (per input column), colsum = rowsum(w') in fp32 (of the
+    bf16-rounded w', so the correction matches what the MFMAs multiply) and
+    bias' = bias + w @ beta.  Returns (w', colsum, bias')."""
+    wf = w.float()
+    w2 = (wf * gamma.float()[None, :]).to(w.dtype)
+    colsum = w2.float().sum(1).contiguous()
+    b2 = wf @ beta.float() if beta is not None else torch.zeros(w.shape[0], device=w.device)
+    if bias is not None:
+        b2 = b2 + bias.float()
+    return w2.contiguous(), colsum, b2.to(w.dtype)
+
+
+LN_FUSE = os.environ.get("CSK_LN_FUSE", "1") != "0"
+
+
+def row_stats_wanted(x: torch.Tensor) -> bool:
+    """Should a producer GEMM emit row statistics for a LayerNorm consumer?"""
+    return LN_FUSE and use_hip(x)
+
+
+def ln_fusable(x: torch.Tensor) -> bool:
+    """x carries the producer's row statistics (HIP path) for ``layer_norm_gemm``."""
+    rows = getattr(x, "_csk_rows", None)
+    return (LN_FUSE and use_hip(x) and rows is not None and rows[1] <= 32 and x.shape[-1] % 8 == 0)
+
+
+def layer_norm_gemm(x, norm, w, bias, folded, act=None, residual=None, row_stats=False):
+    """act(LayerNorm(x) @ w^T + bias) + residual.  On the HIP path with the
+    producer's row statistics attached to ``x`` the LayerNorm runs inside the
+    GEMM epilogue (``folded`` = fold_layer_norm(w, bias, norm.weight, norm.bias));
+    otherwise LayerNorm kernel + GEMM."""
+    if ln_fusable(x):
+        from . import hip_ops
+
+        w2, colsum, b2 = folded
+        lead = x.shape[:-1]
+        y = hip_ops.gemm(x.reshape(-1, x.shape[-1]), w2, b2, residual, act,
+                         ln=(x._csk_rows, colsum, float(norm.eps)), row_stats=row_stats)
+        out = y.view(*lead, y.shape[-1])
+        if getattr(y, "_csk_rows", None) is not None:
+            out._csk_rows = y._csk_rows
+        return out
+    return gemm(layer_norm(x, norm.weight, norm.bias, norm.eps), w, bias, residual=residual, act=act,
+                row_stats=row_stats)
 
 
 def cat_channels(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -22,6 +22,12 @@ sig("csk_gemm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
 sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
     c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
+sig("csk_gemm_ln", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
+    c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p, c_void_p)
+sig("csk_conv2d_ex", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
 sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
     c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
 
@@ -29,12 +35,23 @@ sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void
 # ---------------------------------------------------------------------------
 # GroupNorm statistics fused into producer epilogues
 # ---------------------------------------------------------------------------
+GN_FINE = 0  # mirrors the library's g_gn_fine (set_gn_fine)
+
+
+def set_gn_fine(v: int):
+    global GN_FINE
+    GN_FINE = int(v)
+    _lib.call("csk_set_gn_fine", GN_FINE)
+
+
 def _gn_seg(tile, split, rows_per_b, M, code):
-    """Row-tile height usable for fused GN statistics, or 0."""
-    bm = tuning.TILES.get(tile, (0, 0))[0]
+    """Rows per fused-GN statistics segment (fine: the epilogue's column pass
+    splits each BM-row tile into 256/BN segments of BM*BN/256 rows; else one
+    segment per tile), or 0."""
+    bm, bn = tuning.TILES.get(tile, (0, 0))
     if split != 1 or code == 3 or bm == 0 or rows_per_b <= 0 or rows_per_b % bm or M % bm:
         return 0
-    return bm
+    return bm * bn // 256 if GN_FINE else bm
 
 
 def _gn_part(M, N, seg, device):
@@ -55,6 +72,22 @@ sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p
 sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_softmax_rows", c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
+sig("csk_set_gn_prologue_max", c_int)
+sig("csk_set_gn_fine", c_int)
+sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
+
+
+def timestep_embedding(t, batch, dim, flip_sin_to_cos=True, shift=0.0, max_period=10000.0):
+    """bf16 [batch, dim] sinusoidal embedding of fp32 timesteps t ([1] broadcast or [batch])."""
+    t = t.reshape(-1)
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.float().contiguous()
+    if t.numel() not in (1, batch):
+        raise ValueError(f"timestep_embedding: {t.numel()} timesteps for batch {batch}")
+    y = torch.empty((batch, dim), dtype=torch.bfloat16, device=t.device)
+    _lib.call("csk_timestep_embedding", _p(y), _p(t), 0 if t.numel() == 1 else 1, batch, dim,
+              int(bool(flip_sin_to_cos)), float(shift), float(max_period), _s())
+    return y
 
 
 def _bf16(t, name):
@@ -87,9 +120,15 @@ def pad_last(x: torch.Tensor, n: int) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
-def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0):
+def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None, row_stats=False):
     """``gn_rows`` > 0: also produce GroupNorm statistics of the output for a
-    consumer GN (rows per sample = gn_rows), attached as ``out._csk_gn``."""
+    consumer GN (rows per sample = gn_rows), attached as ``out._csk_gn``.
+
+    ``row_stats``: also produce per-row (mean, M2) partials of the output for a
+    consumer's fused LayerNorm, attached as ``out._csk_rows = (part, nparts, pcols)``.
+    ``ln = (rows, colsum, eps)``: this GEMM's input rows are LayerNorm'd on the
+    fly — ``w``/``bias`` are the gamma/beta-folded weights (``fold_layer_norm``)
+    and ``rows`` the producer's ``_csk_rows``."""
     _bf16(a2, "gemm.a")
     _bf16(w, "gemm.w")
     M, K = a2.shape
@@ -124,9 +163,30 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0):
                   M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
+    if ln is not None or row_stats:
+        if split > 1:  # the split-K reduce has no LN / row-statistics epilogue
+            tile, split = (19 if N <= 1280 else 20), 1
+        if ln is None and code == 3:
+            row_stats = False
     seg = _gn_seg(tile, split, gn_rows, M, code) if gn_rows and out.is_contiguous() else 0
     part = _gn_part(M, N, seg, a2.device) if seg else None
-    run(tile, split, part)
+    if ln is None and not row_stats:
+        run(tile, split, part)
+    else:
+        bn = tuning.TILES[tile][1]
+        rp = torch.empty(-(-N // bn) * M * 2, dtype=torch.float32, device=a2.device) if row_stats else None
+        lp = lc = None
+        nparts = pcols = 0
+        eps = 0.0
+        if ln is not None:
+            (lp, nparts, pcols), lc, eps = ln
+            if K % 8 or nparts * pcols < K or lp.numel() < nparts * M * 2:
+                raise ValueError("gemm: fused LayerNorm statistics do not match the input")
+        _lib.call("csk_gemm_ln", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
+                  M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), _p(lp), _p(lc), nparts, pcols,
+                  float(eps), _p(rp), tile, 1, None, _s())
+        if rp is not None:
+            out._csk_rows = (rp, -(-N // bn), bn)
     if part is not None:
         out._csk_gn = (part, seg)
     return out
@@ -182,16 +242,22 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
         if rs is None:
             residual = residual.contiguous()
             rs = Cout
+    b2s = 0
     if bias2d is not None:
-        bias2d = bias2d.contiguous()
+        # a column slice of the UNet's one batched time-embedding GEMM: pass its
+        # row stride instead of copying it out (one copy kernel per ResNet)
         if bias2d.shape != (B, Cout):
             raise ValueError("conv2d bias2d shape")
+        _bf16(bias2d, "conv.bias2d")
+        if bias2d.stride(1) != 1 or bias2d.data_ptr() % 16 or bias2d.stride(0) % 8:
+            bias2d = bias2d.contiguous()
+        b2s = bias2d.stride(0) if B > 1 else Cout
     M, K = B * Ho * Wo, kh * kw * Cin
     code = ACT[act]
 
     def run(tile, split, part=None):
         ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
-        _lib.call("csk_conv2d", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), _p(residual),
+        _lib.call("csk_conv2d_ex", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), b2s, _p(residual),
                   B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
                   float(out_scale), int(dilation), _p(part), tile, split, _p(ws), _s())
 

@@ -42,6 +42,16 @@ def encode_arrays(arrays, content_type: str = "image/jpeg", output_list=("primar
     return op.get_results()
 
 
+def encode_artifact(arrays, content_type: str = "image/jpeg") -> dict:
+    """uint8 HWC arrays -> ONE artifact (grid, encode, thumbnail, base64, sha256)."""
+    from PIL import Image
+
+    from .processor import image_to_buffer, make_result, post_process
+
+    buf = image_to_buffer(post_process([Image.fromarray(a) for a in arrays]), content_type)
+    return make_result(buf, buf, content_type)
+
+
 def _gpu_initialised() -> bool:
     torch = sys.modules.get("torch")
     if torch is None:
@@ -81,6 +91,9 @@ class EncoderPool:
 
     def submit(self, arrays, content_type: str = "image/jpeg", output_list=("primary",)) -> cf.Future:
         return self._pool.submit(encode_arrays, list(arrays), content_type, tuple(output_list))
+
+    def submit_artifact(self, arrays, content_type: str = "image/jpeg") -> cf.Future:
+        return self._pool.submit(encode_artifact, list(arrays), content_type)
 
     def shutdown(self):
         self._pool.shutdown(wait=True)

@@ -20,6 +20,22 @@ import json
 from PIL import Image, ImageDraw
 
 THUMB = (100, 100)
+_ENCODER = None  # output.encoder.EncoderPool of this process (None: encode inline)
+
+
+def set_encoder_pool(pool) -> None:
+    global _ENCODER
+    _ENCODER = pool
+
+
+def resolve_artifacts(result: dict) -> dict:
+    """Replace Future-valued artifacts (deferred encoding) by their dicts."""
+    arts = result.get("artifacts")
+    if isinstance(arts, dict):
+        for k, v in list(arts.items()):
+            if hasattr(v, "result") and callable(v.result):
+                arts[k] = v.result()
+    return result
 
 
 class OutputProcessor:
@@ -36,6 +52,25 @@ class OutputProcessor:
         self.other_outputs[name] = images
 
     def get_results(self) -> dict:
+        """{name: artifact}.  With an encoder pool registered (the GPU worker
+        process does this at startup, ``set_encoder_pool``) image artifacts are
+        returned as Futures resolved by the pool's processes, so the GPU thread
+        goes straight on to the next job; the worker resolves them before posting."""
+        if _ENCODER is not None and self.main_content_type.startswith("image") and all(
+                isinstance(im, Image.Image) for ims in [self.outputs] + list(self.other_outputs.values())
+                for im in ims):
+            import numpy as np
+
+            results = {}
+            if "primary" in self.output_list:
+                grid_shape(len(self.outputs))  # >9 images: ValueError (fatal) raised here, not in the pool
+                results["primary"] = _ENCODER.submit_artifact([np.asarray(im.convert("RGB")) for im in self.outputs],
+                                                              self.main_content_type)
+            for key, images in self.other_outputs.items():
+                grid_shape(len(images))
+                results[key] = _ENCODER.submit_artifact([np.asarray(im.convert("RGB")) for im in images],
+                                                        self.main_content_type)
+            return results
         results = {}
         if "primary" in self.output_list:
             buf = image_to_buffer(post_process(self.outputs), self.main_content_type)

@@ -1,7 +1,10 @@
 """One OS process per GPU: the reference ran every GPU as a
 thread of one Python process (swarm/generator.py:13-14, one shared GIL); here
-each GPU gets its own process that owns its HBM-resident model cache, runs jobs
-and encodes results (JPEG/base64/sha256) locally.
+each GPU gets its own process that owns its HBM-resident model cache and runs
+jobs.  Results are encoded (grid, JPEG, thumbnail, base64, sha256) by a small
+pool of encoder processes this process starts BEFORE it touches the GPU
+(output/encoder.py): the GPU thread hands over uint8 pixels and goes straight on
+to the next job; a finisher thread resolves the encodings and posts results.
 
 This module must not import torch at import time: the child selects its GPU via
 HIP_VISIBLE_DEVICES *before* torch initialises.
@@ -20,6 +23,26 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     for k, v in (env or {}).items():
         os.environ[k] = v
+    # encoder processes first: spawning is only safe before this process initialises HIP
+    from ..output.encoder import EncoderPool
+    from ..output.processor import resolve_artifacts, set_encoder_pool
+
+    encoders = EncoderPool() if gpu_index != "cpu" else None
+    if encoders is not None and encoders.kind == "process":
+        set_encoder_pool(encoders)
+    import concurrent.futures as cf
+
+    finisher = cf.ThreadPoolExecutor(max_workers=1)
+
+    def post(jid, result):
+        """Resolve deferred artifacts off the GPU thread, then hand the result over."""
+        def run():
+            try:
+                outbox.put((gpu_index, jid, resolve_artifacts(result), None))
+            except BaseException as e:
+                outbox.put((gpu_index, jid, None, f"result encoding failed: {e}\n{traceback.format_exc()}"))
+        finisher.submit(run)
+
     from ..log_setup import setup_logging
     from ..settings import load_settings, resolve_path
     from .device import Device
@@ -41,7 +64,7 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
 
             try:
                 for res in run_jobs(job, device, max(1, settings.max_batch)):
-                    outbox.put((gpu_index, res["id"], res, None))
+                    post(res["id"], res)
             except BaseException as e:
                 for j in job:
                     outbox.put((gpu_index, j.get("id"), None, f"{e}\n{traceback.format_exc()}"))
@@ -49,6 +72,9 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         jid = job.get("id")
         try:
             result = synchronous_do_work_function(job, device)
-            outbox.put((gpu_index, jid, result, None))
+            post(jid, result)
         except BaseException as e:  # never let the loop die silently
             outbox.put((gpu_index, jid, None, f"{e}\n{traceback.format_exc()}"))
+    finisher.shutdown(wait=True)  # every pending result is posted before the process exits
+    if encoders is not None:
+        encoders.shutdown()

@@ -235,3 +235,31 @@ CSK_API int csk_pad_channels(void* y, const void* x, long long rows, int cin, in
                                                                          cout);
   CSK_CHECK_LAUNCH();
 }
+
+// Sinusoidal timestep embedding (diffusers `Timesteps`) in ONE launch
+// (it was ~12 small torch kernels at the head of every UNet step):
+//   freq_i = exp(-ln(max_period) * i / (half - shift)),  a = t[b] * freq_i
+//   out[b] = flip ? [cos(a), sin(a)] : [sin(a), cos(a)]     (bf16)
+// t: fp32 [B] with element stride ts (0 broadcasts one timestep over the batch).
+__global__ void timestep_emb_kernel(bf16_t* __restrict__ y, const float* __restrict__ t, int ts, int B, int dim,
+                                    int flip, float shift, float log_max_period) {
+  const int half = dim / 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * half) return;
+  const int b = i / half, j = i - b * half;
+  const float freq = expf(-log_max_period * (float)j / ((float)half - shift));
+  const float a = t[(size_t)b * ts] * freq;
+  const float s = sinf(a), c = cosf(a);
+  bf16_t* yb = y + (size_t)b * dim;
+  yb[j] = f2bf(flip ? c : s);
+  yb[half + j] = f2bf(flip ? s : c);
+}
+
+CSK_API int csk_timestep_embedding(void* y, const void* t, int ts, int B, int dim, int flip, float shift,
+                                   float max_period, hipStream_t stream) {
+  if (dim % 2 != 0 || B <= 0) return (int)hipErrorInvalidValue;
+  const int n = B * (dim / 2);
+  timestep_emb_kernel<<<(n + 255) / 256, 256, 0, stream>>>((bf16_t*)y, (const float*)t, ts, B, dim, flip, shift,
+                                                           logf(max_period));
+  return (int)hipGetLastError();
+}

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   constexpr int CA = BM * 8 / 256, CB = BN * 8 / 256;  // 16B chunks per thread per K-step
   constexpr int SMEM_MAIN = 2 * (BM + BN) * BK;          // bf16 elements
   constexpr int LDC_S = BN + 4;                          // fp32 staging row stride (floats)
-  constexpr int SMEM_EPI = BM * LDC_S * 2;               // in bf16-element units
+  constexpr int SMEM_EPI = epi_smem_elems<BM, BN>();    // in bf16-element units
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
   bf16_t* As = smem;                 // [2][BM*BK]
@@ -194,6 +194,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 
   const int nk = (kend - kbeg + BK - 1) / BK;
   load_tiles(0);
+  const float2 lnrow = ln_row_stats<BM>(args, m0);
   store_tiles(0);
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
@@ -220,11 +221,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split);
+  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split, lnrow);
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV>
-static int launch(const GemmArgs& a, int ksplit, hipStream_t s) {
+static int launch(const GemmArgs& a0, int ksplit, hipStream_t s) {
+  GemmArgs a = a0;
+  a.gn_seg = gn_seg_for<BM, BN>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int span = ksplit > 1 ? a.kchunk : a.K;
   // FAST staging measured SLOWER on this register-staged pipeline (127 -> 309 us on
@@ -250,7 +253,7 @@ __global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
     float v = 0.f;
     for (int sidx = 0; sidx < ksplit; ++sidx) v += a.ws[(size_t)sidx * total + i];
     if (a.bias) v += bf2f(a.bias[n]);
-    if (a.bias2d) v += bf2f(a.bias2d[(size_t)(m / a.rows_per_b) * N + n]);
+    if (a.bias2d) v += bf2f(a.bias2d[(size_t)(m / a.rows_per_b) * a.ldb2 + n]);
     v = apply_act(a.act, v);
     v *= a.out_scale;
     if (a.res) v += bf2f(a.res[(size_t)m * a.ldr + n]);
@@ -271,6 +274,9 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (ksplit > 1 || a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
+  if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
+  if (a.ln_part && tile >= 21) tile = (tile == 21) ? 11 : (tile == 23 ? 18 : 19);  // persistent: no per-tile LN stats
+  if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;
     const int nk = (a.K + BK - 1) / BK;
@@ -308,29 +314,53 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
 }
 
 // y[M, ldc] = act(A[M, lda] . W[N, ldb]^T + bias + bias2d) * out_scale + res[M, ldr]
-CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
-                     int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
-                     void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {
+// (+ fused input LayerNorm / output row statistics: GemmArgs::ln_part / row_part)
+int g_gn_fine = 0;  // tile segments: same step time as fine ones (tools/abstep.py), 4x fewer partials
+CSK_API int csk_set_gn_fine(int v) {
+  g_gn_fine = v;
+  return 0;
+}
+
+CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
+                        int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act,
+                        float out_scale, void* gn_part, const void* ln_part, const void* ln_colsum, int ln_nparts,
+                        int ln_pcols, float ln_eps, void* row_part, int tile, int ksplit, void* ws,
+                        hipStream_t stream) {
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (act == ACT_GEGLU && N % 32 != 0)) return (int)hipErrorInvalidValue;
+  if (ln_part && (!ln_colsum || ln_nparts <= 0 || ln_nparts > 32 || ln_pcols <= 0 ||
+                  (long long)ln_nparts * ln_pcols < K))
+    return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.bias2d = (const bf16_t*)bias2d; a.res = (const bf16_t*)res;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr > 0 ? ldr : ldc;
   a.rows_per_b = rows_per_b > 0 ? rows_per_b : 1; a.act = act; a.out_scale = out_scale;
+  a.ldb2 = N;
   a.ws = (float*)ws;
   a.gn_part = (float*)gn_part;
+  a.ln_part = (const float*)ln_part; a.ln_colsum = (const float*)ln_colsum;
+  a.ln_nparts = ln_nparts; a.ln_pcols = ln_pcols; a.ln_eps = ln_eps;
+  a.row_part = (float*)row_part;
   if (M == 0 || N == 0) return 0;
   return dispatch<false>(a, tile, ksplit, stream);
+}
+
+CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
+                     int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
+                     void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {
+  return csk_gemm_ln(C, A, W, bias, bias2d, res, M, N, K, lda, ldb, ldc, ldr, rows_per_b, act, out_scale, gn_part,
+                     nullptr, nullptr, 0, 0, 0.f, nullptr, tile, ksplit, ws, stream);
 }
 
 // NHWC conv; xs / ys / rs: pixel strides (elements) of input / output / residual
 // buffers (>= channel counts: lets dense blocks read and write channel slices of
 // one concat buffer without copies).
-CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
-                       int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
-                       int up2x, int xs, int ys, int rs, int act, float out_scale, int dil, void* gn_part, int tile,
-                       int ksplit, void* ws, hipStream_t stream) {
-  if (Cin % 8 != 0 || xs % 8 != 0 || xs < Cin) return (int)hipErrorInvalidValue;
+// b2s: row stride of bias2d ([B][b2s], 0 -> Cout)
+CSK_API int csk_conv2d_ex(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, int b2s,
+                          const void* res, int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt,
+                          int pl, int Ho, int Wo, int up2x, int xs, int ys, int rs, int act, float out_scale, int dil,
+                          void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {
+  if (Cin % 8 != 0 || xs % 8 != 0 || xs < Cin || (b2s != 0 && b2s < Cout)) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.W = (const bf16_t*)Wp; a.C = (bf16_t*)Y;
   a.bias = (const bf16_t*)bias; a.bias2d = (const bf16_t*)bias2d; a.res = (const bf16_t*)res;
@@ -340,8 +370,17 @@ CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias,
   a.H = H; a.Wd = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.kh = kh; a.kw = kw; a.stride = stride; a.pt = pt; a.pl = pl;
   a.up2x = up2x;
   a.dil = dil > 0 ? dil : 1;
+  a.ldb2 = b2s > 0 ? b2s : Cout;
   a.ws = (float*)ws;
   a.gn_part = (float*)gn_part;
   if (a.M == 0) return 0;
   return dispatch<true>(a, tile, ksplit, stream);
+}
+
+CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias, const void* bias2d, const void* res,
+                       int B, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl, int Ho, int Wo,
+                       int up2x, int xs, int ys, int rs, int act, float out_scale, int dil, void* gn_part, int tile,
+                       int ksplit, void* ws, hipStream_t stream) {
+  return csk_conv2d_ex(Y, X, Wp, bias, bias2d, 0, res, B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, up2x, xs, ys,
+                       rs, act, out_scale, dil, gn_part, tile, ksplit, ws, stream);
 }

@@ -36,11 +36,12 @@ struct GemmArgs {
   const bf16_t* W;  // [N][ldb] (K-contiguous rows)
   bf16_t* C;        // [M][ldc]
   const bf16_t* bias;    // [N] or null
-  const bf16_t* bias2d;  // [B][N] or null (row m uses b = m / rows_per_b)
+  const bf16_t* bias2d;  // [B][ldb2] or null (row m uses b = m / rows_per_b)
   const bf16_t* res;     // [M][ldc] or null
   const bf16_t* zero;    // >= 16 zero bytes in global memory (LDS-DMA source for padding)
   int M, N, K, lda, ldb, ldc, rows_per_b, act;  // CONV: lda = input pixel stride (>= Cin)
   int ldr;          // residual row stride
+  int ldb2;         // bias2d row stride (a column slice of one batched time-embedding GEMM)
   float out_scale;  // y = act(acc + bias + bias2d) * out_scale + residual
   float* ws;   // split-K fp32 partials [ksplit][M][N] (null: no split)
   int kchunk;  // K elements per split (multiple of BK)
@@ -51,7 +52,29 @@ struct GemmArgs {
   // (mean, M2) over the tile's BM rows; requires rows_per_batch % BM == 0, no
   // split-K, no GEGLU.  gn_part[((m0 / BM) * N + n) * 2 + {0, 1}]
   float* gn_part;
+  int gn_seg;  // rows per gn_part segment (divides BM; 0 -> BM)
+  // fused LayerNorm of the INPUT rows (SURVEY K11 folded into K9/K10): the
+  // weight was pre-multiplied by gamma (W' = W diag(gamma)), the bias holds
+  // b + W beta, and the epilogue applies
+  //   y = rstd_m * (acc - mean_m * ln_colsum[n]) + bias'
+  // with (mean_m, rstd_m) merged from the PRODUCER's row partials
+  // ln_part[(p * M + m) * 2 + {mean, M2}], p < ln_nparts, ln_pcols columns each
+  // (the last part may be short; K columns in all).  No split-K.
+  const float* ln_part;
+  const float* ln_colsum;
+  int ln_nparts, ln_pcols;
+  float ln_eps;
+  // row statistics of the OUTPUT for a consumer's fused LayerNorm:
+  // row_part[((n0 / BN) * M + m) * 2 + {mean, M2}] over the tile's columns.
+  // No split-K, no GEGLU.
+  float* row_part;
 };
+
+// epilogue LDS (bf16-element units): fp32 [BM][BN + 4] tile + [BM][2] row LN stats
+template <int BM, int BN>
+constexpr int epi_smem_elems() {
+  return BM * (BN + 4) * 2 + 4 * BM;
+}
 
 #define BK 64
 
@@ -110,9 +133,44 @@ __device__ __forceinline__ void act8(int act, float (&f)[8]) {
 #undef CSK_ACT8
 }
 
+// Fused-LayerNorm statistics (mean, rstd) of input row m0 + threadIdx.x
+// (threads < BM): merged from the producer's column-slab partials.  Called
+// BEFORE the K loop so the L2/HBM round trips overlap the operand staging
+// (in the epilogue they stalled every tile by ~2 us); the two floats ride in
+// registers to the epilogue.
+template <int BM>
+__device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
+  constexpr int MAXP = 32;
+  const int r = threadIdx.x;
+  if (!args.ln_part || r >= BM) return make_float2(0.f, 0.f);
+  const int m = min(m0 + r, args.M - 1);
+  float2 st[MAXP];
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p)
+    st[p] = p < args.ln_nparts ? *reinterpret_cast<const float2*>(args.ln_part + ((size_t)p * args.M + m) * 2)
+                               : make_float2(0.f, 0.f);
+  float sn = 0.f, sm = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const float cnt = p < args.ln_nparts ? (float)min(args.ln_pcols, args.K - p * args.ln_pcols) : 0.f;
+    sn += cnt;
+    sm += cnt * st[p].x;
+  }
+  const float mean = sm / sn;
+  float q = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const float cnt = p < args.ln_nparts ? (float)min(args.ln_pcols, args.K - p * args.ln_pcols) : 0.f;
+    const float d = st[p].x - mean;
+    q += st[p].y + cnt * d * d;
+  }
+  return make_float2(mean, rsqrtf(q / sn + args.ln_eps));
+}
+
 template <int BM, int BN, int WM, int WN, bool RAW = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
-                                              bf16_t* smem, int m0, int n0, int split) {
+                                              bf16_t* smem, int m0, int n0, int split,
+                                              float2 lnrow = make_float2(0.f, 0.f)) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int LDC_S = BN + 4;
@@ -137,7 +195,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     return;
   }
   float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC_S]
+  float* lnst = cs + BM * LDC_S;               // [BM][2]: (mean, rstd) of the input rows (fused LN)
   const int act = args.act;
+  const bool ln = args.ln_part != nullptr;
+  if (ln) {
+    if (tid < BM) *reinterpret_cast<float2*>(lnst + 2 * tid) = lnrow;
+    epi_barrier<RAW>();
+  }
+  // this lane's column sums of the folded weight, loaded once (fused LN)
+  float lncs[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) lncs[j] = ln ? args.ln_colsum[min(n0 + wn * WTN + j * 16 + fr, N - 1)] : 0.f;
+  // acc -> LayerNorm-corrected value (identity without a fused LN)
+  auto lnfix = [&](float v, int row, int j) {
+    if (!ln) return v;
+    return lnst[2 * row + 1] * (v - lnst[2 * row] * lncs[j]);
+  };
   if (act == ACT_GEGLU) {
     // packed columns: even 16-tiles = hidden, odd = gate (same output column in the same lane)
 #pragma unroll
@@ -151,7 +224,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WTM + i * 16 + fq * 4 + r;
-          cs[row * LDC_S + oc] = (acc[i][j][r] + bh) * gelu_f(acc[i][j + 1][r] + bg);
+          cs[row * LDC_S + oc] = (lnfix(acc[i][j][r], row, j) + bh) * gelu_f(lnfix(acc[i][j + 1][r], row, j + 1) + bg);
         }
       }
   } else {
@@ -160,76 +233,123 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          cs[(wm * WTM + i * 16 + fq * 4 + r) * LDC_S + wn * WTN + j * 16 + fr] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + fq * 4 + r, col = wn * WTN + j * 16 + fr;
+          cs[row * LDC_S + col] = lnfix(acc[i][j][r], row, j);
+        }
   }
   epi_barrier<RAW>();
   const int outN = act == ACT_GEGLU ? N / 2 : N;
   const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
   const int vpr = BNo / 8;
+  // BM * vpr is a multiple of 256 for every tile, so each wave runs the same
+  // number of iterations and the row-statistics shuffles below see all lanes
   for (int v = tid; v < BM * vpr; v += 256) {
     const int row = v / vpr, cv = v - row * vpr;
     const int m = m0 + row, n = on0 + cv * 8;
-    if (m >= M || n >= outN) continue;
+    const bool live = m < M && n < outN;
     float f[8];
-    const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
-    const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
-    f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
-    const bool full = n + 8 <= outN;
-    if (act != ACT_GEGLU) {
-      // bias / bias2d: one 16-byte load for a full, aligned group of 8 columns
-      // (per-element guarded loads otherwise) — keeps the epilogue branch-free
-      // in the common case, which matters for short-K GEMMs (K = 320)
-      if (args.bias) add8(f, args.bias + n, full && (N % 8 == 0), outN - n);
-      if (args.bias2d) add8(f, args.bias2d + (size_t)(m / args.rows_per_b) * N + n, full && (N % 8 == 0), outN - n);
-      act8(act, f);  // one uniform switch per 8 values, not per value
-    }
-    if (args.out_scale != 1.0f) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= args.out_scale;
-    }
-    bf16_t* cp = args.C + (size_t)m * args.ldc + n;
-    float* crow = cs + row * LDC_S + cv * 8;  // final values back into LDS for the GN statistics
-    if (full && ((((size_t)cp) & 15) == 0)) {
-      if (args.res) {
-        float rf[8];
-        unpack8(*reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n), rf);
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    if (live) {
+      const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
+      f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
+      const bool full = n + 8 <= outN;
+      if (act != ACT_GEGLU) {
+        // bias / bias2d: one 16-byte load for a full, aligned group of 8 columns
+        // (per-element guarded loads otherwise) — keeps the epilogue branch-free
+        // in the common case, which matters for short-K GEMMs (K = 320)
+        if (args.bias) add8(f, args.bias + n, full && (N % 8 == 0), outN - n);
+        if (args.bias2d) add8(f, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + n,
+                                   full && (N % 8 == 0) && (args.ldb2 % 8 == 0), outN - n);
+        act8(act, f);  // one uniform switch per 8 values, not per value
+      }
+      if (args.out_scale != 1.0f) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += rf[j];
+        for (int j = 0; j < 8; ++j) f[j] *= args.out_scale;
       }
-      *reinterpret_cast<uint4*>(cp) = pack8(f);
-      if (args.gn_part) {
-        *reinterpret_cast<float4*>(crow) = make_float4(f[0], f[1], f[2], f[3]);
-        *reinterpret_cast<float4*>(crow + 4) = make_float4(f[4], f[5], f[6], f[7]);
+      bf16_t* cp = args.C + (size_t)m * args.ldc + n;
+      float* crow = cs + row * LDC_S + cv * 8;  // final values back into LDS for the GN statistics
+      if (full && ((((size_t)cp) & 15) == 0)) {
+        if (args.res) {
+          float rf[8];
+          unpack8(*reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n), rf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] += rf[j];
+        }
+        *reinterpret_cast<uint4*>(cp) = pack8(f);
+        if (args.gn_part) {
+          *reinterpret_cast<float4*>(crow) = make_float4(f[0], f[1], f[2], f[3]);
+          *reinterpret_cast<float4*>(crow + 4) = make_float4(f[4], f[5], f[6], f[7]);
+        }
+      } else {
+        for (int j = 0; j < 8 && n + j < outN; ++j) {
+          float o = f[j];
+          if (args.res) o += bf2f(args.res[(size_t)m * args.ldr + n + j]);
+          cp[j] = f2bf(o);
+          crow[j] = o;
+          f[j] = o;
+        }
       }
-    } else {
-      for (int j = 0; j < 8 && n + j < outN; ++j) {
-        float o = f[j];
-        if (args.res) o += bf2f(args.res[(size_t)m * args.ldr + n + j]);
-        cp[j] = f2bf(o);
-        crow[j] = o;
+    }
+    if (args.row_part) {
+      // (mean, M2) of this output row over the tile's columns for a consumer
+      // GEMM's fused LayerNorm: the row's vpr chunks sit in vpr consecutive
+      // lanes, so two xor-butterflies (sum, then squared deviations) finish it
+      // in registers
+      const int nv = live ? min(8, outN - n) : 0;
+      float sm = 0.f, cnt = (float)nv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm += j < nv ? f[j] : 0.f;
+      for (int o = 1; o < vpr; o <<= 1) {
+        sm += __shfl_xor(sm, o, 64);
+        cnt += __shfl_xor(cnt, o, 64);
       }
+      const float mean = cnt > 0.f ? sm / cnt : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = j < nv ? f[j] - mean : 0.f;
+        q += d * d;
+      }
+      for (int o = 1; o < vpr; o <<= 1) q += __shfl_xor(q, o, 64);
+      if (cv == 0 && m < M)
+        *reinterpret_cast<float2*>(args.row_part + ((size_t)(n0 / BN) * M + m) * 2) = make_float2(mean, q);
     }
   }
   if (args.gn_part) {
-    // column pass: (mean, M2) of each output channel over this tile's rows
-    // (two-pass in LDS: exact, no E[x^2]-E[x]^2 cancellation)
+    // column pass: (mean, M2) of each output channel over row segments of
+    // gn_seg rows (a divisor of BM chosen by the host, _gn_seg): thread =
+    // (segment, channel) with consecutive channels in consecutive lanes
+    // (conflict-free LDS reads); two-pass in LDS: exact, no E[x^2]-E[x]^2
+    // cancellation.  The consumer GroupNorm merges the segments.
+    const int seg = args.gn_seg > 0 ? args.gn_seg : BM;
     epi_barrier<RAW>();
-    const int rows = min(BM, M - m0);
-    for (int c = tid; c < BN; c += 256) {
-      const int n = n0 + c;
-      if (n >= N || rows <= 0) continue;
+    for (int t = tid; t < BN * (BM / seg); t += 256) {
+      const int c = t % BN, sq = t / BN;
+      const int n = n0 + c, r0 = sq * seg;
+      if (n >= N || m0 + r0 >= M) continue;
       float sm = 0.f;
-      for (int r = 0; r < rows; ++r) sm += cs[r * LDC_S + c];
-      const float mean = sm / (float)rows;
+#pragma unroll 8
+      for (int r = 0; r < seg; ++r) sm += cs[(r0 + r) * LDC_S + c];
+      const float mean = sm / (float)seg;
       float m2 = 0.f;
-      for (int r = 0; r < rows; ++r) { const float d = cs[r * LDC_S + c] - mean; m2 += d * d; }
-      float* o = args.gn_part + ((size_t)(m0 / BM) * N + n) * 2;
-      o[0] = mean;
-      o[1] = m2;
+#pragma unroll 8
+      for (int r = 0; r < seg; ++r) { const float d = cs[(r0 + r) * LDC_S + c] - mean; m2 += d * d; }
+      *reinterpret_cast<float2*>(args.gn_part + ((size_t)((m0 + r0) / seg) * N + n) * 2) = make_float2(mean, m2);
     }
   }
+}
+
+// GN statistics granularity: 1 = fine segments (BM*BN/256 rows, every thread of
+// the column pass busy), 0 = one segment per BM-row tile.  The host mirrors it
+// (hip_ops._gn_seg).
+extern int g_gn_fine;
+template <int BM, int BN>
+__host__ __forceinline__ int gn_seg_for() {
+  return g_gn_fine ? BM * BN / 256 : BM;
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);

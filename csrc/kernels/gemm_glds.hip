@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
   constexpr int LPG = IA + IB;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SMEM_MAIN = S * STAGE;
-  constexpr int SMEM_EPI = BM * (BN + 4) * 2;
+  constexpr int SMEM_EPI = epi_smem_elems<BM, BN>();
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
 
@@ -196,6 +196,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s, s);
+  const float2 lnrow = ln_row_stats<BM>(args, m0);  // fused-LN row stats while the first stages land
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
     }
   }
   __syncthreads();
-  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split);
+  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split, lnrow);
 }
 
 // ---------------------------------------------------------------------------
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
   constexpr int LPG = IA + IB;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SMEM_MAIN = S * STAGE;
-  constexpr int SMEM_EPI = BM * (BN + 4) * 2;
+  constexpr int SMEM_EPI = epi_smem_elems<BM, BN>();
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM_MAIN + SMEM_EPI];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -418,7 +419,9 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
 static int g_num_cus = 0;
 
 template <int BM, int BN, int WM, int WN, int S>
-static int launch_persist(const GemmArgs& a, bool conv, hipStream_t s) {
+static int launch_persist(const GemmArgs& a0, bool conv, hipStream_t s) {
+  GemmArgs a = a0;
+  a.gn_seg = gn_seg_for<BM, BN>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (!g_num_cus) {
     int dev = 0;
@@ -426,7 +429,7 @@ static int launch_persist(const GemmArgs& a, bool conv, hipStream_t s) {
         hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       g_num_cus = 256;
   }
-  constexpr int LDS = (S * (BM + BN) * BK + BM * (BN + 4) * 2) * 2;
+  constexpr int LDS = (S * (BM + BN) * BK + epi_smem_elems<BM, BN>()) * 2;
   const int per_cu = LDS <= 80 * 1024 ? 2 : 1;
   int grid = g_num_cus * per_cu;
   if (grid > tiles) grid = tiles;
@@ -438,7 +441,9 @@ static int launch_persist(const GemmArgs& a, bool conv, hipStream_t s) {
 }
 
 template <int BM, int BN, int WM, int WN, int S>
-static int launch_glds(const GemmArgs& a, int ksplit, bool conv, hipStream_t s) {
+static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
+  GemmArgs a = a0;
+  a.gn_seg = gn_seg_for<BM, BN>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   // FAST staging: K-steps never straddle a tap / the K tail, and every running
   // offset stays inside the zero page
@@ -471,12 +476,13 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   if (!g_zero) return (int)hipErrorNotInitialized;
   GemmArgs a = a0;
   a.zero = g_zero;
-  if (a.act == ACT_GEGLU && !(tile == 11 || tile == 13 || tile == 15)) tile = 11;
+  // GEGLU pairs 16-column (hidden, gate) tiles inside one wave's columns: every
+  // tile below has a per-wave width (BN / WN) that is a multiple of 32
   if (tile >= 21) {  // persistent continuous-ring variants: FAST staging, no split-K
     const bool fast = (conv ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
                       (size_t)(a.K + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
                       (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
-    if (!fast || ksplit > 1 || a.act == ACT_GEGLU) tile = 11;  // fall back to the tiled kernel
+    if (!fast || ksplit > 1) tile = 11;  // fall back to the tiled kernel
   }
   switch (tile) {
     case 21: return launch_persist<128, 128, 2, 2, 2>(a, conv, s);

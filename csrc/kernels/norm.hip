@@ -15,6 +15,14 @@
 #define GN_THREADS 256
 #define GN_MAXC 4096
 
+// Largest number of statistics partials per sample that every apply workgroup
+// merges itself in a prologue; above it a finalize kernel merges them once.
+static int g_gn_prologue_max = 1024;
+CSK_API int csk_set_gn_prologue_max(int n) {
+  g_gn_prologue_max = n;
+  return 0;
+}
+
 // Thread layout shared by the stats and apply kernels: thread = (cv, r); cv is
 // the 8-channel vector column the thread owns for the whole chunk (so its
 // per-channel constants live in registers), r its pixel row; R = 256 / NVT rows
@@ -307,7 +315,10 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* part, int se
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0 || seg_rows <= 0 || P % seg_rows != 0) return (int)hipErrorInvalidValue;
   float* st = (float*)stat;
   const int nseg = P / seg_rows;
-  if (G <= 64 && nseg * (C / G) <= 512) {  // few entries per group: merge in the apply prologue
+  // every apply workgroup re-reads ALL of its sample's partials in a prologue
+  // merge; past ~1K entries that L2 traffic (1024 workgroups x nseg*C*8 bytes)
+  // costs more than a finalize launch (measured: 24 vs ~12 us at 64x64x320 B8)
+  if (G <= 64 && nseg * C <= g_gn_prologue_max) {
     gn_apply_kernel<2><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>(
         (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G, chunk,
         silu, affine_bstride, nseg, seg_rows, eps);
@@ -330,7 +341,7 @@ CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
   gn_stats_kernel<<<grid, GN_THREADS, gn_stats_lds(C), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
-  if (G <= 64 && nchunk <= 512) {  // merge the chunk partials in the apply prologue (no finalize launch)
+  if (G <= 64 && nchunk * G <= g_gn_prologue_max) {  // few partials: merge them in the apply prologue (no finalize launch)
     gn_apply_kernel<1><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, pt, (const bf16_t*)gamma,
                                                         (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride,
                                                         nchunk, 0, eps);

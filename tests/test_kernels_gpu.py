@@ -73,6 +73,24 @@ def test_gemm_strided_a_and_geglu(gpu):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [1, 3, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 23, 24])
+def test_geglu_every_tile(gpu, tile):
+    """GEGLU pairs (hidden, gate) 16-column tiles inside each wave's columns: every
+    tile (incl. the persistent ones) must produce the same gated output."""
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, K, F_ = 333, 320, 640
+    a = rnd(M, K, dev=gpu)
+    w, b = rnd(2 * F_, K, dev=gpu, scale=K ** -0.5), rnd(2 * F_, dev=gpu)
+    wp, bp = ops.pack_geglu(w, b)
+    y = torch.empty(M, F_, dtype=torch.bfloat16, device=gpu)
+    _lib.call("csk_gemm", _p(y), _p(a), _p(wp), _p(bp), None, None, M, 2 * F_, K, K, K, F_, F_, 1, 3, 1.0, None,
+              tile, 1, None, _s())
+    h, g = (a.float() @ w.float().t() + b.float()).chunk(2, dim=-1)
+    assert rel_err(y, h * F.gelu(g)) < 1e-2
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,pad,up", [
     (2, 16, 16, 320, 320, 3, 1, 1, False), (2, 16, 16, 64, 128, 3, 2, 1, False), (1, 8, 8, 128, 64, 3, 1, 1, True),
     (2, 9, 7, 32, 32, 3, 1, 1, False), (1, 16, 16, 4, 320, 3, 1, 1, False), (1, 16, 16, 320, 4, 3, 1, 1, False),
@@ -295,3 +313,47 @@ def test_canny_matches_numpy(gpu, size):
     got = hip_ops.canny(torch.from_numpy(img).to(gpu), 100.0, 200.0).cpu().numpy()
     # direction quantisation at exact 22.5-degree boundaries may differ (f32 atan2 vs f64)
     assert (got != ref).mean() < 2e-3
+
+
+def test_timestep_embedding_kernel(gpu):
+    from chiaswarm_amd.models.layers import timestep_embedding
+
+    for t in (torch.tensor([999.0], device=gpu), torch.tensor([0.0, 1.5, 500.25, 981.0], device=gpu)):
+        y = hip_ops.timestep_embedding(t, 4, 320)
+        ref = timestep_embedding(t.expand(4) if t.numel() == 1 else t, 320)
+        assert y.shape == (4, 320) and y.dtype == torch.bfloat16
+        assert (y.float() - ref).abs().max().item() < 1e-2
+
+
+def test_conv_bias2d_row_stride(gpu):
+    """A column slice of the batched time-embedding GEMM as per-sample conv bias (no copy)."""
+    B, H, W, Cin, Cout = 2, 8, 8, 64, 96
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    big = rnd(B, 3 * Cout, dev=gpu)
+    b2 = big[:, Cout:2 * Cout]
+    y = hip_ops.conv2d(x, wp, None, 1, 1, None, False, b2)
+    ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), None, 1, 1, None, False, b2.float().cpu())
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,act", [(960, None), (320, None), (2 * 1280, "geglu")])
+def test_layer_norm_fused_into_gemm(gpu, N, act):
+    """Producer GEMM emits per-row statistics; the consumer GEMM applies the
+    LayerNorm in its epilogue with gamma/beta folded into its weights."""
+    from types import SimpleNamespace
+
+    M, C, Kp = 1000, 320, 640
+    a = rnd(M, Kp, dev=gpu)
+    wp_, res = rnd(C, Kp, dev=gpu, scale=Kp ** -0.5), rnd(M, C, dev=gpu, scale=3.0) + 1.5
+    x = ops.gemm(a, wp_, None, residual=res, row_stats=True)  # residual stream with an offset
+    assert getattr(x, "_csk_rows", None) is not None
+    norm = SimpleNamespace(weight=rnd(C, dev=gpu) + 1.0, bias=rnd(C, dev=gpu), eps=1e-5)
+    w, b = rnd(N, C, dev=gpu, scale=C ** -0.5), rnd(N, dev=gpu)
+    if act == "geglu":
+        w, b = ops.pack_geglu(w, b)
+    y = ops.layer_norm_gemm(x, norm, w, b, ops.fold_layer_norm(w, b, norm.weight, norm.bias), act=act)
+    xn = F.layer_norm(x.float(), (C,), norm.weight.float(), norm.bias.float(), 1e-5)
+    ref = ops._ref_gemm(xn.cpu(), w.float().cpu(), b.float().cpu(), None, act)
+    assert y.shape == ref.shape
+    assert rel_err(y.cpu(), ref) < 1.5e-2

@@ -77,3 +77,34 @@ def test_bad_content_type():
         op.image_to_buffer(img(), "image/gif")
     with pytest.raises(ValueError):
         op.image_to_buffer(img(), "video/mp4")
+
+
+def test_deferred_encoding_in_encoder_processes_matches_inline():
+    """GPU worker mode: artifacts come back as Futures from spawned encoder
+    processes and resolve to exactly the inline envelope."""
+    import numpy as np
+
+    from chiaswarm_amd.output.encoder import EncoderPool
+
+    rng = np.random.default_rng(0)
+    ims = [Image.fromarray(rng.integers(0, 255, (64, 64, 3), dtype=np.uint8)) for _ in range(3)]
+    p = op.OutputProcessor(["primary"], "image/jpeg")
+    p.add_outputs(ims)
+    inline = p.get_results()
+    pool = EncoderPool(1)
+    assert pool.kind == "process"
+    op.set_encoder_pool(pool)
+    try:
+        p2 = op.OutputProcessor(["primary"], "image/jpeg")
+        p2.add_outputs(ims)
+        res = p2.get_results()
+        assert hasattr(res["primary"], "result")  # deferred
+        out = op.resolve_artifacts({"artifacts": res})["artifacts"]
+        assert out == inline
+        with pytest.raises(ValueError):  # >9 images: still raised in-line (fatal class)
+            p3 = op.OutputProcessor(["primary"], "image/jpeg")
+            p3.add_outputs(ims * 4)
+            p3.get_results()
+    finally:
+        op.set_encoder_pool(None)
+        pool.shutdown()

@@ -1,0 +1,70 @@
+#!/usr/bin/env python
+"""A/B the hipGraph-replayed SD2.1 UNet step (CFG batch 8, 64x64 latents) over
+runtime kernel knobs, each arm captured in its own graph, arms interleaved:
+
+    python tools/abstep.py --arms gn0,gn1024,gnmax --rounds 5
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from chiaswarm_amd import ops  # noqa: E402
+from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
+
+
+def apply_arm(arm):
+    if arm in ("gnfine", "gntile"):
+        hip_ops.set_gn_fine(arm == "gnfine")
+    elif arm.startswith("gn"):
+        v = arm[2:]
+        _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("attn"):
+        hip_ops.ATTN_VARIANT = int(arm[4:])
+    elif arm in ("lnoff", "lnon"):
+        ops.LN_FUSE = arm == "lnon"
+    elif arm != "base":
+        raise SystemExit(f"unknown arm {arm}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arms", default="base")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
+
+    ops._lib.load()
+    dev = torch.device("cuda", 0)
+    p = StableDiffusion("sd21", device=dev, seed=0)
+    x = torch.randn(8, 64, 64, 4, device=dev).bfloat16()
+    ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
+    kv = p.unet.encode_context(ctx)
+    graphs = {}
+    for arm in a.arms.split(","):
+        apply_arm(arm)
+        graphs[arm] = _UNetGraph(p.unet, x, kv, None, None)
+    res = {arm: [] for arm in graphs}
+    for _ in range(a.rounds):
+        for arm, g in graphs.items():
+            g.run(x, 500.0, kv, None, None)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                g.graph.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            res[arm].append(e0.elapsed_time(e1) / a.iters)
+    for arm, ts in res.items():
+        print(f"{arm:10s} median {statistics.median(ts):7.3f} ms  min {min(ts):7.3f}  all {[round(t, 3) for t in ts]}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
