@@ -1,0 +1,747 @@
+"""Neural ControlNet annotators (reference: swarm/controlnet/input_processor.py:17-115,
+which calls controlnet_aux / transformers detectors):
+
+  scribble  -> HED (ControlNetHED_Apache2) + scribble post-process (nms, blur, threshold)
+  softedge  -> HED soft edge map (the reference's PiDiNet is a drop-in alternative
+               checkpoint for the same control type)
+  lineart   -> "informative drawings" generator (sk_model / sk_model2 coarse)
+  mlsd      -> M-LSD large (MobileNetV2 encoder + line-segment decoder)
+  depth     -> DPT-Large (ViT-L/16 + reassemble/fusion neck + depth head)
+  seg       -> UperNet + ConvNeXt backbone, ADE20K palette
+
+Module and parameter names follow the public checkpoints (controlnet_aux .pth
+files / transformers safetensors) so real weights load unchanged from
+``$CSK_ANNOTATOR_DIR`` (default ``<settings dir>/annotators``); loaders never
+unpickle (safetensors, or ``torch.load(weights_only=True)``).  Without weights
+a detector keeps a seeded random init (like every model in this framework
+offline) and says so in the log.
+
+Each detector is built once per process, kept resident on the GPU (bf16 there,
+fp32 on CPU) and runs as plain PyTorch modules: these run once per job on one
+image, far off the denoising hot path.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from PIL import Image
+
+_CACHE: dict = {}
+_FILES = {
+    "hed": ["ControlNetHED.pth", "hed.safetensors"],
+    "lineart": ["sk_model.pth", "lineart.safetensors"],
+    "lineart_coarse": ["sk_model2.pth", "lineart_coarse.safetensors"],
+    "mlsd": ["mlsd_large_512_fp32.pth", "mlsd.safetensors"],
+    "depth": ["dpt-large.safetensors", "dpt-large/model.safetensors"],
+    "seg": ["upernet-convnext-small.safetensors", "upernet-convnext-small/model.safetensors"],
+}
+
+
+def annotator_dir() -> str:
+    d = os.environ.get("CSK_ANNOTATOR_DIR")
+    if d:
+        return d
+    from ..settings import get_settings_dir
+
+    return os.path.join(get_settings_dir(), "annotators")
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def load_checkpoint(path: str) -> dict:
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+
+        return load_file(path, device="cpu")
+    sd = torch.load(path, map_location="cpu", weights_only=True)  # never unpickles code
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+
+
+def _build(name: str, ctor):
+    """Resident detector ``name``: constructed, weights loaded if present, on device."""
+    m = _CACHE.get(name)
+    if m is not None:
+        return m
+    torch.manual_seed(1234)
+    m = ctor().eval().requires_grad_(False)
+    src = "random-init"
+    for f in _FILES.get(name, []):
+        p = os.path.join(annotator_dir(), f)
+        if os.path.exists(p):
+            sd = load_checkpoint(p)
+            missing, unexpected = m.load_state_dict(sd, strict=False)
+            if len(missing) < len(m.state_dict()) // 2:
+                src = p
+            break
+    if src == "random-init":
+        logging.warning(f"annotator '{name}': no weights in {annotator_dir()} -> random init")
+    dev = _device()
+    m = m.to(dev, torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    m.weights_source = src
+    _CACHE[name] = m
+    return m
+
+
+def _to_tensor(img: np.ndarray, m: nn.Module) -> torch.Tensor:
+    p = next(m.parameters())
+    return torch.from_numpy(np.ascontiguousarray(img)).to(p.device).permute(2, 0, 1)[None].to(p.dtype)
+
+
+def _hwc3(a: np.ndarray) -> np.ndarray:
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.shape[2] == 1:
+        a = np.concatenate([a] * 3, axis=2)
+    return a
+
+
+def _resize_short(img: Image.Image, res: int, mult: int = 64) -> Image.Image:
+    """controlnet_aux resize_image: short side -> res, both sides multiples of 64."""
+    w, h = img.size
+    k = float(res) / min(h, w)
+    return img.resize((int(round(w * k / mult)) * mult, int(round(h * k / mult)) * mult), Image.Resampling.LANCZOS)
+
+
+# ---------------------------------------------------------------------------
+# HED (ControlNetHED_Apache2)
+# ---------------------------------------------------------------------------
+class DoubleConvBlock(nn.Module):
+    def __init__(self, cin, cout, n):
+        super().__init__()
+        self.convs = nn.ModuleList([nn.Conv2d(cin if i == 0 else cout, cout, 3, padding=1) for i in range(n)])
+        self.projection = nn.Conv2d(cout, 1, 1)
+
+    def forward(self, x, down_sampling=False):
+        h = F.max_pool2d(x, 2, 2) if down_sampling else x
+        for c in self.convs:
+            h = F.relu(c(h))
+        return h, self.projection(h)
+
+
+class ControlNetHED(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.norm = nn.Parameter(torch.zeros(1, 3, 1, 1))
+        self.block1 = DoubleConvBlock(3, 64, 2)
+        self.block2 = DoubleConvBlock(64, 128, 2)
+        self.block3 = DoubleConvBlock(128, 256, 3)
+        self.block4 = DoubleConvBlock(256, 512, 3)
+        self.block5 = DoubleConvBlock(512, 512, 3)
+
+    def forward(self, x):
+        h = x - self.norm
+        outs = []
+        for i, b in enumerate([self.block1, self.block2, self.block3, self.block4, self.block5]):
+            h, p = b(h, down_sampling=i > 0)
+            outs.append(p)
+        return outs
+
+
+def _nms(x: np.ndarray, t: float, s: float) -> np.ndarray:
+    """controlnet_aux nms: directional line maxima of a blurred edge map."""
+    from scipy import ndimage
+
+    x = ndimage.gaussian_filter(x.astype(np.float32), sigma=s)
+    f1 = np.array([[0, 0, 0], [1, 1, 1], [0, 0, 0]], dtype=bool)
+    f2 = np.array([[0, 1, 0], [0, 1, 0], [0, 1, 0]], dtype=bool)
+    f3 = np.eye(3, dtype=bool)
+    f4 = np.fliplr(np.eye(3, dtype=bool))
+    y = np.zeros_like(x)
+    for f in (f1, f2, f3, f4):
+        np.putmask(y, ndimage.grey_dilation(x, footprint=f) == x, x)
+    z = np.zeros_like(y, dtype=np.uint8)
+    z[y > t] = 255
+    return z
+
+
+@torch.no_grad()
+def hed(image: Image.Image, scribble=False, res=512) -> Image.Image:
+    from scipy import ndimage
+
+    m = _build("hed", ControlNetHED)
+    img = np.asarray(_resize_short(image.convert("RGB"), res)).astype(np.float32)
+    H, W = img.shape[:2]
+    edges = m(_to_tensor(img, m))
+    edges = [F.interpolate(e.float(), size=(H, W), mode="bilinear", align_corners=False)[0, 0] for e in edges]
+    edge = torch.sigmoid(torch.stack(edges, 0).mean(0)).cpu().numpy()
+    out = (edge * 255.0).clip(0, 255).astype(np.uint8)
+    if scribble:
+        out = _nms(out, 127, 3.0)
+        out = ndimage.gaussian_filter(out.astype(np.float32), sigma=3.0)
+        out = np.where(out > 4, 255, 0).astype(np.uint8)
+    return Image.fromarray(_hwc3(out)).resize(image.size, Image.Resampling.BILINEAR)
+
+
+# ---------------------------------------------------------------------------
+# Lineart ("informative drawings" generator)
+# ---------------------------------------------------------------------------
+class ResidualBlock(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv_block = nn.Sequential(nn.ReflectionPad2d(1), nn.Conv2d(c, c, 3), nn.InstanceNorm2d(c), nn.ReLU(True),
+                                        nn.ReflectionPad2d(1), nn.Conv2d(c, c, 3), nn.InstanceNorm2d(c))
+
+    def forward(self, x):
+        return x + self.conv_block(x)
+
+
+class LineartGenerator(nn.Module):
+    def __init__(self, input_nc=3, output_nc=1, n_residual_blocks=3):
+        super().__init__()
+        self.model0 = nn.Sequential(nn.ReflectionPad2d(3), nn.Conv2d(input_nc, 64, 7), nn.InstanceNorm2d(64),
+                                    nn.ReLU(True))
+        down, c = [], 64
+        for _ in range(2):
+            down += [nn.Conv2d(c, c * 2, 3, stride=2, padding=1), nn.InstanceNorm2d(c * 2), nn.ReLU(True)]
+            c *= 2
+        self.model1 = nn.Sequential(*down)
+        self.model2 = nn.Sequential(*[ResidualBlock(c) for _ in range(n_residual_blocks)])
+        up = []
+        for _ in range(2):
+            up += [nn.ConvTranspose2d(c, c // 2, 3, stride=2, padding=1, output_padding=1), nn.InstanceNorm2d(c // 2),
+                   nn.ReLU(True)]
+            c //= 2
+        self.model3 = nn.Sequential(*up)
+        self.model4 = nn.Sequential(nn.ReflectionPad2d(3), nn.Conv2d(64, output_nc, 7), nn.Sigmoid())
+
+    def forward(self, x):
+        return self.model4(self.model3(self.model2(self.model1(self.model0(x)))))
+
+
+@torch.no_grad()
+def lineart(image: Image.Image, coarse=False, res=512) -> Image.Image:
+    m = _build("lineart_coarse" if coarse else "lineart", LineartGenerator)
+    img = np.asarray(_resize_short(image.convert("RGB"), res)).astype(np.float32) / 255.0
+    line = m(_to_tensor(img, m))[0, 0].float().cpu().numpy()
+    line = (line * 255.0).clip(0, 255).astype(np.uint8)
+    out = Image.fromarray(_hwc3(line)).resize(image.size, Image.Resampling.BILINEAR)
+    return Image.fromarray(255 - np.asarray(out))  # white lines on black, as ControlNet-lineart expects
+
+
+# ---------------------------------------------------------------------------
+# M-LSD (MobileV2_MLSD_Large) line segments
+# ---------------------------------------------------------------------------
+def _make_divisible(v, divisor=8):
+    new_v = max(divisor, int(v + divisor / 2) // divisor * divisor)
+    return new_v + divisor if new_v < 0.9 * v else new_v
+
+
+class ConvBNReLU(nn.Sequential):
+    """TFLite-style padding: stride-2 convs pad (0, 1, 0, 1) and use padding 0."""
+
+    def __init__(self, cin, cout, kernel_size=3, stride=1, groups=1):
+        pad = 0 if stride == 2 else (kernel_size - 1) // 2
+        super().__init__(nn.Conv2d(cin, cout, kernel_size, stride, pad, groups=groups, bias=False),
+                         nn.BatchNorm2d(cout), nn.ReLU6(inplace=True))
+        self.stride = stride
+
+    def forward(self, x):
+        if self.stride == 2:
+            x = F.pad(x, (0, 1, 0, 1))
+        for mod in self:
+            x = mod(x)
+        return x
+
+
+class InvertedResidual(nn.Module):
+    def __init__(self, inp, oup, stride, expand_ratio):
+        super().__init__()
+        hidden = int(round(inp * expand_ratio))
+        self.use_res_connect = stride == 1 and inp == oup
+        layers = [ConvBNReLU(inp, hidden, kernel_size=1)] if expand_ratio != 1 else []
+        layers += [ConvBNReLU(hidden, hidden, stride=stride, groups=hidden), nn.Conv2d(hidden, oup, 1, 1, 0, bias=False),
+                   nn.BatchNorm2d(oup)]
+        self.conv = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return x + self.conv(x) if self.use_res_connect else self.conv(x)
+
+
+class MobileNetV2Trunk(nn.Module):
+    """MobileNetV2 up to the 96-channel stage; 4 input channels (RGB + ones)."""
+
+    def __init__(self):
+        super().__init__()
+        cin = _make_divisible(32)
+        feats = [ConvBNReLU(4, cin, stride=2)]
+        for t, c, n, s in [[1, 16, 1, 1], [6, 24, 2, 2], [6, 32, 3, 2], [6, 64, 4, 2], [6, 96, 3, 1]]:
+            cout = _make_divisible(c)
+            for i in range(n):
+                feats.append(InvertedResidual(cin, cout, s if i == 0 else 1, t))
+                cin = cout
+        self.features = nn.Sequential(*feats)
+        self.fpn_selected = [1, 3, 6, 10, 13]
+
+    def forward(self, x):
+        outs = []
+        for i, f in enumerate(self.features):
+            if i > self.fpn_selected[-1]:
+                break
+            x = f(x)
+            if i in self.fpn_selected:
+                outs.append(x)
+        return outs
+
+
+def _cbr(cin, cout, k=1, pad=0, dil=1, relu=True):
+    return nn.Sequential(nn.Conv2d(cin, cout, k, padding=pad, dilation=dil), nn.BatchNorm2d(cout),
+                         nn.ReLU(inplace=True) if relu else nn.Identity())
+
+
+class BlockTypeA(nn.Module):
+    def __init__(self, in_c1, in_c2, out_c1, out_c2, upscale=True):
+        super().__init__()
+        self.conv1 = _cbr(in_c2, out_c2)
+        self.conv2 = _cbr(in_c1, out_c1)
+        self.upscale = upscale
+
+    def forward(self, a, b):
+        b = self.conv1(b)
+        a = self.conv2(a)
+        if self.upscale:
+            b = F.interpolate(b, scale_factor=2.0, mode="bilinear", align_corners=True)
+        return torch.cat((a, b), dim=1)
+
+
+class BlockTypeB(nn.Module):
+    def __init__(self, in_c, out_c):
+        super().__init__()
+        self.conv1 = _cbr(in_c, in_c, 3, 1)
+        self.conv2 = _cbr(in_c, out_c, 3, 1)
+
+    def forward(self, x):
+        return self.conv2(self.conv1(x) + x)
+
+
+class BlockTypeC(nn.Module):
+    def __init__(self, in_c, out_c):
+        super().__init__()
+        self.conv1 = _cbr(in_c, in_c, 3, 5, 5)
+        self.conv2 = _cbr(in_c, in_c, 3, 1)
+        self.conv3 = nn.Conv2d(in_c, out_c, 1)
+
+    def forward(self, x):
+        return self.conv3(self.conv2(self.conv1(x)))
+
+
+class MLSDLarge(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.backbone = MobileNetV2Trunk()
+        self.block15 = BlockTypeA(64, 96, 64, 64, upscale=False)
+        self.block16 = BlockTypeB(128, 64)
+        self.block17 = BlockTypeA(32, 64, 64, 64)
+        self.block18 = BlockTypeB(128, 64)
+        self.block19 = BlockTypeA(24, 64, 64, 64)
+        self.block20 = BlockTypeB(128, 64)
+        self.block21 = BlockTypeA(16, 64, 64, 64)
+        self.block22 = BlockTypeB(128, 64)
+        self.block23 = BlockTypeC(64, 16)
+
+    def forward(self, x):
+        c1, c2, c3, c4, c5 = self.backbone(x)
+        x = self.block16(self.block15(c4, c5))
+        x = self.block18(self.block17(c3, x))
+        x = self.block20(self.block19(c2, x))
+        x = self.block22(self.block21(c1, x))
+        return self.block23(x)[:, 7:]
+
+
+def _draw_line(img: np.ndarray, p0, p1):
+    n = int(max(abs(p1[0] - p0[0]), abs(p1[1] - p0[1]))) + 1
+    xs = np.rint(np.linspace(p0[0], p1[0], n)).astype(int)
+    ys = np.rint(np.linspace(p0[1], p1[1], n)).astype(int)
+    ok = (xs >= 0) & (xs < img.shape[1]) & (ys >= 0) & (ys < img.shape[0])
+    img[ys[ok], xs[ok]] = 255
+
+
+@torch.no_grad()
+def mlsd(image: Image.Image, thr_v=0.1, thr_d=0.1, res=512, topk=200, ksize=3) -> Image.Image:
+    m = _build("mlsd", MLSDLarge)
+    img = np.asarray(_resize_short(image.convert("RGB"), res)).astype(np.float32)
+    H, W = img.shape[:2]
+    x = np.concatenate([img, np.ones((H, W, 1), np.float32)], -1) / 127.5 - 1.0
+    tp = m(_to_tensor(x, m)).float()
+    disp = tp[0, 1:5]
+    heat = torch.sigmoid(tp[:, 0])
+    hmax = F.max_pool2d(heat, ksize, stride=1, padding=(ksize - 1) // 2)
+    heat = (heat * (hmax == heat).float()).reshape(-1)
+    scores, idx = torch.topk(heat, min(topk, heat.numel()))
+    h, w = tp.shape[2], tp.shape[3]
+    yy, xx = (idx // w).cpu().numpy(), (idx % w).cpu().numpy()
+    scores, disp = scores.cpu().numpy(), disp.permute(1, 2, 0).cpu().numpy()
+    dist = np.sqrt(((disp[..., :2] - disp[..., 2:]) ** 2).sum(-1))
+    out = np.zeros((H, W), np.uint8)
+    for y, x_, sc in zip(yy, xx, scores):
+        if sc > thr_v and dist[y, x_] > thr_d:
+            dx0, dy0, dx1, dy1 = disp[y, x_]
+            # the map is at half resolution: x2 back to the detect resolution
+            _draw_line(out, (2 * (x_ + dx0), 2 * (y + dy0)), (2 * (x_ + dx1), 2 * (y + dy1)))
+    return Image.fromarray(_hwc3(out)).resize(image.size, Image.Resampling.NEAREST)
+
+
+# ---------------------------------------------------------------------------
+# DPT-Large depth (transformers DPTForDepthEstimation, Intel/dpt-large)
+# ---------------------------------------------------------------------------
+class _Lin(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.dense = nn.Linear(cin, cout)
+
+
+class _ViTSelfAttn(nn.Module):
+    def __init__(self, c, heads):
+        super().__init__()
+        self.query, self.key, self.value = nn.Linear(c, c), nn.Linear(c, c), nn.Linear(c, c)
+        self.heads = heads
+
+    def forward(self, x):
+        b, s, c = x.shape
+        q, k, v = (t(x).view(b, s, self.heads, -1).transpose(1, 2) for t in (self.query, self.key, self.value))
+        return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, s, c)
+
+
+class _ViTAttention(nn.Module):
+    def __init__(self, c, heads):
+        super().__init__()
+        self.attention = _ViTSelfAttn(c, heads)
+        self.output = _Lin(c, c)
+
+
+class _ViTLayer(nn.Module):
+    def __init__(self, c, heads, mlp):
+        super().__init__()
+        self.attention = _ViTAttention(c, heads)
+        self.intermediate = _Lin(c, mlp)
+        self.output = _Lin(mlp, c)
+        self.layernorm_before = nn.LayerNorm(c, eps=1e-12)
+        self.layernorm_after = nn.LayerNorm(c, eps=1e-12)
+
+    def forward(self, x):
+        x = x + self.attention.output.dense(self.attention.attention(self.layernorm_before(x)))
+        return x + self.output.dense(F.gelu(self.intermediate.dense(self.layernorm_after(x))))
+
+
+class _PatchEmb(nn.Module):
+    def __init__(self, c, patch):
+        super().__init__()
+        self.projection = nn.Conv2d(3, c, patch, stride=patch)
+
+
+class _DPTEmbeddings(nn.Module):
+    def __init__(self, c, patch, image):
+        super().__init__()
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, c))
+        self.position_embeddings = nn.Parameter(torch.randn(1, (image // patch) ** 2 + 1, c) * 0.02)
+        self.patch_embeddings = _PatchEmb(c, patch)
+        self.patch = patch
+
+    def forward(self, x):
+        b, _, h, w = x.shape
+        t = self.patch_embeddings.projection(x).flatten(2).transpose(1, 2)
+        pos = self.position_embeddings
+        n0 = int(math.sqrt(pos.shape[1] - 1))
+        gh, gw = h // self.patch, w // self.patch
+        if (gh, gw) != (n0, n0):  # bilinear resize of the grid (DPT _resize_pos_embed)
+            grid = pos[:, 1:].reshape(1, n0, n0, -1).permute(0, 3, 1, 2).float()
+            grid = F.interpolate(grid, size=(gh, gw), mode="bilinear").to(pos.dtype)
+            pos = torch.cat([pos[:, :1], grid.permute(0, 2, 3, 1).reshape(1, gh * gw, -1)], 1)
+        return torch.cat([self.cls_token.expand(b, -1, -1), t], 1) + pos
+
+
+class _DPTEncoder(nn.Module):
+    def __init__(self, c, heads, mlp, n):
+        super().__init__()
+        self.layer = nn.ModuleList([_ViTLayer(c, heads, mlp) for _ in range(n)])
+
+
+class _DPTViT(nn.Module):
+    def __init__(self, c=1024, heads=16, mlp=4096, n=24, patch=16, image=384):
+        super().__init__()
+        self.embeddings = _DPTEmbeddings(c, patch, image)
+        self.encoder = _DPTEncoder(c, heads, mlp, n)
+
+
+class _Reassemble(nn.Module):
+    def __init__(self, c, out, factor):
+        super().__init__()
+        self.projection = nn.Conv2d(c, out, 1)
+        if factor > 1:
+            self.resize = nn.ConvTranspose2d(out, out, factor, stride=factor)
+        elif factor == 1:
+            self.resize = nn.Identity()
+        else:
+            self.resize = nn.Conv2d(out, out, 3, stride=int(1 / factor), padding=1)
+
+    def forward(self, x):
+        return self.resize(self.projection(x))
+
+
+class _ReassembleStage(nn.Module):
+    def __init__(self, c, sizes, factors):
+        super().__init__()
+        self.layers = nn.ModuleList([_Reassemble(c, s, f) for s, f in zip(sizes, factors)])
+        self.readout_projects = nn.ModuleList([nn.Sequential(nn.Linear(2 * c, c), nn.GELU()) for _ in sizes])
+
+    def forward(self, hs, gh, gw):
+        out = []
+        for i, h in enumerate(hs):
+            cls, tok = h[:, :1], h[:, 1:]
+            tok = self.readout_projects[i](torch.cat([tok, cls.expand_as(tok)], -1))
+            tok = tok.transpose(1, 2).reshape(h.shape[0], -1, gh, gw)
+            out.append(self.layers[i](tok))
+        return out
+
+
+class _PreActRes(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.convolution1 = nn.Conv2d(c, c, 3, padding=1)
+        self.convolution2 = nn.Conv2d(c, c, 3, padding=1)
+
+    def forward(self, x):
+        return x + self.convolution2(F.relu(self.convolution1(F.relu(x))))
+
+
+class _Fusion(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.projection = nn.Conv2d(c, c, 1)
+        self.residual_layer1 = _PreActRes(c)
+        self.residual_layer2 = _PreActRes(c)
+
+    def forward(self, x, residual=None):
+        if residual is not None:
+            if residual.shape != x.shape:
+                residual = F.interpolate(residual, size=x.shape[2:], mode="bilinear", align_corners=False)
+            x = x + self.residual_layer1(residual)
+        x = self.residual_layer2(x)
+        x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
+        return self.projection(x)
+
+
+class _FusionStage(nn.Module):
+    def __init__(self, c, n):
+        super().__init__()
+        self.layers = nn.ModuleList([_Fusion(c) for _ in range(n)])
+
+
+class _DPTNeck(nn.Module):
+    def __init__(self, c, sizes=(256, 512, 1024, 1024), factors=(4, 2, 1, 0.5), fusion=256):
+        super().__init__()
+        self.reassemble_stage = _ReassembleStage(c, sizes, factors)
+        self.convs = nn.ModuleList([nn.Conv2d(s, fusion, 3, padding=1, bias=False) for s in sizes])
+        self.fusion_stage = _FusionStage(fusion, len(sizes))
+
+    def forward(self, hs, gh, gw):
+        feats = [conv(f) for conv, f in zip(self.convs, self.reassemble_stage(hs, gh, gw))]
+        fused = None
+        for f, layer in zip(feats[::-1], self.fusion_stage.layers):
+            fused = layer(f) if fused is None else layer(fused, f)
+        return fused
+
+
+class _DPTHead(nn.Module):
+    def __init__(self, c=256):
+        super().__init__()
+        self.head = nn.Sequential(nn.Conv2d(c, c // 2, 3, padding=1),
+                                  nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True),
+                                  nn.Conv2d(c // 2, 32, 3, padding=1), nn.ReLU(), nn.Conv2d(32, 1, 1), nn.ReLU())
+
+
+class DPTDepth(nn.Module):
+    out_indices = (5, 11, 17, 23)
+
+    def __init__(self):
+        super().__init__()
+        self.dpt = _DPTViT()
+        self.neck = _DPTNeck(1024)
+        self.head = _DPTHead()
+
+    def forward(self, x):
+        h = self.dpt.embeddings(x)
+        hs = []
+        for i, layer in enumerate(self.dpt.encoder.layer):
+            h = layer(h)
+            if i in self.out_indices:
+                hs.append(h)
+        gh, gw = x.shape[2] // 16, x.shape[3] // 16
+        return self.head.head(self.neck(hs, gh, gw))[:, 0]
+
+
+@torch.no_grad()
+def depth(image: Image.Image, size=384) -> Image.Image:
+    m = _build("depth", DPTDepth)
+    img = np.asarray(image.convert("RGB").resize((size, size), Image.Resampling.BICUBIC)).astype(np.float32)
+    x = (img / 255.0 - 0.5) / 0.5
+    pred = m(_to_tensor(x, m)).float()
+    pred = F.interpolate(pred[:, None], size=(image.size[1], image.size[0]), mode="bicubic", align_corners=False)
+    d = pred[0, 0].cpu().numpy()
+    mx = float(d.max())
+    out = (d * 255.0 / mx).clip(0, 255).astype(np.uint8) if mx > 0 else np.zeros_like(d, np.uint8)
+    return Image.fromarray(out).convert("RGB")
+
+
+# ---------------------------------------------------------------------------
+# UperNet + ConvNeXt (transformers UperNetForSemanticSegmentation,
+# openmmlab/upernet-convnext-small), ADE20K classes
+# ---------------------------------------------------------------------------
+class _LNcf(nn.Module):
+    """LayerNorm over channels of an NCHW map (ConvNeXt "channels_first")."""
+
+    def __init__(self, c, eps=1e-6):
+        super().__init__()
+        self.weight, self.bias, self.eps = nn.Parameter(torch.ones(c)), nn.Parameter(torch.zeros(c)), eps
+
+    def forward(self, x):
+        return F.layer_norm(x.permute(0, 2, 3, 1), x.shape[1:2], self.weight, self.bias, self.eps).permute(0, 3, 1, 2)
+
+
+class _CNBlock(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.dwconv = nn.Conv2d(c, c, 7, padding=3, groups=c)
+        self.layernorm = nn.LayerNorm(c, eps=1e-6)
+        self.pwconv1 = nn.Linear(c, 4 * c)
+        self.pwconv2 = nn.Linear(4 * c, c)
+        self.layer_scale_parameter = nn.Parameter(torch.full((c,), 1e-6))
+
+    def forward(self, x):
+        h = self.dwconv(x).permute(0, 2, 3, 1)
+        h = self.pwconv2(F.gelu(self.pwconv1(self.layernorm(h)))) * self.layer_scale_parameter
+        return x + h.permute(0, 3, 1, 2)
+
+
+class _CNStage(nn.Module):
+    def __init__(self, cin, c, depth, down):
+        super().__init__()
+        self.downsampling_layer = nn.Sequential(_LNcf(cin), nn.Conv2d(cin, c, 2, stride=2)) if down else nn.Identity()
+        self.layers = nn.Sequential(*[_CNBlock(c) for _ in range(depth)])
+
+    def forward(self, x):
+        return self.layers(self.downsampling_layer(x))
+
+
+class _CNEmb(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.patch_embeddings = nn.Conv2d(3, c, 4, stride=4)
+        self.layernorm = _LNcf(c)
+
+
+class _CNEncoder(nn.Module):
+    def __init__(self, dims, depths):
+        super().__init__()
+        self.stages = nn.ModuleList([_CNStage(dims[max(i - 1, 0)], dims[i], depths[i], i > 0) for i in range(4)])
+
+
+class ConvNextBackbone(nn.Module):
+    def __init__(self, dims=(96, 192, 384, 768), depths=(3, 3, 27, 3)):
+        super().__init__()
+        self.embeddings = _CNEmb(dims[0])
+        self.encoder = _CNEncoder(dims, depths)
+        self.hidden_states_norms = nn.ModuleDict({f"stage{i + 1}": _LNcf(d) for i, d in enumerate(dims)})
+
+    def forward(self, x):
+        h = self.embeddings.layernorm(self.embeddings.patch_embeddings(x))
+        outs = []
+        for i, st in enumerate(self.encoder.stages):
+            h = st(h)
+            outs.append(self.hidden_states_norms[f"stage{i + 1}"](h))
+        return outs
+
+
+class _ConvModule(nn.Module):
+    def __init__(self, cin, cout, k=1, pad=0):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, padding=pad, bias=False)
+        self.batch_norm = nn.BatchNorm2d(cout)
+
+    def forward(self, x):
+        return F.relu(self.batch_norm(self.conv(x)))
+
+
+class _PPMStage(nn.Module):
+    def __init__(self, scale, cin, c):
+        super().__init__()
+        self.scale = scale
+        self.layers = nn.ModuleList([nn.AdaptiveAvgPool2d(scale), _ConvModule(cin, c)])
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x
+
+
+class UperHead(nn.Module):
+    def __init__(self, in_channels=(96, 192, 384, 768), c=512, num_classes=150, scales=(1, 2, 3, 6)):
+        super().__init__()
+        self.psp_modules = nn.ModuleList([_PPMStage(s, in_channels[-1], c) for s in scales])
+        self.bottleneck = _ConvModule(in_channels[-1] + len(scales) * c, c, 3, 1)
+        self.lateral_convs = nn.ModuleList([_ConvModule(ci, c) for ci in in_channels[:-1]])
+        self.fpn_convs = nn.ModuleList([_ConvModule(c, c, 3, 1) for _ in in_channels[:-1]])
+        self.fpn_bottleneck = _ConvModule(len(in_channels) * c, c, 3, 1)
+        self.classifier = nn.Conv2d(c, num_classes, 1)
+
+    def forward(self, feats):
+        x = feats[-1]
+        psp = [x] + [F.interpolate(p(x), size=x.shape[2:], mode="bilinear", align_corners=False) for p in self.psp_modules]
+        lat = [conv(f) for conv, f in zip(self.lateral_convs, feats)] + [self.bottleneck(torch.cat(psp, 1))]
+        for i in range(len(lat) - 1, 0, -1):
+            lat[i - 1] = lat[i - 1] + F.interpolate(lat[i], size=lat[i - 1].shape[2:], mode="bilinear",
+                                                    align_corners=False)
+        outs = [conv(lat[i]) for i, conv in enumerate(self.fpn_convs)] + [lat[-1]]
+        outs = [outs[0]] + [F.interpolate(o, size=outs[0].shape[2:], mode="bilinear", align_corners=False)
+                            for o in outs[1:]]
+        return self.classifier(self.fpn_bottleneck(torch.cat(outs, 1)))
+
+
+class UperNetConvNext(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.backbone = ConvNextBackbone()
+        self.decode_head = UperHead()
+
+    def forward(self, x):
+        return self.decode_head(self.backbone(x))
+
+
+# ADE20K colour table used for ControlNet-seg conditioning images (data; the
+# reference keeps the same 151 entries at swarm/controlnet/input_processor.py:118-272)
+_ADE_HEX = (
+    "000000787878b4787806e6e650323204c8037878508c8c8ccc05ffe6e6e604fa07e005ffebff0796053d78784608ff33"
+    "ff06528fff8cccff04ff3307cc46030066c83de6faff06330b66ffff0747ff09e00907e6dcdcdcff095c7009ff08ffd6"
+    "07ffe0ffb8060aff47ff290a07ffffe0ff086608ffff3d06ffc207ff7a0800ff14ff0829ff05990633ffeb0cffa09614"
+    "00a3ff8c8c8cfa0a0f14ff001fff00ff1f00ffe00099ff000000ffff470000ebff00adff1f00ff0bc8c8ff520000fff5"
+    "003dff00ff7000ff85ff0000ffa300ff6600c2ff00008fff33ff000052ff00ff2900ffad0a00ffadff0000ff99ff5c00"
+    "ff00ffff00f5ff0066ffad00ff0014ffb8b8001fff00ff3d0047ffff00cc00ffc200ff52000aff0070ff3300ff00c2ff"
+    "007aff00ffa3ff990000ff0aff70008fff005200ffa3ff00ffeb0008b8aa8500ff00ff5cb800ffff001f00b8ff00d6ff"
+    "ff00705cff0000e0ff70e0ff46b8a0a300ff9900ff47ff00ff00a3ffcc00ff008f00ffeb85ff00ff00ebf500ffff007a"
+    "fff5000abed4d6ff0000ccff1400ffffff000099ff0029ff00ffcc2900ff29ff00ad00ff00f5ff4700ff7a00ff00ffb8"
+    "005cffb8ff000085ffffd60019c2c266ff005c00ff"
+)
+ADE_PALETTE = np.frombuffer(bytes.fromhex(_ADE_HEX), dtype=np.uint8).reshape(-1, 3)
+
+
+@torch.no_grad()
+def segmentation(image: Image.Image, res=512) -> Image.Image:
+    m = _build("seg", UperNetConvNext)
+    w, h = image.size
+    k = res / min(w, h)
+    rw, rh = max(32, int(round(w * k / 32)) * 32), max(32, int(round(h * k / 32)) * 32)
+    img = np.asarray(image.convert("RGB").resize((rw, rh), Image.Resampling.BILINEAR)).astype(np.float32) / 255.0
+    x = (img - np.array([0.485, 0.456, 0.406], np.float32)) / np.array([0.229, 0.224, 0.225], np.float32)
+    logits = m(_to_tensor(x, m)).float()
+    logits = F.interpolate(logits, size=(h, w), mode="bilinear", align_corners=False)
+    seg = logits.argmax(1)[0].cpu().numpy()
+    return Image.fromarray(ADE_PALETTE[np.clip(seg, 0, len(ADE_PALETTE) - 1)].astype(np.uint8))

@@ -6,17 +6,18 @@ Dispatch on ``parameters.controlnet.type`` when ``preprocess`` is true:
               kernel on the GPU when a CUDA tensor path is requested, numpy on CPU
   tile     -> resize so the short side is a multiple of 64 (reference image_to_tile)
   shuffle  -> content shuffle (random smooth flow warp, seeded)
-  scribble / softedge -> thick edge map (Canny + dilation) stand-in
-  depth / seg / normalbae / mlsd / lineart / openpose / pix2pix annotators need
-  their own networks' checkpoints (DPT, UperNet, ...): without local weights
-  they raise ValueError -> fatal job error, like an incompatible model.
+  scribble / softedge / lineart / mlsd / depth / seg -> neural annotators
+              (controlnet/annotators.py: HED, informative-drawings lineart,
+              M-LSD, DPT-Large, UperNet-ConvNeXt), resident per process
+  normalbae / openpose -> not available on this worker: ValueError -> fatal
+              job error, like an incompatible model
 """
 from __future__ import annotations
 
 import numpy as np
 from PIL import Image
 
-NEURAL = {"depth", "seg", "normalbae", "mlsd", "lineart", "openpose"}
+UNAVAILABLE = {"normalbae", "openpose"}
 
 
 def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
@@ -29,12 +30,24 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
         return image_to_tile(image)
     if t == "shuffle":
         return content_shuffle(image)
-    if t in ("scribble", "softedge"):
-        return edges_thick(image)
     if t == "pix2pix":
         return image
-    if t in NEURAL:
-        raise ValueError(f"controlnet preprocessor '{t}' needs its annotator checkpoint, not available on this worker")
+    if t in ("scribble", "softedge", "lineart", "mlsd", "depth", "seg"):
+        from . import annotators as an
+
+        if t == "scribble":
+            return an.hed(image, scribble=True)
+        if t == "softedge":
+            return an.hed(image)
+        if t == "lineart":
+            return an.lineart(image, coarse=bool(controlnet.get("coarse", False)))
+        if t == "mlsd":
+            return an.mlsd(image)
+        if t == "depth":
+            return an.depth(image)
+        return an.segmentation(image)
+    if t in UNAVAILABLE:
+        raise ValueError(f"controlnet preprocessor '{t}' is not available on this worker")
     raise ValueError(f"unknown controlnet type {t}")
 
 
@@ -102,15 +115,6 @@ def image_to_canny(image: Image.Image, low=100, high=200, device=None) -> Image.
             return Image.fromarray(np.stack([e] * 3, axis=-1))
     e = canny_np(arr, float(low), float(high))
     return Image.fromarray(np.stack([e] * 3, axis=-1))
-
-
-def edges_thick(image: Image.Image) -> Image.Image:
-    from scipy import ndimage
-
-    e = canny_np(np.asarray(image.convert("L")), 50, 120) > 0
-    e = ndimage.binary_dilation(e, iterations=2)
-    a = (e * 255).astype(np.uint8)
-    return Image.fromarray(np.stack([a] * 3, axis=-1))
 
 
 def content_shuffle(image: Image.Image, seed: int = 0, f: int = 256) -> Image.Image:

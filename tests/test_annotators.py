@@ -1,0 +1,75 @@
+"""ControlNet neural annotators (controlnet/annotators.py): every detector runs
+end to end on the CPU with its seeded random init (no checkpoints offline) and
+returns a conditioning image of the input's size; state-dict layouts load back
+into themselves (the names the public checkpoints use); the post-processing
+(scribble NMS, M-LSD decoding, ADE palette) is checked on constructed inputs.
+Parity with the real detectors is unpinned: their checkpoints are not in this
+image."""
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from chiaswarm_amd.controlnet import annotators as an
+from chiaswarm_amd.controlnet.preprocess import preprocess_image
+
+
+@pytest.fixture(autouse=True)
+def _no_weights(tmp_path, monkeypatch):
+    monkeypatch.setenv("CSK_ANNOTATOR_DIR", str(tmp_path))
+    an._CACHE.clear()
+    yield
+    an._CACHE.clear()
+
+
+def _img(w=96, h=80):
+    rng = np.random.default_rng(0)
+    a = np.zeros((h, w, 3), np.uint8)
+    a[20:60, 30:70] = 200
+    a += rng.integers(0, 20, a.shape, dtype=np.uint8)
+    return Image.fromarray(a)
+
+
+@pytest.mark.parametrize("kind", ["scribble", "softedge", "lineart", "mlsd"])
+def test_conv_annotators_shape(kind):
+    out = preprocess_image(_img(), {"preprocess": True, "type": kind})
+    assert out.size == (96, 80) and out.mode == "RGB"
+    a = np.asarray(out)
+    assert a.dtype == np.uint8
+
+
+def test_depth_dpt_shape():
+    out = an.depth(_img(), size=64)  # 4x4 patch grid: position-embedding resize path
+    assert out.size == (96, 80)
+
+
+def test_seg_upernet_palette():
+    out = an.segmentation(_img(), res=64)
+    a = np.asarray(out).reshape(-1, 3)
+    pal = {tuple(c) for c in an.ADE_PALETTE.tolist()}
+    assert all(tuple(c) in pal for c in np.unique(a, axis=0).tolist())
+    assert an.ADE_PALETTE.shape == (151, 3) and tuple(an.ADE_PALETTE[1]) == (120, 120, 120)
+
+
+def test_weights_load_from_dir(tmp_path):
+    from safetensors.torch import save_file
+
+    m = an.LineartGenerator()
+    sd = {k: torch.randn_like(v) if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    save_file(sd, str(tmp_path / "lineart.safetensors"))
+    an._CACHE.clear()
+    g = an._build("lineart", an.LineartGenerator)
+    assert g.weights_source.endswith("lineart.safetensors")
+    assert torch.allclose(g.state_dict()["model0.1.weight"].float(), sd["model0.1.weight"])
+
+
+def test_scribble_nms_keeps_thin_ridges():
+    x = np.zeros((40, 40), np.uint8)
+    x[:, 18:23] = 255  # a 5-px stroke: its blurred ridge is the centre column
+    y = an._nms(x, 127, 1.0)
+    assert y[:, 20].all() and not y[:, 10].any()
+
+
+def test_unavailable_types_are_fatal():
+    with pytest.raises(ValueError):
+        preprocess_image(_img(), {"preprocess": True, "type": "openpose"})
