@@ -24,7 +24,7 @@ sig("csk_conv2d", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
 sig("csk_gemm_ln", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
-    c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p, c_void_p)
+    c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
 sig("csk_conv2d_ex", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
     c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
@@ -175,16 +175,17 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
     else:
         bn = tuning.TILES[tile][1]
         rp = torch.empty(-(-N // bn) * M * 2, dtype=torch.float32, device=a2.device) if row_stats else None
-        lp = lc = None
+        lp = lc = rowbuf = None
         nparts = pcols = 0
         eps = 0.0
         if ln is not None:
             (lp, nparts, pcols), lc, eps = ln
             if K % 8 or nparts * pcols < K or lp.numel() < nparts * M * 2:
                 raise ValueError("gemm: fused LayerNorm statistics do not match the input")
+            rowbuf = torch.empty(M * 2, dtype=torch.float32, device=a2.device)
         _lib.call("csk_gemm_ln", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
                   M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), _p(lp), _p(lc), nparts, pcols,
-                  float(eps), _p(rp), tile, 1, None, _s())
+                  float(eps), _p(rowbuf), _p(rp), tile, 1, None, _s())
         if rp is not None:
             out._csk_rows = (rp, -(-N // bn), bn)
     if part is not None:

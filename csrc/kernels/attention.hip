@@ -59,7 +59,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   const int fr = lane & 15, fg = lane >> 4;
   const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
-  const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  // XCD-aware: the query blocks of one (batch, head) run on one XCD, so its
+  // K/V (re-read by every query block) is fetched into one L2, not eight
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = wg / nqb, qb = wg % nqb;
   const int b = bh / a.H, h = bh % a.H;
   const int q0 = qb * QROWS + wid * QT * 16;
 
@@ -278,7 +281,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   const int fr = lane & 15, fg = lane >> 4;
   const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
-  const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  // XCD-aware: the query blocks of one (batch, head) run on one XCD, so its
+  // K/V (re-read by every query block) is fetched into one L2, not eight
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = wg / nqb, qb = wg % nqb;
   const int b = bh / a.H, h = bh % a.H;
   const int q0 = qb * QROWS + wid * QT * 16;
   const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;

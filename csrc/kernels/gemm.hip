@@ -315,6 +315,21 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
 
 // y[M, ldc] = act(A[M, lda] . W[N, ldb]^T + bias + bias2d) * out_scale + res[M, ldr]
 // (+ fused input LayerNorm / output row statistics: GemmArgs::ln_part / row_part)
+// Per-row LayerNorm statistics for a fused-LN consumer GEMM: row m merges the
+// producer's column-slab partials part[(p * M + m) * 2 + {mean, M2}] (Chan,
+// exact) into out[m] = (mean, rstd).  One thread per row.
+__global__ void ln_rowstats_kernel(const float* __restrict__ part, float* __restrict__ out, int M, int K, int nparts,
+                                   int pcols, float eps) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float2 st = *reinterpret_cast<const float2*>(part + ((size_t)p * M + m) * 2);
+    chan_combine(n, mean, m2, (float)min(pcols, K - p * pcols), st.x, st.y);
+  }
+  *reinterpret_cast<float2*>(out + (size_t)m * 2) = make_float2(mean, rsqrtf(m2 / fmaxf(n, 1.f) + eps));
+}
+
 int g_gn_fine = 0;  // tile segments: same step time as fine ones (tools/abstep.py), 4x fewer partials
 CSK_API int csk_set_gn_fine(int v) {
   g_gn_fine = v;
@@ -324,10 +339,10 @@ CSK_API int csk_set_gn_fine(int v) {
 CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
                         int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act,
                         float out_scale, void* gn_part, const void* ln_part, const void* ln_colsum, int ln_nparts,
-                        int ln_pcols, float ln_eps, void* row_part, int tile, int ksplit, void* ws,
+                        int ln_pcols, float ln_eps, void* ln_rowbuf, void* row_part, int tile, int ksplit, void* ws,
                         hipStream_t stream) {
   if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (act == ACT_GEGLU && N % 32 != 0)) return (int)hipErrorInvalidValue;
-  if (ln_part && (!ln_colsum || ln_nparts <= 0 || ln_nparts > 32 || ln_pcols <= 0 ||
+  if (ln_part && (!ln_colsum || ln_nparts <= 0 || ln_pcols <= 0 ||
                   (long long)ln_nparts * ln_pcols < K))
     return (int)hipErrorInvalidValue;
   GemmArgs a{};
@@ -342,6 +357,13 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   a.ln_nparts = ln_nparts; a.ln_pcols = ln_pcols; a.ln_eps = ln_eps;
   a.row_part = (float*)row_part;
   if (M == 0 || N == 0) return 0;
+  if (ln_part) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
+    float* rows = (float*)ln_rowbuf;
+    if (!rows) return (int)hipErrorInvalidValue;
+    ln_rowstats_kernel<<<(M + 255) / 256, 256, 0, stream>>>((const float*)ln_part, rows, M, K, ln_nparts, ln_pcols,
+                                                           ln_eps);
+    a.ln_row = rows;
+  }
   return dispatch<false>(a, tile, ksplit, stream);
 }
 
@@ -349,7 +371,7 @@ CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, co
                      int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
                      void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {
   return csk_gemm_ln(C, A, W, bias, bias2d, res, M, N, K, lda, ldb, ldc, ldr, rows_per_b, act, out_scale, gn_part,
-                     nullptr, nullptr, 0, 0, 0.f, nullptr, tile, ksplit, ws, stream);
+                     nullptr, nullptr, 0, 0, 0.f, nullptr, nullptr, tile, ksplit, ws, stream);
 }
 
 // NHWC conv; xs / ys / rs: pixel strides (elements) of input / output / residual

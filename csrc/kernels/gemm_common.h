@@ -64,6 +64,7 @@ struct GemmArgs {
   const float* ln_colsum;
   int ln_nparts, ln_pcols;
   float ln_eps;
+  const float* ln_row;  // [M][2] (mean, rstd) merged from ln_part (ln_rowstats_kernel)
   // row statistics of the OUTPUT for a consumer's fused LayerNorm:
   // row_part[((n0 / BN) * M + m) * 2 + {mean, M2}] over the tile's columns.
   // No split-K, no GEGLU.
@@ -134,37 +135,16 @@ __device__ __forceinline__ void act8(int act, float (&f)[8]) {
 }
 
 // Fused-LayerNorm statistics (mean, rstd) of input row m0 + threadIdx.x
-// (threads < BM): merged from the producer's column-slab partials.  Called
-// BEFORE the K loop so the L2/HBM round trips overlap the operand staging
-// (in the epilogue they stalled every tile by ~2 us); the two floats ride in
-// registers to the epilogue.
+// (threads < BM), precomputed per row by ln_rowstats_kernel (gemm.hip) from
+// the producer's column-slab partials.  Loaded BEFORE the K loop so the
+// L2/HBM round trip overlaps the operand staging; one float2 in registers
+// (merging the partials here raised every tile's VGPR peak and cost the
+// small tiles a workgroup per CU).
 template <int BM>
 __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
-  constexpr int MAXP = 32;
   const int r = threadIdx.x;
-  if (!args.ln_part || r >= BM) return make_float2(0.f, 0.f);
-  const int m = min(m0 + r, args.M - 1);
-  float2 st[MAXP];
-#pragma unroll
-  for (int p = 0; p < MAXP; ++p)
-    st[p] = p < args.ln_nparts ? *reinterpret_cast<const float2*>(args.ln_part + ((size_t)p * args.M + m) * 2)
-                               : make_float2(0.f, 0.f);
-  float sn = 0.f, sm = 0.f;
-#pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const float cnt = p < args.ln_nparts ? (float)min(args.ln_pcols, args.K - p * args.ln_pcols) : 0.f;
-    sn += cnt;
-    sm += cnt * st[p].x;
-  }
-  const float mean = sm / sn;
-  float q = 0.f;
-#pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const float cnt = p < args.ln_nparts ? (float)min(args.ln_pcols, args.K - p * args.ln_pcols) : 0.f;
-    const float d = st[p].x - mean;
-    q += st[p].y + cnt * d * d;
-  }
-  return make_float2(mean, rsqrtf(q / sn + args.ln_eps));
+  if (!args.ln_row || r >= BM) return make_float2(0.f, 0.f);
+  return *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + r, args.M - 1) * 2);
 }
 
 template <int BM, int BN, int WM, int WN, bool RAW = false>

@@ -338,10 +338,13 @@ def test_conv_bias2d_row_stride(gpu):
 
 
 @pytest.mark.parametrize("N,act", [(960, None), (320, None), (2 * 1280, "geglu")])
-def test_layer_norm_fused_into_gemm(gpu, N, act):
+def test_layer_norm_fused_into_gemm(gpu, N, act, monkeypatch):
     """Producer GEMM emits per-row statistics; the consumer GEMM applies the
-    LayerNorm in its epilogue with gamma/beta folded into its weights."""
+    LayerNorm in its epilogue with gamma/beta folded into its weights
+    (opt-in path, CSK_LN_FUSE=1)."""
     from types import SimpleNamespace
+
+    monkeypatch.setattr(ops, "LN_FUSE", True)
 
     M, C, Kp = 1000, 320, 640
     a = rnd(M, Kp, dev=gpu)

@@ -185,3 +185,22 @@ def test_tiny_cascades_gpu(gpu):
     o = up(["x"], [Image.new("RGB", (64, 64), (9, 99, 199))], num_inference_steps=3,
            generator=torch.Generator(device=gpu).manual_seed(0))
     assert o[0].size == (128, 128)
+
+
+@pytest.mark.parametrize("kind", ["scribble", "lineart", "mlsd", "depth", "seg"])
+def test_controlnet_annotators_on_gpu(gpu, kind, tmp_path, monkeypatch):
+    """Neural annotators run resident on the GPU in bf16 (random init offline)."""
+    import numpy as np
+    from PIL import Image
+
+    from chiaswarm_amd.controlnet import annotators as an
+    from chiaswarm_amd.controlnet.preprocess import preprocess_image
+
+    monkeypatch.setenv("CSK_ANNOTATOR_DIR", str(tmp_path))
+    an._CACHE.clear()
+    img = Image.fromarray(np.random.default_rng(0).integers(0, 255, (300, 400, 3), dtype=np.uint8))
+    out = preprocess_image(img, {"preprocess": True, "type": kind})
+    assert out.size == (400, 300)
+    m = next(iter(an._CACHE.values()))
+    assert next(m.parameters()).is_cuda
+    an._CACHE.clear()

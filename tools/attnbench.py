@@ -1,0 +1,43 @@
+#!/usr/bin/env python
+"""Attention-only loop on the SD2.1 64x64-level self-attention shape (for PMC
+counter runs and variant timing):
+
+    python tools/attnbench.py --variant 3 --iters 50
+    rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA ... -- python3 tools/attnbench.py --iters 5
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--shape", default="8,4096,4096,5,64")
+    a = ap.parse_args()
+    _lib.load()
+    B, Sq, Skv, H, D = map(int, a.shape.split(","))
+    q, k, v = (torch.randn(B, s, H, D, device="cuda").bfloat16() for s in (Sq, Skv, Skv))
+    hip_ops.ATTN_VARIANT = a.variant
+    for _ in range(3):
+        hip_ops.attention(q, k, v, D ** -0.5)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        hip_ops.attention(q, k, v, D ** -0.5)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(f"variant {a.variant} {a.shape}: {ms * 1000:.1f} us  {4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
