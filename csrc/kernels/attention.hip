@@ -407,13 +407,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
             if (key >= kv_end || (a.causal && key > qi)) sc[kt][qt][r] = -INFINITY;
           }
       }
-      float mx = -1e30f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) mx = fmaxf(mx, fmaxf(sc[kt][qt][r], sc[kt][qt][r + 1]));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      // 16 scores -> 8 v_max3, then the 4 row groups via permlane swaps
+      float mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+      mx = vmax3(mx, sc[0][qt][3], sc[1][qt][0]);
+      mx = vmax3(mx, sc[1][qt][1], sc[1][qt][2]);
+      mx = vmax3(mx, sc[1][qt][3], sc[2][qt][0]);
+      mx = vmax3(mx, sc[2][qt][1], sc[2][qt][2]);
+      mx = vmax3(mx, sc[2][qt][3], sc[3][qt][0]);
+      mx = vmax3(mx, sc[3][qt][1], sc[3][qt][2]);
+      mx = max_rowgroups(vmax3(mx, sc[3][qt][3], sc[3][qt][3]));
       // lazy rescale (cdna_hip_programming.md T13): keep the reference max unless
       // the block max exceeds it by > 2^8; p stays <= 256, exact after the final 1/l
       const float mb = PRE ? mx + muc[qt] : mx * sl2;  // block max in log2 units
@@ -446,12 +448,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
             sc[kt][qt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][qt][r], sl2, -mref));
       }
       if constexpr (!ONES) {
-        float ls = 0.f;
+        // 4 independent single-instruction chains (no v_pk_add_f32 beside MFMAs)
+        float l4[4];
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int r = 0; r < 4; ++r) l4[r] = vadd(sc[0][qt][r], sc[1][qt][r]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ls += sc[kt][qt][r];
-        lrow[qt] += ls;
+        for (int r = 0; r < 4; ++r) l4[r] = vadd(l4[r], vadd(sc[2][qt][r], sc[3][qt][r]));
+        lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
       }
 #pragma unroll
       for (int kp2 = 0; kp2 < 2; ++kp2) {
@@ -548,7 +551,7 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
     if (variant >= 2 || (variant == 0 && Skv > 128)) {
-      if (variant == 0) variant = 3;  // PRE: 0.283 vs 0.318 ms at B8 S4096 H5 (profiles/opbench_attn_r1e.json)
+      if (variant == 0) variant = 5;  // PRE+ONES: 279 vs 283 (PRE) vs 306 us (plain) at B8 S4096 H5, same box
       const int nqb = (Sq + 127) / 128;
       const dim3 grid(B * H * nqb);
       switch (variant) {

@@ -49,6 +49,30 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float qgelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
 
+// Single-instruction max / add for values straight out of MFMA accumulators:
+// hipcc inserts a canonicalising v_max before every fmaxf on them and SLP-packs
+// adjacent f32 adds into v_pk_add_f32 (an anti-lever beside MFMAs,
+// MI355X_MICROARCH.md constants table) — inline asm keeps each one instruction.
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vadd(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max over lanes {l, l^16, l^32, l^48} (the four 16-lane row groups of a
+// 16x16 MFMA fragment) with two permlane swaps: no LDS round trip (the
+// ds_bpermute that __shfl_xor lowers to sat in the softmax's critical chain)
+__device__ __forceinline__ float max_rowgroups(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float m = vmax3(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return vmax3(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[1]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
