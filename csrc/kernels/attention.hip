@@ -170,26 +170,25 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
             if (key >= kv_end || (a.causal && key > qi)) s[kt][qt][r] = -INFINITY;
           }
       }
-      float mx = -1e30f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float mx = vmax3(s[0][qt][0], s[0][qt][1], s[0][qt][2]);
+      mx = vmax3(mx, s[0][qt][3], s[1][qt][0]);
+      mx = vmax3(mx, s[1][qt][1], s[1][qt][2]);
+      mx = vmax3(mx, s[1][qt][3], s[2][qt][0]);
+      mx = vmax3(mx, s[2][qt][1], s[2][qt][2]);
+      mx = vmax3(mx, s[2][qt][3], s[3][qt][0]);
+      mx = vmax3(mx, s[3][qt][1], s[3][qt][2]);
+      mx = max_rowgroups(vmax3(mx, s[3][qt][3], s[3][qt][3]));
       const float mnew = fmaxf(mrow[qt], mx * sl2);
       const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
       mrow[qt] = mnew;
-      float ls = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][qt][r], sl2, -mnew));
-          s[kt][qt][r] = p;
-          ls += p;
-        }
-      lrow[qt] = lrow[qt] * alpha + ls;
+        for (int r = 0; r < 4; ++r) s[kt][qt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][qt][r], sl2, -mnew));
+      float l4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) l4[r] = vadd(vadd(s[0][qt][r], s[1][qt][r]), vadd(s[2][qt][r], s[3][qt][r]));
+      lrow[qt] = lrow[qt] * alpha + vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3]));
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
 #pragma unroll

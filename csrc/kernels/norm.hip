@@ -162,6 +162,50 @@ __device__ __forceinline__ void group_moments(const Get& get, int ne, int sub, i
   rstd = rsqrtf(sq / fmaxf(sn, 1.f) + eps);
 }
 
+// One wave per group: up to 8 entries per lane are loaded ONCE (all in flight
+// together) and kept in registers for both passes, so a finalize over <= 512
+// partials costs one memory round trip instead of two dependent loops.
+template <class Get>
+__device__ __forceinline__ void group_moments_wave(const Get& get, int ne, int lane, float& mean, float& rstd,
+                                                   float eps) {
+  constexpr int CAP = 8;
+  float en[CAP], em[CAP], eq[CAP];
+#pragma unroll
+  for (int j = 0; j < CAP; ++j) {
+    const int e = lane + 64 * j;
+    en[j] = em[j] = eq[j] = 0.f;
+    if (e < ne) get(e, en[j], em[j], eq[j]);
+  }
+  float sn = 0.f, sm = 0.f;
+#pragma unroll
+  for (int j = 0; j < CAP; ++j) {
+    sn += en[j];
+    sm = __builtin_fmaf(en[j], em[j], sm);
+  }
+  for (int e = lane + 64 * CAP; e < ne; e += 64) {  // > 512 partials (large VAE maps)
+    float n, m, q;
+    get(e, n, m, q);
+    sn += n;
+    sm = __builtin_fmaf(n, m, sm);
+  }
+  sn = wave_sum(sn);
+  sm = wave_sum(sm);
+  mean = sn > 0.f ? sm / sn : 0.f;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < CAP; ++j) {
+    const float d = em[j] - mean;
+    sq += __builtin_fmaf(en[j] * d, d, eq[j]);
+  }
+  for (int e = lane + 64 * CAP; e < ne; e += 64) {
+    float n, m, q;
+    get(e, n, m, q);
+    const float d = m - mean;
+    sq += __builtin_fmaf(n * d, d, q);
+  }
+  rstd = rsqrtf(wave_sum(sq) / fmaxf(sn, 1.f) + eps);
+}
+
 // stat[(b * G + g) * 2 + {mean, rstd}]: merge chunk partials (Chan); one wave
 // per (b, g) so the merge is spread over B*G/4 workgroups instead of B.
 __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stat,
@@ -171,12 +215,12 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __
   if (bg >= B * G) return;  // whole waves leave together (one (b, g) per wave)
   const int b = bg / G, g = bg - b * G;
   float mean, rstd;
-  group_moments(
+  group_moments_wave(
       [&](int c, float& n, float& m, float& q) {
         const float* pp = part + (((size_t)b * nchunk + c) * G + g) * 3;
         n = pp[0]; m = pp[1]; q = pp[2];
       },
-      nchunk, lane, 64, mean, rstd, eps);
+      nchunk, lane, mean, rstd, eps);
   if (lane == 0) {
     stat[bg * 2] = mean;
     stat[bg * 2 + 1] = rstd;
@@ -295,13 +339,13 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
   const int b = bg / G, g = bg - b * G, Cg = C / G;
   const float fn = (float)seg_rows;
   float mean, rstd;
-  group_moments(
+  group_moments_wave(
       [&](int e, float& n, float& m, float& q) {
         const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
         const float2 mq = *reinterpret_cast<const float2*>(part + ((size_t)sg * C + c) * 2);
         n = fn; m = mq.x; q = mq.y;
       },
-      nseg * Cg, lane, 64, mean, rstd, eps);
+      nseg * Cg, lane, mean, rstd, eps);
   if (lane == 0) {
     stat[bg * 2] = mean;
     stat[bg * 2 + 1] = rstd;
