@@ -261,8 +261,45 @@ __global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
   }
 }
 
+// 8 columns per thread: 2x float4 per split, 16-byte bias / residual / output
+// accesses (the scalar kernel above issues one 4-byte load per split per value)
+__global__ void splitk_reduce8_kernel(const GemmArgs a, int ksplit) {
+  const int M = a.M, N = a.N, NV = N / 8;
+  const size_t total = (size_t)M * N, nvec = (size_t)M * NV;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / NV), n = (int)(i - (size_t)m * NV) * 8;
+    const float* w = a.ws + (size_t)m * N + n;
+    float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
+    for (int sidx = 1; sidx < ksplit; ++sidx) {
+      const float4 l2 = *reinterpret_cast<const float4*>(w + sidx * total);
+      const float4 h2 = *reinterpret_cast<const float4*>(w + sidx * total + 4);
+      lo.x += l2.x; lo.y += l2.y; lo.z += l2.z; lo.w += l2.w;
+      hi.x += h2.x; hi.y += h2.y; hi.z += h2.z; hi.w += h2.w;
+    }
+    float f[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (a.bias) add8(f, a.bias + n, true, 8);
+    if (a.bias2d) add8(f, a.bias2d + (size_t)(m / a.rows_per_b) * a.ldb2 + n, true, 8);
+    act8(a.act, f);
+    if (a.out_scale != 1.0f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= a.out_scale;
+    }
+    if (a.res) add8(f, a.res + (size_t)m * a.ldr + n, true, 8);
+    *reinterpret_cast<uint4*>(a.C + (size_t)m * a.ldc + n) = pack8(f);
+  }
+}
+
 static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
   const size_t total = (size_t)a.M * a.N;
+  const bool vec = a.N % 8 == 0 && a.ldc % 8 == 0 && (!a.res || a.ldr % 8 == 0) && (!a.bias2d || a.ldb2 % 8 == 0) &&
+                   ((size_t)a.C % 16 == 0) && (!a.res || (size_t)a.res % 16 == 0) && (!a.bias || (size_t)a.bias % 16 == 0) &&
+                   (!a.bias2d || (size_t)a.bias2d % 16 == 0) && ((size_t)a.ws % 16 == 0);
+  if (vec) {
+    int grid = (int)((total / 8 + 255) / 256);
+    if (grid > 8192) grid = 8192;
+    splitk_reduce8_kernel<<<grid, 256, 0, s>>>(a, ksplit);
+    return (int)hipGetLastError();
+  }
   int grid = (int)((total + 255) / 256);
   if (grid > 8192) grid = 8192;
   splitk_reduce_kernel<<<grid, 256, 0, s>>>(a, ksplit);
