@@ -344,6 +344,27 @@ class ResnetBlock2D(nn.Module):
         sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
         return self.conv2(h, residual=sc, gn_stats=True)  # block output usually feeds the next GroupNorm
 
+    def forward_cat(self, a, b, temb_proj=None):
+        """forward() of the channel concat [a | b] (a UNet skip connection)
+        without materialising the concat on the HIP path: norm1 reads both
+        tensors in place and the 1x1 shortcut runs as two accumulating GEMMs
+        (the concat cost a full read + write of both tensors per up-block
+        ResNet)."""
+        sc_conv = self.conv_shortcut
+        hn = None
+        if ops.use_hip(a) and sc_conv is not None and sc_conv.kernel_size == (1, 1) and self.norm1.weight.dim() == 1:
+            hn = ops.group_norm_cat(a, b, self.norm1.weight, self.norm1.bias, self.norm1.num_groups,
+                                    self.norm1.eps, silu=True)
+        if hn is None:
+            return self.forward(ops.cat_channels(a, b), temb_proj)
+        h = self.conv1(hn, bias2d=temb_proj, gn_stats=True)
+        h = self.norm2(h, silu=True)
+        w = sc_conv.weight.view(sc_conv.out_channels, sc_conv.in_channels)
+        ca = a.shape[-1]
+        sc = ops.gemm(a, w[:, :ca])
+        sc = ops.gemm(b, w[:, ca:], sc_conv.bias, residual=sc)
+        return self.conv2(h, residual=sc, gn_stats=True)
+
 
 class Downsample2D(nn.Module):
     def __init__(self, channels, padding=1):

@@ -294,7 +294,7 @@ class UNet2DConditionModel(Prepared):
         for blk in self.up_blocks:
             for j, r in enumerate(blk.resnets):
                 s = skips.pop()
-                h = r(ops.cat_channels(h, s), next(tprojs))
+                h = r.forward_cat(h, s, next(tprojs))
                 if blk.attentions is not None:
                     h = run_attn(blk.attentions[j], h)
             if blk.upsamplers is not None:

@@ -389,6 +389,16 @@ def group_norm(x, gamma, beta, groups=32, eps=1e-5, silu=False):
     return _ref_group_norm(x, gamma, beta, groups, eps, silu)
 
 
+def group_norm_cat(a, b, gamma, beta, groups=32, eps=1e-5, silu=False):
+    """GroupNorm of the channel concat [a | b] read in place (HIP path, when
+    both carry fused epilogue statistics); None when not possible."""
+    if use_hip(a):
+        from . import hip_ops
+
+        return hip_ops.group_norm_cat(a, b, gamma, beta, groups, eps, silu)
+    return None
+
+
 def _ref_layer_norm(x, gamma, beta, eps):
     dt = _cdt(x)
     return F.layer_norm(x.to(dt), (x.shape[-1],), gamma.to(dt), beta.to(dt) if beta is not None else None,

@@ -28,8 +28,8 @@ sig("csk_gemm_ln", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
 sig("csk_conv2d_ex", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
     c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
-sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-    c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
+sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
 
 
 # ---------------------------------------------------------------------------
@@ -324,13 +324,47 @@ def group_norm(x, gamma, beta, groups, eps, silu):
         fpart, seg = fused
         if P % seg == 0 and fpart.numel() == (B * P // seg) * C * 2:
             stat = torch.empty(B * groups * 2, dtype=torch.float32, device=x.device)
-            _lib.call("csk_group_norm_part", _p(y), _p(x), _p(fpart), seg, _p(stat), _p(gamma), _p(beta), B, P, C,
-                      groups, chunk, nchunk, float(eps), int(bool(silu)), bstride, _s())
+            _lib.call("csk_group_norm_part", _p(y), _p(x), None, 0, _p(fpart), seg, _p(stat), _p(gamma), _p(beta),
+                      B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), bstride, _s())
             return y
     part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
               float(eps), int(bool(silu)), bstride, _s())
     return y
+
+
+def group_norm_cat(a, b, gamma, beta, groups, eps, silu):
+    """GroupNorm(+SiLU) of the channel concat [a | b] without materialising it
+    (UNet skip connections): the apply kernel reads both tensors in place.
+    Needs the fused epilogue statistics of both (same segment height);
+    returns None otherwise (the caller concatenates)."""
+    sa, sb = getattr(a, "_csk_gn", None), getattr(b, "_csk_gn", None)
+    GN_CAT_STATS[1] += 1
+    if sa is None or sb is None or sa[1] != sb[1] or a.shape[:-1] != b.shape[:-1]:
+        return None
+    if not (a.is_contiguous() and b.is_contiguous()) or a.shape[-1] % 8 or gamma.dim() != 1:
+        return None
+    B, Ca, Cb = a.shape[0], a.shape[-1], b.shape[-1]
+    C = Ca + Cb
+    P = a.numel() // (B * Ca)
+    seg = sa[1]
+    nseg = sa[0].numel() // (2 * Ca)
+    if P % seg or nseg * 2 * Cb != sb[0].numel() or C % groups or C > 4096:
+        return None
+    part = torch.cat([sa[0].view(nseg, Ca, 2), sb[0].view(nseg, Cb, 2)], 1).view(-1)
+    rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
+    chunk = max(4 * rows, -(-P * B // 1024))
+    nchunk = -(-P // chunk)
+    chunk = -(-P // nchunk)
+    y = torch.empty(a.shape[:-1] + (C,), dtype=torch.bfloat16, device=a.device)
+    stat = torch.empty(B * groups * 2, dtype=torch.float32, device=a.device)
+    _lib.call("csk_group_norm_part", _p(y), _p(a), _p(b), Ca, _p(part), seg, _p(stat), _p(gamma), _p(beta),
+              B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), 0, _s())
+    GN_CAT_STATS[0] += 1
+    return y
+
+
+GN_CAT_STATS = [0, 0]  # (concats normalised in place, attempts)
 
 
 def layer_norm(x, gamma, beta, eps):

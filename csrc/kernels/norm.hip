@@ -238,8 +238,12 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ gamma,
                                                               const bf16_t* __restrict__ beta, int P, int C, int G,
                                                               int chunk, int silu, int affine_bstride, int nent,
-                                                              int seg_rows, float eps) {
+                                                              int seg_rows, float eps,
+                                                              const bf16_t* __restrict__ x2 = nullptr, int C1 = 0) {
+  // x2 != null: the input is the channel concat [x (C1 channels) | x2 (C - C1)]
+  // of two separate tensors (UNet skip connections), read in place
   __shared__ float gst[2 * 64];
+  if (!x2) C1 = C;
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
   gamma += (size_t)b * affine_bstride;  // per-sample affine ([B, C]) when affine_bstride == C
   beta += (size_t)b * affine_bstride;
@@ -302,11 +306,14 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
   for (int u = 0; u < 2; ++u) {
     const int v = L.cv + u * L.NVT;
     if (u < L.TPV && v < L.NV) {
+      const bool second = v * 8 >= C1;  // this column vector lives in x2
+      const int xst = second ? C - C1 : C1;
+      const bf16_t* xsrc = (second ? x2 : x) + (size_t)b * P * xst + (second ? v * 8 - C1 : v * 8);
       for (int p = p0 + L.r; p < p1; p += GN_UNROLL * L.R) {
         uint4 q[GN_UNROLL];
 #pragma unroll
         for (int w = 0; w < GN_UNROLL; ++w)
-          q[w] = *reinterpret_cast<const uint4*>(x + boff + (size_t)min(p + w * L.R, p1 - 1) * C + v * 8);
+          q[w] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p + w * L.R, p1 - 1) * xst);
 #pragma unroll
         for (int w = 0; w < GN_UNROLL; ++w) {
           const int pp = p + w * L.R;
@@ -353,10 +360,12 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
 }
 
 // stat: B*G*2 floats of workspace
-CSK_API int csk_group_norm_part(void* y, const void* x, const void* part, int seg_rows, void* stat, const void* gamma,
-                                const void* beta, int B, int P, int C, int G, int chunk, int nchunk, float eps,
-                                int silu, int affine_bstride, hipStream_t stream) {
+// x2 / C1: optional second input (channel concat [x | x2], x has C1 channels)
+CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, const void* part, int seg_rows,
+                                void* stat, const void* gamma, const void* beta, int B, int P, int C, int G, int chunk,
+                                int nchunk, float eps, int silu, int affine_bstride, hipStream_t stream) {
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0 || seg_rows <= 0 || P % seg_rows != 0) return (int)hipErrorInvalidValue;
+  if (x2 && (C1 <= 0 || C1 >= C || C1 % 8 != 0)) return (int)hipErrorInvalidValue;
   float* st = (float*)stat;
   const int nseg = P / seg_rows;
   // every apply workgroup re-reads ALL of its sample's partials in a prologue
@@ -365,14 +374,15 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* part, int se
   if (G <= 64 && nseg * C <= g_gn_prologue_max) {
     gn_apply_kernel<2><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>(
         (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G, chunk,
-        silu, affine_bstride, nseg, seg_rows, eps);
+        silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1);
     CSK_CHECK_LAUNCH();
   }
   gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
       (const float*)part, st, B, C, G, nseg, seg_rows, eps);
   gn_apply_kernel<0><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st,
                                                                  (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G,
-                                                                 chunk, silu, affine_bstride, 0, 0, eps);
+                                                                 chunk, silu, affine_bstride, 0, 0, eps,
+                                                                 (const bf16_t*)x2, C1);
   CSK_CHECK_LAUNCH();
 }
 

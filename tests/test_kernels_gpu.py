@@ -360,3 +360,19 @@ def test_layer_norm_fused_into_gemm(gpu, N, act, monkeypatch):
     ref = ops._ref_gemm(xn.cpu(), w.float().cpu(), b.float().cpu(), None, act)
     assert y.shape == ref.shape
     assert rel_err(y.cpu(), ref) < 1.5e-2
+
+
+def test_group_norm_of_concat_in_place(gpu):
+    """GroupNorm of [a | b] read from the two tensors (UNet skip concat) == GN of torch.cat."""
+    B, H, W, Ca, Cb, K = 2, 32, 32, 320, 320, 256
+    xa, xb = rnd(B, H, W, K, dev=gpu), rnd(B, H, W, K, dev=gpu)
+    wa, wb = rnd(Ca, K, dev=gpu, scale=K ** -0.5), rnd(Cb, K, dev=gpu, scale=K ** -0.5)
+    a = ops.gemm(xa, wa, gn_rows=H * W)  # producers emit fused GN statistics
+    b = ops.gemm(xb, wb, gn_rows=H * W)
+    assert getattr(a, "_csk_gn", None) is not None and getattr(b, "_csk_gn", None) is not None
+    g, bt = rnd(Ca + Cb, dev=gpu), rnd(Ca + Cb, dev=gpu)
+    y = hip_ops.group_norm_cat(a, b, g, bt, 32, 1e-5, True)
+    if y is None:
+        pytest.skip("segment heights differ")
+    ref = ops._ref_group_norm(torch.cat([a, b], -1).float().cpu(), g.float().cpu(), bt.float().cpu(), 32, 1e-5, True)
+    assert rel_err(y.cpu(), ref) < 1e-2

@@ -87,3 +87,21 @@ def test_graph_requests_match_eager_across_prompts(gpu):
         assert ((a - b).norm() / b.norm()).item() < 2e-2, prompt
     c, d = runs[(True, "a cat")], runs[(True, "a red sports car")]
     assert ((c - d).norm() / d.norm()).item() > 1e-2  # different prompts -> different latents
+
+
+@torch.no_grad()
+def test_unet_up_blocks_read_skip_concats_in_place(gpu):
+    """The SD2.1 up-block ResNets normalise [h | skip] without building the
+    concat (ops.group_norm_cat) and match the reference-mode UNet."""
+    from chiaswarm_amd.ops import hip_ops
+
+    m = _build(unet.UNet2DConditionModel, unet.SD21, gpu)
+    x = torch.randn(2, 32, 32, 4, device=gpu)
+    ctx = torch.randn(2, 77, 1024, device=gpu).bfloat16()
+    t = torch.tensor([500.0], device=gpu)
+    hip_ops.GN_CAT_STATS[:] = [0, 0]
+    y = m(x, t, encoder_hidden_states=ctx)
+    assert hip_ops.GN_CAT_STATS[0] > 0, hip_ops.GN_CAT_STATS
+    with ops.ops_mode("reference"):
+        ref = m(x, t, encoder_hidden_states=ctx)
+    assert rel_err(y, ref) < 5e-2
