@@ -8,6 +8,7 @@ which calls controlnet_aux / transformers detectors):
   mlsd      -> M-LSD large (MobileNetV2 encoder + line-segment decoder)
   depth     -> DPT-Large (ViT-L/16 + reassemble/fusion neck + depth head)
   seg       -> UperNet + ConvNeXt backbone, ADE20K palette
+  openpose  -> CMU body-pose model (18 keypoints, PAF grouping), skeleton canvas
 
 Module and parameter names follow the public checkpoints (controlnet_aux .pth
 files / transformers safetensors) so real weights load unchanged from
@@ -40,6 +41,7 @@ _FILES = {
     "mlsd": ["mlsd_large_512_fp32.pth", "mlsd.safetensors"],
     "depth": ["dpt-large.safetensors", "dpt-large/model.safetensors"],
     "seg": ["upernet-convnext-small.safetensors", "upernet-convnext-small/model.safetensors"],
+    "openpose": ["body_pose_model.pth", "openpose.safetensors"],
 }
 
 
@@ -745,3 +747,206 @@ def segmentation(image: Image.Image, res=512) -> Image.Image:
     logits = F.interpolate(logits, size=(h, w), mode="bilinear", align_corners=False)
     seg = logits.argmax(1)[0].cpu().numpy()
     return Image.fromarray(ADE_PALETTE[np.clip(seg, 0, len(ADE_PALETTE) - 1)].astype(np.uint8))
+
+
+# ---------------------------------------------------------------------------
+# OpenPose body (CMU 18-keypoint model: VGG stem + 6 two-branch stages, PAF
+# grouping) — the controlnet_aux OpenposeDetector default (body only)
+# ---------------------------------------------------------------------------
+def _openpose_stages():
+    from collections import OrderedDict
+
+    b0 = OrderedDict([("conv1_1", [3, 64, 3, 1, 1]), ("conv1_2", [64, 64, 3, 1, 1]), ("pool1_stage1", [2, 2, 0]),
+                      ("conv2_1", [64, 128, 3, 1, 1]), ("conv2_2", [128, 128, 3, 1, 1]), ("pool2_stage1", [2, 2, 0]),
+                      ("conv3_1", [128, 256, 3, 1, 1]), ("conv3_2", [256, 256, 3, 1, 1]),
+                      ("conv3_3", [256, 256, 3, 1, 1]), ("conv3_4", [256, 256, 3, 1, 1]), ("pool3_stage1", [2, 2, 0]),
+                      ("conv4_1", [256, 512, 3, 1, 1]), ("conv4_2", [512, 512, 3, 1, 1]),
+                      ("conv4_3_CPM", [512, 256, 3, 1, 1]), ("conv4_4_CPM", [256, 128, 3, 1, 1])])
+    blocks = {"model0": b0}
+    for br, cout in ((1, 38), (2, 19)):
+        blocks[f"model1_{br}"] = OrderedDict(
+            [(f"conv5_{i}_CPM_L{br}", [128, 128, 3, 1, 1]) for i in (1, 2, 3)]
+            + [(f"conv5_4_CPM_L{br}", [128, 512, 1, 1, 0]), (f"conv5_5_CPM_L{br}", [512, cout, 1, 1, 0])])
+        for st in range(2, 7):
+            blocks[f"model{st}_{br}"] = OrderedDict(
+                [(f"Mconv1_stage{st}_L{br}", [185, 128, 7, 1, 3])]
+                + [(f"Mconv{i}_stage{st}_L{br}", [128, 128, 7, 1, 3]) for i in (2, 3, 4, 5)]
+                + [(f"Mconv6_stage{st}_L{br}", [128, 128, 1, 1, 0]), (f"Mconv7_stage{st}_L{br}", [128, cout, 1, 1, 0])])
+    return blocks
+
+
+def _make_layers(block):
+    from collections import OrderedDict
+
+    layers = []
+    for name, v in block.items():
+        if "pool" in name:
+            layers.append((name, nn.MaxPool2d(v[0], v[1], v[2])))
+        else:
+            layers.append((name, nn.Conv2d(v[0], v[1], v[2], v[3], v[4])))
+            if not (name.startswith("conv5_5") or name.startswith("Mconv7")):  # the output convs: no ReLU
+                layers.append(("relu_" + name, nn.ReLU(inplace=True)))
+    return nn.Sequential(OrderedDict(layers))
+
+
+class BodyPoseModel(nn.Module):
+    def __init__(self):
+        super().__init__()
+        for k, b in _openpose_stages().items():
+            setattr(self, k, _make_layers(b))
+
+    def forward(self, x):
+        f = self.model0(x)
+        paf, heat = self.model1_1(f), self.model1_2(f)
+        for st in range(2, 7):
+            h = torch.cat([paf, heat, f], 1)
+            paf, heat = getattr(self, f"model{st}_1")(h), getattr(self, f"model{st}_2")(h)
+        return paf, heat
+
+    def load_state_dict(self, sd, strict=True):  # the published .pth keys lack the "modelX_Y." prefix
+        own = self.state_dict()
+        flat = {k.split(".", 1)[1]: k for k in own}
+        remapped = {flat.get(k, k): v for k, v in sd.items()}
+        return super().load_state_dict(remapped, strict=strict)
+
+
+_LIMBS = [[2, 3], [2, 6], [3, 4], [4, 5], [6, 7], [7, 8], [2, 9], [9, 10], [10, 11], [2, 12], [12, 13], [13, 14],
+          [2, 1], [1, 15], [15, 17], [1, 16], [16, 18], [3, 17], [6, 18]]
+_PAF_IDX = [[31, 32], [39, 40], [33, 34], [35, 36], [41, 42], [43, 44], [19, 20], [21, 22], [23, 24], [25, 26],
+            [27, 28], [29, 30], [47, 48], [49, 50], [53, 54], [51, 52], [55, 56], [37, 38], [45, 46]]
+_POSE_COLORS = [[255, 0, 0], [255, 85, 0], [255, 170, 0], [255, 255, 0], [170, 255, 0], [85, 255, 0], [0, 255, 0],
+                [0, 255, 85], [0, 255, 170], [0, 255, 255], [0, 170, 255], [0, 85, 255], [0, 0, 255], [85, 0, 255],
+                [170, 0, 255], [255, 0, 255], [255, 0, 170], [255, 0, 85]]
+
+
+def _pose_peaks(heat: np.ndarray, thre1=0.1):
+    from scipy import ndimage
+
+    peaks, pid = [], 0
+    for part in range(18):
+        m = heat[:, :, part]
+        s = ndimage.gaussian_filter(m, sigma=3)
+        c = s[1:-1, 1:-1]
+        ok = ((c >= s[1:-1, :-2]) & (c >= s[1:-1, 2:]) & (c >= s[:-2, 1:-1]) & (c >= s[2:, 1:-1]) & (c > thre1))
+        ys, xs = np.nonzero(ok)
+        ys, xs = ys + 1, xs + 1
+        peaks.append([(int(x), int(y), float(m[y, x]), pid + i) for i, (x, y) in enumerate(zip(xs, ys))])
+        pid += len(xs)
+    return peaks
+
+
+def _pose_group(peaks, paf: np.ndarray, img_h: int, thre2=0.05, mid_num=10):
+    """Part-affinity-field limb scoring + greedy person assembly (OpenPose)."""
+    conns, special = [], []
+    for k, (ia, ib) in enumerate(_LIMBS):
+        score_mid = paf[:, :, [x - 19 for x in _PAF_IDX[k]]]
+        ca, cb = peaks[ia - 1], peaks[ib - 1]
+        if not ca or not cb:
+            special.append(k)
+            conns.append(np.zeros((0, 5)))
+            continue
+        cand = []
+        for i, a in enumerate(ca):
+            for j, b in enumerate(cb):
+                vec = np.array([b[0] - a[0], b[1] - a[1]], np.float64)
+                norm = max(0.001, float(np.hypot(*vec)))
+                vec /= norm
+                xs = np.rint(np.linspace(a[0], b[0], mid_num)).astype(int)
+                ys = np.rint(np.linspace(a[1], b[1], mid_num)).astype(int)
+                sc = score_mid[ys, xs, 0] * vec[0] + score_mid[ys, xs, 1] * vec[1]
+                prior = sc.mean() + min(0.5 * img_h / norm - 1, 0)
+                if (sc > thre2).sum() > 0.8 * len(sc) and prior > 0:
+                    cand.append((i, j, prior, prior + a[2] + b[2]))
+        cand.sort(key=lambda c: c[2], reverse=True)
+        conn = np.zeros((0, 5))
+        for i, j, s, _ in cand:
+            if i not in conn[:, 3] and j not in conn[:, 4]:
+                conn = np.vstack([conn, [ca[i][3], cb[j][3], s, i, j]])
+                if len(conn) >= min(len(ca), len(cb)):
+                    break
+        conns.append(conn)
+    cands = np.array([p for part in peaks for p in part], np.float64).reshape(-1, 4)
+    subset = -np.ones((0, 20))
+    for k, (ia, ib) in enumerate(_LIMBS):
+        if k in special:
+            continue
+        A, B = ia - 1, ib - 1
+        for c in conns[k]:
+            pa, pb = c[0], c[1]
+            found = [j for j in range(len(subset)) if subset[j][A] == pa or subset[j][B] == pb][:2]
+            if len(found) == 1:
+                j = found[0]
+                if subset[j][B] != pb:
+                    subset[j][B] = pb
+                    subset[j][-1] += 1
+                    subset[j][-2] += cands[int(pb), 2] + c[2]
+            elif len(found) == 2:
+                j1, j2 = found
+                member = ((subset[j1] >= 0).astype(int) + (subset[j2] >= 0).astype(int))[:-2]
+                if not (member == 2).any():
+                    subset[j1][:-2] += subset[j2][:-2] + 1
+                    subset[j1][-2:] += subset[j2][-2:]
+                    subset[j1][-2] += c[2]
+                    subset = np.delete(subset, j2, 0)
+                else:
+                    subset[j1][B] = pb
+                    subset[j1][-1] += 1
+                    subset[j1][-2] += cands[int(pb), 2] + c[2]
+            elif k < 17:
+                row = -np.ones(20)
+                row[A], row[B] = pa, pb
+                row[-1] = 2
+                row[-2] = cands[[int(pa), int(pb)], 2].sum() + c[2]
+                subset = np.vstack([subset, row])
+    keep = [i for i in range(len(subset)) if subset[i][-1] >= 4 and subset[i][-2] / subset[i][-1] >= 0.4]
+    return cands, subset[keep]
+
+
+def _draw_pose(h, w, cands, subset):
+    """Skeleton canvas: limbs as filled 4-px sticks, joints as 4-px discs (OpenPose colours)."""
+    canvas = np.zeros((h, w, 3), np.float32)
+    yy, xx = np.mgrid[0:h, 0:w]
+    for k in range(17):
+        for person in subset:
+            idx = person[np.array(_LIMBS[k]) - 1]
+            if (idx < 0).any():
+                continue
+            (x0, y0), (x1, y1) = cands[int(idx[0]), :2], cands[int(idx[1]), :2]
+            d = np.array([x1 - x0, y1 - y0])
+            L2 = max(float(d @ d), 1e-6)
+            t = np.clip(((xx - x0) * d[0] + (yy - y0) * d[1]) / L2, 0, 1)
+            dist2 = (xx - (x0 + t * d[0])) ** 2 + (yy - (y0 + t * d[1])) ** 2
+            m = dist2 <= 16
+            canvas[m] = canvas[m] * 0.4 + np.array(_POSE_COLORS[k], np.float32) * 0.6
+    for part in range(18):
+        for person in subset:
+            i = int(person[part])
+            if i < 0:
+                continue
+            x, y = cands[i, :2]
+            m = (xx - x) ** 2 + (yy - y) ** 2 <= 16
+            canvas[m] = _POSE_COLORS[part]
+    return canvas.clip(0, 255).astype(np.uint8)
+
+
+@torch.no_grad()
+def openpose(image: Image.Image, res=512, boxsize=368, stride=8) -> Image.Image:
+    m = _build("openpose", BodyPoseModel)
+    img = np.asarray(_resize_short(image.convert("RGB"), res)).astype(np.float32)
+    H, W = img.shape[:2]
+    scale = boxsize / H
+    sh, sw = max(stride, int(round(H * scale))), max(stride, int(round(W * scale)))
+    test = np.asarray(Image.fromarray(img.astype(np.uint8)).resize((sw, sh), Image.Resampling.BICUBIC), np.float32)
+    ph, pw = (-sh) % stride, (-sw) % stride
+    test = np.pad(test, ((0, ph), (0, pw), (0, 0)), constant_values=128)
+    x = test[:, :, ::-1] / 256.0 - 0.5  # BGR, as the model was trained
+    paf, heat = m(_to_tensor(x, m))
+    out = []
+    for t in (heat, paf):
+        t = F.interpolate(t.float(), scale_factor=stride, mode="bicubic", align_corners=False)[:, :, :sh, :sw]
+        out.append(F.interpolate(t, size=(H, W), mode="bicubic", align_corners=False)[0].permute(1, 2, 0).cpu().numpy())
+    heat_np, paf_np = out
+    peaks = _pose_peaks(heat_np)
+    cands, subset = _pose_group(peaks, paf_np, H)
+    canvas = _draw_pose(H, W, cands, subset)
+    return Image.fromarray(canvas).resize(image.size, Image.Resampling.BILINEAR)

@@ -6,18 +6,19 @@ Dispatch on ``parameters.controlnet.type`` when ``preprocess`` is true:
               kernel on the GPU when a CUDA tensor path is requested, numpy on CPU
   tile     -> resize so the short side is a multiple of 64 (reference image_to_tile)
   shuffle  -> content shuffle (random smooth flow warp, seeded)
-  scribble / softedge / lineart / mlsd / depth / seg -> neural annotators
-              (controlnet/annotators.py: HED, informative-drawings lineart,
-              M-LSD, DPT-Large, UperNet-ConvNeXt), resident per process
-  normalbae / openpose -> not available on this worker: ValueError -> fatal
-              job error, like an incompatible model
+  scribble / softedge / lineart / mlsd / depth / seg / openpose -> neural
+              annotators (controlnet/annotators.py: HED, informative-drawings
+              lineart, M-LSD, DPT-Large, UperNet-ConvNeXt, OpenPose body),
+              resident per process
+  normalbae -> not available on this worker: ValueError -> fatal job error,
+              like an incompatible model
 """
 from __future__ import annotations
 
 import numpy as np
 from PIL import Image
 
-UNAVAILABLE = {"normalbae", "openpose"}
+UNAVAILABLE = {"normalbae"}
 
 
 def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
@@ -32,7 +33,7 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
         return content_shuffle(image)
     if t == "pix2pix":
         return image
-    if t in ("scribble", "softedge", "lineart", "mlsd", "depth", "seg"):
+    if t in ("scribble", "softedge", "lineart", "mlsd", "depth", "seg", "openpose"):
         from . import annotators as an
 
         if t == "scribble":
@@ -45,6 +46,8 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
             return an.mlsd(image)
         if t == "depth":
             return an.depth(image)
+        if t == "openpose":
+            return an.openpose(image)
         return an.segmentation(image)
     if t in UNAVAILABLE:
         raise ValueError(f"controlnet preprocessor '{t}' is not available on this worker")

@@ -72,4 +72,42 @@ def test_scribble_nms_keeps_thin_ridges():
 
 def test_unavailable_types_are_fatal():
     with pytest.raises(ValueError):
-        preprocess_image(_img(), {"preprocess": True, "type": "openpose"})
+        preprocess_image(_img(), {"preprocess": True, "type": "normalbae"})
+
+
+def test_openpose_end_to_end_shape():
+    out = preprocess_image(_img(), {"preprocess": True, "type": "openpose"})
+    assert out.size == (96, 80) and out.mode == "RGB"
+
+
+def test_openpose_checkpoint_key_layout():
+    """body_pose_model.pth stores flat layer names (conv1_1.weight, Mconv7_stage6_L2.bias, ...)."""
+    m = an.BodyPoseModel()
+    flat = {k.split(".", 1)[1]: torch.randn_like(v) for k, v in m.state_dict().items()}
+    assert "conv1_1.weight" in flat and "Mconv7_stage6_L2.bias" in flat
+    missing, unexpected = m.load_state_dict(flat, strict=False)
+    assert not missing and not unexpected
+    assert torch.equal(m.model6_2.Mconv7_stage6_L2.bias, flat["Mconv7_stage6_L2.bias"])
+
+
+def test_openpose_paf_grouping_one_arm():
+    """Peaks for neck -> right shoulder -> elbow -> wrist joined by part-affinity
+    fields pointing along each limb assemble into one 4-part person."""
+    H = W = 64
+    heat = np.zeros((H, W, 19), np.float32)
+    paf = np.zeros((H, W, 38), np.float32)
+    pts = {1: (20, 20), 2: (30, 20), 3: (40, 28), 4: (48, 38)}  # part index (0-based) -> (x, y)
+    yy, xx = np.mgrid[0:H, 0:W]
+    for p, (x, y) in pts.items():
+        heat[:, :, p] = np.exp(-((xx - x) ** 2 + (yy - y) ** 2) / 8.0)
+    for k, (a, b) in ((0, (1, 2)), (2, (2, 3)), (3, (3, 4))):
+        v = np.subtract(pts[b], pts[a]).astype(np.float32)
+        v /= np.linalg.norm(v)
+        c0, c1 = [x - 19 for x in an._PAF_IDX[k]]
+        paf[:, :, c0], paf[:, :, c1] = v[0], v[1]
+    peaks = an._pose_peaks(heat)
+    assert [len(peaks[p]) for p in (1, 2, 3, 4)] == [1, 1, 1, 1]
+    cands, subset = an._pose_group(peaks, paf, H)
+    assert len(subset) == 1 and subset[0][-1] == 4
+    canvas = an._draw_pose(H, W, cands, subset)
+    assert canvas.shape == (H, W, 3) and canvas.any()
