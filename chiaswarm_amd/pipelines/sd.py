@@ -34,6 +34,7 @@ from ..models import vae as vae_mod
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
 from ..schedulers import Scheduler, get_scheduler
+from ..utils.trace import trace_range
 
 
 @dataclasses.dataclass
@@ -298,7 +299,8 @@ class StableDiffusion:
             cross_kv = self.unet.encode_context(ctx)
         else:
             # text encoders + cross-attention K/V in one hipGraph replay on the GPU
-            ctx, added, cross_kv = self.encode(prompts, negs, cfg)
+            with trace_range("text_encode"):
+                ctx, added, cross_kv = self.encode(prompts, negs, cfg)
             cross_kv = list(cross_kv)
         # K/V are the text graph's static outputs (rewritten in place per request)
         self._kv_static = (not is_pix2pix) and self.use_graphs and hasattr(self, "_text_graphs") and \
@@ -355,15 +357,17 @@ class StableDiffusion:
                                                     ctx, controlnet_conditioning_scale, self.dtype)
         timings["prepare"] = time.perf_counter() - t0 - timings["text_encode"]
         t1 = time.perf_counter()
-        x = self.denoise(x, sched, cross_kv, guidance_scale, added, generator,
-                         image_latents=image_latents, image_guidance=img_guid,
-                         mask=mask_t, init_latents=init_latents, noise=noise, controlnet_fn=controlnet_fn)
-        self._phase_sync()
+        with trace_range("denoise"):
+            x = self.denoise(x, sched, cross_kv, guidance_scale, added, generator,
+                             image_latents=image_latents, image_guidance=img_guid,
+                             mask=mask_t, init_latents=init_latents, noise=noise, controlnet_fn=controlnet_fn)
+            self._phase_sync()
         timings["denoise"] = time.perf_counter() - t1
         if output_type == "latent":
             return PipelineOutput([], [False] * b, x, timings)
         t2 = time.perf_counter()
-        imgs = self.decode(x, to_host=False)
+        with trace_range("vae_decode"):
+            imgs = self.decode(x, to_host=False)
         nsfw = [False] * b
         if self.safety_checker is not None:  # on the device, before the D2H copy
             nsfw, imgs = self.safety_checker(imgs)

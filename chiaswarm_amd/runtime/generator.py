@@ -16,6 +16,7 @@ import time
 from .. import __version__
 from ..jobs.router import format_args
 from ..output.processor import image_from_text, image_to_buffer, make_result, make_text_result
+from ..utils.trace import trace_range
 
 
 async def do_work(job, device):
@@ -47,7 +48,8 @@ def synchronous_do_work_function(job, device):
         logging.exception(e)
         return _error_result(job_id, e, content_type, True)
     try:
-        artifacts, pipeline_config = device(worker_function, **kwargs)
+        with trace_range(f"job {job_id}"):
+            artifacts, pipeline_config = device(worker_function, **kwargs)
     except ValueError as e:  # (b) fatal
         logging.exception(e)
         return _error_result(job_id, e, content_type, True)

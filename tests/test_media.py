@@ -115,3 +115,18 @@ def test_type_helpers_and_device_pool():
 
     with pytest.raises(RuntimeError):
         device_pool.remove_device_from_pool()
+
+
+def test_roctx_ranges_are_safe_without_a_profiler():
+    from chiaswarm_amd.utils import trace
+
+    old = trace.enabled()
+    try:
+        trace.set_enabled(True)
+        with trace.trace_range("unit-test"):
+            trace.mark("inside")
+        trace.set_enabled(False)
+        with trace.trace_range("disabled"):
+            pass
+    finally:
+        trace.set_enabled(old)
