@@ -550,7 +550,20 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
     if (variant >= 2 || (variant == 0 && Skv > 128)) {
-      if (variant == 0) variant = 5;  // PRE+ONES: 279 vs 283 (PRE) vs 306 us (plain) at B8 S4096 H5, same box
+      // PRE+ONES: 279 vs 283 (PRE) vs 306 us (plain) at B8 S4096 H5, same box; for
+      // short grids (< 1024 workgroups of 128 rows: S1024 H10) 64-row workgroups
+      // fill the chip better (55 vs 58 us)
+      if (variant == 0) variant = ((long long)B * H * ((Sq + 127) / 128) < 1024) ? 7 : 5;
+      if (variant == 6) {  // 48 query rows per wave (QT = 3): more MFMA work per K/V block and barrier
+        const dim3 grid3(B * H * ((Sq + 191) / 192));
+        attn_fwd_pipe_kernel<3, true, true><<<grid3, 256, 0, stream>>>(a);
+        return (int)hipGetLastError();
+      }
+      if (variant == 7) {  // 16 query rows per wave (QT = 1): twice the workgroups for short sequences
+        const dim3 grid1(B * H * ((Sq + 63) / 64));
+        attn_fwd_pipe_kernel<1, true, true><<<grid1, 256, 0, stream>>>(a);
+        return (int)hipGetLastError();
+      }
       const int nqb = (Sq + 127) / 128;
       const dim3 grid(B * H * nqb);
       switch (variant) {
