@@ -58,8 +58,8 @@ def _gn_part(M, N, seg, device):
     return torch.empty((M // seg) * N * 2, dtype=torch.float32, device=device)
 sig("csk_axpby", c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p)
 ACT.update({"lrelu": 5, "lrelu0.1": 6, "tanh": 7, "relu": 8, "lrelu0.01": 9, "elu": 10, "gelu_tanh": 11})
-sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_float, c_int, c_int, c_void_p)
+sig("csk_group_norm", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_float, c_int, c_int, c_void_p)
 sig("csk_layer_norm", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 ATTN_VARIANT = int(os.environ.get("CSK_ATTN", "0"))  # 0 auto, 1 plain, 2 pipelined (D <= 64)
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
@@ -328,7 +328,7 @@ def group_norm(x, gamma, beta, groups, eps, silu):
                       B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), bstride, _s())
             return y
     part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
-    _lib.call("csk_group_norm", _p(y), _p(x), _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
+    _lib.call("csk_group_norm", _p(y), _p(x), None, 0, _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
               float(eps), int(bool(silu)), bstride, _s())
     return y
 
@@ -340,26 +340,32 @@ def group_norm_cat(a, b, gamma, beta, groups, eps, silu):
     returns None otherwise (the caller concatenates)."""
     sa, sb = getattr(a, "_csk_gn", None), getattr(b, "_csk_gn", None)
     GN_CAT_STATS[1] += 1
-    if sa is None or sb is None or sa[1] != sb[1] or a.shape[:-1] != b.shape[:-1]:
-        return None
-    if not (a.is_contiguous() and b.is_contiguous()) or a.shape[-1] % 8 or gamma.dim() != 1:
+    if a.shape[:-1] != b.shape[:-1] or not (a.is_contiguous() and b.is_contiguous()):
         return None
     B, Ca, Cb = a.shape[0], a.shape[-1], b.shape[-1]
     C = Ca + Cb
     P = a.numel() // (B * Ca)
-    seg = sa[1]
-    nseg = sa[0].numel() // (2 * Ca)
-    if P % seg or nseg * 2 * Cb != sb[0].numel() or C % groups or C > 4096:
+    if Ca % 8 or Cb % 8 or gamma.dim() != 1 or C % groups or C > 4096:
         return None
-    part = torch.cat([sa[0].view(nseg, Ca, 2), sb[0].view(nseg, Cb, 2)], 1).view(-1)
     rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
     chunk = max(4 * rows, -(-P * B // 1024))
     nchunk = -(-P // chunk)
     chunk = -(-P // nchunk)
     y = torch.empty(a.shape[:-1] + (C,), dtype=torch.bfloat16, device=a.device)
-    stat = torch.empty(B * groups * 2, dtype=torch.float32, device=a.device)
-    _lib.call("csk_group_norm_part", _p(y), _p(a), _p(b), Ca, _p(part), seg, _p(stat), _p(gamma), _p(beta),
-              B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), 0, _s())
+    fused = sa is not None and sb is not None and sa[1] == sb[1] and P % sa[1] == 0
+    if fused:
+        seg = sa[1]
+        nseg = sa[0].numel() // (2 * Ca)
+        fused = nseg * 2 * Cb == sb[0].numel()
+    if fused:  # both producers emitted epilogue statistics: merge them
+        part = torch.cat([sa[0].view(nseg, Ca, 2), sb[0].view(nseg, Cb, 2)], 1).view(-1)
+        stat = torch.empty(B * groups * 2, dtype=torch.float32, device=a.device)
+        _lib.call("csk_group_norm_part", _p(y), _p(a), _p(b), Ca, _p(part), seg, _p(stat), _p(gamma), _p(beta),
+                  B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), 0, _s())
+    else:  # statistics pass over both tensors in place (e.g. a split-K producer)
+        part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=a.device)
+        _lib.call("csk_group_norm", _p(y), _p(a), _p(b), Ca, _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk,
+                  nchunk, float(eps), int(bool(silu)), 0, _s())
     GN_CAT_STATS[0] += 1
     return y
 

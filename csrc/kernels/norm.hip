@@ -52,12 +52,14 @@ static inline size_t gn_stats_lds(int C) {
   return (size_t)(GN_THREADS / NVT) * 2 * C * sizeof(float);
 }
 __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
-                                                              int P, int C, int G, int chunk, int nchunk) {
+                                                              int P, int C, int G, int chunk, int nchunk,
+                                                              const bf16_t* __restrict__ x2 = nullptr, int C1 = 0) {
+  // x2 != null: statistics of the channel concat [x (C1) | x2 (C - C1)] read in place
   extern __shared__ float red[];  // [R][2][C]: per-row partials, reduced in a fixed order (deterministic)
   const int b = blockIdx.y, ck = blockIdx.x, tid = threadIdx.x;
   const GnLayout L(C, tid);
   const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
-  const bf16_t* xb = x + (size_t)b * P * C;
+  if (!x2) C1 = C;
   float s[2][8], ss[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -68,13 +70,16 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const bf16_t* __re
     for (int u = 0; u < 2; ++u) {
       const int v = L.cv + u * L.NVT;
       if (u < L.TPV && v < L.NV) {
+        const bool second = v * 8 >= C1;
+        const int xst = second ? C - C1 : C1;
+        const bf16_t* xsrc = (second ? x2 : x) + (size_t)b * P * xst + (second ? v * 8 - C1 : v * 8);
         for (int p = p0 + L.r; p < p1; p += GN_UNROLL * L.R) {
           // unconditional loads from clamped rows (a select around each load would
           // make hipcc wait vmcnt(0) per element); out-of-chunk rows are masked
           uint4 q[GN_UNROLL];
 #pragma unroll
           for (int w = 0; w < GN_UNROLL; ++w)
-            q[w] = *reinterpret_cast<const uint4*>(xb + (size_t)min(p + w * L.R, p1 - 1) * C + v * 8);
+            q[w] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p + w * L.R, p1 - 1) * xst);
 #pragma unroll
           for (int w = 0; w < GN_UNROLL; ++w) {
             const float mk = (p + w * L.R < p1) ? 1.f : 0.f;
@@ -387,25 +392,28 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, 
 }
 
 // part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
-CSK_API int csk_group_norm(void* y, const void* x, void* part, const void* gamma, const void* beta, int B, int P, int C,
-                           int G, int chunk, int nchunk, float eps, int silu, int affine_bstride,
-                           hipStream_t stream) {
+// x2 / C1: optional second input (channel concat [x | x2] read in place, x has C1 channels)
+CSK_API int csk_group_norm(void* y, const void* x, const void* x2, int C1, void* part, const void* gamma,
+                           const void* beta, int B, int P, int C, int G, int chunk, int nchunk, float eps, int silu,
+                           int affine_bstride, hipStream_t stream) {
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0) return (int)hipErrorInvalidValue;
+  if (x2 && (C1 <= 0 || C1 >= C || C1 % 8 != 0)) return (int)hipErrorInvalidValue;
   float* pt = (float*)part;
   float* st = pt + (size_t)B * nchunk * G * 3;
   dim3 grid(nchunk, B);
-  gn_stats_kernel<<<grid, GN_THREADS, gn_stats_lds(C), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk);
+  gn_stats_kernel<<<grid, GN_THREADS, gn_stats_lds(C), stream>>>((const bf16_t*)x, pt, P, C, G, chunk, nchunk,
+                                                                 (const bf16_t*)x2, C1);
   if (G <= 64 && nchunk * G <= g_gn_prologue_max) {  // few partials: merge them in the apply prologue (no finalize launch)
     gn_apply_kernel<1><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, pt, (const bf16_t*)gamma,
                                                         (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride,
-                                                        nchunk, 0, eps);
+                                                        nchunk, 0, eps, (const bf16_t*)x2, C1);
     CSK_CHECK_LAUNCH();
   }
   gn_finalize_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(pt, st, B, G,
                                                                                                   nchunk, eps);
   gn_apply_kernel<0><<<grid, GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st, (const bf16_t*)gamma,
                                                       (const bf16_t*)beta, P, C, G, chunk, silu, affine_bstride, 0,
-                                                      0, eps);
+                                                      0, eps, (const bf16_t*)x2, C1);
   CSK_CHECK_LAUNCH();
 }
 

@@ -376,3 +376,14 @@ def test_group_norm_of_concat_in_place(gpu):
         pytest.skip("segment heights differ")
     ref = ops._ref_group_norm(torch.cat([a, b], -1).float().cpu(), g.float().cpu(), bt.float().cpu(), 32, 1e-5, True)
     assert rel_err(y.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("Ca,Cb", [(640, 320), (1280, 1280)])
+def test_group_norm_of_concat_without_fused_stats(gpu, Ca, Cb):
+    """Concat inputs without epilogue statistics (split-K producers): the
+    statistics pass reads both tensors in place too."""
+    a, b = rnd(2, 16, 16, Ca, dev=gpu, scale=2.0) + 1.0, rnd(2, 16, 16, Cb, dev=gpu)
+    g, bt = rnd(Ca + Cb, dev=gpu), rnd(Ca + Cb, dev=gpu)
+    y = hip_ops.group_norm_cat(a, b, g, bt, 32, 1e-5, True)
+    ref = ops._ref_group_norm(torch.cat([a, b], -1).float().cpu(), g.float().cpu(), bt.float().cpu(), 32, 1e-5, True)
+    assert rel_err(y.cpu(), ref) < 1e-2
