@@ -9,6 +9,7 @@ which calls controlnet_aux / transformers detectors):
   depth     -> DPT-Large (ViT-L/16 + reassemble/fusion neck + depth head)
   seg       -> UperNet + ConvNeXt backbone, ADE20K palette
   openpose  -> CMU body-pose model (18 keypoints, PAF grouping), skeleton canvas
+  normalbae -> surface normals: EfficientNet-B5 encoder + MLP-refined decoder (NNET)
 
 Module and parameter names follow the public checkpoints (controlnet_aux .pth
 files / transformers safetensors) so real weights load unchanged from
@@ -42,6 +43,7 @@ _FILES = {
     "depth": ["dpt-large.safetensors", "dpt-large/model.safetensors"],
     "seg": ["upernet-convnext-small.safetensors", "upernet-convnext-small/model.safetensors"],
     "openpose": ["body_pose_model.pth", "openpose.safetensors"],
+    "normalbae": ["scannet.pt", "normalbae.safetensors"],
 }
 
 
@@ -64,8 +66,9 @@ def load_checkpoint(path: str) -> dict:
 
         return load_file(path, device="cpu")
     sd = torch.load(path, map_location="cpu", weights_only=True)  # never unpickles code
-    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
-        sd = sd["state_dict"]
+    for key in ("state_dict", "model"):  # scannet.pt nests its weights under "model"
+        if isinstance(sd, dict) and key in sd and isinstance(sd[key], dict):
+            sd = sd[key]
     return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
 
 
@@ -950,3 +953,189 @@ def openpose(image: Image.Image, res=512, boxsize=368, stride=8) -> Image.Image:
     cands, subset = _pose_group(peaks, paf_np, H)
     canvas = _draw_pose(H, W, cands, subset)
     return Image.fromarray(canvas).resize(image.size, Image.Resampling.BILINEAR)
+
+
+# ---------------------------------------------------------------------------
+# NormalBae (Bae et al. 2021 surface-normal net "NNET", the controlnet_aux
+# NormalBaeDetector, checkpoint scannet.pt): EfficientNet-B5 (TF "same"
+# padding, AP weights) encoder + UpSampleBN decoder, coarse-to-fine per-pixel
+# MLP refinement at 1/4, 1/2 and 1/1 resolution.  In eval every pixel is
+# refined (no uncertainty-guided point sampling, which only trains).
+# ---------------------------------------------------------------------------
+class _Conv2dSame(nn.Conv2d):
+    """TF 'same' padding for strided convs (pad split low/high, extra on the high side)."""
+
+    def forward(self, x):
+        ih, iw = x.shape[-2:]
+        kh, kw = self.weight.shape[-2:]
+        sh, sw = self.stride
+        ph = max((math.ceil(ih / sh) - 1) * sh + kh - ih, 0)
+        pw = max((math.ceil(iw / sw) - 1) * sw + kw - iw, 0)
+        if ph or pw:
+            x = F.pad(x, [pw // 2, pw - pw // 2, ph // 2, ph - ph // 2])
+        return F.conv2d(x, self.weight, self.bias, self.stride, 0, self.dilation, self.groups)
+
+
+def _tf_conv(cin, cout, k, stride=1, groups=1, bias=False):
+    if stride == 1:
+        return nn.Conv2d(cin, cout, k, 1, k // 2, groups=groups, bias=bias)
+    return _Conv2dSame(cin, cout, k, stride, 0, groups=groups, bias=bias)
+
+
+def _bn_tf(c):
+    return nn.BatchNorm2d(c, eps=1e-3)
+
+
+class _SE(nn.Module):
+    def __init__(self, c, rd):
+        super().__init__()
+        self.conv_reduce = nn.Conv2d(c, rd, 1)
+        self.conv_expand = nn.Conv2d(rd, c, 1)
+
+    def forward(self, x):
+        s = F.silu(self.conv_reduce(x.mean((2, 3), keepdim=True)))
+        return x * torch.sigmoid(self.conv_expand(s))
+
+
+class _DSConv(nn.Module):
+    """Depthwise-separable block (EfficientNet stage 0)."""
+
+    def __init__(self, cin, cout, k):
+        super().__init__()
+        self.conv_dw, self.bn1 = _tf_conv(cin, cin, k, groups=cin), _bn_tf(cin)
+        self.se = _SE(cin, max(1, int(cin * 0.25 + 0.5)))
+        self.conv_pw, self.bn2 = nn.Conv2d(cin, cout, 1, bias=False), _bn_tf(cout)
+        self.skip = cin == cout
+
+    def forward(self, x):
+        h = self.bn2(self.conv_pw(self.se(F.silu(self.bn1(self.conv_dw(x))))))
+        return x + h if self.skip else h
+
+
+class _IRBlock(nn.Module):
+    """Inverted residual (MBConv) with squeeze-excite sized from the block input."""
+
+    def __init__(self, cin, cout, k, stride, expand=6):
+        super().__init__()
+        mid = cin * expand
+        self.conv_pw, self.bn1 = nn.Conv2d(cin, mid, 1, bias=False), _bn_tf(mid)
+        self.conv_dw, self.bn2 = _tf_conv(mid, mid, k, stride, groups=mid), _bn_tf(mid)
+        self.se = _SE(mid, max(1, int(cin * 0.25 + 0.5)))
+        self.conv_pwl, self.bn3 = nn.Conv2d(mid, cout, 1, bias=False), _bn_tf(cout)
+        self.skip = stride == 1 and cin == cout
+
+    def forward(self, x):
+        h = F.silu(self.bn1(self.conv_pw(x)))
+        h = self.se(F.silu(self.bn2(self.conv_dw(h))))
+        h = self.bn3(self.conv_pwl(h))
+        return x + h if self.skip else h
+
+
+class EfficientNetB5(nn.Module):
+    """tf_efficientnet_b5_ap trunk (channel x1.6, depth x2.2); classifier removed."""
+
+    # (kernel, stride, expand, channels, repeats) after width/depth scaling
+    STAGES = ((3, 1, 1, 24, 3), (3, 2, 6, 40, 5), (5, 2, 6, 64, 5), (3, 2, 6, 128, 7), (5, 1, 6, 176, 7),
+              (5, 2, 6, 304, 9), (3, 1, 6, 512, 3))
+
+    def __init__(self, stem=48, head=2048):
+        super().__init__()
+        self.conv_stem, self.bn1 = _tf_conv(3, stem, 3, 2), _bn_tf(stem)
+        stages, cin = [], stem
+        for k, s, e, c, r in self.STAGES:
+            blocks = []
+            for i in range(r):
+                blocks.append(_DSConv(cin, c, k) if e == 1 else _IRBlock(cin, c, k, s if i == 0 else 1, e))
+                cin = c
+            stages.append(nn.Sequential(*blocks))
+        self.blocks = nn.Sequential(*stages)
+        self.conv_head, self.bn2 = nn.Conv2d(cin, head, 1, bias=False), _bn_tf(head)
+
+    def features(self, x):
+        """The decoder's taps: stage 0/1/2/4 outputs and the (pre-BN) conv_head output."""
+        h = F.silu(self.bn1(self.conv_stem(x)))
+        taps = []
+        for i, st in enumerate(self.blocks):
+            h = st(h)
+            if i in (0, 1, 2, 4):
+                taps.append(h)
+        taps.append(self.conv_head(h))
+        return taps
+
+
+class _NormalEncoder(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.original_model = EfficientNetB5()
+
+
+class _UpSampleBN(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self._net = nn.Sequential(nn.Conv2d(cin, cout, 3, 1, 1), nn.BatchNorm2d(cout), nn.LeakyReLU(),
+                                  nn.Conv2d(cout, cout, 3, 1, 1), nn.BatchNorm2d(cout), nn.LeakyReLU())
+
+    def forward(self, x, skip):
+        x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=True)
+        return self._net(torch.cat([x, skip], 1))
+
+
+def _pixel_mlp(cin):
+    return nn.Sequential(nn.Conv1d(cin, 128, 1), nn.ReLU(), nn.Conv1d(128, 128, 1), nn.ReLU(),
+                         nn.Conv1d(128, 128, 1), nn.ReLU(), nn.Conv1d(128, 4, 1))
+
+
+def _norm_normalize(out, min_kappa=0.01):
+    n, kappa = out[:, :3], out[:, 3:]
+    n = n / (n.float().pow(2).sum(1, keepdim=True).sqrt() + 1e-10).to(n.dtype)
+    return torch.cat([n, F.elu(kappa) + 1.0 + min_kappa], 1)
+
+
+class _NormalDecoder(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv2 = nn.Conv2d(2048, 2048, 1)
+        self.up1, self.up2 = _UpSampleBN(2048 + 176, 1024), _UpSampleBN(1024 + 64, 512)
+        self.up3, self.up4 = _UpSampleBN(512 + 40, 256), _UpSampleBN(256 + 24, 128)
+        self.out_conv_res8 = nn.Conv2d(512, 4, 3, 1, 1)
+        self.out_conv_res4, self.out_conv_res2, self.out_conv_res1 = _pixel_mlp(516), _pixel_mlp(260), _pixel_mlp(132)
+
+    @staticmethod
+    def _refine(mlp, coarse, feat):
+        up = lambda t: F.interpolate(t, scale_factor=2, mode="bilinear", align_corners=True)
+        pred, feat = up(coarse), up(feat)
+        B, _, H, W = pred.shape
+        return _norm_normalize(mlp(torch.cat([pred, feat], 1).view(B, -1, H * W)).view(B, 4, H, W))
+
+    def forward(self, taps):
+        b0, b1, b2, b3, b4 = taps
+        d1 = self.up1(self.conv2(b4), b3)
+        d2 = self.up2(d1, b2)
+        d3 = self.up3(d2, b1)
+        d4 = self.up4(d3, b0)
+        r8 = _norm_normalize(self.out_conv_res8(d2))
+        r4 = self._refine(self.out_conv_res4, r8, d2)
+        r2 = self._refine(self.out_conv_res2, r4, d3)
+        r1 = self._refine(self.out_conv_res1, r2, d4)
+        return [r8, r4, r2, r1]
+
+
+class NormalBaeNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.encoder = _NormalEncoder()
+        self.decoder = _NormalDecoder()
+
+    def forward(self, x):
+        return self.decoder(self.encoder.original_model.features(x))
+
+
+@torch.no_grad()
+def normalbae(image: Image.Image, res=512) -> Image.Image:
+    m = _build("normalbae", NormalBaeNet)
+    img = np.asarray(_resize_short(image.convert("RGB"), res)).astype(np.float32) / 255.0
+    x = (img - np.array([0.485, 0.456, 0.406], np.float32)) / np.array([0.229, 0.224, 0.225], np.float32)
+    normal = m(_to_tensor(x, m))[-1][0, :3].float()
+    normal = ((normal + 1) * 0.5).clamp(0, 1).permute(1, 2, 0).cpu().numpy()
+    out = (normal * 255.0).clip(0, 255).astype(np.uint8)
+    return Image.fromarray(out).resize(image.size, Image.Resampling.BILINEAR)

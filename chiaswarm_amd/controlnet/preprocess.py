@@ -6,11 +6,11 @@ Dispatch on ``parameters.controlnet.type`` when ``preprocess`` is true:
               kernel on the GPU when a CUDA tensor path is requested, numpy on CPU
   tile     -> resize so the short side is a multiple of 64 (reference image_to_tile)
   shuffle  -> content shuffle (random smooth flow warp, seeded)
-  scribble / softedge / lineart / mlsd / depth / seg / openpose -> neural
-              annotators (controlnet/annotators.py: HED, informative-drawings
-              lineart, M-LSD, DPT-Large, UperNet-ConvNeXt, OpenPose body),
-              resident per process
-  normalbae -> not available on this worker: ValueError -> fatal job error,
+  scribble / softedge / lineart / mlsd / depth / seg / openpose / normalbae
+           -> neural annotators (controlnet/annotators.py: HED, informative-
+              drawings lineart, M-LSD, DPT-Large, UperNet-ConvNeXt, OpenPose
+              body, NormalBae NNET), resident per process
+  a type listed in UNAVAILABLE (none today) -> ValueError -> fatal job error,
               like an incompatible model
 """
 from __future__ import annotations
@@ -18,7 +18,7 @@ from __future__ import annotations
 import numpy as np
 from PIL import Image
 
-UNAVAILABLE = {"normalbae"}
+UNAVAILABLE: set = set()
 
 
 def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
@@ -33,7 +33,7 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
         return content_shuffle(image)
     if t == "pix2pix":
         return image
-    if t in ("scribble", "softedge", "lineart", "mlsd", "depth", "seg", "openpose"):
+    if t in ("scribble", "softedge", "lineart", "mlsd", "depth", "seg", "openpose", "normalbae"):
         from . import annotators as an
 
         if t == "scribble":
@@ -48,6 +48,8 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
             return an.depth(image)
         if t == "openpose":
             return an.openpose(image)
+        if t == "normalbae":
+            return an.normalbae(image)
         return an.segmentation(image)
     if t in UNAVAILABLE:
         raise ValueError(f"controlnet preprocessor '{t}' is not available on this worker")

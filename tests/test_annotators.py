@@ -70,9 +70,44 @@ def test_scribble_nms_keeps_thin_ridges():
     assert y[:, 20].all() and not y[:, 10].any()
 
 
-def test_unavailable_types_are_fatal():
+def test_unknown_types_are_fatal():
     with pytest.raises(ValueError):
-        preprocess_image(_img(), {"preprocess": True, "type": "normalbae"})
+        preprocess_image(_img(), {"preprocess": True, "type": "no-such-annotator"})
+
+
+def test_normalbae_end_to_end_shape():
+    out = preprocess_image(_img(), {"preprocess": True, "type": "normalbae"})
+    assert out.size == (96, 80) and out.mode == "RGB"
+
+
+def test_normalbae_architecture_and_key_layout():
+    """tf_efficientnet_b5 trunk (39 blocks, 2048-ch head) + NNET decoder, with
+    the scannet.pt key names; outputs are unit normals at 1/8..1/1 resolution."""
+    m = an.NormalBaeNet().eval()
+    sd = m.state_dict()
+    for k in ("encoder.original_model.conv_stem.weight", "encoder.original_model.blocks.0.0.se.conv_reduce.weight",
+              "encoder.original_model.blocks.6.2.conv_pwl.weight", "encoder.original_model.conv_head.weight",
+              "decoder.up1._net.0.weight", "decoder.out_conv_res1.6.weight"):
+        assert k in sd, k
+    assert sum(len(s) for s in m.encoder.original_model.blocks) == 39
+    assert sd["encoder.original_model.blocks.1.0.se.conv_reduce.weight"].shape == (6, 144, 1, 1)
+    assert sd["decoder.out_conv_res4.0.weight"].shape == (128, 516, 1)
+    with torch.no_grad():
+        outs = m(torch.randn(1, 3, 64, 96))
+    assert [tuple(o.shape[2:]) for o in outs] == [(8, 12), (16, 24), (32, 48), (64, 96)]
+    n = outs[-1][0, :3].norm(dim=0)
+    assert torch.allclose(n, torch.ones_like(n), atol=1e-4)
+    assert (outs[-1][:, 3] > 0).all()  # kappa = elu + 1 + 0.01
+
+
+def test_normalbae_same_padding_matches_tf():
+    """Stride-2 'same' conv pads (k - s) split low/high with the extra row/column high."""
+    c = an._Conv2dSame(1, 1, 3, 2, 0, bias=False)
+    torch.nn.init.ones_(c.weight)
+    y = c(torch.ones(1, 1, 6, 6))
+    assert y.shape[2:] == (3, 3)
+    # no padding on the low side (first window fully inside); one zero row/column on the high side
+    assert y[0, 0, 0, 0].item() == 9.0 and y[0, 0, 2, 2].item() == 4.0 and y[0, 0, 0, 2].item() == 6.0
 
 
 def test_openpose_end_to_end_shape():

@@ -131,6 +131,16 @@ def test_layer_norm(gpu, C):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("rows,C", [(32768, 320), (4099, 640), (4101, 512), (5000, 96)])
+def test_layer_norm_multirow(gpu, rows, C):
+    """Four-rows-per-wave kernel (C <= 512, many rows), incl. a ragged tail."""
+    x = rnd(rows, C, dev=gpu, scale=2.0) + 1.0
+    g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
+    y = hip_ops.layer_norm(x, g, b, 1e-5)
+    ref = F.layer_norm(x.float(), (C,), g.float(), b.float(), 1e-5)
+    assert rel_err(y, ref) < 1e-2
+
+
 def _attn_ref(q, k, v, scale, causal):
     return ops._ref_attention(q.float().cpu(), k.float().cpu(), v.float().cpu(), scale, causal)
 

@@ -187,7 +187,7 @@ def test_tiny_cascades_gpu(gpu):
     assert o[0].size == (128, 128)
 
 
-@pytest.mark.parametrize("kind", ["scribble", "lineart", "mlsd", "depth", "seg", "openpose"])
+@pytest.mark.parametrize("kind", ["scribble", "lineart", "mlsd", "depth", "seg", "openpose", "normalbae"])
 def test_controlnet_annotators_on_gpu(gpu, kind, tmp_path, monkeypatch):
     """Neural annotators run resident on the GPU in bf16 (random init offline)."""
     import numpy as np
