@@ -51,7 +51,9 @@ def _gn_seg(tile, split, rows_per_b, M, code):
     bm, bn = tuning.TILES.get(tile, (0, 0))
     if split != 1 or code == 3 or bm == 0 or rows_per_b <= 0 or rows_per_b % bm or M % bm:
         return 0
-    return bm * bn // 256 if GN_FINE else bm
+    seg = bm * bn // 256 if GN_FINE else bm
+    band = bm // 2 if (bm > 128 or bn == 160) else bm  # epilogue row band (gemm_common.h epi_passes, WM = 2)
+    return min(seg, band)
 
 
 def _gn_part(M, N, seg, device):

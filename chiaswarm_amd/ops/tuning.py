@@ -28,7 +28,9 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64),
          18: (64, 64), 19: (128, 64), 20: (64, 128),
          # persistent continuous-ring LDS-DMA variants (K % 64 == 0, no split-K)
-         21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64)}
+         21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64),
+         # one 256x160 workgroup per CU (3-stage, 156 KB LDS): least L2->LDS traffic per output
+         25: (256, 160), 26: (128, 160)}
 
 
 def _user_path():
@@ -99,7 +101,7 @@ def candidates(M, N, K):
     return out
 
 
-def _time(fn, reps=3):
+def _time(fn, reps=10):
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 template <int BM, int BN, int WM, int WN, bool CONV>
 static int launch(const GemmArgs& a0, int ksplit, hipStream_t s) {
   GemmArgs a = a0;
-  a.gn_seg = gn_seg_for<BM, BN>();
+  a.gn_seg = gn_seg_for<BM, BN, WM>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int span = ksplit > 1 ? a.kchunk : a.K;
   // FAST staging measured SLOWER on this register-staged pipeline (127 -> 309 us on

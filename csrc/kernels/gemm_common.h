@@ -71,10 +71,19 @@ struct GemmArgs {
   float* row_part;
 };
 
-// epilogue LDS (bf16-element units): fp32 [BM][BN + 4] tile + [BM][2] row LN stats
-template <int BM, int BN>
+// Epilogue passes: tiles taller than 128 rows, and the 160-column tiles, stage
+// their fp32 accumulators one wave-row band at a time (a 256x160 tile would need
+// 168 KB of LDS at once; a 128x160 one 84 KB, more than its 74 KB 2-stage ring,
+// which would cost it its second workgroup per CU)
+template <int BM, int BN, int WM>
+constexpr int epi_passes() {
+  return (BM > 128 || BN == 160) ? WM : 1;
+}
+
+// epilogue LDS (bf16-element units): fp32 [BM / EP][BN + 4] band + [BM][2] row LN stats
+template <int BM, int BN, int EP = 1>
 constexpr int epi_smem_elems() {
-  return BM * (BN + 4) * 2 + 4 * BM;
+  return BM / EP * (BN + 4) * 2 + 4 * BM;
 }
 
 #define BK 64
@@ -147,7 +156,7 @@ __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
   return *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + r, args.M - 1) * 2);
 }
 
-template <int BM, int BN, int WM, int WN, bool RAW = false>
+template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                               bf16_t* smem, int m0, int n0, int split,
                                               float2 lnrow = make_float2(0.f, 0.f)) {
@@ -174,8 +183,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       }
     return;
   }
-  float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC_S]
-  float* lnst = cs + BM * LDC_S;               // [BM][2]: (mean, rstd) of the input rows (fused LN)
+  static_assert(WM % EP == 0, "epilogue passes split the wave rows");
+  constexpr int PR = BM / EP;                  // tile rows staged per pass
+  float* cs = reinterpret_cast<float*>(smem);  // [PR][LDC_S]
+  float* lnst = cs + PR * LDC_S;               // [BM][2]: (mean, rstd) of the input rows (fused LN)
   const int act = args.act;
   const bool ln = args.ln_part != nullptr;
   if (ln) {
@@ -191,7 +202,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     if (!ln) return v;
     return lnst[2 * row + 1] * (v - lnst[2 * row] * lncs[j]);
   };
-  if (act == ACT_GEGLU) {
+  for (int pass = 0; pass < EP; ++pass) {
+  const int pr0 = pass * PR;  // first tile row of this pass
+  if (pass) epi_barrier<RAW>();  // the previous band's readers are done with cs
+  const bool mine = EP == 1 || (wm * WTM) / PR == pass;
+  if (!mine) {
+  } else if (act == ACT_GEGLU) {
     // packed columns: even 16-tiles = hidden, odd = gate (same output column in the same lane)
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -204,7 +220,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WTM + i * 16 + fq * 4 + r;
-          cs[row * LDC_S + oc] = (lnfix(acc[i][j][r], row, j) + bh) * gelu_f(lnfix(acc[i][j + 1][r], row, j + 1) + bg);
+          cs[(row - pr0) * LDC_S + oc] =
+              (lnfix(acc[i][j][r], row, j) + bh) * gelu_f(lnfix(acc[i][j + 1][r], row, j + 1) + bg);
         }
       }
   } else {
@@ -215,7 +232,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WTM + i * 16 + fq * 4 + r, col = wn * WTN + j * 16 + fr;
-          cs[row * LDC_S + col] = lnfix(acc[i][j][r], row, j);
+          cs[(row - pr0) * LDC_S + col] = lnfix(acc[i][j][r], row, j);
         }
   }
   epi_barrier<RAW>();
@@ -223,11 +240,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
   const int vpr = BNo / 8;
-  // BM * vpr is a multiple of 256 for every tile, so each wave runs the same
+  // PR * vpr is a multiple of 256 for every tile, so each wave runs the same
   // number of iterations and the row-statistics shuffles below see all lanes
-  for (int v = tid; v < BM * vpr; v += 256) {
-    const int row = v / vpr, cv = v - row * vpr;
-    const int m = m0 + row, n = on0 + cv * 8;
+  for (int v = tid; v < PR * vpr; v += 256) {
+    const int row = v / vpr, cv = v - row * vpr;  // row within the band
+    const int m = m0 + pr0 + row, n = on0 + cv * 8;
     const bool live = m < M && n < outN;
     float f[8];
 #pragma unroll
@@ -305,12 +322,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     // (segment, channel) with consecutive channels in consecutive lanes
     // (conflict-free LDS reads); two-pass in LDS: exact, no E[x^2]-E[x]^2
     // cancellation.  The consumer GroupNorm merges the segments.
-    const int seg = args.gn_seg > 0 ? args.gn_seg : BM;
+    const int seg = args.gn_seg > 0 ? args.gn_seg : PR;
     epi_barrier<RAW>();
-    for (int t = tid; t < BN * (BM / seg); t += 256) {
+    for (int t = tid; t < BN * (PR / seg); t += 256) {
       const int c = t % BN, sq = t / BN;
       const int n = n0 + c, r0 = sq * seg;
-      if (n >= N || m0 + r0 >= M) continue;
+      if (n >= N || m0 + pr0 + r0 >= M) continue;
       float sm = 0.f;
 #pragma unroll 8
       for (int r = 0; r < seg; ++r) sm += cs[(r0 + r) * LDC_S + c];
@@ -318,18 +335,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       float m2 = 0.f;
 #pragma unroll 8
       for (int r = 0; r < seg; ++r) { const float d = cs[(r0 + r) * LDC_S + c] - mean; m2 += d * d; }
-      *reinterpret_cast<float2*>(args.gn_part + ((size_t)((m0 + r0) / seg) * N + n) * 2) = make_float2(mean, m2);
+      *reinterpret_cast<float2*>(args.gn_part + ((size_t)((m0 + pr0 + r0) / seg) * N + n) * 2) =
+          make_float2(mean, m2);
     }
   }
+  }  // passes
 }
 
 // GN statistics granularity: 1 = fine segments (BM*BN/256 rows, every thread of
 // the column pass busy), 0 = one segment per BM-row tile.  The host mirrors it
 // (hip_ops._gn_seg).
 extern int g_gn_fine;
-template <int BM, int BN>
+template <int BM, int BN, int WM>
 __host__ __forceinline__ int gn_seg_for() {
-  return g_gn_fine ? BM * BN / 256 : BM;
+  constexpr int PR = BM / epi_passes<BM, BN, WM>();  // the epilogue's row band
+  const int seg = g_gn_fine ? BM * BN / 256 : BM;
+  return seg > PR ? PR : seg;
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);

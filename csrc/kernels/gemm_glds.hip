@@ -31,15 +31,23 @@ __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// waves per SIMD the register budget must allow: the 128x160 tile runs two
+// workgroups per CU (its 74 KB ring), so <= 256 registers per lane
+template <int BM, int BN>
+constexpr int glds_min_waves() {
+  return (BM == 128 && BN == 160) ? 2 : 1;
+}
+
 template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST>
-__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) {
+__global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_kernel(const GemmArgs args) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int IA = BM / 32, IB = BN / 32;  // LDS-DMA instructions per wave per stage (8 rows each)
   constexpr int LPG = IA + IB;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SMEM_MAIN = S * STAGE;
-  constexpr int SMEM_EPI = epi_smem_elems<BM, BN>();
+  constexpr int EP = epi_passes<BM, BN, WM>();
+  constexpr int SMEM_EPI = epi_smem_elems<BM, BN, EP>();
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
 
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(const GemmArgs args) 
     }
   }
   __syncthreads();
-  gemm_epilogue<BM, BN, WM, WN>(args, acc, smem, m0, n0, split, lnrow);
+  gemm_epilogue<BM, BN, WM, WN, false, EP>(args, acc, smem, m0, n0, split, lnrow);
 }
 
 // ---------------------------------------------------------------------------
@@ -421,7 +429,7 @@ static int g_num_cus = 0;
 template <int BM, int BN, int WM, int WN, int S>
 static int launch_persist(const GemmArgs& a0, bool conv, hipStream_t s) {
   GemmArgs a = a0;
-  a.gn_seg = gn_seg_for<BM, BN>();
+  a.gn_seg = gn_seg_for<BM, BN, WM>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (!g_num_cus) {
     int dev = 0;
@@ -443,7 +451,7 @@ static int launch_persist(const GemmArgs& a0, bool conv, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int S>
 static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   GemmArgs a = a0;
-  a.gn_seg = gn_seg_for<BM, BN>();
+  a.gn_seg = gn_seg_for<BM, BN, WM>();
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   // FAST staging: K-steps never straddle a tap / the K tail, and every running
   // offset stays inside the zero page
@@ -484,6 +492,9 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
                       (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
     if (!fast || ksplit > 1) tile = 11;  // fall back to the tiled kernel
   }
+  // 256x160: 80 columns per wave (odd 16-column tile count: no GEGLU pairing),
+  // 20 vectors per output row (no power-of-two row-statistics butterfly)
+  if ((tile == 25 || tile == 26) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 11;
   switch (tile) {
     case 21: return launch_persist<128, 128, 2, 2, 2>(a, conv, s);
     case 22: return launch_persist<128, 64, 4, 1, 3>(a, conv, s);
@@ -501,6 +512,13 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     case 18: return launch_glds<64, 64, 2, 2, 2>(a, ksplit, conv, s);
     case 19: return launch_glds<128, 64, 4, 1, 2>(a, ksplit, conv, s);
     case 20: return launch_glds<64, 128, 2, 2, 2>(a, ksplit, conv, s);
+    // one 256x160 workgroup per CU, 3-stage ring (156 KB): 2.3x fewer L2->LDS
+    // bytes per output than 128x64 for the N = 320 / 1280 layers of the 64x64
+    // level, whose convs are bound by the LDS-DMA fill rate (~80 GB/s per CU)
+    case 25: return launch_glds<256, 160, 2, 2, 3>(a, ksplit, conv, s);
+    // 128x160, 2-stage (74 KB): two workgroups per CU, 1.66x fewer L2->LDS bytes
+    // per output than 128x64 and no padded columns at N = 320 (2 x 160)
+    case 26: return launch_glds<128, 160, 2, 2, 2>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }
 }

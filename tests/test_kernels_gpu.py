@@ -33,7 +33,7 @@ def test_gemm(gpu, M, N, K, act):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26])
 @pytest.mark.parametrize("split", [1, 3])
 def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     from chiaswarm_amd.ops import _lib
@@ -73,7 +73,7 @@ def test_gemm_strided_a_and_geglu(gpu):
     assert rel_err(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 3, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("tile", [1, 3, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26])
 def test_geglu_every_tile(gpu, tile):
     """GEGLU pairs (hidden, gate) 16-column tiles inside each wave's columns: every
     tile (incl. the persistent ones) must produce the same gated output."""
@@ -133,7 +133,7 @@ def test_layer_norm(gpu, C):
 
 @pytest.mark.parametrize("rows,C", [(32768, 320), (4099, 640), (4101, 512), (5000, 96)])
 def test_layer_norm_multirow(gpu, rows, C):
-    """Four-rows-per-wave kernel (C <= 512, many rows), incl. a ragged tail."""
+    """UNet-sized row counts (one wave per row, 4 rows per workgroup), incl. a ragged tail."""
     x = rnd(rows, C, dev=gpu, scale=2.0) + 1.0
     g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
     y = hip_ops.layer_norm(x, g, b, 1e-5)
@@ -248,7 +248,7 @@ def test_sched_step(gpu, cfg, prev, noise):
     assert n == x.numel()
 
 
-@pytest.mark.parametrize("tile", [21, 22, 23, 24])
+@pytest.mark.parametrize("tile", [21, 22, 23, 24, 25, 26])
 def test_persistent_tiles_many_tiles_per_workgroup(gpu, tile):
     """Persistent continuous-ring kernels with more tiles than workgroups (GEMM and conv)."""
     from chiaswarm_amd.ops import _lib
@@ -271,7 +271,7 @@ def test_persistent_tiles_many_tiles_per_workgroup(gpu, tile):
     assert rel_err(y, refc) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 17, 21, 23])
+@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 16, 17, 21, 23, 25, 26])
 def test_fused_group_norm_stats(gpu, tile):
     """GroupNorm fed by conv-epilogue statistics == GroupNorm with its own stats pass."""
     from chiaswarm_amd.ops import tuning
