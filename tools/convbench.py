@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--split", type=int, default=1)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--act", type=int, default=0, help="GEMM epilogue activation code (3 = GEGLU, N = 2 x out)")
     a = ap.parse_args()
     _lib.load()
     dev = "cuda"
@@ -34,16 +35,21 @@ def main():
         M, N, K = map(int, a.gemm.split(","))
         x = torch.randn(M, K, device=dev).bfloat16()
         w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        No = N // 2 if a.act == 3 else N
+        y = torch.empty(M, No, dtype=torch.bfloat16, device=dev)
         flops = 2 * M * N * K
         ws = torch.empty(a.split * M * N, dtype=torch.float32, device=dev)
 
         def run(tile):
-            _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, N, N, 1, 0, 1.0, None, tile,
-                      a.split, _p(ws), _s())
+            _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, No, No, 1, a.act, 1.0, None,
+                      tile, a.split, _p(ws), _s())
 
         def ref():
-            return x.float() @ w.float().t()
+            r = x.float() @ w.float().t()
+            if a.act == 3:  # packed (hidden, gate) 16-column pairs
+                r = r.view(M, N // 32, 2, 16)
+                r = (r[:, :, 0] * torch.nn.functional.gelu(r[:, :, 1])).reshape(M, No)
+            return r
     else:
         B, H, W, Cin, Cout = map(int, a.shape.split(","))
         x = torch.randn(B, H, W, Cin, device=dev).bfloat16()
