@@ -137,6 +137,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     const bf16_t* vs = ks + TILE;
 
     // ---- S^T = K Q^T : 4 key tiles x QT query tiles ----
+    // key tiles wholly past kv_end (the tail block: Skv = 77 cross-attention
+    // keeps 1 of its 4) skip their QK^T and PV MFMAs (wave-uniform branches)
+    const int ktn = DP == 64 ? min(4, (kv_end - kb * KB + 15) >> 4) : 4;
     v4f s[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     for (int ds = 0; ds < DS; ++ds) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
+        if (kt >= ktn) continue;
         const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, ds * 4 + fg));
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
@@ -203,6 +207,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     // ---- O^T += V^T P^T ; V^T fragments via ds_read_b64_tr_b16 ----
 #pragma unroll
     for (int kp2 = 0; kp2 < 2; ++kp2) {
+      if (2 * kp2 >= ktn) continue;  // keys kp2*32 .. +31 all masked: P^T is zero there
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         // group fg reads rows (keys) kp2*32 + 4*fg + {0..3} and kp2*32 + 16 + 4*fg + {0..3},
