@@ -30,6 +30,8 @@ sig("csk_conv2d_ex", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_
     c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p)
 sig("csk_group_norm_part", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
+sig("csk_group_norm_part2", c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+    c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p)
 
 
 # ---------------------------------------------------------------------------
@@ -359,11 +361,10 @@ def group_norm_cat(a, b, gamma, beta, groups, eps, silu):
         seg = sa[1]
         nseg = sa[0].numel() // (2 * Ca)
         fused = nseg * 2 * Cb == sb[0].numel()
-    if fused:  # both producers emitted epilogue statistics: merge them
-        part = torch.cat([sa[0].view(nseg, Ca, 2), sb[0].view(nseg, Cb, 2)], 1).view(-1)
+    if fused:  # both producers emitted epilogue statistics: merged from both buffers in place
         stat = torch.empty(B * groups * 2, dtype=torch.float32, device=a.device)
-        _lib.call("csk_group_norm_part", _p(y), _p(a), _p(b), Ca, _p(part), seg, _p(stat), _p(gamma), _p(beta),
-                  B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), 0, _s())
+        _lib.call("csk_group_norm_part2", _p(y), _p(a), _p(b), Ca, _p(sa[0]), _p(sb[0]), seg, _p(stat), _p(gamma),
+                  _p(beta), B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), 0, _s())
     else:  # statistics pass over both tensors in place (e.g. a split-K producer)
         part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=a.device)
         _lib.call("csk_group_norm", _p(y), _p(a), _p(b), Ca, _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk,

@@ -232,6 +232,15 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(const float* __
   }
 }
 
+// Epilogue partial (mean, M2) of channel c in segment sg: [seg][C][2] in `part`,
+// or, for a channel concat whose producers each wrote their own partials,
+// channels < C1 in part ([seg][C1][2]) and the rest in part2 ([seg][C - C1][2])
+__device__ __forceinline__ float2 load_part(const float* part, const float* part2, int sg, int c, int C, int C1) {
+  if (part2 == nullptr) return *reinterpret_cast<const float2*>(part + ((size_t)sg * C + c) * 2);
+  if (c < C1) return *reinterpret_cast<const float2*>(part + ((size_t)sg * C1 + c) * 2);
+  return *reinterpret_cast<const float2*>(part2 + ((size_t)sg * (C - C1) + c - C1) * 2);
+}
+
 // MODE 0: `stat` holds final (mean, rstd) per (b, g) (a finalize kernel ran).
 // MODE 1: `stat` is the stats kernel's chunk partials [b][nent][g][3];
 // MODE 2: `stat` is epilogue partials [seg][c][2] (nent = segments per sample,
@@ -244,7 +253,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ beta, int P, int C, int G,
                                                               int chunk, int silu, int affine_bstride, int nent,
                                                               int seg_rows, float eps,
-                                                              const bf16_t* __restrict__ x2 = nullptr, int C1 = 0) {
+                                                              const bf16_t* __restrict__ x2 = nullptr, int C1 = 0,
+                                                              const float* __restrict__ part2 = nullptr) {
   // x2 != null: the input is the channel concat [x (C1 channels) | x2 (C - C1)]
   // of two separate tensors (UNet skip connections), read in place
   __shared__ float gst[2 * 64];
@@ -271,7 +281,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
       group_moments(
           [&](int e, float& n, float& m, float& q) {
             const int sg = b * nent + e / Cg, c = g * Cg + e % Cg;
-            const float2 mq = *reinterpret_cast<const float2*>(stat + ((size_t)sg * C + c) * 2);
+            const float2 mq = load_part(stat, part2, sg, c, C, C1);
             n = fn; m = mq.x; q = mq.y;
           },
           g < G ? nent * Cg : 0, sub, tpg, mean, rstd, eps);
@@ -344,7 +354,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
 // stats pass over the tensor disappears.
 __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const float* __restrict__ part,
                                                                       float* __restrict__ stat, int B, int C, int G,
-                                                                      int nseg, int seg_rows, float eps) {
+                                                                      int nseg, int seg_rows, float eps,
+                                                                      const float* __restrict__ part2, int C1) {
   const int lane = threadIdx.x & 63;
   const int bg = blockIdx.x * (GN_THREADS / 64) + (threadIdx.x >> 6);
   if (bg >= B * G) return;
@@ -354,7 +365,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
   group_moments_wave(
       [&](int e, float& n, float& m, float& q) {
         const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
-        const float2 mq = *reinterpret_cast<const float2*>(part + ((size_t)sg * C + c) * 2);
+        const float2 mq = load_part(part, part2, sg, c, C, C1);
         n = fn; m = mq.x; q = mq.y;
       },
       nseg * Cg, lane, mean, rstd, eps);
@@ -366,11 +377,15 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
 
 // stat: B*G*2 floats of workspace
 // x2 / C1: optional second input (channel concat [x | x2], x has C1 channels)
-CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, const void* part, int seg_rows,
-                                void* stat, const void* gamma, const void* beta, int B, int P, int C, int G, int chunk,
-                                int nchunk, float eps, int silu, int affine_bstride, hipStream_t stream) {
+// part2: optional partials of x2's channels (then `part` holds only x's), so a
+// skip concat's two producers' statistics are merged without concatenating them
+CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1, const void* part, const void* part2,
+                                 int seg_rows, void* stat, const void* gamma, const void* beta, int B, int P, int C,
+                                 int G, int chunk, int nchunk, float eps, int silu, int affine_bstride,
+                                 hipStream_t stream) {
   if (C % 8 != 0 || C > GN_MAXC || C % G != 0 || seg_rows <= 0 || P % seg_rows != 0) return (int)hipErrorInvalidValue;
   if (x2 && (C1 <= 0 || C1 >= C || C1 % 8 != 0)) return (int)hipErrorInvalidValue;
+  if (part2 && !x2) return (int)hipErrorInvalidValue;
   float* st = (float*)stat;
   const int nseg = P / seg_rows;
   // every apply workgroup re-reads ALL of its sample's partials in a prologue
@@ -379,16 +394,23 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, 
   if (G <= 64 && nseg * C <= g_gn_prologue_max) {
     gn_apply_kernel<2><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>(
         (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G, chunk,
-        silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1);
+        silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1, (const float*)part2);
     CSK_CHECK_LAUNCH();
   }
   gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
-      (const float*)part, st, B, C, G, nseg, seg_rows, eps);
+      (const float*)part, st, B, C, G, nseg, seg_rows, eps, (const float*)part2, C1);
   gn_apply_kernel<0><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st,
                                                                  (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G,
                                                                  chunk, silu, affine_bstride, 0, 0, eps,
                                                                  (const bf16_t*)x2, C1);
   CSK_CHECK_LAUNCH();
+}
+
+CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, const void* part, int seg_rows,
+                                void* stat, const void* gamma, const void* beta, int B, int P, int C, int G, int chunk,
+                                int nchunk, float eps, int silu, int affine_bstride, hipStream_t stream) {
+  return csk_group_norm_part2(y, x, x2, C1, part, nullptr, seg_rows, stat, gamma, beta, B, P, C, G, chunk, nchunk,
+                              eps, silu, affine_bstride, stream);
 }
 
 // part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
