@@ -167,13 +167,13 @@ __device__ __forceinline__ void group_moments(const Get& get, int ne, int sub, i
   rstd = rsqrtf(sq / fmaxf(sn, 1.f) + eps);
 }
 
-// One wave per group: up to 8 entries per lane are loaded ONCE (all in flight
-// together) and kept in registers for both passes, so a finalize over <= 512
+// One wave per group: up to 16 entries per lane are loaded ONCE (all in flight
+// together) and kept in registers for both passes, so a finalize over <= 1024
 // partials costs one memory round trip instead of two dependent loops.
 template <class Get>
 __device__ __forceinline__ void group_moments_wave(const Get& get, int ne, int lane, float& mean, float& rstd,
                                                    float eps) {
-  constexpr int CAP = 8;
+  constexpr int CAP = 16;  // 1024 entries in one round trip (64x64x320 fused stats: 640 per group)
   float en[CAP], em[CAP], eq[CAP];
 #pragma unroll
   for (int j = 0; j < CAP; ++j) {
@@ -187,7 +187,7 @@ __device__ __forceinline__ void group_moments_wave(const Get& get, int ne, int l
     sn += en[j];
     sm = __builtin_fmaf(en[j], em[j], sm);
   }
-  for (int e = lane + 64 * CAP; e < ne; e += 64) {  // > 512 partials (large VAE maps)
+  for (int e = lane + 64 * CAP; e < ne; e += 64) {  // > 1024 partials (large VAE maps)
     float n, m, q;
     get(e, n, m, q);
     sn += n;
