@@ -236,6 +236,57 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         }
   }
   epi_barrier<RAW>();
+  // Fast store path — the common short-K GEMM case (no GN / row statistics /
+  // fused LN / GEGLU / per-sample bias; full, 16-byte-aligned 8-column vectors).
+  // Each thread keeps ONE column vector for the whole band (VPR divides 256), so
+  // its bias is loaded once and the row loop is pointer increments; the generic
+  // loop below re-derives row and column (a runtime division), the bias and the
+  // addresses for every 8 outputs, and at K = 320 the epilogue is most of a
+  // tile's instruction stream (the SIMDs were issue-saturated, PMC r1i).
+  constexpr int VPR = BN / 8;
+  if constexpr (256 % VPR == 0 && PR % (256 / VPR) == 0) {
+    const bool fast = !args.gn_part && !args.row_part && !ln && act != ACT_GEGLU && !args.bias2d &&
+                      (N % 8) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
+                      (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
+                      (!args.res || ((args.ldr % 8) == 0 && ((((size_t)args.res) & 15) == 0)));
+    if (fast) {
+      constexpr int RPI = 256 / VPR;  // band rows per iteration
+      const int cv = tid % VPR, r0 = tid / VPR;
+      const int n = n0 + cv * 8;
+      if (n < N) {
+        float bb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+        if (args.bias) add8(bb, args.bias + n, true, 8);
+        const float osc = args.out_scale;
+        int m = m0 + pr0 + r0;
+        bf16_t* cp = args.C + (size_t)m * args.ldc + n;
+        const bf16_t* rp = args.res ? args.res + (size_t)m * args.ldr + n : nullptr;
+        const size_t cstep = (size_t)RPI * args.ldc, rstep = (size_t)RPI * args.ldr;
+        for (int row = r0; row < PR && m < M; row += RPI, m += RPI) {
+          const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
+          const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
+          float f[8] = {lo.x + bb[0], lo.y + bb[1], lo.z + bb[2], lo.w + bb[3],
+                        hi.x + bb[4], hi.y + bb[5], hi.z + bb[6], hi.w + bb[7]};
+          act8(act, f);
+          if (osc != 1.0f) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] *= osc;
+          }
+          if (rp) {
+            float rf[8];
+            unpack8(*reinterpret_cast<const uint4*>(rp), rf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] += rf[j];
+            rp += rstep;
+          }
+          *reinterpret_cast<uint4*>(cp) = pack8(f);
+          cp += cstep;
+        }
+      }
+      continue;  // next band: nothing else to do without GN / row statistics
+    }
+  }
   const int outN = act == ACT_GEGLU ? N / 2 : N;
   const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
