@@ -77,6 +77,7 @@ sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_softmax_rows", c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
 sig("csk_set_gn_prologue_max", c_int)
+sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_gn_fine", c_int)
 sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
 

@@ -534,6 +534,16 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Short-KV (Skv <= 128, D <= 64: UNet cross-attention over 77 text tokens)
+// kernel choice for variant 0: 0 = plain loop, 128-row workgroups; 1 = plain,
+// 64-row workgroups (twice the grid: the loop is only 2 key blocks long, so
+// per-workgroup latency, not MFMA work, sets the time); 2 = pipelined QT=1.
+static int g_short_kv_variant = 2;
+CSK_API int csk_set_short_kv_variant(int v) {
+  g_short_kv_variant = v;
+  return 0;
+}
+
 // variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64),
 // 3 = pipelined + PRE, 4 = pipelined + ONES, 5 = pipelined + PRE + ONES
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
@@ -578,6 +588,13 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
         default: attn_fwd_pipe_kernel<2, true, true><<<grid, 256, 0, stream>>>(a); break;
       }
       return (int)hipGetLastError();
+    }
+    if (variant == 0 && Skv <= 128) {
+      if (g_short_kv_variant == 1) return launch_attn<64, 1>(a, stream);
+      if (g_short_kv_variant == 2) {
+        attn_fwd_pipe_kernel<1, true, true><<<dim3(B * H * ((Sq + 63) / 64)), 256, 0, stream>>>(a);
+        return (int)hipGetLastError();
+      }
     }
     return launch_attn<64, 2>(a, stream);
   }

@@ -440,46 +440,57 @@ CSK_API int csk_group_norm(void* y, const void* x, const void* x2, int C1, void*
 }
 
 // --------------------------------------------------------------------------
-// LayerNorm: one wave per row, row held in registers (C <= 64*8*NVMAX).
+// LayerNorm: a row is owned by LPR lanes (a power of two dividing 64), each
+// holding VPL 16-byte vectors in registers, so one wave normalises 64/LPR rows
+// and issues VPL loads per lane up front.  One wave per row (the earlier form)
+// left 24 of 64 lanes idle at C = 320 and kept only 640 B in flight per wave:
+// the UNet's LayerNorms ran at 2.3-3.5 TB/s, latency-bound.  Reductions are
+// xor-shuffles inside the lane group.
 // --------------------------------------------------------------------------
-template <int NVMAX>
+template <int VPL>
 __global__ __launch_bounds__(256) void layer_norm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          const bf16_t* __restrict__ gamma,
-                                                         const bf16_t* __restrict__ beta, int rows, int C, float eps) {
+                                                         const bf16_t* __restrict__ beta, int rows, int C, float eps,
+                                                         int lpr_log2) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int LPR = 1 << lpr_log2;
+  const int rpw = 64 >> lpr_log2;  // rows per wave
+  const int sub = lane & (LPR - 1);
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + (lane >> lpr_log2);
+  const bool live = row < rows;
   const int NV = C >> 3;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * C);
-  float f[NVMAX][8];
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)(live ? row : 0) * C);
+  uint4 raw[VPL];
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int cv = sub + LPR * u;
+    raw[u] = (live && cv < NV) ? xr[cv] : make_uint4(0, 0, 0, 0);
+  }
+  float f[VPL][8];
   float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < NVMAX; ++u) {
-    int cv = lane + 64 * u;
-    if (cv < NV) {
-      unpack8(xr[cv], f[u]);
+  for (int u = 0; u < VPL; ++u) {
+    unpack8(raw[u], f[u]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += f[u][j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[u][j] = 0.f;
-    }
+    for (int j = 0; j < 8; ++j) s += f[u][j];
   }
-  const float mean = wave_sum(s) / (float)C;
+  for (int o = LPR >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)C;
   float q = 0.f;
 #pragma unroll
-  for (int u = 0; u < NVMAX; ++u) {
-    int cv = lane + 64 * u;
-    if (cv < NV) {
+  for (int u = 0; u < VPL; ++u) {
+    if (sub + LPR * u < NV) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { float d = f[u][j] - mean; q += d * d; }
+      for (int j = 0; j < 8; ++j) { const float d = f[u][j] - mean; q += d * d; }
     }
   }
-  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+  for (int o = LPR >> 1; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / (float)C + eps);
+  if (!live) return;
   uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * C);
 #pragma unroll
-  for (int u = 0; u < NVMAX; ++u) {
-    int cv = lane + 64 * u;
+  for (int u = 0; u < VPL; ++u) {
+    const int cv = sub + LPR * u;
     if (cv < NV) {
       float gg[8], bb[8], o[8];
       unpack8(reinterpret_cast<const uint4*>(gamma)[cv], gg);
@@ -499,18 +510,27 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const bf16_t* __restric
 CSK_API int csk_layer_norm(void* y, const void* x, const void* gamma, const void* beta, int rows, int C, float eps,
                            hipStream_t stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
-  int nv = C / 8;
-  dim3 grid((rows + 3) / 4);
-  if (nv <= 64)
-    layer_norm_kernel<1><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
-                                                    (const bf16_t*)beta, rows, C, eps);
-  else if (nv <= 128)
-    layer_norm_kernel<2><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
-                                                    (const bf16_t*)beta, rows, C, eps);
-  else if (nv <= 256)
-    layer_norm_kernel<4><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
-                                                    (const bf16_t*)beta, rows, C, eps);
-  else
-    return (int)hipErrorInvalidValue;
+  const int nv = C / 8;
+  if (nv > 64 * 8) return (int)hipErrorInvalidValue;
+  // smallest lane group with <= 8 vectors per lane: C = 320 -> 8 lanes x 5,
+  // 640 -> 16 x 5, 1280 -> 32 x 5, 768 -> 16 x 6, 1024 -> 16 x 8
+  int l2 = 0;
+  while ((1 << l2) * 8 < nv) ++l2;
+  const int vpl = (nv + (1 << l2) - 1) >> l2;
+  const int rows_per_block = 4 * (64 >> l2);
+  const dim3 grid((rows + rows_per_block - 1) / rows_per_block);
+#define CSK_LN(V)                                                                                                  \
+  layer_norm_kernel<V><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,               \
+                                                 (const bf16_t*)beta, rows, C, eps, l2)
+  switch (vpl) {
+    case 1: CSK_LN(1); break;
+    case 2: CSK_LN(2); break;
+    case 3: CSK_LN(3); break;
+    case 4: CSK_LN(4); break;
+    case 5: CSK_LN(5); break;
+    case 6: CSK_LN(6); break;
+    default: CSK_LN(8); break;
+  }
+#undef CSK_LN
   CSK_CHECK_LAUNCH();
 }

@@ -131,9 +131,11 @@ def test_layer_norm(gpu, C):
     assert rel_err(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("rows,C", [(32768, 320), (4099, 640), (4101, 512), (5000, 96)])
+@pytest.mark.parametrize("rows,C", [(32768, 320), (4099, 640), (4101, 512), (5000, 96), (8191, 1280), (77, 1024),
+                                    (1001, 768), (333, 2048), (130, 4096), (65, 8), (99, 56)])
 def test_layer_norm_multirow(gpu, rows, C):
-    """UNet-sized row counts (one wave per row, 4 rows per workgroup), incl. a ragged tail."""
+    """UNet-sized row counts (64/LPR rows per wave, lane groups of LPR per row), incl. ragged tails
+    and every vectors-per-lane instantiation."""
     x = rnd(rows, C, dev=gpu, scale=2.0) + 1.0
     g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
     y = hip_ops.layer_norm(x, g, b, 1e-5)

@@ -23,6 +23,8 @@ def apply_arm(arm):
     elif arm.startswith("gn"):
         v = arm[2:]
         _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("xkv"):
+        _lib.call("csk_set_short_kv_variant", int(arm[3:]))
     elif arm.startswith("attn"):
         hip_ops.ATTN_VARIANT = int(arm[4:])
     elif arm in ("lnoff", "lnon"):

@@ -44,16 +44,20 @@ def main():
     a = ap.parse_args()
     ops._lib.load()
     t = tuning.table()
+    dropped = {}
     if a.drop:
         rx = re.compile(a.drop)
         for k in [k for k in t if rx.search(k)]:
-            print("re-measure", k, t.pop(k), flush=True)
+            dropped[k] = t.pop(k)
+            print("re-measure", k, dropped[k], flush=True)
     before = set(t)
     dev = torch.device("cuda", 0)
     for m in a.models.split(","):
         run_model(m, dev)
     for k in sorted(set(t) - before):
-        print("measured", k, t[k], flush=True)
+        print("measured", k, t[k], "was", dropped.get(k), flush=True)
+    for k, v in dropped.items():  # entries of models not run this time stay as they were
+        t.setdefault(k, v)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(t, f, indent=0, sort_keys=True)

@@ -1,0 +1,150 @@
+#!/usr/bin/env python
+"""In-step tuning of the per-shape (tile, split-K) table: every candidate is
+judged by the time of the WHOLE hipGraph-replayed SD2.1 UNet step (CFG batch 8,
+64x64 latents), not by back-to-back launches of the one kernel.
+
+Isolated timing (``ops/tuning.py``) runs a kernel with its weights and inputs
+hot in L2 and its ramp hidden behind the previous launch; inside the step the
+weights come from HBM and every kernel pays its own ramp, so the long-K /
+small-grid shapes of the 8x8 and 16x16 levels run up to 2x slower than their
+table entry says (profiles/unet_step_kernel_stats_r1k.txt) and the table's
+choice is not the step's best.  Flushing L2 and MALL before every isolated
+launch mis-ranks the other way (that table was 0.16 ms per step slower, same
+box), so this tool measures the thing that matters.
+
+Greedy coordinate descent over the table keys the step uses (smallest M
+first: that is where isolated timing is least representative); a candidate is
+kept only if it wins twice (A/B/A/B).  Writes the merged table after every
+accepted change, so a run cut short still leaves its progress:
+
+    python tools/steptune.py --budget 900 --out gpurun_out/tune_step.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from chiaswarm_amd import ops  # noqa: E402
+from chiaswarm_amd.ops import _lib, tuning  # noqa: E402
+
+SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--budget", type=float, default=900.0, help="seconds")
+    ap.add_argument("--out", default="gpurun_out/tune_step.json")
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--min-gain-us", type=float, default=6.0)
+    ap.add_argument("--keys", default="", help="only keys containing this substring")
+    ap.add_argument("--all-tiles", action="store_true", help="every candidate, not the shortlist")
+    a = ap.parse_args()
+    t_start = time.time()
+    from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
+
+    _lib.load()
+    dev = torch.device("cuda", 0)
+    p = StableDiffusion("sd21", device=dev, seed=0)
+    x = torch.randn(8, 64, 64, 4, device=dev).bfloat16()
+    ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
+    kv = p.unet.encode_context(ctx)
+
+    used = {}
+    orig_choose = tuning.choose
+
+    def spy(key, M, N, K, runner):
+        r = orig_choose(key, M, N, K, runner)
+        used.setdefault(key, (M, N, K, r))
+        return r
+
+    tuning.choose = spy
+    table = tuning.table()
+
+    def capture():
+        return _UNetGraph(p.unet, x, kv, None, None, warmup=1)
+
+    def timed(g, rounds=3):
+        for _ in range(2):
+            g.graph.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                g.graph.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / a.iters)
+        return best
+
+    base_g = capture()
+    base = timed(base_g)
+    t0_ms = base
+    print(f"start step {base:.4f} ms, {len(used)} table keys in the step", flush=True)
+    keys = sorted(used, key=lambda k: used[k][0])  # smallest M first
+    if a.keys:
+        keys = [k for k in keys if a.keys in k]
+
+    def save():
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(table, f, indent=0, sort_keys=True)
+
+    changes = []
+    for key in keys:
+        M, N, K, cur = used[key]
+        cands = [c for c in tuning.candidates(M, N, K) if (a.all_tiles or c[0] in SHORTLIST) and c != tuple(cur)]
+        best_c, best_t = None, base
+        for c in cands:
+            if time.time() - t_start > a.budget:
+                break
+            old = table.get(key)
+            table[key] = [c[0], c[1], 0.0]
+            try:
+                g = capture()
+                tc = timed(g)
+            except RuntimeError as e:
+                print(f"  {key} {c} failed: {e}", flush=True)
+                tc = float("inf")
+                g = None
+            finally:
+                if old is None:
+                    table.pop(key, None)
+                else:
+                    table[key] = old
+            if tc < best_t - a.min_gain_us / 1000:
+                # confirm against a fresh measurement of the base graph
+                tb2, tc2 = timed(base_g), timed(g)
+                if tc2 < tb2 - a.min_gain_us / 1000:
+                    best_c, best_t = c, tc2
+                    base = tb2
+            del g
+        if best_c is not None:
+            table[key] = [best_c[0], best_c[1], round(best_t * 1000, 1)]
+            used[key] = (M, N, K, best_c)
+            del base_g
+            torch.cuda.empty_cache()
+            base_g = capture()
+            base = timed(base_g)
+            changes.append((key, cur, best_c))
+            print(f"{key}: {tuple(cur)} -> {best_c}  step {base:.4f} ms", flush=True)
+            save()
+        else:
+            print(f"{key}: keep {tuple(cur)} ({len(cands)} tried, step {base:.4f} ms, "
+                  f"{time.time() - t_start:.0f} s)", flush=True)
+        torch.cuda.empty_cache()
+        if time.time() - t_start > a.budget:
+            print("budget reached", flush=True)
+            break
+    save()
+    print(f"done: {len(changes)} changes, step {t0_ms:.4f} -> {base:.4f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
