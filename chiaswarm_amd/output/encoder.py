@@ -48,8 +48,8 @@ def encode_artifact(arrays, content_type: str = "image/jpeg") -> dict:
 
     from .processor import image_to_buffer, make_result, post_process
 
-    buf = image_to_buffer(post_process([Image.fromarray(a) for a in arrays]), content_type)
-    return make_result(buf, buf, content_type)
+    img = post_process([Image.fromarray(a) for a in arrays])
+    return make_result(image_to_buffer(img, content_type), img, content_type)
 
 
 def _gpu_initialised() -> bool:

@@ -68,8 +68,8 @@ def _message(e) -> str:
 
 def exception_image(e, content_type):
     message = _message(e)
-    buf = image_to_buffer(image_from_text(str(message)), content_type)
-    return {"primary": make_result(buf, buf, content_type)}, {"error": message}
+    img = image_from_text(str(message))
+    return {"primary": make_result(image_to_buffer(img, content_type), img, content_type)}, {"error": message}
 
 
 def exception_message(e):

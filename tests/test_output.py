@@ -108,3 +108,22 @@ def test_deferred_encoding_in_encoder_processes_matches_inline():
     finally:
         op.set_encoder_pool(None)
         pool.shutdown()
+
+
+def test_thumbnail_from_image_matches_decoded_bytes():
+    """make_thumbnail(PIL image) skips the JPEG re-decode; the 100x100 tile must
+    match the reference path (thumbnail of the decoded blob) up to JPEG noise."""
+    import numpy as np
+    from PIL import Image
+
+    from chiaswarm_amd.output.processor import image_to_buffer, make_thumbnail
+
+    rng = np.random.default_rng(0)
+    base = rng.integers(0, 255, (8, 8, 3), dtype=np.uint8)
+    img = Image.fromarray(base).resize((1024, 1024), Image.Resampling.BILINEAR)
+    buf = image_to_buffer(img, "image/jpeg")
+    a = np.asarray(Image.open(make_thumbnail(img)), dtype=np.int16)
+    b = np.asarray(Image.open(make_thumbnail(buf.getvalue())), dtype=np.int16)
+    assert a.shape == b.shape == (100, 100, 3)
+    assert np.abs(a - b).mean() < 3.0
+    assert img.size == (1024, 1024)  # the caller's image is not resized in place
