@@ -44,6 +44,17 @@ def _digest(path: str, extra: str) -> str:
     return h.hexdigest()[:16]
 
 
+def source_digest() -> str:
+    """Digest of every kernel source + header + the compile flags: the identity
+    of the library they build (stored next to it as ``libcsk.so.src``)."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for f in sorted(glob.glob(os.path.join(SRC, "*.hip")) + glob.glob(os.path.join(SRC, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _compile(src: str, force: bool) -> str:
     name = os.path.splitext(os.path.basename(src))[0]
     dig = _digest(src, " ".join(FLAGS))
@@ -68,6 +79,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     stamp = OUT + ".stamp"
     if os.path.exists(OUT) and not force and os.path.exists(stamp) and open(stamp).read() == key:
         os.utime(OUT)
+        with open(OUT + ".src", "w") as f:
+            f.write(source_digest())
         if verbose:
             print(f"[csk] up to date: {OUT}")
         return OUT
@@ -78,6 +91,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     os.replace(OUT + ".tmp", OUT)
     with open(stamp, "w") as f:
         f.write(key)
+    with open(OUT + ".src", "w") as f:
+        f.write(source_digest())
     if verbose:
         print(f"[csk] built {OUT} from {len(srcs)} sources")
     return OUT

@@ -79,7 +79,7 @@ def format_args(job: dict):
 
 
 def format_txt2audio_args(args):
-    parameters = args.pop("parameters", {})
+    parameters = dict(args.pop("parameters", None) or {})  # never mutate the caller's job
     args.setdefault("prompt", "")
     args.setdefault("num_inference_steps", 25)
     args["pipeline_type"] = get_pipeline_type(parameters.pop("pipeline_type", "AudioLDMPipeline"))
@@ -90,7 +90,7 @@ def format_txt2audio_args(args):
 
 
 def format_txt2vid_args(args):
-    parameters = args.pop("parameters", {})
+    parameters = dict(args.pop("parameters", None) or {})  # never mutate the caller's job
     args.setdefault("prompt", "")
     args.setdefault("num_inference_steps", 25)
     args.pop("num_images_per_prompt", None)
@@ -112,7 +112,7 @@ def format_stable_diffusion_args(args):
         if size[0] > MAX_SIZE or size[1] > MAX_SIZE:
             raise Exception(f"The max image size is (1024, 1024); got ({size[0]}, {size[1]}).")
 
-    parameters = args.pop("parameters", {})
+    parameters = dict(args.pop("parameters", None) or {})  # never mutate the caller's job
     args.setdefault("prompt", "")
     args["supports_xformers"] = parameters.get("supports_xformers", True)
     args["upscale"] = parameters.get("upscale", False)

@@ -2,8 +2,14 @@
 ``pipeline.unet.load_attn_procs(lora)`` / ``pipeline.load_textual_inversion``).
 
 LoRA weights are merged into the resident UNet (W += scale * up @ down) for the
-duration of one job and subtracted again afterwards (``unload_lora``), so the
-hot path keeps running the plain fused GEMMs — no per-step adapter cost.
+duration of one job, so the hot path keeps running the plain fused GEMMs — no
+per-step adapter cost.  ``unload_lora`` restores the ORIGINAL weights bit for
+bit (``copy_`` from saved copies: in bf16, W + d - d != W, so subtracting the
+delta again would drift the shared resident model job after job).  Packed
+buffers are rebuilt in place (stable pointers), and the owning pipeline's
+hipGraphs are invalidated on every adapter change (``_invalidate``).
+Textual inversion is per job too: ``unload_textual_inversion`` restores the
+original embedding table and removes the placeholder token.
 Supported key layouts: diffusers attn-procs (``...attn1.processor.to_q_lora.
 {down,up}.weight``), diffusers PEFT (``...attn1.to_q.lora_A/B.weight``) and kohya
 (``lora_unet_down_blocks_0_..._to_q.lora_down/up.weight`` + ``.alpha``).
@@ -73,47 +79,58 @@ def _pairs(sd: dict):
             yield t, g["down"], g["up"], g.get("alpha")
 
 
-def load_lora(unet, path_or_name: str, scale: float = 1.0):
+def load_lora(unet, path_or_name: str, scale: float = 1.0, pipe=None):
     sd = _read(_resolve(path_or_name))
     idx = _linear_index(unet)
     merged = []
     with torch.no_grad():
-        for target, down, up, alpha in _pairs(sd):
-            key = target[len("kohya:"):] if target.startswith("kohya:") else target
-            mod = idx.get(key)
-            if mod is None:
-                raise KeyError(f"LoRA target {key} not in this UNet")
-            down2, up2 = down.float().flatten(1), up.float().flatten(1)
-            rank = down2.shape[0]
-            s = scale * ((alpha / rank) if alpha else 1.0)
-            delta = (up2 @ down2) * s
-            if delta.shape != mod.weight.shape:
-                raise ValueError(f"LoRA shape {tuple(delta.shape)} != {tuple(mod.weight.shape)} for {key}")
-            delta = delta.to(mod.weight.device)
-            mod.weight.add_(delta.to(mod.weight.dtype))
-            merged.append((mod, delta))
+        try:
+            for target, down, up, alpha in _pairs(sd):
+                key = target[len("kohya:"):] if target.startswith("kohya:") else target
+                mod = idx.get(key)
+                if mod is None:
+                    raise KeyError(f"LoRA target {key} not in this UNet")
+                down2, up2 = down.float().flatten(1), up.float().flatten(1)
+                rank = down2.shape[0]
+                s = scale * ((alpha / rank) if alpha else 1.0)
+                delta = (up2 @ down2) * s
+                if delta.shape != mod.weight.shape:
+                    raise ValueError(f"LoRA shape {tuple(delta.shape)} != {tuple(mod.weight.shape)} for {key}")
+                orig = mod.weight.detach().clone()
+                merged.append((mod, orig))
+                mod.weight.copy_((orig.float() + delta.to(orig.device)).to(orig.dtype))
+        except Exception:
+            for mod, orig in merged:  # leave the resident model untouched on failure
+                mod.weight.copy_(orig)
+            raise
     if not merged:
         raise ValueError("no LoRA weights recognised in file")
     unet._lora_merged = merged
-    _reprepare(unet)
+    _reprepare(unet, pipe)
     return len(merged)
 
 
-def unload_lora(unet):
+def unload_lora(unet, pipe=None):
     merged = getattr(unet, "_lora_merged", None)
     if not merged:
         return
     with torch.no_grad():
-        for mod, delta in merged:
-            mod.weight.sub_(delta.to(mod.weight.dtype))
+        for mod, orig in merged:
+            mod.weight.copy_(orig)  # bitwise restore
     unet._lora_merged = None
-    _reprepare(unet)
+    _reprepare(unet, pipe)
 
 
-def _reprepare(unet):
+def _invalidate(pipe):
+    if pipe is not None and hasattr(pipe, "invalidate_graphs"):
+        pipe.invalidate_graphs()
+
+
+def _reprepare(unet, pipe=None):
     from .layers import prepare_model
 
     prepare_model(unet)
+    _invalidate(pipe)
 
 
 def load_textual_inversion(pipe, path_or_name: str, token: str | None = None):
@@ -133,11 +150,34 @@ def load_textual_inversion(pipe, path_or_name: str, token: str | None = None):
     emb = te.text_model.embeddings.token_embedding
     if vecs.shape[-1] != emb.weight.shape[1]:
         raise ValueError(f"embedding width {vecs.shape[-1]} != text encoder width {emb.weight.shape[1]}")
+    tokz = pipe.tokenizers[0]
+    added = getattr(tokz, "added_tokens", None) or {}
+    if tok in added:
+        raise ValueError(f"token {tok!r} is already registered")
     with torch.no_grad():
-        start = emb.weight.shape[0]
-        new = torch.cat([emb.weight, vecs.to(emb.weight)], 0)
+        orig = emb.weight
+        start = orig.shape[0]
+        new = torch.cat([orig, vecs.to(orig)], 0)
         emb.weight = torch.nn.Parameter(new, requires_grad=False)
         emb.num_embeddings = new.shape[0]
-    pipe.tokenizers[0].added_tokens = getattr(pipe.tokenizers[0], "added_tokens", {})
-    pipe.tokenizers[0].added_tokens[tok] = list(range(start, start + vecs.shape[0]))
+    te._ti_orig = getattr(te, "_ti_orig", None) or (orig, start)
+    tokz.added_tokens = dict(added)
+    tokz.added_tokens[tok] = list(range(start, start + vecs.shape[0]))
+    _invalidate(pipe)
     return tok
+
+
+def unload_textual_inversion(pipe):
+    """Drop every per-job embedding row and placeholder token (bitwise the
+    original table object comes back)."""
+    te = pipe.text_encoders[0]
+    saved = getattr(te, "_ti_orig", None)
+    if saved is None:
+        return
+    orig, n = saved
+    emb = te.text_model.embeddings.token_embedding
+    emb.weight = orig
+    emb.num_embeddings = n
+    te._ti_orig = None
+    pipe.tokenizers[0].added_tokens = {}
+    _invalidate(pipe)

@@ -40,24 +40,48 @@ def sig(name: str, *argtypes):
     _SIGS[name] = list(argtypes)
 
 
-def _maybe_rebuild():
-    """Rebuild libcsk.so if any csrc/kernels source is newer than it (a stale
-    library with an old launcher signature would be called with the wrong
-    arguments).  Needs hipcc, which both this image and the GPU boxes have."""
-    src_dir = os.path.join(os.path.dirname(LIB_DIR), "..", "csrc", "kernels")
-    src_dir = os.path.normpath(src_dir)
-    if not os.path.isdir(src_dir) or os.environ.get("CSK_NO_AUTOBUILD"):
-        return
-    srcs = [os.path.join(src_dir, f) for f in os.listdir(src_dir) if f.endswith((".hip", ".h"))]
-    newest = max((os.path.getmtime(s) for s in srcs), default=0.0)
-    if os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
-        return
-    try:
-        from .. import _build
+class StaleLibraryError(RuntimeError):
+    pass
 
-        _build.build(verbose=False)
-    except Exception as e:  # surfaced by the existence check / first call
-        print(f"[csk] rebuild failed: {e}")
+
+def check_fresh():
+    """Raise if libcsk.so was built from other kernel sources than the ones in
+    this tree (a stale launcher signature would be called with the wrong
+    arguments).  Content digest, not mtimes (a copied tree reorders mtimes).
+
+    Never rebuilds here: this runs inside GPU worker processes that have
+    already initialised HIP, where fork+exec of hipcc is unsafe and N
+    children would race on the same output files.  Build at install time or
+    in the supervisor before any GPU work (``ensure_built``)."""
+    src_dir = os.path.normpath(os.path.join(os.path.dirname(LIB_DIR), "..", "csrc", "kernels"))
+    if not os.path.isdir(src_dir) or os.environ.get("CSK_ALLOW_STALE"):
+        return
+    from .. import _build
+
+    want = _build.source_digest()
+    try:
+        with open(LIB_PATH + ".src") as f:
+            have = f.read().strip()
+    except OSError:
+        have = None
+    if have != want:
+        raise StaleLibraryError(
+            f"{LIB_PATH} is stale or unstamped (built from {have}, sources are {want}): "
+            "run `python -m chiaswarm_amd._build` before starting GPU work")
+
+
+def ensure_built():
+    """Build the library if it is missing or stale.  Only for processes that
+    have NOT initialised the GPU (the supervisor, install scripts, tests)."""
+    try:
+        if os.path.exists(LIB_PATH):
+            check_fresh()
+            return
+    except StaleLibraryError:
+        pass
+    from .. import _build
+
+    _build.build(verbose=False)
 
 
 def load():
@@ -68,12 +92,12 @@ def load():
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        _maybe_rebuild()
         if not os.path.exists(LIB_PATH):
             _LOAD_ERR = FileNotFoundError(
                 f"{LIB_PATH} not built: run `python -m chiaswarm_amd._build`"
             )
             raise _LOAD_ERR
+        check_fresh()
         lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGS.items():
             fn = getattr(lib, name)

@@ -56,7 +56,7 @@ def _apply_lora(pipe, lora, scale):
     from ..models.lora import load_lora
 
     try:
-        load_lora(pipe.unet, lora, scale)
+        load_lora(pipe.unet, lora, scale, pipe=pipe)
     except Exception as e:
         raise ValueError(f"Could not load lora \n{lora}\nIt might be incompatible with {pipe.family.name}\n{e}") from e
 
@@ -93,17 +93,26 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     if textual_inversion is not None:
         _apply_textual_inversion(pipe, textual_inversion, model_name)
     if lora is not None:
-        _apply_lora(pipe, lora, cross_attention_scale)
+        try:
+            _apply_lora(pipe, lora, cross_attention_scale)
+        except Exception:
+            if textual_inversion is not None:
+                from ..models.lora import unload_textual_inversion
+
+                unload_textual_inversion(pipe)
+            raise
 
     sched = get_scheduler(scheduler_type, prediction_type=pipe.family.prediction_type)
     load_s = time.perf_counter() - t0
     try:
         p = pipe(scheduler=sched, **kwargs)
     finally:
-        if lora is not None:
-            from ..models.lora import unload_lora
+        from ..models.lora import unload_lora, unload_textual_inversion
 
-            unload_lora(pipe.unet)
+        if lora is not None:
+            unload_lora(pipe.unet, pipe=pipe)
+        if textual_inversion is not None:
+            unload_textual_inversion(pipe)
 
     config = dict(pipe.config)
     config["scheduler"] = ["chiaswarm_amd", sched.name]
@@ -152,7 +161,8 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
         lat.append(noise.permute(0, 2, 3, 1) * sched.init_noise_sigma)
     p = pipe(prompt=prompts, negative_prompt=negs, num_inference_steps=steps,
              guidance_scale=float(k0.get("guidance_scale", 7.5)), height=height, width=width,
-             latents=torch.cat(lat, 0).contiguous(), scheduler=sched, generator=k0["generator"])
+             latents=torch.cat(lat, 0).contiguous(), scheduler=sched,
+             generator=[(kw["generator"], n) for kw, n in zip(jobs, counts)])  # per-job sampler noise
     outs, i = [], 0
     for kw, n in zip(jobs, counts):
         op = OutputProcessor(kw.get("outputs", ["primary"]), kw.get("content_type", "image/jpeg"))

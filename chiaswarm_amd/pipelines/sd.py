@@ -33,7 +33,7 @@ from ..models import unet as unet_mod
 from ..models import vae as vae_mod
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
-from ..schedulers import Scheduler, get_scheduler
+from ..schedulers import Scheduler, batch_randn, get_scheduler
 from ..utils.trace import trace_range
 
 
@@ -134,6 +134,17 @@ class StableDiffusion:
         self._graphs: dict = {}
         self.use_graphs = self.device.type == "cuda"
 
+    def invalidate_graphs(self):
+        """Drop every captured hipGraph (they hold raw pointers to the weights
+        and packed buffers): called whenever an adapter changes the weights."""
+        self._graphs = {}
+        if hasattr(self, "_text_graphs"):
+            del self._text_graphs
+        self._kv_static = False
+        for m in [self.unet] + self.text_encoders:
+            for sub in m.modules():
+                sub.__dict__.pop("_ln_folds", None)
+
     # ------------------------------------------------------------------
     def _text_fn(self, ids, with_kv=True):
         """Device part of prompt encoding: every text encoder (+ the UNet's
@@ -229,8 +240,7 @@ class StableDiffusion:
                 x = sched.step(e_g, x, generator)
             elif coeffs is not None and ops.use_hip(x) and nrep <= 2:
                 need_noise = coeffs.D != 0.0
-                nz = (torch.randn(x.shape, generator=generator, device=x.device, dtype=torch.float32)
-                      if need_noise else None)
+                nz = batch_randn(x.shape, generator, x.device) if need_noise else None
                 x = ops.sched_step(e, x, sched, coeffs, guidance if cfg else None, nz)
             else:
                 if cfg:
@@ -313,8 +323,11 @@ class StableDiffusion:
         timings["text_encode"] = time.perf_counter() - t0
 
         sched.set_timesteps(num_inference_steps)
-        noise = torch.randn((b, 4, lh, lw), generator=generator, device=self.device,
-                            dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
+        # caller-supplied latents (coalesced batches) already consumed the
+        # generators' initial-noise draw: drawing again would shift every
+        # later sampler-noise draw away from the job's solo run
+        noise = None if (latents is not None and image is None) else batch_randn(
+            (b, 4, lh, lw), generator, self.device).permute(0, 2, 3, 1).contiguous()
         image_latents = mask_t = init_latents = None
         start = 0
         img_guid = None
@@ -346,7 +359,7 @@ class StableDiffusion:
                     image_latents = torch.cat([il] * (2 if cfg else 1), 0)
                     mask_t = None
                     init_latents = None
-        else:
+        elif noise is not None:
             x = noise * sched.init_noise_sigma
         if latents is not None:
             x = latents.to(self.device).float()

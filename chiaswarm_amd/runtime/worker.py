@@ -216,6 +216,11 @@ class Supervisor:
         gpus = visible_gpus(self.settings)
         if not gpus:
             return [ThreadExecutor("cpu")]
+        # (re)build the kernel library HERE, before any child initialises HIP:
+        # GPU children only check it (ops/_lib.py::check_fresh) and never run hipcc
+        from ..ops._lib import ensure_built
+
+        ensure_built()
         return [ProcessExecutor(g) for g in gpus]
 
     def _drain_compatible(self, first) -> list:

@@ -45,6 +45,20 @@ def _betas(n=1000, start=0.00085, end=0.012, schedule="scaled_linear"):
     return np.linspace(start, end, n, dtype=np.float64)
 
 
+def batch_randn(shape, generator=None, device=None) -> torch.Tensor:
+    """fp32 N(0, 1) of ``shape``.  ``generator`` may be a list of
+    ``(generator, rows)`` pairs: a coalesced batch (runtime.batcher) draws each
+    job's rows from that job's own generator, so a stochastic sampler gives
+    every job exactly the images it would get alone."""
+    if isinstance(generator, (list, tuple)):
+        parts = [torch.randn((n,) + tuple(shape[1:]), generator=g, device=device, dtype=torch.float32)
+                 for g, n in generator]
+        out = torch.cat(parts, 0)
+        assert out.shape == tuple(shape), (out.shape, shape)
+        return out
+    return torch.randn(shape, generator=generator, device=device, dtype=torch.float32)
+
+
 def karras_sigmas(sigma_min, sigma_max, n, rho=7.0):
     ramp = np.linspace(0, 1, n)
     lo, hi = sigma_min ** (1 / rho), sigma_max ** (1 / rho)
@@ -163,7 +177,7 @@ class Scheduler:
         if c.C != 0.0 and self.prev_x0 is not None:
             out = out + c.C * self.prev_x0
         if c.D != 0.0:
-            out = out + c.D * torch.randn(x.shape, generator=generator, device=x.device, dtype=torch.float32)
+            out = out + c.D * batch_randn(x.shape, generator, x.device)
         self.prev_x0 = x0
         self.step_index += 1
         return out

@@ -185,3 +185,24 @@ def test_supervisor_coalesces_queued_jobs():
         assert any(r["pipeline_config"].get("batched_with", 1) > 1 for r in hive.results)
     finally:
         hive.stop()
+
+
+def test_batched_stochastic_sampler_matches_solo():
+    """Ancestral sampler: each coalesced job draws its per-step noise from its own
+    generator, so its images do not depend on which jobs it was batched with."""
+    import numpy as np
+
+    from chiaswarm_amd.runtime.batcher import run_jobs
+
+    jobs = [{"id": f"a{i}", **TINY, "parameters": {"scheduler_type": "EulerAncestralDiscreteScheduler"},
+             "seed": 300 + i, "num_images_per_prompt": 1 + i,
+             "prompt": f"owl {i}", "content_type": "image/png"} for i in range(2)]
+    dev = Device("cpu")
+    batched = run_jobs([dict(j) for j in jobs], dev, max_images=8)
+    assert batched[0]["pipeline_config"].get("batched_with") == 2
+    for j, r in zip(jobs, batched):
+        solo = synchronous_do_work_function(dict(j), dev)
+        a = np.asarray(Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"]))), np.int16)
+        b = np.asarray(Image.open(io.BytesIO(base64.b64decode(solo["artifacts"]["primary"]["blob"]))), np.int16)
+        d = np.abs(a - b)
+        assert d.mean() < 0.5 and d.max() <= 24
