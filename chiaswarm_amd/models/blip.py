@@ -20,6 +20,73 @@ from PIL import Image
 from .layers import LayerNorm, Linear
 from .transformer import PostLNBlock, ViT
 
+_HF_TEXT = {"attention.self.query": "attn.q", "attention.self.key": "attn.k", "attention.self.value": "attn.v",
+            "attention.output.dense": "attn.o", "attention.output.LayerNorm": "ln1",
+            "crossattention.self.query": "cross.q", "crossattention.self.key": "cross.k",
+            "crossattention.self.value": "cross.v", "crossattention.output.dense": "cross.o",
+            "crossattention.output.LayerNorm": "ln_x", "intermediate.dense": "fc1", "output.dense": "fc2",
+            "output.LayerNorm": "ln2"}
+_HF_VIS = {"self_attn.projection": "attn.o", "layer_norm1": "ln1", "layer_norm2": "ln2", "mlp.fc1": "fc1",
+           "mlp.fc2": "fc2"}
+
+
+def convert_hf_blip(sd: dict) -> dict:
+    """transformers ``BlipForConditionalGeneration`` state dict -> this module's
+    keys (fused vision qkv split into q/k/v; the LM head decoder weight is tied
+    to the word embeddings and its bias duplicates ``cls.predictions.bias``)."""
+    out = {}
+    for k, v in sd.items():
+        if k.startswith("text_decoder.cls.predictions.decoder."):
+            continue
+        if k == "text_decoder.cls.predictions.bias":
+            out["head_bias"] = v
+            continue
+        m = k.removeprefix("text_decoder.")
+        if m.startswith("cls.predictions.transform."):
+            r = m.removeprefix("cls.predictions.transform.")
+            out[("head_transform." if r.startswith("dense.") else "head_ln.") + r.split(".", 1)[1]] = v
+            continue
+        if m.startswith("bert.embeddings."):
+            r = m.removeprefix("bert.embeddings.")
+            out[r.replace("LayerNorm.", "emb_ln.")] = v
+            continue
+        if m.startswith("bert.encoder.layer."):
+            n, rest = m.removeprefix("bert.encoder.layer.").split(".", 1)
+            for a, b in _HF_TEXT.items():
+                if rest.startswith(a + "."):
+                    out[f"layers.{n}.{b}.{rest[len(a) + 1:]}"] = v
+                    break
+            else:
+                out[k] = v  # surfaces as an unexpected key
+            continue
+        if k.startswith("vision_model.embeddings."):
+            r = k.removeprefix("vision_model.embeddings.")
+            if r == "class_embedding":
+                v = v.reshape(-1)
+            elif r == "position_embedding":
+                v = v.reshape(v.shape[-2], v.shape[-1])
+            out["vision_model." + r] = v
+            continue
+        if k.startswith("vision_model.post_layernorm."):
+            out["vision_model.post_ln." + k.rsplit(".", 1)[1]] = v
+            continue
+        if k.startswith("vision_model.encoder.layers."):
+            n, rest = k.removeprefix("vision_model.encoder.layers.").split(".", 1)
+            pre = f"vision_model.layers.{n}."
+            if rest.startswith("self_attn.qkv."):
+                for name, part in zip("qkv", v.chunk(3, 0)):
+                    out[pre + f"attn.{name}." + rest.rsplit(".", 1)[1]] = part.contiguous()
+                continue
+            for a, b in _HF_VIS.items():
+                if rest.startswith(a + "."):
+                    out[pre + b + rest[len(a):]] = v
+                    break
+            else:
+                out[k] = v
+            continue
+        out[k] = v
+    return out
+
 
 @dataclasses.dataclass
 class BlipConfig:
@@ -68,7 +135,13 @@ class BlipCaptioner(nn.Module):
         return torch.from_numpy(a)[None]
 
     @torch.no_grad()
-    def generate(self, image: Image.Image, prefix_ids: list[int], max_new_tokens=30) -> list[int]:
+    def generate(self, image: Image.Image, prefix_ids: list[int], max_new_tokens: int | None = None,
+                 max_length: int = 20) -> list[int]:
+        """Greedy decode from ``[DEC] + prefix``.  Default length cap: transformers'
+        ``generate`` default ``max_length=20`` total tokens, which the reference
+        call (swarm/captioning/caption_image.py:29, no length kwargs) runs with."""
+        if max_new_tokens is None:
+            max_new_tokens = max(0, max_length - 1 - len(prefix_ids))
         dev = self.head_bias.device
         dt = self.word_embeddings.weight.dtype
         img = self.preprocess(image).to(dev)

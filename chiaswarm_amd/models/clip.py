@@ -112,6 +112,7 @@ class CLIPTextModel(Prepared):
         super().__init__()
         self.cfg = cfg
         self.text_model = _TextTransformer(cfg)
+        self.checkpoint_alias_prefix = "text_model."  # transformers>=5 saves CLIPTextModel without it
         if cfg.projection_dim:
             self.text_projection = nn.Linear(cfg.hidden_size, cfg.projection_dim, bias=False)
 

@@ -131,6 +131,7 @@ class T5Encoder(nn.Module):
         self.encoder = nn.Module()
         self.encoder.block = nn.ModuleList([_Block(c, i == 0) for i in range(c.layers)])
         self.encoder.final_layer_norm = T5RMSNorm(c.d_model, c.eps)
+        self.checkpoint_ignore = ("encoder.embed_tokens.",)  # tied to ``shared`` in transformers checkpoints
 
     @torch.no_grad()
     def forward(self, ids: torch.Tensor, mask: torch.Tensor | None = None) -> torch.Tensor:
@@ -157,6 +158,8 @@ class T5Tokenizer:
             self.sp = sentencepiece.SentencePieceProcessor(model_file=path)
 
     def encode(self, text: str) -> list[int]:
+        # IFPipeline without bs4/ftfy caption cleaning: lower-case + strip
+        text = text.lower().strip()
         if self.sp is not None:
             return list(self.sp.encode(text))
         return [int.from_bytes(hashlib.blake2b(w.encode(), digest_size=8).digest(), "little") % (self.vocab - 100) + 3

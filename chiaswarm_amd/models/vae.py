@@ -135,6 +135,8 @@ class AutoencoderKL(Prepared):
         if with_encoder:
             self.encoder = Encoder(cfg)
             self.quant_conv = Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1, padding=0)
+        else:  # decoder-only: a full checkpoint's encoder tensors are expected extras
+            self.checkpoint_ignore = ("encoder.", "quant_conv.")
 
     def decode(self, z):
         """z: NHWC latents (already divided by scaling_factor) -> NHWC [-1, 1] image."""

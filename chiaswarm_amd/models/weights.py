@@ -3,56 +3,143 @@
 Reads a diffusers-layout model directory (``unet/``, ``vae/``, ``text_encoder/``
 [, ``text_encoder_2/``] each holding ``*.safetensors``) into our modules, whose
 parameter names follow the diffusers / transformers keys.  Older VAE attention
-names (``query/key/value/proj_attn``) are remapped.  Returns False when no
-weights are found (the caller keeps its random init and says so in
-``pipeline_config.weights``).
+names (``query/key/value/proj_attn``) are remapped.
+
+Loading is STRICT: every parameter of the module must be present with the right
+shape and every checkpoint tensor must land somewhere (up to a short list of
+known-harmless extras such as ``position_ids`` buffers), otherwise
+``CheckpointMismatch`` is raised — a partially loaded model would otherwise run
+with random layers and produce plausible-looking garbage.  The reference gets
+the same guarantee from ``from_pretrained`` (swarm/diffusion/diffusion_func.py:41-46).
+Every load returns a ``LoadReport`` (loaded / missing / unexpected / mismatched).
 """
 from __future__ import annotations
 
+import dataclasses
 import glob
 import os
 
 import torch
 
 _VAE_RENAMES = {".query.": ".to_q.", ".key.": ".to_k.", ".value.": ".to_v.", ".proj_attn.": ".to_out.0."}
+# checkpoint tensors that legitimately have no parameter here
+_HARMLESS = ("position_ids", "token_type_ids", "num_batches_tracked", "logit_scale")
+
+
+class CheckpointMismatch(ValueError):
+    pass
+
+
+@dataclasses.dataclass
+class LoadReport:
+    name: str
+    loaded: int
+    total: int
+    missing: list
+    unexpected: list
+    mismatched: list
+
+    @property
+    def complete(self) -> bool:
+        return not self.missing and not self.mismatched and self.loaded == self.total
+
+    def __int__(self):
+        return self.loaded
+
+    def __radd__(self, other):
+        return other + self.loaded
+
+    def summary(self, n=6) -> str:
+        def cut(xs):
+            return ", ".join(map(str, xs[:n])) + (f" (+{len(xs) - n} more)" if len(xs) > n else "")
+        parts = [f"{self.name or 'module'}: {self.loaded}/{self.total} tensors loaded"]
+        if self.missing:
+            parts.append(f"missing [{cut(self.missing)}]")
+        if self.unexpected:
+            parts.append(f"unexpected [{cut(self.unexpected)}]")
+        if self.mismatched:
+            parts.append(f"shape mismatch [{cut(self.mismatched)}]")
+        return "; ".join(parts)
 
 
 def _read_dir(d: str) -> dict:
     from safetensors.torch import load_file
 
     out = {}
-    for f in sorted(glob.glob(os.path.join(d, "*.safetensors"))):
+    files = sorted(glob.glob(os.path.join(d, "*.safetensors")))
+    # diffusers ships fp32 and fp16 variants side by side: take one of each model file
+    fp16 = [f for f in files if ".fp16." in os.path.basename(f)]
+    if fp16 and len(fp16) < len(files):
+        files = [f for f in files if f not in fp16]
+    for f in files:
         out.update(load_file(f, device="cpu"))
     return out
 
 
-def load_into(module: torch.nn.Module, sd: dict, renames: dict | None = None, prefix_strip: str = "") -> int:
+def load_into(module: torch.nn.Module, sd: dict, renames: dict | None = None, prefix_strip: str = "",
+              strict: bool = True, allow_unexpected: bool = False, name: str = "") -> LoadReport:
+    """Copy ``sd`` into ``module``'s parameters/buffers (cast to their dtype).
+    Raises ``CheckpointMismatch`` under ``strict`` unless the match is complete."""
     own = module.state_dict()
-    n = 0
+    ignore = tuple(getattr(module, "checkpoint_ignore", ()))  # e.g. a decoder-only VAE: encoder.*
+    alias = getattr(module, "checkpoint_alias_prefix", "")  # e.g. transformers>=5 drops "text_model."
+    done: set = set()
+    unexpected, mismatched = [], []
     with torch.no_grad():
         for k, v in sd.items():
             kk = k[len(prefix_strip):] if prefix_strip and k.startswith(prefix_strip) else k
             for a, b in (renames or {}).items():
                 kk = kk.replace(a, b)
-            if kk in own:
-                t = own[kk]
-                if t.shape != v.shape and v.numel() == t.numel():
-                    v = v.reshape(t.shape)  # e.g. VAE attention 1x1-conv weights
-                if t.shape == v.shape:
-                    t.copy_(v.to(t.dtype))
-                    n += 1
-    return n
+            if kk not in own and alias and alias + kk in own:
+                kk = alias + kk
+            if kk not in own:
+                if not kk.endswith(_HARMLESS) and not (ignore and kk.startswith(ignore)):
+                    unexpected.append(k)
+                continue
+            t = own[kk]
+            if t.shape != v.shape and v.numel() == t.numel() and v.dim() != t.dim():
+                v = v.reshape(t.shape)  # e.g. VAE attention 1x1-conv weights
+            if t.shape != v.shape:
+                mismatched.append(f"{kk} {tuple(v.shape)}!={tuple(t.shape)}")
+                continue
+            t.copy_(v.to(t.dtype))
+            done.add(kk)
+    missing = [k for k in own if k not in done and not k.endswith(_HARMLESS)]
+    rep = LoadReport(name, len(done), len([k for k in own if not k.endswith(_HARMLESS)]), missing, unexpected,
+                     mismatched)
+    if strict and (missing or mismatched or (unexpected and not allow_unexpected)):
+        raise CheckpointMismatch(rep.summary())
+    return rep
+
+
+def load_component(module, weights_dir: str, sub: str, renames=None, **kw) -> LoadReport | None:
+    """Strict load of ``weights_dir/sub/*.safetensors`` (None if that dir is absent)."""
+    d = os.path.join(weights_dir, sub) if sub else weights_dir
+    if not os.path.isdir(d) or not glob.glob(os.path.join(d, "*.safetensors")):
+        return None
+    return load_into(module, _read_dir(d), renames, name=sub or os.path.basename(d), **kw)
 
 
 def load_sd_weights(pipe, weights_dir: str) -> bool:
+    """All SD components of a diffusers directory; True if any was present.
+    ``pipe.load_reports`` keeps one ``LoadReport`` per component."""
     if not weights_dir or not os.path.isdir(weights_dir):
         return False
-    loaded = 0
     parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)]
     for i, te in enumerate(pipe.text_encoders):
         parts.append(("text_encoder" if i == 0 else f"text_encoder_{i + 1}", te, None))
+    reports = {}
     for sub, mod, ren in parts:
-        d = os.path.join(weights_dir, sub)
-        if os.path.isdir(d):
-            loaded += load_into(mod, _read_dir(d), ren)
-    return loaded > 0
+        r = load_component(mod, weights_dir, sub, ren)
+        if r is not None:
+            reports[sub] = r
+    pipe.load_reports = reports
+    return bool(reports)
+
+
+def tokenizer_dir(weights_dir: str | None, sub: str = "tokenizer") -> str | None:
+    if not weights_dir:
+        return None
+    d = os.path.join(weights_dir, sub)
+    return d if os.path.exists(os.path.join(d, "vocab.json")) or os.path.exists(os.path.join(d, "spiece.model")) \
+        else None

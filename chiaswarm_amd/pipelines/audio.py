@@ -64,17 +64,12 @@ class AudioLDM:
                        "sampling_rate": self.vocoder.cfg.sampling_rate, "weights": self.weights_source}
 
     def _load(self, d) -> bool:
-        import os
+        from ..models.weights import _VAE_RENAMES, load_component
 
-        from ..models.weights import _VAE_RENAMES, _read_dir, load_into
-
-        n = 0
-        for sub, mod, ren in (("text_encoder", self.text_encoder, HF_RENAMES), ("unet", self.unet, None),
-                              ("vae", self.vae, _VAE_RENAMES), ("vocoder", self.vocoder, None)):
-            p = os.path.join(d, sub)
-            if os.path.isdir(p):
-                n += load_into(mod, _read_dir(p), ren)
-        return n > 0
+        reps = [load_component(mod, d, sub, ren)
+                for sub, mod, ren in (("text_encoder", self.text_encoder, HF_RENAMES), ("unet", self.unet, None),
+                                      ("vae", self.vae, _VAE_RENAMES), ("vocoder", self.vocoder, None))]
+        return any(r is not None for r in reps)
 
     # ------------------------------------------------------------------
     def _unet_fn(self, x, t, class_labels):

@@ -26,6 +26,15 @@ def load_captioner(model_name: str, device: str):
             m = BlipCaptioner(cfg).to(dt).eval().requires_grad_(False)
         init_random_fast_(m, seed=11)
         w = find_weights(model_name)
+        m.weights_source = "random-init"
+        if w:
+            from ..models.blip import convert_hf_blip
+            from ..models.weights import _read_dir, load_into
+
+            sd = _read_dir(w)
+            if sd:
+                m.load_report = load_into(m, convert_hf_blip(sd), name=model_name)
+                m.weights_source = w
         prepare_model(m)
         return m, WordPiece(w, cfg.vocab)
 
@@ -41,7 +50,9 @@ def caption_callback(device_identifier, model_name, **kwargs):
         image = kwargs["image"]
         prompt = kwargs.get("prompt") or ""
         prefix = tok.encode(prompt) if prompt else []
-        ids = model.generate(image, prefix, max_new_tokens=int(kwargs.get("max_new_tokens", 30)))
+        mnt = kwargs.get("max_new_tokens")
+        ids = model.generate(image, prefix, max_new_tokens=None if mnt is None else int(mnt),
+                             max_length=int(kwargs.get("max_length", 20)))
         caption = tok.decode(ids)
         results["primary"] = make_text_result(caption)
         config["caption"] = caption

@@ -59,23 +59,23 @@ class IFCascade:
         self._load(weights_dir, stage2_dir)
         for m in mods:
             prepare_model(m)
-        self.tokenizer = T5Tokenizer(None, 77, vocab=self.t5.cfg.vocab)
+        from ..models.weights import tokenizer_dir
+
+        self.tokenizer = T5Tokenizer(tokenizer_dir(weights_dir), 77, vocab=self.t5.cfg.vocab)
         self.tiny = tiny
         self.acp = _cos_acp()
         self._g1 = GraphCache(self._s1)
         self._g2 = GraphCache(self._s2)
 
     def _load(self, d1, d2):
-        import os
 
-        from ..models.weights import _read_dir, load_into
+        from ..models.weights import load_component
 
         n = 0
         for d, parts in ((d1, (("text_encoder", self.t5), ("unet", self.stage1))), (d2, (("unet", self.stage2),))):
             for sub, m in parts if d else ():
-                p = os.path.join(d, sub)
-                if os.path.isdir(p):
-                    n += load_into(m, _read_dir(p))
+                if load_component(m, d, sub) is not None:
+                    n += 1
         if n:
             self.weights_source = str(d1)
 

@@ -116,8 +116,12 @@ class StableDiffusion:
                 self.weights_source = str(weights_dir)
         for m in [self.unet, self.vae] + self.text_encoders:
             prepare_model(m)
-        self.tokenizers = [CLIPTokenizer(None, 77, pad_with_eos=fam.pad_with_eos and i == 0,
-                                         vocab_size=c.vocab_size) for i, c in enumerate(fam.text)]
+        from ..models.weights import tokenizer_dir
+
+        # tokenizer/ (+ tokenizer_2/ for SDXL, whose OpenCLIP-bigG tokenizer pads with "!")
+        self.tokenizers = [CLIPTokenizer(tokenizer_dir(weights_dir, "tokenizer" if i == 0 else f"tokenizer_{i + 1}"),
+                                         77, pad_with_eos=fam.pad_with_eos and i == 0, vocab_size=c.vocab_size)
+                           for i, c in enumerate(fam.text)]
         self.controlnet = controlnet
         self.safety_checker = None
         self.config: dict[str, Any] = {

@@ -24,6 +24,7 @@ from .. import ops
 from ..models import clip as clip_mod
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
+from ..models.weights import tokenizer_dir
 from ..models.unet import LATENT_X2, TINY_X2, TINY_X4, X4_UPSCALER, UNet2DConditionModel
 from ..models.vae import SD_VAE, TINY_VAE, AutoencoderKL, VAEConfig
 from ..runtime.model_cache import cache, find_weights
@@ -53,16 +54,10 @@ class _Base:
             init_random_fast_(m, seed=seed + i)
         self.weights_source = "random-init"
         if weights_dir:
-            import os
+            from ..models.weights import _VAE_RENAMES, load_component
 
-            from ..models.weights import _VAE_RENAMES, _read_dir, load_into
-
-            n = 0
-            for sub, m in parts:
-                d = os.path.join(weights_dir, sub)
-                if os.path.isdir(d):
-                    n += load_into(m, _read_dir(d), _VAE_RENAMES if sub == "vae" else None)
-            if n:
+            reps = [load_component(m, weights_dir, sub, _VAE_RENAMES if sub == "vae" else None) for sub, m in parts]
+            if any(r is not None for r in reps):
                 self.weights_source = str(weights_dir)
         for m in mods:
             prepare_model(m)
@@ -114,7 +109,7 @@ class LatentUpscaler(_Base):
             self.text_encoder = clip_mod.CLIPTextModel(tcfg).to(self.dtype)
         self._init([self.unet, self.vae, self.text_encoder], seed, weights_dir,
                    [("unet", self.unet), ("vae", self.vae), ("text_encoder", self.text_encoder)])
-        self.tokenizer = CLIPTokenizer(None, 77, vocab_size=tcfg.vocab_size)
+        self.tokenizer = CLIPTokenizer(tokenizer_dir(weights_dir), 77, vocab_size=tcfg.vocab_size)
         self._graphs = GraphCache(self._unet_fn)
         self.f = 2 ** (len(self.vae.cfg.block_out_channels) - 1)
 
@@ -149,7 +144,7 @@ class X4Upscaler(_Base):
             self.text_encoder = clip_mod.CLIPTextModel(tcfg).to(self.dtype)
         self._init([self.unet, self.vae, self.text_encoder], seed, weights_dir,
                    [("unet", self.unet), ("vae", self.vae), ("text_encoder", self.text_encoder)])
-        self.tokenizer = CLIPTokenizer(None, 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
+        self.tokenizer = CLIPTokenizer(tokenizer_dir(weights_dir), 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
         self._graphs = GraphCache(self._unet_fn)
         # low_res_scheduler: DDPM linear betas 1e-4 .. 2e-2
         betas = np.linspace(1e-4, 0.02, 1000, dtype=np.float64)

@@ -46,15 +46,14 @@ class TextToVideo:
             m.eval().requires_grad_(False)
             init_random_fast_(m, seed=21 + i)
         w = find_weights(model_name)
-        if w:
-            from ..models.weights import _read_dir, load_into
+        from ..models.weights import _VAE_RENAMES, load_component, tokenizer_dir
 
+        if w:
             for sub, m in (("unet", self.unet), ("vae", self.vae), ("text_encoder", self.text)):
-                if os.path.isdir(os.path.join(w, sub)):
-                    load_into(m, _read_dir(os.path.join(w, sub)))
+                load_component(m, w, sub, _VAE_RENAMES if sub == "vae" else None)
         for m in (self.unet, self.vae, self.text):
             prepare_model(m)
-        self.tok = CLIPTokenizer(None, 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
+        self.tok = CLIPTokenizer(tokenizer_dir(w), 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
         self.config = {"_class_name": "TextToVideoSDPipeline", "_framework": "chiaswarm_amd",
                        "unet": ["chiaswarm_amd", "UNet3DConditionModel"], "weights": w or "random-init"}
 
