@@ -30,7 +30,9 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # persistent continuous-ring LDS-DMA variants (K % 64 == 0, no split-K)
          21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64),
          # one 256x160 workgroup per CU (3-stage, 156 KB LDS): least L2->LDS traffic per output
-         25: (256, 160), 26: (128, 160)}
+         25: (256, 160), 26: (128, 160),
+         # 8-wave 256-row phased tiles (gemm8p.hip): half the L2->LDS bytes per FLOP of 128x128
+         31: (256, 256), 32: (256, 128)}
 
 
 def _user_path():

@@ -332,7 +332,10 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else tile = 4;
   }
   int err;
-  if (tile >= 11) {
+  if (tile >= 31) {
+    err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
+    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, 11, ksplit, CONV, s);
+  } else if (tile >= 11) {
     err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
   } else {
     if (a.act == ACT_GEGLU && tile != 1 && tile != 3) tile = 1;  // needs >= 32 cols per wave

@@ -156,7 +156,7 @@ __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
   return *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + r, args.M - 1) * 2);
 }
 
-template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1>
+template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                               bf16_t* smem, int m0, int n0, int split,
                                               float2 lnrow = make_float2(0.f, 0.f)) {
@@ -244,13 +244,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   // addresses for every 8 outputs, and at K = 320 the epilogue is most of a
   // tile's instruction stream (the SIMDs were issue-saturated, PMC r1i).
   constexpr int VPR = BN / 8;
-  if constexpr (256 % VPR == 0 && PR % (256 / VPR) == 0) {
+  if constexpr (NTHR % VPR == 0 && PR % (NTHR / VPR) == 0) {
     const bool fast = !args.gn_part && !args.row_part && !ln && act != ACT_GEGLU && !args.bias2d &&
                       (N % 8) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
                       (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
                       (!args.res || ((args.ldr % 8) == 0 && ((((size_t)args.res) & 15) == 0)));
     if (fast) {
-      constexpr int RPI = 256 / VPR;  // band rows per iteration
+      constexpr int RPI = NTHR / VPR;  // band rows per iteration
       const int cv = tid % VPR, r0 = tid / VPR;
       const int n = n0 + cv * 8;
       if (n < N) {
@@ -291,9 +291,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   const int BNo = act == ACT_GEGLU ? BN / 2 : BN;
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
   const int vpr = BNo / 8;
-  // PR * vpr is a multiple of 256 for every tile, so each wave runs the same
+  // PR * vpr is a multiple of NTHR for every tile, so each wave runs the same
   // number of iterations and the row-statistics shuffles below see all lanes
-  for (int v = tid; v < PR * vpr; v += 256) {
+  for (int v = tid; v < PR * vpr; v += NTHR) {
     const int row = v / vpr, cv = v - row * vpr;  // row within the band
     const int m = m0 + pr0 + row, n = on0 + cv * 8;
     const bool live = m < M && n < outN;
@@ -375,7 +375,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     // cancellation.  The consumer GroupNorm merges the segments.
     const int seg = args.gn_seg > 0 ? args.gn_seg : PR;
     epi_barrier<RAW>();
-    for (int t = tid; t < BN * (PR / seg); t += 256) {
+    for (int t = tid; t < BN * (PR / seg); t += NTHR) {
       const int c = t % BN, sq = t / BN;
       const int n = n0 + c, r0 = sq * seg;
       if (n >= N || m0 + pr0 + r0 >= M) continue;
@@ -405,3 +405,4 @@ __host__ __forceinline__ int gn_seg_for() {
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);
+int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);

@@ -399,3 +399,70 @@ def test_group_norm_of_concat_without_fused_stats(gpu, Ca, Cb):
     y = hip_ops.group_norm_cat(a, b, g, bt, 32, 1e-5, True)
     ref = ops._ref_group_norm(torch.cat([a, b], -1).float().cpu(), g.float().cpu(), bt.float().cpu(), 32, 1e-5, True)
     assert rel_err(y.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [31, 32])
+@pytest.mark.parametrize("split", [1, 3])
+def test_phased_256_tiles_gemm_conv(gpu, tile, split):
+    """8-wave 256-row phased kernels (gemm8p.hip): ragged M / N edges, split-K,
+    and the implicit-GEMM conv FAST staging (stride 1 / 2, fused nearest-x2)."""
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, N, K = 600, 320, 640  # M and N not multiples of the tile
+    a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=gpu)
+    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, None, tile, split,
+              _p(ws), _s())
+    ref = ops._ref_gemm(a.float().cpu(), w.float().cpu(), b.float().cpu(), r.float().cpu(), "silu")
+    assert rel_err(out.cpu(), ref) < 1e-2
+    for (B, H, W, Cin, Cout, stride, up) in ((2, 20, 24, 128, 192, 1, 0), (2, 17, 16, 64, 320, 2, 0),
+                                             (1, 9, 12, 128, 64, 1, 1)):
+        x = rnd(B, H, W, Cin, dev=gpu)
+        wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+        b2 = rnd(B, Cout, dev=gpu)
+        Ho, Wo = ops.conv_out_size(H, W, 3, 3, stride, 1, bool(up))
+        y = torch.empty(B, Ho, Wo, Cout, dtype=torch.bfloat16, device=gpu)
+        ws = torch.empty(split * B * Ho * Wo * Cout, dtype=torch.float32, device=gpu)
+        _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, _p(b2), None, B, H, W, Cin, Cout, 3, 3, stride, 1, 1, Ho,
+                  Wo, up, Cin, Cout, 0, 0, 1.0, 1, None, tile, split, _p(ws), _s())
+        ref = ops._ref_conv2d(x.float().cpu(), wp.float().cpu(), None, stride, 1, None, bool(up), b2.float().cpu())
+        assert rel_err(y.cpu(), ref) < 1e-2, (B, H, W, Cin, Cout, stride, up)
+
+
+@pytest.mark.parametrize("tile", [31, 32])
+def test_phased_256_tiles_geglu_and_gn_stats(gpu, tile):
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, K, F_ = 700, 320, 640
+    a = rnd(M, K, dev=gpu)
+    w, b = rnd(2 * F_, K, dev=gpu, scale=K ** -0.5), rnd(2 * F_, dev=gpu)
+    wp, bp = ops.pack_geglu(w, b)
+    y = torch.empty(M, F_, dtype=torch.bfloat16, device=gpu)
+    _lib.call("csk_gemm", _p(y), _p(a), _p(wp), _p(bp), None, None, M, 2 * F_, K, K, K, F_, F_, 1, 3, 1.0, None,
+              tile, 1, None, _s())
+    h, g = (a.float() @ w.float().t() + b.float()).chunk(2, dim=-1)
+    assert rel_err(y, h * F.gelu(g)) < 1e-2
+    # conv producing fused GroupNorm statistics of its output (64x64 UNet level shape, small batch)
+    from chiaswarm_amd.ops import tuning
+
+    x = rnd(2, 32, 32, 128, dev=gpu)
+    wt = rnd(256, 128, 3, 3, dev=gpu, scale=(9 * 128) ** -0.5)
+    wp = ops.pack_conv_weight(wt)
+    key = "c:2:32:32:128:256:3:1:0"
+    t = tuning.table()
+    old = t.get(key)
+    t[key] = [tile, 1, 0.0]
+    try:
+        yc = hip_ops.conv2d(x, wp, None, 1, 1, None, False, None, gn_stats=True)
+        gamma, beta = rnd(256, dev=gpu), rnd(256, dev=gpu)
+        gn = hip_ops.group_norm(yc, gamma, beta, 32, 1e-5, silu=True)
+    finally:
+        if old is None:
+            t.pop(key, None)
+        else:
+            t[key] = old
+    ref = F.silu(F.group_norm(yc.float().permute(0, 3, 1, 2), 32, gamma.float(), beta.float(), 1e-5)).permute(0, 2, 3, 1)
+    assert rel_err(gn, ref) < 1e-2

@@ -1,0 +1,88 @@
+#!/usr/bin/env python
+"""Same-process A/B of GEMM / conv tiles on the SD2.1 UNet step's hot shapes
+(interleaved rounds, random operands, median us and TFLOP/s per tile):
+
+    python tools/tilebench.py --tiles 11,26,31,32 --rounds 5
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from chiaswarm_amd import ops  # noqa: E402
+from chiaswarm_amd.ops import _lib  # noqa: E402
+from chiaswarm_amd.ops.hip_ops import _p, _s  # noqa: E402
+
+CONVS = ["8,64,64,320,320", "8,64,64,640,320", "8,64,64,960,320", "8,32,32,640,640", "8,32,32,1280,640",
+         "8,32,32,1920,640", "8,16,16,1280,1280", "8,16,16,2560,1280", "8,32,32,320,640", "8,16,16,640,1280"]
+GEMMS = ["32768,320,320", "32768,960,320", "32768,2560,320:geglu", "32768,320,1280", "8192,640,640",
+         "8192,5120,640:geglu", "8192,640,2560", "2048,1280,1280", "2048,10240,1280:geglu", "2048,1280,5120"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="11,26,31,32")
+    ap.add_argument("--splits", default="1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="", help="conv|gemm")
+    a = ap.parse_args()
+    _lib.load()
+    dev = torch.device("cuda", 0)
+    tiles = [int(t) for t in a.tiles.split(",")]
+    splits = [int(s) for s in a.splits.split(",")]
+    jobs = []
+    if a.only != "gemm":
+        for spec in CONVS:
+            B, H, W, Cin, Cout = map(int, spec.split(","))
+            x = (torch.randn(B, H, W, Cin, device=dev)).to(torch.bfloat16)
+            wp = ops.pack_conv_weight((torch.randn(Cout, Cin, 3, 3, device=dev) * (9 * Cin) ** -0.5).to(torch.bfloat16))
+            y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
+            fl = 2.0 * B * H * W * Cout * 9 * Cin
+
+            def run(tile, split, x=x, wp=wp, y=y, B=B, H=H, W=W, Cin=Cin, Cout=Cout):
+                ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=dev) if split > 1 else None
+                _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1,
+                          H, W, 0, Cin, Cout, 0, 0, 1.0, 1, None, tile, split, _p(ws), _s())
+            jobs.append((f"conv {spec}", fl, run))
+    if a.only != "conv":
+        for spec in GEMMS:
+            geglu = spec.endswith(":geglu")
+            M, N, K = map(int, spec.split(":")[0].split(","))
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            w = (torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
+            no = N // 2 if geglu else N
+            y = torch.empty(M, no, dtype=torch.bfloat16, device=dev)
+            fl = 2.0 * M * N * K
+
+            def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu):
+                ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
+                _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, no, no, 1,
+                          3 if geglu else 0, 1.0, None, tile, split, _p(ws), _s())
+            jobs.append((f"gemm {spec}", fl, run))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for name, fl, run in jobs:
+        res = {}
+        arms = [(t, s) for t in tiles for s in splits]
+        for t, s in arms:
+            run(t, s)
+        torch.cuda.synchronize()
+        for _ in range(a.rounds):
+            for t, s in arms:
+                ev[0].record()
+                for _ in range(a.iters):
+                    run(t, s)
+                ev[1].record()
+                ev[1].synchronize()
+                res.setdefault((t, s), []).append(ev[0].elapsed_time(ev[1]) * 1e3 / a.iters)
+        line = "  ".join(f"t{t}/s{s}: {statistics.median(v):7.1f}us {fl / statistics.median(v) / 1e6:6.0f}TF"
+                         for (t, s), v in res.items())
+        print(f"{name:28s} {line}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
