@@ -73,10 +73,18 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
   // outputs are never stored), which keeps the 256-register budget spill-free.
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
+  // Ragged last tiles: a lane's rows r0 + 64 i past the end re-read its last valid
+  // row (clamped count; that row's outputs are never stored).  Interior tiles —
+  // all but the last row / column of tiles — skip the clamp (wave-uniform branch).
   const size_t bstride = (size_t)64 * args.ldb;
-  const bf16_t* fb = args.W + (size_t)min(n0 + wid * 8 + lrow, N - 1) * args.ldb + kbeg + lchunk * 8;
+  const int rb0 = n0 + wid * 8 + lrow;
+  const bool b_full = n0 + BN <= N;
+  const int b_cnt = max(1, min(IB, (N - rb0 + 63) / 64));
+  const bf16_t* fb = args.W + (size_t)min(rb0, N - 1) * args.ldb + kbeg + lchunk * 8;
   const bf16_t* fa0 = nullptr;
   size_t astride = 0;
+  const bool a_full = m0 + BM <= M;
+  int a_cnt = IA;
   // conv rows: sample base pixel + packed (oh*stride - pt, ow*stride - pl); an
   // out-of-range row gets an impossible ih so every tap reads the zero page
   int a_pix[CONV ? IA : 1], a_hw[CONV ? IA : 1];
@@ -96,7 +104,9 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
     }
   } else {
     astride = (size_t)64 * args.lda;
-    fa0 = args.A + (size_t)min(m0 + wid * 8 + lrow, M - 1) * args.lda + kbeg + lchunk * 8;
+    const int ra0 = m0 + wid * 8 + lrow;
+    a_cnt = max(1, min(IA, (M - ra0 + 63) / 64));
+    fa0 = args.A + (size_t)min(ra0, M - 1) * args.lda + kbeg + lchunk * 8;
   }
   int f_ky = 0, f_kx = 0, f_c = 0;
   auto set_rows = [&]() {
@@ -118,10 +128,17 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
 
   auto issue_a = [&](int buf) {
     bf16_t* as = smem + buf * STAGE;
+    if (CONV || a_full) {
 #pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const bf16_t* src = CONV ? fa[CONV ? i : 0] + f_c : fa0 + i * astride;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+      for (int i = 0; i < IA; ++i) {
+        const bf16_t* src = CONV ? fa[CONV ? i : 0] + f_c : fa0 + i * astride;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IA; ++i)
+        __builtin_amdgcn_global_load_lds((gptr_t)(fa0 + min(i, a_cnt - 1) * astride),
+                                         (lptr_t)(as + (i * 8 + wid) * 8 * BK), 16, 0, 0);
     }
     if constexpr (CONV) {
       f_c += BK;
@@ -136,9 +153,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
   };
   auto issue_b = [&](int buf) {
     bf16_t* bs = smem + buf * STAGE + BM * BK;
+    if (b_full) {
 #pragma unroll
-    for (int i = 0; i < IB; ++i)
-      __builtin_amdgcn_global_load_lds((gptr_t)(fb + i * bstride), (lptr_t)(bs + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+      for (int i = 0; i < IB; ++i)
+        __builtin_amdgcn_global_load_lds((gptr_t)(fb + i * bstride), (lptr_t)(bs + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < IB; ++i)
+        __builtin_amdgcn_global_load_lds((gptr_t)(fb + min(i, b_cnt - 1) * bstride),
+                                         (lptr_t)(bs + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+    }
     fb += BK;
   };
 
