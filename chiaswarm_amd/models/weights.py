@@ -112,12 +112,31 @@ def load_into(module: torch.nn.Module, sd: dict, renames: dict | None = None, pr
     return rep
 
 
+def read_checkpoint(d: str, like: torch.nn.Module | None = None) -> dict:
+    """All tensors of a directory's safetensors files.  Inside
+    ``comm.collective_loading()`` with a process group, each rank reads only
+    its 1/world share of the bytes and an all_gather assembles the rest
+    (parallel/sharded.py); otherwise a plain local read."""
+    from ..parallel import comm
+
+    if comm.collective_load_active():
+        from ..parallel.sharded import safetensors_files, sharded_state_dict
+
+        p = next(like.parameters(), None) if like is not None else None
+        dt = p.dtype if p is not None else torch.float32
+        dev = p.device if p is not None else "cpu"
+        if dev is not None and getattr(dev, "type", dev) == "cuda" and torch.distributed.get_backend() == "gloo":
+            dev = "cpu"
+        return sharded_state_dict(safetensors_files(d), dt, dev)
+    return _read_dir(d)
+
+
 def load_component(module, weights_dir: str, sub: str, renames=None, **kw) -> LoadReport | None:
     """Strict load of ``weights_dir/sub/*.safetensors`` (None if that dir is absent)."""
     d = os.path.join(weights_dir, sub) if sub else weights_dir
     if not os.path.isdir(d) or not glob.glob(os.path.join(d, "*.safetensors")):
         return None
-    return load_into(module, _read_dir(d), renames, name=sub or os.path.basename(d), **kw)
+    return load_into(module, read_checkpoint(d, module), renames, name=sub or os.path.basename(d), **kw)
 
 
 def load_sd_weights(pipe, weights_dir: str) -> bool:

@@ -93,11 +93,12 @@ def candidates(M, N, K):
             continue
         if tile in (2, 6, 12, 17, 19, 22, 24) and N > 1280:
             continue
-        if tile >= 21 and K % 64:
+        persistent = 21 <= tile <= 24
+        if (persistent or tile >= 31) and K % 64:
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8):
-            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split or tile >= 21):
+            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split or persistent):
                 continue
             out.append((tile, split))
     return out

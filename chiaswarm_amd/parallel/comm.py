@@ -51,6 +51,31 @@ def is_dist():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+_COLLECTIVE_LOAD = False
+
+
+class collective_loading:
+    """Within this context every rank of the process group loads the SAME
+    models in the SAME order, so checkpoint reads may be sharded across ranks
+    (parallel/sharded.py).  Outside it, loads are rank-local (a job-triggered
+    load on one GPU must never wait on the others)."""
+
+    def __enter__(self):
+        global _COLLECTIVE_LOAD
+        self._prev = _COLLECTIVE_LOAD
+        _COLLECTIVE_LOAD = is_dist()
+        return self
+
+    def __exit__(self, *exc):
+        global _COLLECTIVE_LOAD
+        _COLLECTIVE_LOAD = self._prev
+        return False
+
+
+def collective_load_active() -> bool:
+    return _COLLECTIVE_LOAD and is_dist()
+
+
 def barrier():
     if is_dist():
         if dist.get_backend() == "nccl":
