@@ -30,6 +30,7 @@ import torch.nn as nn
 
 from .. import ops
 from .layers import Conv1d, ConvTranspose1d, LayerNorm, Linear, init_random_fast_, prepare_model
+from ..utils import stable_seed
 
 # token conventions (Bark generation constants)
 CONTEXT_WINDOW = 1024
@@ -512,4 +513,4 @@ def load_bark(model_name: str, device: str) -> Bark:
     size = "tiny" if name.startswith("tiny") else ("small" if "small" in name else "large")
     return cache().get(("bark", model_name, device),
                        lambda: Bark(device, size=size, weights_dir=find_weights(model_name),
-                                    seed=abs(hash(model_name)) % (1 << 31)))
+                                    seed=stable_seed(model_name)))

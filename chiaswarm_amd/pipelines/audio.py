@@ -32,6 +32,7 @@ from ..output.processor import make_result
 from ..runtime.model_cache import cache, find_weights
 from ..schedulers import get_scheduler
 from .graphs import GraphCache
+from ..utils import stable_seed
 
 # AudioLDM's training noise schedule (scheduler/scheduler_config.json of cvssp/audioldm*)
 AUDIOLDM_SCHED = dict(beta_start=0.0015, beta_end=0.0195, beta_schedule="scaled_linear",
@@ -148,7 +149,7 @@ def load_audioldm(model_name: str, device: str) -> AudioLDM:
     tiny = model_name.lower().startswith("tiny")
     return cache().get(("audioldm", model_name, device),
                        lambda: AudioLDM(device, tiny=tiny, weights_dir=find_weights(model_name),
-                                        seed=abs(hash(model_name)) % (1 << 31)))
+                                        seed=stable_seed(model_name)))
 
 
 def _scheduler_for(scheduler_type):

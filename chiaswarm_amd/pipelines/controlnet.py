@@ -16,6 +16,7 @@ from PIL import Image
 from ..models.controlnet import ControlNetModel
 from ..models.layers import init_random_fast_, prepare_model
 from ..runtime.model_cache import cache, find_weights
+from ..utils import stable_seed
 
 
 class ControlNetRunner:
@@ -48,7 +49,7 @@ def load_controlnet(name: str, pipe, device_identifier: str, revision: str = "ma
         cfg = pipe.unet.cfg
         with torch.device(device_identifier):
             m = ControlNetModel(cfg).to(pipe.dtype).eval().requires_grad_(False)
-        init_random_fast_(m, seed=abs(hash(name)) % (1 << 31))
+        init_random_fast_(m, seed=stable_seed(name))
         w = find_weights(name, revision)
         if w:
             from ..models.weights import _read_dir, load_into

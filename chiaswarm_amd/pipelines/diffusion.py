@@ -21,6 +21,7 @@ from ..output.processor import OutputProcessor
 from ..runtime.model_cache import cache, find_weights
 from ..schedulers import get_scheduler
 from .sd import StableDiffusion, family_for_model
+from ..utils import stable_seed
 
 _DROP = ("supports_xformers", "cross_attention_kwargs", "eta", "callback", "callback_steps", "output_type",
          "return_dict", "prompt_embeds", "negative_prompt_embeds", "guidance_rescale", "clip_skip")
@@ -32,7 +33,7 @@ def load_sd(model_name: str, device_identifier: str, revision: str = "main", con
 
     def make():
         return StableDiffusion(fam, device=device_identifier, weights_dir=find_weights(model_name, revision),
-                               seed=abs(hash(model_name)) % (1 << 31))
+                               seed=stable_seed(model_name))
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)
     if not hasattr(pipe, "_safety_probed"):
@@ -89,6 +90,24 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     if kwargs.pop("save_preprocessed_input", False) and kwargs.get("image") is not None:
         output_processor.add_other_outputs("preprocessed_input", [kwargs.get("image")])
 
+    # Multi-image txt2img: image j is seeded with (job seed + j) — its own
+    # generator for the initial noise AND every sampler-noise draw — so a job
+    # gives the same images whether it runs on one GPU or is split across
+    # several (runtime.worker: ``_image_range`` sub-jobs).  The reference drew
+    # all images from one generator stream (swarm/gpu/device.py:35-41).
+    image_range = kwargs.pop("_image_range", None)
+    return_images = bool(kwargs.pop("_return_images", False))
+    gen = kwargs.get("generator")
+    n_img = int(kwargs.get("num_images_per_prompt", 1) or 1)
+    if (isinstance(gen, torch.Generator) and kwargs.get("image") is None
+            and (n_img > 1 or image_range is not None)):
+        lo = int(image_range[0]) if image_range is not None else 0
+        hi = int(image_range[1]) if image_range is not None else n_img
+        base = gen.initial_seed()
+        kwargs["num_images_per_prompt"] = hi - lo
+        kwargs["generator"] = [(torch.Generator(device=gen.device).manual_seed((base + j) % (1 << 63)), 1)
+                               for j in range(lo, hi)]
+
     pipe = load_sd(model_name, device_identifier, revision, controlnet_name, controlnet_revision)
     if textual_inversion is not None:
         _apply_textual_inversion(pipe, textual_inversion, model_name)
@@ -121,10 +140,17 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
         config["nsfw"] = True
 
     images = p.images
+    if return_images:  # a split sub-job: the supervisor assembles and encodes the whole job
+        import numpy as np
+
+        config["_images"] = [np.asarray(im) for im in images]
+        return {}, config
     if upscale:
         from .upscale import upscale_images
 
-        images = upscale_images(images, device_identifier, kwargs.get("prompt", ""), kwargs.get("generator"))
+        g = kwargs.get("generator")
+        images = upscale_images(images, device_identifier, kwargs.get("prompt", ""),
+                                g[0][0] if isinstance(g, list) else g)
     output_processor.add_outputs(images)
     results = output_processor.get_results()
     if os.environ.get("SDAAS_TIMINGS"):
@@ -150,19 +176,25 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
     sched.set_timesteps(steps)
     height = int(k0.get("height") or pipe.family.default_size) // 8 * 8
     width = int(k0.get("width") or pipe.family.default_size) // 8 * 8
-    prompts, negs, lat, counts = [], [], [], []
+    prompts, negs, lat, counts, gens = [], [], [], [], []
     for kw in jobs:
         n = max(1, int(kw.get("num_images_per_prompt", 1) or 1))
         counts.append(n)
         prompts += [kw.get("prompt", "")] * n
         negs += [kw.get("negative_prompt") or ""] * n
-        noise = torch.randn((n, 4, height // 8, width // 8), generator=kw["generator"], device=pipe.device,
-                            dtype=torch.float32)
-        lat.append(noise.permute(0, 2, 3, 1) * sched.init_noise_sigma)
+        g = kw["generator"]
+        # same per-image seeding as diffusion_callback (image j of a job: seed + j)
+        jg = [(g, n)] if n == 1 else [(torch.Generator(device=g.device).manual_seed((g.initial_seed() + j) % (1 << 63)), 1)
+                                      for j in range(n)]
+        gens += jg
+        for gj, nj in jg:
+            noise = torch.randn((nj, 4, height // 8, width // 8), generator=gj, device=pipe.device,
+                                dtype=torch.float32)
+            lat.append(noise.permute(0, 2, 3, 1) * sched.init_noise_sigma)
     p = pipe(prompt=prompts, negative_prompt=negs, num_inference_steps=steps,
              guidance_scale=float(k0.get("guidance_scale", 7.5)), height=height, width=width,
              latents=torch.cat(lat, 0).contiguous(), scheduler=sched,
-             generator=[(kw["generator"], n) for kw, n in zip(jobs, counts)])  # per-job sampler noise
+             generator=gens)  # per-job / per-image sampler noise
     outs, i = [], 0
     for kw, n in zip(jobs, counts):
         op = OutputProcessor(kw.get("outputs", ["primary"]), kw.get("content_type", "image/jpeg"))

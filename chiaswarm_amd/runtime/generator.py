@@ -15,6 +15,7 @@ import time
 
 from .. import __version__
 from ..jobs.router import format_args
+from ..log_setup import log_job
 from ..output.processor import image_from_text, image_to_buffer, make_result, make_text_result
 from ..utils.trace import trace_range
 
@@ -42,22 +43,39 @@ def synchronous_do_work_function(job, device):
     print(f"Processing {job_id} on {device.descriptor()}")
     content_type = job.get("content_type", "image/jpeg")
     t0 = time.perf_counter()
+    rec = {"id": job_id, "workflow": job.get("workflow", "txt2img"), "model": job.get("model_name"),
+           "device": device.descriptor(), "images": job.get("num_images_per_prompt", 1)}
+
+    def done(status, cfg=None, err=None):
+        rec.update(status=status, seconds=round(time.perf_counter() - t0, 4))
+        if err is not None:
+            rec["error"] = str(err)[:300]
+        if cfg:
+            for k in ("seed", "timings", "batched_with", "split", "weights"):
+                if k in cfg:
+                    rec[k] = cfg[k]
+        log_job(rec)  # one structured JSON line per job
+
     try:
         worker_function, kwargs = format_args(job)
     except Exception as e:  # (a) fatal: bad input
         logging.exception(e)
+        done("fatal", err=e)
         return _error_result(job_id, e, content_type, True)
     try:
         with trace_range(f"job {job_id}"):
             artifacts, pipeline_config = device(worker_function, **kwargs)
     except ValueError as e:  # (b) fatal
         logging.exception(e)
+        done("fatal", err=e)
         return _error_result(job_id, e, content_type, True)
     except Exception as e:  # (c) retryable
         logging.exception(e)
+        done("error", err=e)
         return _error_result(job_id, e, content_type, False)
     if isinstance(pipeline_config.get("timings"), dict):  # only with SDAAS_TIMINGS=1
         pipeline_config["timings"]["total"] = round(time.perf_counter() - t0, 4)
+    done("ok", pipeline_config)
     return {"id": job_id, "artifacts": artifacts, "nsfw": pipeline_config.get("nsfw", False),
             "worker_version": __version__, "pipeline_config": pipeline_config}
 

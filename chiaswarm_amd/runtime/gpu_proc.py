@@ -6,6 +6,12 @@ pool of encoder processes this process starts BEFORE it touches the GPU
 (output/encoder.py): the GPU thread hands over uint8 pixels and goes straight on
 to the next job; a finisher thread resolves the encodings and posts results.
 
+With ``WORLD_SIZE`` > 1 in its environment (set by the supervisor) the child
+joins the node's process group — RCCL over xGMI (``nccl`` backend), gloo for
+CPU children — before any GPU work.  The group is used for collective model
+preloads: every child reads 1/N of each checkpoint's bytes and an all_gather
+assembles the rest (parallel/sharded.py).  Job-triggered loads stay local.
+
 This module must not import torch at import time: the child selects its GPU via
 HIP_VISIBLE_DEVICES *before* torch initialises.
 """
@@ -13,6 +19,51 @@ from __future__ import annotations
 
 import os
 import traceback
+
+
+def _join_group(gpu_index) -> str:
+    """Join the node's process group (RANK / WORLD_SIZE / MASTER_* in the env).
+    Returns a status string; a failure leaves the child working rank-local."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return "single"
+    os.environ["LOCAL_RANK"] = "0"  # this child sees exactly one GPU (HIP_VISIBLE_DEVICES)
+    from ..parallel import comm
+
+    backend = "gloo" if gpu_index == "cpu" else os.environ.get("CSK_DIST_BACKEND", "nccl")
+    try:
+        comm.init_distributed(backend=backend, timeout_s=int(os.environ.get("CSK_DIST_TIMEOUT", "600")))
+        return f"{backend} rank {os.environ.get('RANK')}/{os.environ.get('WORLD_SIZE')}"
+    except Exception as e:  # pragma: no cover - depends on the node
+        import logging
+
+        logging.exception(e)
+        return f"no group ({e})"
+
+
+def _preload(names: list, device_id: str) -> dict:
+    """Collective preload of SD-family models (every child, same list, same order)."""
+    from ..parallel import comm
+    from ..pipelines.diffusion import load_sd
+
+    done = {}
+    with comm.collective_loading():
+        for name in names:
+            pipe = load_sd(name, device_id)
+            done[name] = pipe.config.get("weights", "random-init")
+    return done
+
+
+def _test_hook(job):
+    """CSK_TEST_HOOKS=1 only: deterministic crash / hang for the watchdog tests."""
+    if os.environ.get("CSK_TEST_HOOKS") != "1" or not isinstance(job, dict):
+        return
+    what = job.get("_test")
+    if what == "exit":
+        os._exit(3)
+    if what == "hang":
+        import time
+
+        time.sleep(3600)
 
 
 def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
@@ -53,12 +104,21 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         setup_logging(resolve_path(settings.log_filename), settings.log_level, suffix=f"gpu{gpu_index}")
     except Exception:
         pass
+    group = _join_group(gpu_index)
     device = Device("cpu" if gpu_index == "cpu" else 0)
-    outbox.put((gpu_index, "__ready__", None, device.descriptor()))
+    outbox.put((gpu_index, "__ready__", None, f"{device.descriptor()} [{group}]"))
     while True:
         job = inbox.get()
         if job is None:
             break
+        if isinstance(job, dict) and "__preload__" in job:
+            try:
+                res = _preload(list(job["__preload__"]), device.identifier())
+                outbox.put((gpu_index, "__preloaded__", res, None))
+            except BaseException as e:
+                outbox.put((gpu_index, "__preloaded__", None, f"{e}\n{traceback.format_exc()}"))
+            continue
+        _test_hook(job)
         if isinstance(job, list):  # a coalesced batch (runtime.batcher)
             from .batcher import run_jobs
 

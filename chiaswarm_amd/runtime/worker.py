@@ -10,6 +10,13 @@ MI355X-first changes:
     models; results are encoded in the GPU's process.
   * per-GPU watchdog: a crashed / hung child is restarted and its in-flight job
     is reported as a NON-fatal error (the hive may retry it), SURVEY §5.3.
+  * the GPU children form one process group (RCCL over xGMI): models listed in
+    ``settings.preload`` are read once across the node — each GPU reads 1/N of
+    the checkpoint bytes, one all_gather per dtype fills every GPU
+    (parallel/sharded.py).  A restarted child leaves the group (rank-local).
+  * split jobs: a multi-image txt2img job may run on several idle GPUs at once
+    (image j always uses seed + j, so the images do not depend on the split);
+    the supervisor assembles the images in order and builds the one envelope.
   * ``ThreadExecutor`` (reference-style, in-process) for CPU plumbing runs and
     tests.
 """
@@ -69,6 +76,9 @@ class ProcessExecutor:
         self.name = f"gpu{gpu_index}"
         self.pending: dict = {}
         self.loop = None
+        self.restarts = 0
+        self.ready = threading.Event()
+        self.ready_info = ""
         self._start()
 
     def _start(self):
@@ -92,6 +102,8 @@ class ProcessExecutor:
                 return
             _, jid, result, err = item
             if jid == "__ready__":
+                self.ready_info = str(err)
+                self.ready.set()
                 print(f"Started device {err}")
                 continue
             fut = self.pending.pop(jid, None)
@@ -104,7 +116,21 @@ class ProcessExecutor:
         except Exception:
             pass
         self.proc.join(timeout=10)
+        # the process group cannot re-admit a rank: the fresh child works rank-local
+        self.env["WORLD_SIZE"] = "1"
+        self.restarts += 1
         self._start()
+
+    async def preload(self, names, timeout_s: float = 3600.0):
+        """Collective model preload (every executor of the group, same list)."""
+        self.loop = asyncio.get_running_loop()
+        fut = self.loop.create_future()
+        self.pending["__preloaded__"] = fut
+        self.inbox.put({"__preload__": list(names)})
+        result, err = await asyncio.wait_for(fut, timeout_s)
+        if err:
+            raise RuntimeError(f"{self.name} preload failed: {err}")
+        return result
 
     async def run(self, job):
         from .generator import _error_result
@@ -192,6 +218,24 @@ def _raw_key(job):
             job.get("revision"))
 
 
+def splittable(job) -> int:
+    """Number of images of a job that may be split across GPUs (0: not splittable)."""
+    if _raw_key(job) is None or not str(job.get("content_type", "image/jpeg")).startswith("image/"):
+        return 0
+    n = int(job.get("num_images_per_prompt", 1) or 1)
+    return n if n >= 2 else 0
+
+
+def _ranges(n, k):
+    q, r = divmod(n, k)
+    out, lo = [], 0
+    for i in range(k):
+        hi = lo + q + (1 if i < r else 0)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
 def _resolve(fut, value):
     if not fut.done():
         fut.set_result(value)
@@ -210,7 +254,9 @@ class Supervisor:
         self.result_queue: asyncio.Queue = asyncio.Queue()
         self.busy = 0
         self.results_submitted = 0
+        self.splits = 0
         self.stop = asyncio.Event()
+        self.locks = {id(ex): asyncio.Lock() for ex in self.executors}
 
     def _default_executors(self):
         gpus = visible_gpus(self.settings)
@@ -221,7 +267,81 @@ class Supervisor:
         from ..ops._lib import ensure_built
 
         ensure_built()
-        return [ProcessExecutor(g) for g in gpus]
+        return [ProcessExecutor(g, env=e) for g, e in zip(gpus, group_envs(len(gpus), self.settings))]
+
+    # ------------------------------------------------------------------ split jobs
+    async def _claim_helpers(self, job, ex) -> list:
+        """Idle executors for a split (an uncontended asyncio.Lock.acquire never
+        suspends, so check-and-take is atomic on the event loop)."""
+        if not getattr(self.settings, "split_jobs", True) or len(self.executors) < 2:
+            return []
+        n = splittable(job)
+        if n < 2:
+            return []
+        helpers = []
+        for other in self.executors:
+            if len(helpers) + 1 >= n:
+                break
+            lk = self.locks[id(other)]
+            if other is not ex and not lk.locked():
+                await lk.acquire()
+                helpers.append(other)
+        return helpers
+
+    async def _run_split(self, job, exs) -> dict:
+        import random
+
+        from .generator import _error_result
+
+        jid = job.get("id")
+        n = splittable(job)
+        seed = job.get("seed")
+        if seed is None:
+            seed = random.SystemRandom().randrange(0, 2 ** 63 - 1)
+        subs = []
+        for i, (lo, hi) in enumerate(_ranges(n, len(exs))):
+            subs.append(dict(job, id=f"{jid}#{i}", seed=seed, num_images_per_prompt=hi - lo,
+                             _image_range=[lo, hi], _return_images=True))
+        results = await asyncio.gather(*(e.run(sj) for e, sj in zip(exs, subs)))
+        for r in results:
+            cfg = r.get("pipeline_config", {})
+            if "_images" not in cfg:  # a part failed: report it for the whole job
+                out = dict(r, id=jid)
+                return out
+        loop = asyncio.get_running_loop()
+        content_type = job.get("content_type", "image/jpeg")
+
+        def assemble():
+            import numpy as np
+            from PIL import Image
+
+            from ..output.processor import OutputProcessor, resolve_artifacts
+
+            images = [Image.fromarray(np.asarray(a)) for r in results for a in r["pipeline_config"]["_images"]]
+            op = OutputProcessor(job.get("outputs", ["primary"]), content_type)
+            op.add_outputs(images)
+            return resolve_artifacts({"artifacts": op.get_results()})["artifacts"]
+
+        try:
+            artifacts = await loop.run_in_executor(None, assemble)
+        except Exception as e:
+            return _error_result(jid, e, content_type, False)
+        cfg = {k: v for k, v in results[0]["pipeline_config"].items() if k != "_images"}
+        cfg["seed"] = seed
+        cfg["split"] = len(exs)
+        nsfw = any(r.get("nsfw", False) for r in results)
+        self.splits += 1
+        from .. import __version__
+
+        return {"id": jid, "artifacts": artifacts, "nsfw": nsfw, "worker_version": __version__,
+                "pipeline_config": cfg}
+
+    async def preload(self, names):
+        """Every executor loads the same models together (sharded reads + all_gather)."""
+        names = [n for n in names if n]
+        if not names:
+            return []
+        return await asyncio.gather(*(ex.preload(names) for ex in self.executors if hasattr(ex, "preload")))
 
     def _drain_compatible(self, first) -> list:
         """Take queued jobs that can share ``first``'s UNet batch (cheap raw-job
@@ -242,22 +362,32 @@ class Supervisor:
         return batch
 
     async def device_worker(self, ex):
+        lock = self.locks[id(ex)]
         while True:
             job = await self.work_queue.get()
             batch = self._drain_compatible(job)
             self.busy += len(batch)
+            helpers = []
             try:
-                if len(batch) == 1:
-                    results = [await ex.run(job)]
-                else:
-                    results = await ex.run_batch(batch, max(1, int(self.settings.max_batch)))
+                async with lock:  # a split job may hold this executor as a helper
+                    if len(batch) == 1:
+                        helpers = await self._claim_helpers(job, ex)
+                        if helpers:
+                            self.busy += len(helpers)
+                            results = [await self._run_split(job, [ex] + helpers)]
+                        else:
+                            results = [await ex.run(job)]
+                    else:
+                        results = await ex.run_batch(batch, max(1, int(self.settings.max_batch)))
                 for result in results:
                     await self.result_queue.put(result)
             except Exception as e:
                 logging.exception(e)
                 print(f"device_worker {e}")
             finally:
-                self.busy -= len(batch)
+                for h in helpers:
+                    self.locks[id(h)].release()
+                self.busy -= len(batch) + len(helpers)
                 self.work_queue.task_done()
 
     async def result_worker(self):
@@ -275,6 +405,13 @@ class Supervisor:
 
     async def run(self, max_polls: int | None = None):
         logging.info(f"worker {__version__}")
+        pre = [n.strip() for n in str(getattr(self.settings, "preload", "") or "").split(",") if n.strip()]
+        if pre:
+            try:
+                await self.preload(pre)
+            except Exception as e:  # a failed preload leaves models to load on demand
+                logging.exception(e)
+                print(f"preload failed: {e}")
         tasks = [asyncio.create_task(self.device_worker(ex)) for ex in self.executors]
         tasks.append(asyncio.create_task(self.result_worker()))
         polls = 0
@@ -299,6 +436,21 @@ class Supervisor:
         finally:
             for t in tasks:
                 t.cancel()
+
+
+def group_envs(n: int, settings=None, port: int | None = None) -> list:
+    """Per-child process-group environment (RANK, WORLD_SIZE, MASTER_*)."""
+    if n <= 1 or (settings is not None and not getattr(settings, "distributed", True)):
+        return [{} for _ in range(n)]
+    if port is None:
+        import socket
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+    return [{"RANK": str(i), "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+             "HSA_ENABLE_IPC_MODE_LEGACY": "0"} for i in range(n)]
 
 
 def startup(settings=None, require_gpu=True):

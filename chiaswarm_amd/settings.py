@@ -25,10 +25,13 @@ class Settings:
     max_batch: int = 8          # max images coalesced into one UNet batch
     cache_gb: float = 200.0     # HBM budget for resident models per GPU
     model_dir: str = ""         # local diffusers-layout model store ("" -> $SDAAS_ROOT/models)
+    preload: str = ""           # comma list of models every GPU loads at startup (sharded RCCL read)
+    distributed: bool = True    # per-GPU processes form one process group (RCCL over xGMI)
+    split_jobs: bool = True     # a multi-image txt2img job may use several idle GPUs
 
     def __init__(self):
         for k in ("huggingface_token", "log_level", "log_filename", "sdaas_token", "sdaas_uri", "worker_name",
-                  "gpus", "max_batch", "cache_gb", "model_dir"):
+                  "gpus", "max_batch", "cache_gb", "model_dir", "preload", "distributed", "split_jobs"):
             setattr(self, k, getattr(type(self), k))
 
 
@@ -51,6 +54,9 @@ def load_settings() -> Settings:
     settings.max_batch = int(d.get("max_batch", 8))
     settings.cache_gb = float(d.get("cache_gb", 200.0))
     settings.model_dir = d.get("model_dir", "")
+    settings.preload = str(d.get("preload", ""))
+    settings.distributed = bool(d.get("distributed", True))
+    settings.split_jobs = bool(d.get("split_jobs", True))
 
     settings.sdaas_token = os.getenv("SDAAS_TOKEN", settings.sdaas_token)
     settings.sdaas_uri = os.getenv("SDAAS_URI", settings.sdaas_uri)
@@ -59,6 +65,9 @@ def load_settings() -> Settings:
     settings.max_batch = int(os.getenv("SDAAS_MAX_BATCH", settings.max_batch))
     settings.cache_gb = float(os.getenv("SDAAS_CACHE_GB", settings.cache_gb))
     settings.model_dir = os.getenv("SDAAS_MODEL_DIR", settings.model_dir)
+    settings.preload = os.getenv("SDAAS_PRELOAD", settings.preload)
+    settings.distributed = os.getenv("SDAAS_DIST", "1" if settings.distributed else "0") != "0"
+    settings.split_jobs = os.getenv("SDAAS_SPLIT_JOBS", "1" if settings.split_jobs else "0") != "0"
     return settings
 
 

@@ -17,3 +17,11 @@ def get_type(module_name: str, type_name: str):
 
 def has_method(o, name: str) -> bool:
     return callable(getattr(o, name, None))
+
+
+def stable_seed(name: str) -> int:
+    """Process-independent 31-bit seed of a string (Python's ``hash`` is salted
+    per process, so random-init weights would differ between GPU workers)."""
+    import zlib
+
+    return zlib.crc32(str(name).encode("utf-8")) & 0x7FFFFFFF

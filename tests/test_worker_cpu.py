@@ -206,3 +206,16 @@ def test_batched_stochastic_sampler_matches_solo():
         b = np.asarray(Image.open(io.BytesIO(base64.b64decode(solo["artifacts"]["primary"]["blob"]))), np.int16)
         d = np.abs(a - b)
         assert d.mean() < 0.5 and d.max() <= 24
+
+
+def test_every_job_writes_a_structured_log_line(caplog):
+    import json
+    import logging
+
+    with caplog.at_level(logging.INFO, logger="chiaswarm_amd.jobs"):
+        synchronous_do_work_function({"id": "L1", **TINY, "seed": 9}, Device("cpu"))
+        synchronous_do_work_function({"id": "L2", "model_name": "m", "height": 9999, "width": 9}, Device("cpu"))
+    recs = [json.loads(r.getMessage()) for r in caplog.records if r.name == "chiaswarm_amd.jobs"]
+    assert [r["id"] for r in recs] == ["L1", "L2"]
+    assert recs[0]["status"] == "ok" and recs[0]["seed"] == 9 and recs[0]["seconds"] > 0
+    assert recs[1]["status"] == "fatal" and "error" in recs[1]

@@ -1,0 +1,132 @@
+"""The multi-process worker on CPU (reference behaviour: swarm/worker.py:40-44
+one worker per GPU, :113-128 device_worker): per-device child processes
+("cpu" children here, GPU children on the box), the watchdog, the node
+process group (gloo here, RCCL over xGMI on the GPU node), collective sharded
+preload, and multi-image jobs split across children.
+
+* a child that dies in the middle of a job -> non-fatal error envelope for that
+  job, a fresh child that runs the next job;
+* a child that hangs past the job timeout -> same;
+* two children form a gloo group, preload a model with sharded reads, and a
+  3-image txt2img job split over both returns the images the unsplit job does.
+"""
+import asyncio
+import base64
+import io
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from chiaswarm_amd.runtime.worker import ProcessExecutor, Supervisor, ThreadExecutor, _ranges, group_envs
+from chiaswarm_amd.settings import Settings
+from tests.fakehive import FakeHive
+
+TINY = {"model_name": "tiny/sd", "prompt": "a red fox", "num_inference_steps": 2, "height": 64, "width": 64}
+
+
+@pytest.fixture(autouse=True)
+def sdaas_root(tmp_path, monkeypatch):
+    monkeypatch.setenv("SDAAS_ROOT", str(tmp_path))
+    monkeypatch.setenv("CSK_TEST_HOOKS", "1")  # inherited by spawned children
+    return tmp_path
+
+
+def _img(result):
+    return np.asarray(Image.open(io.BytesIO(base64.b64decode(result["artifacts"]["primary"]["blob"]))).convert("RGB"),
+                      dtype=np.int16)
+
+
+def test_ranges_cover_all_images():
+    assert _ranges(5, 2) == [(0, 3), (3, 5)]
+    assert _ranges(4, 4) == [(0, 1), (1, 2), (2, 3), (3, 4)]
+
+
+def test_process_executor_recovers_from_crash_and_hang():
+    ex = ProcessExecutor("cpu", job_timeout_s=20)
+    try:
+        async def main():
+            crashed = await ex.run({"id": "c1", **TINY, "_test": "exit"})
+            ok1 = await ex.run({"id": "ok1", **TINY, "seed": 3})
+            ex.job_timeout_s = 4
+            hung = await ex.run({"id": "h1", **TINY, "_test": "hang"})
+            ex.job_timeout_s = 60
+            ok2 = await ex.run({"id": "ok2", **TINY, "seed": 3})
+            return crashed, ok1, hung, ok2
+
+        crashed, ok1, hung, ok2 = asyncio.run(main())
+        assert crashed["id"] == "c1" and "fatal_error" not in crashed
+        assert "crashed" in crashed["pipeline_config"]["error"]
+        assert hung["id"] == "h1" and "fatal_error" not in hung and "timed out" in hung["pipeline_config"]["error"]
+        assert ex.restarts == 2
+        for r in (ok1, ok2):
+            assert "error" not in r["pipeline_config"], r["pipeline_config"]
+        assert np.array_equal(_img(ok1), _img(ok2))  # fresh children reproduce the seed
+    finally:
+        ex.close()
+
+
+def _save_tiny_model(root):
+    """A diffusers-layout tiny checkpoint under $SDAAS_ROOT/models/tiny/sd."""
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    pipe = StableDiffusion("tiny", device="cpu", seed=77)
+    d = root / "models" / "tiny" / "sd"
+    for sub, m in (("unet", pipe.unet), ("vae", pipe.vae), ("text_encoder", pipe.text_encoders[0])):
+        os.makedirs(d / sub, exist_ok=True)
+        save_file({k: v.contiguous() for k, v in m.state_dict().items()}, str(d / sub / "model.safetensors"))
+    return d
+
+
+def test_group_preload_and_split_job_matches_unsplit(sdaas_root):
+    _save_tiny_model(sdaas_root)
+    job = {"id": "multi", **TINY, "seed": 1234, "num_images_per_prompt": 3, "content_type": "image/png"}
+    # unsplit reference: one in-process executor
+    solo_hive = FakeHive(jobs=[dict(job)]).start()
+    try:
+        s = Settings()
+        s.sdaas_uri, s.sdaas_token = solo_hive.base, "t"
+
+        async def solo():
+            sup = Supervisor(s, executors=[ThreadExecutor("cpu")], hive=None)
+            await sup.run(max_polls=1)
+
+        asyncio.run(solo())
+        ref = solo_hive.results[0]
+    finally:
+        solo_hive.stop()
+    assert ref["pipeline_config"].get("split") is None
+
+    hive = FakeHive(jobs=[dict(job)]).start()
+    envs = group_envs(2)
+    exs = [ProcessExecutor("cpu", env=e) for e in envs]
+    try:
+        s = Settings()
+        s.sdaas_uri, s.sdaas_token = hive.base, "t"
+        s.preload = "tiny/sd"
+        s.max_batch = 1
+
+        async def main():
+            sup = Supervisor(s, executors=exs)
+            await sup.run(max_polls=1)
+            return sup
+
+        sup = asyncio.run(main())
+        assert all(e.ready.wait(5) for e in exs)
+        assert all("gloo rank" in e.ready_info for e in exs), [e.ready_info for e in exs]
+        assert sup.splits == 1
+        res = hive.results[0]
+        assert res["id"] == "multi" and res["pipeline_config"]["split"] == 2
+        assert res["pipeline_config"]["seed"] == 1234
+        assert res["pipeline_config"]["weights"].endswith(os.path.join("tiny", "sd"))
+        a, b = _img(res), _img(ref)
+        assert a.shape == b.shape
+        d = np.abs(a - b)
+        assert d.mean() < 0.5 and d.max() <= 24  # same seeds per image; only batch-size summation order differs
+    finally:
+        hive.stop()
+        for e in exs:
+            e.close()
