@@ -63,19 +63,31 @@ def image_to_tile(image: Image.Image, resolution: int = 1024) -> Image.Image:
     return image.convert("RGB").resize((w2, h2), Image.Resampling.LANCZOS)
 
 
-def _sobel(gray: np.ndarray):
-    p = np.pad(gray, 1, mode="reflect")
+def _sobel(img: np.ndarray):
+    """3x3 Sobel dx, dy with BORDER_REPLICATE (OpenCV canny.cpp) of [H, W] or [H, W, C]."""
+    pw = ((1, 1), (1, 1)) + (((0, 0),) if img.ndim == 3 else ())
+    p = np.pad(img, pw, mode="edge")
     gx = (p[:-2, 2:] + 2 * p[1:-1, 2:] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[1:-1, :-2] + p[2:, :-2])
     gy = (p[2:, :-2] + 2 * p[2:, 1:-1] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[:-2, 1:-1] + p[:-2, 2:])
     return gx, gy
 
 
-def canny_np(gray: np.ndarray, low: float, high: float) -> np.ndarray:
-    """cv2.Canny-compatible edge map (uint8 0/255) of a uint8 grayscale image."""
+def canny_np(img: np.ndarray, low: float, high: float) -> np.ndarray:
+    """cv2.Canny-compatible edge map (uint8 0/255) of a uint8 [H, W] or [H, W, C]
+    image.  Multi-channel: each pixel uses the dx/dy of the channel with the
+    largest L1 magnitude (first on ties), as OpenCV does for colour input —
+    the reference calls cv2.Canny on the RGB array
+    (swarm/controlnet/input_processor.py:77-81).  Parity with cv2 itself is
+    unpinned here (OpenCV is not installed); the rules follow canny.cpp."""
     from scipy import ndimage
 
-    g = gray.astype(np.float32)
+    g = img.astype(np.float32)
     gx, gy = _sobel(g)
+    if g.ndim == 3:
+        m = np.abs(gx) + np.abs(gy)
+        k = np.argmax(m, axis=-1)[..., None]  # first max on ties
+        gx = np.take_along_axis(gx, k, -1)[..., 0]
+        gy = np.take_along_axis(gy, k, -1)[..., 0]
     mag = np.abs(gx) + np.abs(gy)  # L1 gradient (cv2 default L2gradient=False)
     ang = np.arctan2(gy, gx)
     # quantise direction to 0/45/90/135 degrees
@@ -83,8 +95,9 @@ def canny_np(gray: np.ndarray, low: float, high: float) -> np.ndarray:
     p = np.pad(mag, 1)
     H, W = mag.shape
     c = p[1:-1, 1:-1]
-    nb = {0: (p[1:-1, 2:], p[1:-1, :-2]), 1: (p[2:, 2:], p[:-2, :-2]),
-          2: (p[2:, 1:-1], p[:-2, 1:-1]), 3: (p[2:, :-2], p[:-2, 2:])}
+    # (previous neighbour: strict, next neighbour: >=), as canny.cpp
+    nb = {0: (p[1:-1, :-2], p[1:-1, 2:]), 1: (p[:-2, :-2], p[2:, 2:]),
+          2: (p[:-2, 1:-1], p[2:, 1:-1]), 3: (p[:-2, 2:], p[2:, :-2])}
     keep = np.zeros_like(mag, dtype=bool)
     for d, (a, b) in nb.items():
         m = q == d
@@ -104,7 +117,7 @@ def canny_np(gray: np.ndarray, low: float, high: float) -> np.ndarray:
 def image_to_canny(image: Image.Image, low=100, high=200, device=None) -> Image.Image:
     """cv2.Canny semantics; on a GPU device the HIP kernel (csrc/kernels/canny.hip)
     runs it in well under a millisecond (the numpy path takes ~0.3 s at 512²)."""
-    arr = np.asarray(image.convert("L"))
+    arr = np.asarray(image.convert("RGB"))  # cv2.Canny on the RGB array, like the reference
     dev = device
     if dev is None:
         import torch

@@ -2,11 +2,15 @@
 provisioning (reference: swarm/initialize.py:19-116).
 
 Prompts for hive URI / token (unless --silent), saves settings, fetches the
-model catalogue (``GET /api/models`` -> ``models.json``) and prepares every
-``can_preload`` model.  The reference downloaded diffusers checkpoints from the
-Hugging Face hub; here "prepare" means: locate a local diffusers-layout copy
-(``$SDAAS_MODEL_DIR`` or the HF cache) and convert it into the packed NHWC/bf16
-cache format, or record that the model will run with synthetic weights.
+model catalogue (``GET /api/models`` -> ``models.json``) and provisions every
+``can_preload`` model the way the reference's ``download_diffusers`` did
+(swarm/initialize.py:62-94, ``from_pretrained`` with revision / variant): a
+``huggingface_hub.snapshot_download`` into the HF cache, restricted to what this
+framework reads — safetensors weights (the requested ``variant`` when given),
+JSON configs and tokenizer files; never pickled ``.bin``/``.ckpt`` files.
+``--offline`` (or no network) only locates local copies (``$SDAAS_MODEL_DIR``
+or the HF cache).  The packed bf16 weight cache (``runtime/packed_cache.py``)
+is written on each model's first load, not here.
 Quirk fixed: the reference's ``settings_exist`` was always true.
 """
 from __future__ import annotations
@@ -49,7 +53,28 @@ def init(argv=None):
     return report
 
 
-def prepare_models(settings, offline=False) -> list:
+# what a snapshot fetch may bring: weights as safetensors only, configs, tokenizers
+ALLOW = ["*.json", "*.txt", "*.model", "*.safetensors"]
+IGNORE = ["*.bin", "*.ckpt", "*.pt", "*.pth", "*.msgpack", "*.h5", "*.onnx", "*.onnx_data", "*.pb", "*.ot"]
+
+
+def allow_patterns(variant: str | None) -> list:
+    """Weight files of the requested variant only (diffusers names them
+    ``<name>.<variant>.safetensors``); config / tokenizer files always."""
+    if not variant:
+        return ALLOW
+    return ["*.json", "*.txt", "*.model", f"*.{variant}.safetensors"]
+
+
+def fetch(name: str, revision: str = "main", variant: str | None = None, token=None, downloader=None) -> str:
+    """Download (or re-validate) one model into the HF cache; returns its path."""
+    if downloader is None:
+        from huggingface_hub import snapshot_download as downloader
+    return downloader(name, revision=revision, allow_patterns=allow_patterns(variant), ignore_patterns=IGNORE,
+                      token=token if isinstance(token, str) and token else None)
+
+
+def prepare_models(settings, offline=False, downloader=None) -> list:
     from .runtime.model_cache import find_weights
 
     models = [] if offline else HiveClient(settings).get_models()
@@ -57,9 +82,18 @@ def prepare_models(settings, offline=False) -> list:
     for model in models:
         name = model["model_name"]
         params = model.get("parameters", {}) or {}
-        entry = {"model_name": name, "revision": model.get("revision", "main"),
+        entry = {"model_name": name, "revision": model.get("revision", "main"), "variant": model.get("variant"),
                  "can_preload": params.get("can_preload", True)}
-        w = find_weights(name, entry["revision"]) if entry["can_preload"] else None
+        w = None
+        if entry["can_preload"] and not offline:
+            try:
+                w = fetch(name, entry["revision"], entry["variant"], settings.huggingface_token, downloader)
+                entry["fetched"] = True
+            except Exception as e:  # no network / unknown repo: fall back to a local copy
+                entry["fetch_error"] = f"{type(e).__name__}: {e}"[:300]
+                print(f"Failed to fetch {name}/{entry['revision']}: {e}")
+        if w is None and entry["can_preload"]:
+            w = find_weights(name, entry["revision"])
         entry["weights"] = w or "synthetic (no local checkpoint)"
         print(f"Initializing {name}/{entry['revision']}: {entry['weights']}")
         report.append(entry)

@@ -73,11 +73,15 @@ def download_video(uri: str) -> str:
             f"Input video too large.\nMax size is {MAX_VIDEO_BYTES} bytes.\nVideo was {content_length}.")
     fd, path = tempfile.mkstemp(suffix=os.path.splitext(uri.split("?")[0])[1] or ".mp4")
     total = 0
-    with os.fdopen(fd, "wb") as f, _http().get(uri, stream=True, allow_redirects=True, timeout=60) as r:
-        r.raise_for_status()
-        for chunk in r.iter_content(1 << 16):
-            total += len(chunk)
-            if total > MAX_VIDEO_BYTES:
-                raise Exception("Input video too large.")
-            f.write(chunk)
+    try:
+        with os.fdopen(fd, "wb") as f, _http().get(uri, stream=True, allow_redirects=True, timeout=60) as r:
+            r.raise_for_status()
+            for chunk in r.iter_content(1 << 16):
+                total += len(chunk)
+                if total > MAX_VIDEO_BYTES:
+                    raise Exception("Input video too large.")
+                f.write(chunk)
+    except BaseException:
+        os.unlink(path)  # never leave a partial download behind
+        raise
     return path

@@ -122,7 +122,9 @@ def unload_lora(unet, pipe=None):
 
 
 def _invalidate(pipe):
-    if pipe is not None and hasattr(pipe, "invalidate_graphs"):
+    from ..utils import has_method
+
+    if pipe is not None and has_method(pipe, "invalidate_graphs"):
         pipe.invalidate_graphs()
 
 

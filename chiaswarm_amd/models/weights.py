@@ -141,17 +141,42 @@ def load_component(module, weights_dir: str, sub: str, renames=None, **kw) -> Lo
 
 def load_sd_weights(pipe, weights_dir: str) -> bool:
     """All SD components of a diffusers directory; True if any was present.
-    ``pipe.load_reports`` keeps one ``LoadReport`` per component."""
+    ``pipe.load_reports`` keeps one ``LoadReport`` per component (or "packed
+    cache" when it came from ``runtime/packed_cache.py``); components loaded
+    here are also prepared (packed), listed in ``pipe.prepared``."""
+    pipe.prepared = set()
     if not weights_dir or not os.path.isdir(weights_dir):
         return False
+    import hashlib
+
+    from ..parallel import comm
+    from ..runtime import packed_cache
+    from .layers import prepare_model
+
+    use_cache = os.environ.get("SDAAS_PACKED_CACHE", "1") != "0" and not comm.collective_load_active()
+    key = hashlib.sha1(os.path.abspath(weights_dir).encode()).hexdigest()[:16]
     parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)]
     for i, te in enumerate(pipe.text_encoders):
         parts.append(("text_encoder" if i == 0 else f"text_encoder_{i + 1}", te, None))
     reports = {}
     for sub, mod, ren in parts:
-        r = load_component(mod, weights_dir, sub, ren)
-        if r is not None:
-            reports[sub] = r
+        src = os.path.join(weights_dir, sub)
+        if not os.path.isdir(src) or not glob.glob(os.path.join(src, "*.safetensors")):
+            continue
+        fp = packed_cache.fingerprint(src, mod)
+        path = packed_cache.cache_path(key, "main", sub)
+        if use_cache and packed_cache.load(mod, path, fp):
+            reports[sub] = "packed cache"
+            pipe.prepared.add(sub)
+            continue
+        reports[sub] = load_component(mod, weights_dir, sub, ren)
+        prepare_model(mod)
+        pipe.prepared.add(sub)
+        if use_cache:
+            try:
+                packed_cache.save(mod, path, fp)
+            except OSError:  # read-only store: run without the cache
+                pass
     pipe.load_reports = reports
     return bool(reports)
 

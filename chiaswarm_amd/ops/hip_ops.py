@@ -69,7 +69,7 @@ ATTN_VARIANT = int(os.environ.get("CSK_ATTN", "0"))  # 0 auto, 1 plain, 2 pipeli
 sig("csk_attention", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_int, c_void_p, c_void_p)
 sig("csk_silu", c_void_p, c_void_p, c_int64, c_void_p)
-sig("csk_canny", c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_void_p)
+sig("csk_canny", c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_void_p, c_void_p)
 sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
     c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p)
@@ -423,21 +423,20 @@ def _attention_gemm(q, k, v, scale):
 
 
 def silu(x):
+    """Any length: the kernel does 8-element vectors plus a scalar tail."""
     _bf16(x, "silu")
     x = x.contiguous()
     y = torch.empty_like(x)
-    if x.numel() % 8:
-        return torch.nn.functional.silu(x)
     _lib.call("csk_silu", _p(y), _p(x), x.numel(), _s())
     return y
 
 
 def add(x, y):
     _bf16(x, "add")
+    if x.shape != y.shape:
+        raise ValueError(f"hip add: shapes {tuple(x.shape)} and {tuple(y.shape)} differ (no broadcasting)")
     x, y = x.contiguous(), y.contiguous().to(x.dtype)
     out = torch.empty_like(x)
-    if x.numel() % 8 or x.shape != y.shape:
-        return x + y
     _lib.call("csk_add", _p(out), _p(x), _p(y), x.numel(), _s())
     return out
 
@@ -467,14 +466,16 @@ def vae_postprocess(img):
     return y
 
 
-def canny(gray, low, high):
-    """uint8 [H, W] device image -> uint8 0/255 edge map (csrc/kernels/canny.hip)."""
-    if gray.dtype != torch.uint8 or gray.dim() != 2:
-        raise TypeError("canny: uint8 [H, W] expected")
-    gray = gray.contiguous()
-    H, W = gray.shape
-    out = torch.empty_like(gray)
+def canny(img, low, high):
+    """uint8 [H, W] or [H, W, C] device image -> uint8 0/255 edge map [H, W]
+    (csrc/kernels/canny.hip; multi-channel: cv2's per-pixel max-gradient channel)."""
+    if img.dtype != torch.uint8 or img.dim() not in (2, 3):
+        raise TypeError("canny: uint8 [H, W] or [H, W, C] expected")
+    img = img.contiguous()
+    H, W = img.shape[:2]
+    C = 1 if img.dim() == 2 else img.shape[2]
+    out = torch.empty((H, W), dtype=torch.uint8, device=img.device)
     a4, a1 = -(-(H * W * 4) // 256) * 256, -(-(H * W) // 256) * 256
-    ws = torch.empty(256 + a4 + 2 * a1, dtype=torch.uint8, device=gray.device)  # torch: 256 B-aligned
-    _lib.call("csk_canny", _p(out), _p(gray), H, W, float(low), float(high), _p(ws), _s())
+    ws = torch.empty(256 + a4 + 2 * a1, dtype=torch.uint8, device=img.device)  # torch: 256 B-aligned
+    _lib.call("csk_canny", _p(out), _p(img), H, W, C, float(low), float(high), _p(ws), _s())
     return out

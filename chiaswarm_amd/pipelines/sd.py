@@ -109,13 +109,17 @@ class StableDiffusion:
             m.eval().requires_grad_(False)
             init_random_fast_(m, seed=seed + i)
         self.weights_source = "random-init"
+        self.prepared = set()
         if weights_dir is not None:
             from ..models.weights import load_sd_weights
 
             if load_sd_weights(self, weights_dir):
                 self.weights_source = str(weights_dir)
-        for m in [self.unet, self.vae] + self.text_encoders:
-            prepare_model(m)
+        names = ["unet", "vae"] + ["text_encoder" if i == 0 else f"text_encoder_{i + 1}"
+                                   for i in range(len(self.text_encoders))]
+        for name, m in zip(names, [self.unet, self.vae] + self.text_encoders):
+            if name not in self.prepared:  # loaded components were packed (or read packed) already
+                prepare_model(m)
         from ..models.weights import tokenizer_dir
 
         # tokenizer/ (+ tokenizer_2/ for SDXL, whose OpenCLIP-bigG tokenizer pads with "!")

@@ -1,11 +1,14 @@
 // Canny edge detector for the ControlNet-canny preprocessor (reference:
-// cv2.Canny at swarm/controlnet/input_processor.py:77-81; SURVEY §2.2 "Canny
-// as a small HIP kernel").  Same definitions as controlnet/preprocess.py::
-// canny_np (itself cv2-compatible): 3x3 Sobel with BORDER_REFLECT_101, L1
-// magnitude, direction quantised to 0/45/90/135 degrees, non-maximum
-// suppression against zero-padded neighbours (c > a && c >= b), double
-// threshold, and 8-connected hysteresis (weak pixels survive when their
-// connected component contains a strong pixel).
+// cv2.Canny(np.array(rgb_image), 100, 200) at swarm/controlnet/input_processor.py:
+// 77-81, i.e. on the 3-CHANNEL image; SURVEY §2.2 "Canny as a small HIP
+// kernel").  Same definitions as controlnet/preprocess.py::canny_np, following
+// OpenCV's canny.cpp: 3x3 Sobel with BORDER_REPLICATE per channel; for a
+// multi-channel image each pixel takes the dx/dy of the channel with the
+// largest L1 magnitude (first channel on ties); direction quantised to
+// 0/45/90/135 degrees; non-maximum suppression against zero-padded
+// neighbours, strict against the previous neighbour (left / up / up-left or
+// up-right) and >= against the next; double threshold; 8-connected
+// hysteresis (weak pixels survive when their component holds a strong one).
 //
 //   canny_grad_kernel : gray u8 -> magnitude f32 + direction u8
 //   canny_nms_kernel  : -> label u8 (0 none, 1 weak, 2 strong)
@@ -16,25 +19,26 @@
 //   canny_out_kernel  : label -> 0/255
 #include "common.h"
 
-__device__ __forceinline__ int reflect101(int i, int n) {
-  if (n == 1) return 0;
-  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
-  return i;
-}
+__device__ __forceinline__ int clampi(int i, int n) { return i < 0 ? 0 : (i >= n ? n - 1 : i); }
 
 __global__ void canny_grad_kernel(const unsigned char* __restrict__ g, float* __restrict__ mag,
-                                  unsigned char* __restrict__ dir, int H, int W) {
+                                  unsigned char* __restrict__ dir, int H, int W, int C) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
   if (x >= W || y >= H) return;
-  float p[3][3];
+  float gx = 0.f, gy = 0.f, best = -1.f;
+  for (int c = 0; c < C; ++c) {
+    float p[3][3];
 #pragma unroll
-  for (int dy = -1; dy <= 1; ++dy)
+    for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-    for (int dx = -1; dx <= 1; ++dx)
-      p[dy + 1][dx + 1] = (float)g[reflect101(y + dy, H) * W + reflect101(x + dx, W)];
-  const float gx = (p[0][2] + 2.f * p[1][2] + p[2][2]) - (p[0][0] + 2.f * p[1][0] + p[2][0]);
-  const float gy = (p[2][0] + 2.f * p[2][1] + p[2][2]) - (p[0][0] + 2.f * p[0][1] + p[0][2]);
-  mag[y * W + x] = fabsf(gx) + fabsf(gy);
+      for (int dx = -1; dx <= 1; ++dx)
+        p[dy + 1][dx + 1] = (float)g[((size_t)clampi(y + dy, H) * W + clampi(x + dx, W)) * C + c];
+    const float cx = (p[0][2] + 2.f * p[1][2] + p[2][2]) - (p[0][0] + 2.f * p[1][0] + p[2][0]);
+    const float cy = (p[2][0] + 2.f * p[2][1] + p[2][2]) - (p[0][0] + 2.f * p[0][1] + p[0][2]);
+    const float m = fabsf(cx) + fabsf(cy);
+    if (m > best) { best = m; gx = cx; gy = cy; }
+  }
+  mag[y * W + x] = best;
   // q = round(atan2(gy, gx) / (pi/4)) mod 4
   const float a = atan2f(gy, gx) * 1.27323954473516f;  // 4/pi
   int q = (int)rintf(a);
@@ -49,11 +53,12 @@ __global__ void canny_nms_kernel(const float* __restrict__ mag, const unsigned c
   auto M = [&](int yy, int xx) -> float { return (yy < 0 || yy >= H || xx < 0 || xx >= W) ? 0.f : mag[yy * W + xx]; };
   const float c = mag[y * W + x];
   float a, b;
+  // a: previous neighbour (strict), b: next neighbour (>=), as cv2's canny.cpp
   switch (dir[y * W + x]) {
-    case 0: a = M(y, x + 1); b = M(y, x - 1); break;
-    case 1: a = M(y + 1, x + 1); b = M(y - 1, x - 1); break;
-    case 2: a = M(y + 1, x); b = M(y - 1, x); break;
-    default: a = M(y + 1, x - 1); b = M(y - 1, x + 1); break;
+    case 0: a = M(y, x - 1); b = M(y, x + 1); break;
+    case 1: a = M(y - 1, x - 1); b = M(y + 1, x + 1); break;
+    case 2: a = M(y - 1, x); b = M(y + 1, x); break;
+    default: a = M(y - 1, x + 1); b = M(y + 1, x - 1); break;
   }
   const float n = (c > a && c >= b) ? c : 0.f;
   lab[y * W + x] = n > high ? 2 : (n > low ? 1 : 0);
@@ -106,8 +111,9 @@ __global__ void canny_out_kernel(const unsigned char* __restrict__ lab, unsigned
 }
 
 // ws: >= canny_ws_bytes(H, W) of 256-byte aligned device workspace
-CSK_API int csk_canny(void* out, const void* gray, int H, int W, float low, float high, void* ws,
+CSK_API int csk_canny(void* out, const void* img, int H, int W, int C, float low, float high, void* ws,
                       hipStream_t stream) {
+  if (C < 1 || C > 4) return (int)hipErrorInvalidValue;
   // workspace layout (every region 256-byte aligned): [changed flag][mag f32][dir u8][label u8]
   char* w = (char*)ws;
   if (((size_t)w) & 255) return (int)hipErrorInvalidValue;
@@ -117,7 +123,7 @@ CSK_API int csk_canny(void* out, const void* gray, int H, int W, float low, floa
   unsigned char* dir = (unsigned char*)(w + 256 + a4);
   unsigned char* lab = dir + a1;
   dim3 b2(16, 16), g2((W + 15) / 16, (H + 15) / 16);
-  canny_grad_kernel<<<g2, b2, 0, stream>>>((const unsigned char*)gray, mag, dir, H, W);
+  canny_grad_kernel<<<g2, b2, 0, stream>>>((const unsigned char*)img, mag, dir, H, W, C);
   canny_nms_kernel<<<g2, b2, 0, stream>>>(mag, dir, lab, H, W, low, high);
   dim3 gt((W + CT - 1) / CT, (H + CT - 1) / CT);
   for (int pass = 0; pass < 4 * (H + W); ++pass) {  // bounded: a pass that changes nothing ends it

@@ -9,7 +9,10 @@ static inline int ew_grid(size_t nvec) {
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
 }
 
-__global__ void silu_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, size_t nvec) {
+// tails (n % 8 != 0): the last n % 8 elements go through a scalar loop in the
+// same kernel, so every length runs on the GPU (no host-side torch fallback)
+__global__ void silu_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, size_t nvec, const bf16_t* xs,
+                            bf16_t* ys, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(x[i], f);
@@ -17,16 +20,22 @@ __global__ void silu_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, 
     for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
     y[i] = pack8(f);
   }
+  if (blockIdx.x == 0 && threadIdx.x < n - nvec * 8) {
+    const size_t k = nvec * 8 + threadIdx.x;
+    ys[k] = f2bf(silu_f(bf2f(xs[k])));
+  }
 }
 
 CSK_API int csk_silu(void* y, const void* x, long long n, hipStream_t stream) {
-  if (n % 8) return (int)hipErrorInvalidValue;
-  size_t nv = n / 8;
-  silu_kernel<<<ew_grid(nv), 256, 0, stream>>>((const uint4*)x, (uint4*)y, nv);
+  if (n <= 0) return 0;
+  const size_t nv = n / 8;
+  silu_kernel<<<ew_grid(nv > 0 ? nv : 1), 256, 0, stream>>>((const uint4*)x, (uint4*)y, nv, (const bf16_t*)x,
+                                                             (bf16_t*)y, (size_t)n);
   CSK_CHECK_LAUNCH();
 }
 
-__global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b, uint4* __restrict__ y, size_t nvec) {
+__global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b, uint4* __restrict__ y, size_t nvec,
+                           const bf16_t* as, const bf16_t* bs, bf16_t* ys, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     float fa[8], fb[8];
     unpack8(a[i], fa);
@@ -35,12 +44,18 @@ __global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict_
     for (int j = 0; j < 8; ++j) fa[j] += fb[j];
     y[i] = pack8(fa);
   }
+  if (blockIdx.x == 0 && threadIdx.x < n - nvec * 8) {
+    const size_t k = nvec * 8 + threadIdx.x;
+    ys[k] = f2bf(bf2f(as[k]) + bf2f(bs[k]));
+  }
 }
 
 CSK_API int csk_add(void* y, const void* a, const void* b, long long n, hipStream_t stream) {
-  if (n % 8) return (int)hipErrorInvalidValue;
-  size_t nv = n / 8;
-  add_kernel<<<ew_grid(nv), 256, 0, stream>>>((const uint4*)a, (const uint4*)b, (uint4*)y, nv);
+  if (n <= 0) return 0;
+  const size_t nv = n / 8;
+  add_kernel<<<ew_grid(nv > 0 ? nv : 1), 256, 0, stream>>>((const uint4*)a, (const uint4*)b, (uint4*)y, nv,
+                                                            (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)y,
+                                                            (size_t)n);
   CSK_CHECK_LAUNCH();
 }
 

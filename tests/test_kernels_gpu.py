@@ -325,6 +325,11 @@ def test_canny_matches_numpy(gpu, size):
     got = hip_ops.canny(torch.from_numpy(img).to(gpu), 100.0, 200.0).cpu().numpy()
     # direction quantisation at exact 22.5-degree boundaries may differ (f32 atan2 vs f64)
     assert (got != ref).mean() < 2e-3
+    # RGB input (the reference runs cv2.Canny on the RGB array): per-pixel max-gradient channel
+    rgb = np.stack([img, np.roll(img, 7, axis=1), (255 - img) // 2], axis=-1).copy()
+    ref3 = canny_np(rgb, 100.0, 200.0)
+    got3 = hip_ops.canny(torch.from_numpy(rgb).to(gpu), 100.0, 200.0).cpu().numpy()
+    assert (got3 != ref3).mean() < 2e-3 and (ref3 != ref).mean() > 1e-3
 
 
 def test_timestep_embedding_kernel(gpu):

@@ -130,3 +130,44 @@ def test_roctx_ranges_are_safe_without_a_profiler():
             pass
     finally:
         trace.set_enabled(old)
+
+
+def test_download_video_removes_partial_file_over_cap(monkeypatch, tmp_path):
+    """The reference leaves nothing behind when a video exceeds its 30 MiB cap
+    (swarm/video/pix2pix.py:95-104); a streamed body larger than its HEAD claims
+    must not leak the temp file either."""
+    import tempfile
+
+    import pytest
+
+    from chiaswarm_amd.jobs import inputs
+
+    class Resp:
+        headers = {"Content-Length": "10", "Content-Type": "video/mp4"}
+
+        def raise_for_status(self):
+            pass
+
+        def iter_content(self, n):
+            for _ in range(8):
+                yield b"x" * 1000
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    class Sess:
+        def head(self, *a, **k):
+            return Resp()
+
+        def get(self, *a, **k):
+            return Resp()
+
+    monkeypatch.setattr(inputs, "_http", lambda: Sess())
+    monkeypatch.setattr(inputs, "MAX_VIDEO_BYTES", 2500)
+    monkeypatch.setattr(tempfile, "tempdir", str(tmp_path))
+    with pytest.raises(Exception, match="too large"):
+        inputs.download_video("http://x/v.mp4")
+    assert list(tmp_path.iterdir()) == []

@@ -83,6 +83,13 @@ def test_canny_matches_known_edges():
     assert set(cols.tolist()) <= {15, 16} and e[5:27].any()
     im = image_to_canny(Image.fromarray(np.stack([a] * 3, -1)))
     assert im.mode == "RGB" and im.size == (32, 32)
+    # colour input: an edge visible in ONE channel only (invisible in luma-equal mixes) is found
+    rgb = np.zeros((32, 32, 3), np.uint8)
+    rgb[:, 16:, 2] = 255
+    e3 = canny_np(rgb, 100, 200)
+    assert set(np.nonzero(e3.any(axis=0))[0].tolist()) <= {15, 16} and e3[5:27].any()
+    # replicate border: a constant image has no edges at its border
+    assert not canny_np(np.full((16, 16, 3), 200, np.uint8), 100, 200).any()
 
 
 def test_baseline_config1_sd21_cpu():
