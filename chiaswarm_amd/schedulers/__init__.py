@@ -159,6 +159,10 @@ class Scheduler:
     def current_t(self) -> float:
         return self.timesteps[self.step_index]
 
+    def eval_sigma(self) -> float:
+        """k-diffusion sigma of the sample the next model evaluation sees."""
+        return float(self.sigmas[self.step_index])
+
     def current_scale(self) -> float:
         return self.scale_in(self.step_index)
 
@@ -301,12 +305,6 @@ class DDIMScheduler(Scheduler):
         return StepCoeffs(p, q, A, B)
 
 
-class PNDMScheduler(DDIMScheduler):
-    """Served with the DDIM update (PLMS warm-up not reproduced; documented)."""
-
-    name = "PNDMScheduler"
-
-
 class DDPMScheduler(DDIMScheduler):
     """Ancestral DDPM posterior sampling on the leading-spacing ladder."""
 
@@ -322,35 +320,6 @@ class DDPMScheduler(DDIMScheduler):
         var = (1 - abar_p) / (1 - abar) * beta_t
         D = math.sqrt(max(var, 0.0)) if i < self.n - 1 else 0.0
         return StepCoeffs(p, q, A, B, 0.0, D)
-
-
-class LMSDiscreteScheduler(EulerDiscreteScheduler):
-    """Linear multistep (order 2 Adams-Bashforth in sigma), k-space."""
-
-    name = "LMSDiscreteScheduler"
-
-    def reset(self):
-        super().reset()
-        self._d_prev = None
-
-    def coeffs(self, i):  # not of the single-history linear form -> torch step
-        return None
-
-    def step(self, e, x, generator=None):
-        i = self.step_index
-        s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
-        p, q = self.x0_coeffs(i)
-        x0 = p * x + q * e.float()
-        d = (x - x0) / s
-        dt = sn - s
-        if self._d_prev is None:
-            out = x + dt * d
-        else:  # 2nd-order Adams-Bashforth in sigma
-            out = x + dt * (1.5 * d - 0.5 * self._d_prev)
-        self._d_prev = d
-        self.prev_x0 = x0
-        self.step_index += 1
-        return out
 
 
 class HeunDiscreteScheduler(EulerDiscreteScheduler):
@@ -411,18 +380,438 @@ class HeunDiscreteScheduler(EulerDiscreteScheduler):
         return out
 
 
+# ---------------------------------------------------------------------------
+# Samplers whose update keeps more history than (x, x0, x0_prev): torch step
+# path (a handful of elementwise ops per step; the UNet dominates).  Reference
+# semantics: the diffusers classes of the same names that the reference
+# instantiates by name (swarm/job_arguments.py:146-148) from the pipeline's
+# scheduler config with ``use_karras_sigmas=True``
+# (swarm/diffusion/diffusion_func.py:71-74).
+# ---------------------------------------------------------------------------
+def _vp(sig):
+    """(alpha, sigma_vp, lambda) of a k-diffusion sigma."""
+    a = 1.0 / math.sqrt(sig * sig + 1.0)
+    return a, sig * a, (-math.log(sig) if sig > 0 else float("inf"))
+
+
+class PNDMScheduler(DDIMScheduler):
+    """Pseudo linear multistep (PLMS, ``skip_prk_steps=True`` as in every SD
+    scheduler config): n+1 model evaluations on the "leading" ladder with the
+    second-highest timestep evaluated twice, 1st..4th-order Adams-Bashforth
+    combinations of the noise predictions, and PNDM's transfer formula
+    x_prev = sqrt(a_prev/a_t) x - (a_prev - a_t) e / (a_t sqrt(1-a_prev) + sqrt(a_t (1-a_t) a_prev))."""
+
+    name = "PNDMScheduler"
+
+    def set_timesteps(self, n):
+        super().set_timesteps(n)  # DDIM ladder: leading spacing + steps_offset, final level acp[0]
+        ts = [int(t) for t in self.timesteps]  # descending e_{n-1} .. e_0
+        asc = ts[::-1]
+        plms = asc[:-1] + asc[-2:-1] + asc[-1:] if n > 1 else asc
+        self.plms = plms[::-1]
+        self.ratio = self.T // n
+        self.n = len(self.plms)
+
+    def reset(self):
+        super().reset()
+        self._ets: list = []
+        self._cur = None
+        self._counter = 0
+
+    def current_t(self):
+        return float(self.plms[self.step_index])
+
+    def eval_sigma(self):
+        return float(self.train_sigmas[int(self.plms[self.step_index])])
+
+    def coeffs(self, i):
+        return None
+
+    def _acp(self, t):
+        return float(self.alphas_cumprod[t]) if t >= 0 else float(self.alphas_cumprod[0])
+
+    def step(self, e, x, generator=None):
+        t = int(self.plms[self.step_index])
+        e = e.float()
+        if self.prediction_type == "v_prediction":
+            a_t = self._acp(t)
+            e = math.sqrt(a_t) * e + math.sqrt(1 - a_t) * x
+        prev_t = t - self.ratio
+        if self._counter != 1:
+            self._ets = (self._ets + [e])[-4:]
+        else:
+            prev_t, t = t, t + self.ratio
+        ets = self._ets
+        if len(ets) == 1 and self._counter == 0:
+            eps, self._cur = e, x
+        elif len(ets) == 1 and self._counter == 1:
+            eps, x = (e + ets[-1]) / 2, self._cur
+            self._cur = None
+        elif len(ets) == 2:
+            eps = (3 * ets[-1] - ets[-2]) / 2
+        elif len(ets) == 3:
+            eps = (23 * ets[-1] - 16 * ets[-2] + 5 * ets[-3]) / 12
+        else:
+            eps = (55 * ets[-1] - 59 * ets[-2] + 37 * ets[-3] - 9 * ets[-4]) / 24
+        a_t, a_p = self._acp(t), self._acp(prev_t)
+        den = a_t * math.sqrt(1 - a_p) + math.sqrt(a_t * (1 - a_t) * a_p)
+        out = math.sqrt(a_p / a_t) * x - (a_p - a_t) * eps / den
+        self.prev_x0 = (x - math.sqrt(1 - a_t) * eps) / math.sqrt(a_t)
+        self._counter += 1
+        self.step_index += 1
+        return out
+
+
+class LMSDiscreteScheduler(EulerDiscreteScheduler):
+    """Linear multistep, order 4 (diffusers default): the derivative history
+    d_k = (x_k - x0_k) / sigma_k combined with the integrals over
+    [sigma_i, sigma_{i+1}] of the Lagrange basis polynomials through the last
+    (up to) four sigmas — integrated exactly (polynomials) where diffusers
+    uses scipy quad."""
+
+    name = "LMSDiscreteScheduler"
+    order = 4
+
+    def reset(self):
+        super().reset()
+        self._ds: list = []
+
+    def coeffs(self, i):
+        return None
+
+    def lms_coeff(self, order, t, k):
+        sig = self.sigmas
+        num = np.poly1d([1.0])
+        den = 1.0
+        for j in range(order):
+            if j == k:
+                continue
+            num = num * np.poly1d([1.0, -sig[t - j]])
+            den *= sig[t - k] - sig[t - j]
+        P = np.polyint(num)
+        return float((P(sig[t + 1]) - P(sig[t])) / den)
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        p, q = self.x0_coeffs(i)
+        x0 = p * x + q * e.float()
+        d = (x - x0) / float(self.sigmas[i])
+        self._ds = (self._ds + [d])[-self.order:]
+        order = min(i + 1, self.order)
+        out = x
+        for k in range(order):
+            out = out + self.lms_coeff(order, i, k) * self._ds[-1 - k]
+        self.prev_x0 = x0
+        self.step_index += 1
+        return out
+
+
+class _TwoStageK(EulerDiscreteScheduler):
+    """k-diffusion two-evaluation samplers (sample_dpm_2 / _ancestral /
+    sample_dpmpp_sde): each sigma interval evaluates the model at sigma_i and
+    at an intermediate sigma; a final interval to sigma = 0 is one Euler step."""
+
+    order = 2
+
+    def reset(self):
+        super().reset()
+        self._phase = 0
+        self._x = self._d = None
+        self._mid = None
+
+    def coeffs(self, i):
+        return None
+
+    def eval_sigma(self):
+        return float(self.sigmas[self.step_index]) if self._phase == 0 else float(self._mid)
+
+    def current_t(self):
+        return self.sigma_to_t(self.eval_sigma())
+
+    def current_scale(self):
+        s = self.eval_sigma()
+        return 1.0 / math.sqrt(s * s + 1)
+
+    def _x0(self, e, x, sig):
+        pt = self.prediction_type
+        e = e.float()
+        if pt == "epsilon":
+            return x - sig * e
+        if pt == "v_prediction":
+            return x / (sig * sig + 1) - sig / math.sqrt(sig * sig + 1) * e
+        return e
+
+
+def ancestral_step(s_from: float, s_to: float, eta: float = 1.0):
+    up = min(s_to, eta * math.sqrt(max(s_to ** 2 * (s_from ** 2 - s_to ** 2) / s_from ** 2, 0.0)))
+    return math.sqrt(max(s_to ** 2 - up ** 2, 0.0)), up
+
+
+class KDPM2DiscreteScheduler(_TwoStageK):
+    """DPM-Solver-2 (k-diffusion sample_dpm_2): Euler to the log-midpoint
+    sigma, re-evaluate, full step with the midpoint derivative."""
+
+    name = "KDPM2DiscreteScheduler"
+
+    def _target(self, i):
+        return float(self.sigmas[i + 1]), 0.0
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        s = float(self.sigmas[i])
+        s_to, up = self._target(i)
+        if self._phase == 0:
+            d = (x - self._x0(e, x, s)) / s
+            if s_to == 0.0:
+                self.step_index += 1
+                return x + d * (s_to - s)
+            self._mid = math.exp(0.5 * (math.log(s) + math.log(s_to)))
+            self._x, self._d, self._phase = x, d, 1
+            return x + d * (self._mid - s)
+        d2 = (x - self._x0(e, x, self._mid)) / self._mid
+        out = self._x + d2 * (s_to - s)
+        if up > 0.0:
+            out = out + up * batch_randn(out.shape, generator, out.device)
+        self._phase = 0
+        self.step_index += 1
+        return out
+
+
+class KDPM2AncestralDiscreteScheduler(KDPM2DiscreteScheduler):
+    """sample_dpm_2_ancestral: the DPM-2 step aimed at sigma_down, then
+    sigma_up of fresh noise (eta = 1)."""
+
+    name = "KDPM2AncestralDiscreteScheduler"
+
+    def _target(self, i):
+        s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
+        if sn == 0.0:
+            return 0.0, 0.0
+        return ancestral_step(s, sn)
+
+
+class DPMSolverSDEScheduler(_TwoStageK):
+    """DPM-Solver++ SDE (k-diffusion sample_dpmpp_sde, r = 1/2, eta = 1): two
+    evaluations per interval with ancestral noise after each half.  The
+    reference draws that noise from torchsde's Brownian tree in sigma
+    (normalised increments (W(s1) - W(s0)) / sqrt|s1 - s0|); torchsde is not
+    available, so the two increments of an interval are built from two seeded
+    N(0, 1) draws with the Brownian-path correlation: n1 = z1 over
+    [sigma, sigma_mid], n2 = (sqrt(d1) z1 + sqrt(d2) z2) / sqrt(d1 + d2) over
+    [sigma, sigma_next] — the same joint law as the tree (parity with
+    diffusers' exact noise stream unpinned)."""
+
+    name = "DPMSolverSDEScheduler"
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
+        if self._phase == 0:
+            x0 = self._x0(e, x, s)
+            if sn == 0.0:
+                self.step_index += 1
+                return x0  # Euler to sigma 0 lands on the denoised sample
+            t, t_next = -math.log(s), -math.log(sn)
+            self._mid = math.exp(-(t + 0.5 * (t_next - t)))
+            sd, su = ancestral_step(s, self._mid)
+            self._z1 = batch_randn(x.shape, generator, x.device)
+            x2 = (sd / s) * x - math.expm1(t + math.log(sd)) * x0 + su * self._z1
+            self._x, self._phase = x, 1
+            return x2
+        x0_2 = self._x0(e, x, self._mid)
+        sd, su = ancestral_step(s, sn)
+        out = (sd / s) * self._x - math.expm1(-math.log(s) + math.log(sd)) * x0_2
+        d1, d2 = s - self._mid, self._mid - sn
+        z2 = batch_randn(out.shape, generator, out.device)
+        out = out + su * (math.sqrt(d1) * self._z1 + math.sqrt(d2) * z2) / math.sqrt(d1 + d2)
+        self._z1 = None
+        self._phase = 0
+        self.step_index += 1
+        return out
+
+
+class UniPCMultistepScheduler(DPMSolverMultistepScheduler):
+    """UniPC (bh2, predict-x0, order 2, lower-order final steps): the UniP
+    multistep predictor plus the UniC corrector applied to the previous step's
+    result with the new model output.  Coefficients from the phi-function
+    recursion (B(h) = e^{-h} - 1), as in diffusers' multistep_uni_p/c_bh_update."""
+
+    name = "UniPCMultistepScheduler"
+
+    def reset(self):
+        super().reset()
+        self._hist: list = []  # (lambda, x0) of the last solver_order steps
+        self._last_x = None
+        self._this_order = 1
+        self._lower = 0
+
+    def coeffs(self, i):
+        return None
+
+    def _lam(self, i):
+        return _vp(float(self.sigmas[i]))
+
+    @staticmethod
+    def _rb(rks, h, order):
+        hh = -h
+        h_phi_1 = math.expm1(hh)
+        h_phi_k = h_phi_1 / hh - 1.0
+        fact = 1.0
+        B_h = math.expm1(hh)
+        R, b = [], []
+        for i in range(1, order + 1):
+            R.append([r ** (i - 1) for r in rks])
+            b.append(h_phi_k * fact / B_h)
+            fact *= i + 1
+            h_phi_k = h_phi_k / hh - 1.0 / fact
+        return np.array(R, dtype=np.float64), np.array(b, dtype=np.float64), h_phi_1, B_h
+
+    def _update(self, x, lam_t, a_t, sv_t, sv_s0, order, model_t=None):
+        """UniP (model_t None) or UniC update from the history's last point."""
+        lam_s0, m0 = self._hist[-1]
+        h = lam_t - lam_s0
+        rks, D1s = [], []
+        for k in range(1, order):
+            lam_si, mi = self._hist[-(k + 1)]
+            rk = (lam_si - lam_s0) / h
+            rks.append(rk)
+            D1s.append((mi - m0) / rk)
+        rks.append(1.0)
+        R, b, h_phi_1, B_h = self._rb(rks, h, order)
+        x_t_ = (sv_t / sv_s0) * x - a_t * h_phi_1 * m0
+        if model_t is None:
+            if not D1s:
+                return x_t_
+            rhos = [0.5] if order == 2 else list(np.linalg.solve(R[:-1, :-1], b[:-1]))
+            res = sum(r * d for r, d in zip(rhos, D1s))
+            return x_t_ - a_t * B_h * res
+        rhos_c = [0.5] if order == 1 else list(np.linalg.solve(R, b))
+        res = sum(r * d for r, d in zip(rhos_c[:-1], D1s)) if D1s else 0.0
+        return x_t_ - a_t * B_h * (res + rhos_c[-1] * (model_t - m0))
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        s = float(self.sigmas[i])
+        p, q = self.x0_coeffs(i)
+        x0 = p * x + q * e.float()
+        a_s, sv_s, lam_s = _vp(s)
+        if i > 0 and self._last_x is not None:  # UniC corrector of the previous step's output
+            a_p, sv_p, _ = self._lam(i - 1)
+            x = self._update(self._last_x, lam_s, a_s, sv_s, sv_p, self._this_order, model_t=x0)
+        self._hist = (self._hist + [(lam_s, x0)])[-self.solver_order:]
+        order = min(self.solver_order, self.n - i) if self.lower_order_final else self.solver_order
+        self._this_order = min(order, self._lower + 1)
+        self._last_x = x
+        sn = float(self.sigmas[i + 1])
+        if sn == 0.0:
+            out = x0
+        else:
+            a_t, sv_t, lam_t = _vp(sn)
+            out = self._update(x, lam_t, a_t, sv_t, sv_s, self._this_order)
+        self._lower = min(self._lower + 1, self.solver_order)
+        self.prev_x0 = x0
+        self.step_index += 1
+        return out
+
+
+class DEISMultistepScheduler(DPMSolverMultistepScheduler):
+    """DEIS (order 2, log-rho): exponential-integrator steps on the noise
+    prediction, the 2nd-order weights integrating the Lagrange interpolant of
+    the last two noise predictions in log(sigma) (diffusers
+    multistep_deis_second_order_update)."""
+
+    name = "DEISMultistepScheduler"
+
+    def reset(self):
+        super().reset()
+        self._eps: list = []
+
+    def coeffs(self, i):
+        return None
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
+        p, q = self.x0_coeffs(i)
+        x0 = p * x + q * e.float()
+        a_s, sv_s, _ = _vp(s)
+        eps = (x - a_s * x0) / sv_s
+        self._eps = (self._eps + [(s, eps)])[-2:]
+        first = (i == 0 or self.solver_order == 1 or
+                 (self.lower_order_final and i == self.n - 1 and self.n < 15) or len(self._eps) < 2)
+        self.prev_x0 = x0
+        self.step_index += 1
+        if sn == 0.0:
+            return x0
+        a_t, sv_t, _ = _vp(sn)
+        if first:
+            h = math.log(s / sn)  # lambda_t - lambda_s
+            return (a_t / a_s) * x - sv_t * math.expm1(h) * eps
+        (s1, m1), (_, m0) = self._eps[-2], self._eps[-1]
+        rho_t, rho_s0, rho_s1 = sn, s, s1  # sigma_vp / alpha = k-sigma
+
+        def ind(t, b, c):
+            return t * (-math.log(c) + math.log(t) - 1.0) / (math.log(b) - math.log(c))
+
+        c1 = ind(rho_t, rho_s0, rho_s1) - ind(rho_s0, rho_s0, rho_s1)
+        c2 = ind(rho_t, rho_s1, rho_s0) - ind(rho_s0, rho_s1, rho_s0)
+        return a_t * (x / a_s + c1 * m0 + c2 * m1)
+
+
+class DPMSolverSinglestepScheduler(DPMSolverMultistepScheduler):
+    """DPM-Solver++ singlestep, order 2 (orders [1, 2, 1, 2, ...], a trailing
+    1 for odd step counts): the second step of each pair restarts from the
+    pair's first sample with both x0 predictions (midpoint form)."""
+
+    name = "DPMSolverSinglestepScheduler"
+
+    def reset(self):
+        super().reset()
+        self._block = None  # (sigma, x, x0) at the start of the current 2-step block
+
+    def coeffs(self, i):
+        return None
+
+    def orders(self):
+        n = self.n
+        if self.solver_order == 1:
+            return [1] * n
+        out = [1, 2] * (n // 2)
+        return out + [1] if n % 2 else out
+
+    def step(self, e, x, generator=None):
+        i = self.step_index
+        s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
+        p, q = self.x0_coeffs(i)
+        x0 = p * x + q * e.float()
+        order = self.orders()[i]
+        self.prev_x0 = x0
+        self.step_index += 1
+        if sn == 0.0:
+            return x0
+        a_t, sv_t, lam_t = _vp(sn)
+        if order == 1:
+            self._block = (s, x, x0)
+            _, sv_s, lam_s = _vp(s)
+            h = lam_t - lam_s
+            return (sv_t / sv_s) * x - a_t * math.expm1(-h) * x0
+        s1, x_s1, m1 = self._block
+        _, sv_s1, lam_s1 = _vp(s1)
+        lam_s0 = _vp(s)[2]
+        h, h0 = lam_t - lam_s1, lam_s0 - lam_s1
+        r0 = h0 / h
+        D0, D1 = m1, (x0 - m1) / r0
+        em = math.expm1(-h)
+        return (sv_t / sv_s1) * x_s1 - a_t * em * D0 - 0.5 * a_t * em * D1
+
+
 _REGISTRY = {c.name: c for c in [
-    DPMSolverMultistepScheduler, DPMSolverSDEScheduler, EulerDiscreteScheduler,
-    EulerAncestralDiscreteScheduler, DDIMScheduler, PNDMScheduler, DDPMScheduler,
-    LMSDiscreteScheduler, HeunDiscreteScheduler]}
-# names the hive may send whose update we serve with the closest sampler
-_ALIASES = {
-    "DPMSolverSinglestepScheduler": "DPMSolverMultistepScheduler",
-    "UniPCMultistepScheduler": "DPMSolverMultistepScheduler",
-    "DEISMultistepScheduler": "DPMSolverMultistepScheduler",
-    "KDPM2DiscreteScheduler": "HeunDiscreteScheduler",
-    "KDPM2AncestralDiscreteScheduler": "EulerAncestralDiscreteScheduler",
-}
+    DPMSolverMultistepScheduler, DPMSolverSinglestepScheduler, DPMSolverSDEScheduler, EulerDiscreteScheduler,
+    EulerAncestralDiscreteScheduler, DDIMScheduler, PNDMScheduler, DDPMScheduler, LMSDiscreteScheduler,
+    HeunDiscreteScheduler, KDPM2DiscreteScheduler, KDPM2AncestralDiscreteScheduler, UniPCMultistepScheduler,
+    DEISMultistepScheduler]}
+# exact equivalents only
+_ALIASES: dict = {}
 
 
 def scheduler_names():

@@ -124,3 +124,104 @@ def test_fused_coeffs_match_step():
             out, x0 = ops._ref_sched_step(e, x2, s2.prev_x0, c, None, None)
             s2.prev_x0, s2.step_index, x2 = x0, s2.step_index + 1, out
         assert torch.allclose(x1, x2, atol=1e-5)
+
+
+# --------------------------------------------------------------------------
+# Gaussian data: the probability-flow ODE has a closed form, so each sampler's
+# integration error is measurable (no diffusers needed).  x0 ~ N(mu, s^2):
+#   D(x, sigma) = (s^2 x + sigma^2 mu) / (s^2 + sigma^2)   (exact denoiser)
+#   x(sigma)    = mu + (x(sigma_0) - mu) * sqrt(s^2 + sigma^2) / sqrt(s^2 + sigma_0^2)
+# --------------------------------------------------------------------------
+MU, SD = 0.5, 0.8
+ALL_DET = ["DPMSolverMultistepScheduler", "DPMSolverSinglestepScheduler", "UniPCMultistepScheduler",
+           "DEISMultistepScheduler", "EulerDiscreteScheduler", "HeunDiscreteScheduler", "KDPM2DiscreteScheduler",
+           "LMSDiscreteScheduler", "DDIMScheduler", "PNDMScheduler"]
+STOCH = ["EulerAncestralDiscreteScheduler", "KDPM2AncestralDiscreteScheduler", "DPMSolverSDEScheduler",
+         "DDPMScheduler"]
+
+
+def _gauss_eps(s, x):
+    sig = s.eval_sigma()
+    xk = x * math.sqrt(sig * sig + 1) if s.space == "vp" else x
+    d = (SD * SD * xk + sig * sig * MU) / (SD * SD + sig * sig)
+    return (xk - d) / sig
+
+
+def _run_gauss(name, n, z, generator=None):
+    s = get_scheduler(name)
+    s.set_timesteps(n)
+    s0 = float(s.sigmas[0]) if not hasattr(s, "plms") else float(s.train_sigmas[int(s.plms[0])])
+    xk0 = MU + z * math.sqrt(SD * SD + s0 * s0)
+    x = xk0 / math.sqrt(s0 * s0 + 1) if s.space == "vp" else xk0
+    while s.step_index < s.n:
+        x = s.step(_gauss_eps(s, x), x, generator)
+    s_end = float(s.sigmas[-1])
+    exact = MU + (xk0 - MU) * math.sqrt(SD * SD + s_end * s_end) / math.sqrt(SD * SD + s0 * s0)
+    if s.space == "vp":
+        exact = exact / math.sqrt(s_end * s_end + 1)
+    return x, exact
+
+
+@pytest.mark.parametrize("n", [10, 25])
+def test_every_deterministic_sampler_integrates_the_gaussian_ode(n):
+    z = torch.randn(4096, generator=torch.Generator().manual_seed(0), dtype=torch.float64).float()
+    err = {}
+    for name in ALL_DET:
+        x, exact = _run_gauss(name, n, z)
+        err[name] = (x - exact).abs().max().item()
+    # (the common floor: every sampler's last step returns the denoised sample
+    # at sigma_min, an O(sigma_min^2) error of the ODE solution itself)
+    assert all(e < (0.6 if n == 10 else 0.3) for e in err.values()), err
+    # second-order methods beat first-order Euler on the same ladder family
+    for name in ("DPMSolverMultistepScheduler", "DPMSolverSinglestepScheduler", "UniPCMultistepScheduler",
+                 "DEISMultistepScheduler", "LMSDiscreteScheduler", "HeunDiscreteScheduler", "KDPM2DiscreteScheduler"):
+        assert err[name] < err["EulerDiscreteScheduler"], (name, err)
+
+
+def test_solver_errors_shrink_with_steps():
+    z = torch.randn(1024, generator=torch.Generator().manual_seed(1))
+    for name in ("UniPCMultistepScheduler", "DEISMultistepScheduler", "DPMSolverSinglestepScheduler",
+                 "LMSDiscreteScheduler", "KDPM2DiscreteScheduler", "PNDMScheduler"):
+        e = []
+        for n in (8, 16, 32):
+            x, exact = _run_gauss(name, n, z)
+            e.append((x - exact).abs().max().item())
+        assert e[2] < e[0], (name, e)
+
+
+@pytest.mark.parametrize("name", STOCH)
+def test_stochastic_samplers_sample_the_data_distribution(name):
+    g = torch.Generator().manual_seed(2)
+    z = torch.randn(20000, generator=g)
+    x, _ = _run_gauss(name, 100, z, generator=g)
+    s = get_scheduler(name)
+    s.set_timesteps(100)
+    s_end = float(s.sigmas[-1])
+    xk = x * math.sqrt(s_end * s_end + 1) if s.space == "vp" else x
+    # ancestral samplers under-disperse by O(1/n) (Euler-a's per-step variance
+    # deficit s^2 (sigma - sigma_down)^2 / (s^2 + sigma^2)); at 100 steps < 5 %
+    assert abs(xk.mean().item() - MU) < 0.02
+    assert abs(xk.std().item() - math.sqrt(SD * SD + s_end * s_end)) < 0.04
+
+
+def test_lms_coefficients_integrate_lagrange_basis():
+    s = get_scheduler("LMSDiscreteScheduler")
+    s.set_timesteps(12)
+    for i in range(3, 11):
+        c = [s.lms_coeff(4, i, k) for k in range(4)]
+        assert abs(sum(c) - (s.sigmas[i + 1] - s.sigmas[i])) < 1e-9  # basis sums to 1
+    assert abs(s.lms_coeff(1, 0, 0) - (s.sigmas[1] - s.sigmas[0])) < 1e-12  # order 1 == Euler
+
+
+def test_pndm_plms_schedule_repeats_second_timestep():
+    s = get_scheduler("PNDMScheduler")
+    s.set_timesteps(10)
+    assert s.n == 11 and s.plms[1] == s.plms[2] and s.plms[0] == 901 and s.plms[-1] == 1
+
+
+def test_no_scheduler_is_an_alias():
+    from chiaswarm_amd.schedulers import _ALIASES, _REGISTRY
+
+    assert not _ALIASES
+    for n in scheduler_names():
+        assert type(get_scheduler(n)).__name__ == n
