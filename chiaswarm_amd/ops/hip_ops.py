@@ -74,7 +74,6 @@ sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
     c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p)
 sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
-sig("csk_softmax_rows", c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
 sig("csk_set_gn_prologue_max", c_int)
 sig("csk_set_short_kv_variant", c_int)
@@ -395,30 +394,14 @@ def attention(q, k, v, scale, causal=False, kv_len=None):
             raise ValueError("attention: last dim must be contiguous")
     B, Sq, H, D = q.shape
     Skv = k.shape[1]
-    if D > 256:
-        return _attention_gemm(q, k, v, scale)
+    if D > 512 or (D > 256 and (causal or kv_len is not None or D % 16)):
+        raise ValueError(f"attention: head dim {D} unsupported (<= 256, or <= 512 non-causal, multiple of 16)")
     o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
     st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
     if kv_len is not None and (kv_len.dtype != torch.int32 or not kv_len.is_cuda):
         raise TypeError("attention: kv_len must be an int32 device tensor")
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
               ATTN_VARIANT, _p(kv_len), _s())
-    return o
-
-
-def _attention_gemm(q, k, v, scale):
-    """Large head dim (VAE mid-block, d=512): S = Q K^T (MFMA GEMM) ->
-    row softmax kernel -> O = P V (MFMA GEMM against V^T)."""
-    B, Sq, H, D = q.shape
-    Skv = k.shape[1]
-    o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
-    for b in range(B):
-        for h in range(H):
-            qb, kb, vb = q[b, :, h], k[b, :, h], v[b, :, h]
-            s = gemm(qb, kb)
-            p = torch.empty_like(s)
-            _lib.call("csk_softmax_rows", _p(p), _p(s), Sq, Skv, float(scale), _s())
-            o[b, :, h] = gemm(p, vb.t().contiguous())
     return o
 
 

@@ -140,6 +140,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     // key tiles wholly past kv_end (the tail block: Skv = 77 cross-attention
     // keeps 1 of its 4) skip their QK^T and PV MFMAs (wave-uniform branches)
     const int ktn = DP == 64 ? min(4, (kv_end - kb * KB + 15) >> 4) : 4;
+    // head dims below the padded DP (SD1.5: 40 / 80 / 160 in 64 / 128 / 256)
+    // skip the QK^T k-steps and O d-tiles that would only multiply zeros
+    const int dsn = (a.D + 31) >> 5, dtn = (a.D + 15) >> 4;
     v4f s[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
       for (int qt = 0; qt < QT; ++qt) s[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
+      if (DP > 64 && ds >= dsn) continue;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         if (kt >= ktn) continue;
@@ -210,6 +214,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
       if (2 * kp2 >= ktn) continue;  // keys kp2*32 .. +31 all masked: P^T is zero there
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
+        if (dt >= dtn) continue;
         // group fg reads rows (keys) kp2*32 + 4*fg + {0..3} and kp2*32 + 16 + 4*fg + {0..3},
         // lane 4q+p of the group addresses row q, columns dt*16 + 4p .. +3
         const int qq = fr >> 2, pp = fr & 3;
@@ -546,10 +551,15 @@ CSK_API int csk_set_short_kv_variant(int v) {
 
 // variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64),
 // 3 = pipelined + PRE, 4 = pipelined + ONES, 5 = pipelined + PRE + ONES
+extern "C" int csk_attention_wide(void* o, const void* q, const void* k, const void* v, const long long* strides,
+                                  int B, int H, int Sq, int Skv, int D, float scale, hipStream_t stream);
+
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
                           int Sq, int Skv, int D, float scale, int causal, int variant, const void* kv_len,
                           hipStream_t stream) {
   // strides: q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h) in elements
+  if (D > 256 && D <= 512 && !causal && !kv_len)  // VAE mid-block: single head, d = 512
+    return csk_attention_wide(o, q, k, v, strides, B, H, Sq, Skv, D, scale, stream);
   if (D % 8 != 0 || D > 256) return (int)hipErrorInvalidValue;
   AttnArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;

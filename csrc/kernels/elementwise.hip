@@ -134,49 +134,6 @@ CSK_API int csk_vae_post(void* y, const void* x, long long n, hipStream_t stream
 }
 
 // --------------------------------------------------------------------------
-// Row softmax with scale: bf16 [rows, n] -> bf16 (fp32 math), one wave per row
-// (used for the d=512 single-head VAE attention via GEMM-softmax-GEMM).
-// --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                           int rows, int n, float scale) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * n);
-  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * n);
-  const int nv = n / 8;
-  float m = -INFINITY;
-  for (int v = lane; v < nv; v += 64) {
-    float f[8];
-    unpack8(xr[v], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, f[j] * scale);
-  }
-  m = wave_max(m);
-  float s = 0.f;
-  for (int v = lane; v < nv; v += 64) {
-    float f[8];
-    unpack8(xr[v], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += __expf(f[j] * scale - m);
-  }
-  const float inv = 1.0f / wave_sum(s);
-  for (int v = lane; v < nv; v += 64) {
-    float f[8];
-    unpack8(xr[v], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = __expf(f[j] * scale - m) * inv;
-    yr[v] = pack8(f);
-  }
-}
-
-CSK_API int csk_softmax_rows(void* y, const void* x, int rows, int n, float scale, hipStream_t stream) {
-  if (n % 8) return (int)hipErrorInvalidValue;
-  softmax_rows_kernel<<<(rows + 3) / 4, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, rows, n, scale);
-  CSK_CHECK_LAUNCH();
-}
-
-// --------------------------------------------------------------------------
 // y = a*x + b*z  (RRDB residual scaling, ControlNet residual scale)
 // --------------------------------------------------------------------------
 __global__ void axpby_kernel(const uint4* __restrict__ x, const uint4* __restrict__ z, uint4* __restrict__ y, size_t nvec,

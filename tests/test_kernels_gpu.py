@@ -471,3 +471,40 @@ def test_phased_256_tiles_geglu_and_gn_stats(gpu, tile):
             t[key] = old
     ref = F.silu(F.group_norm(yc.float().permute(0, 3, 1, 2), 32, gamma.float(), beta.float(), 1e-5)).permute(0, 2, 3, 1)
     assert rel_err(gn, ref) < 1e-2
+
+
+def _attn_ref_chunked(q, k, v, scale, chunk=1024):
+    """fp32 reference on the GPU, query-chunked (never an S x S matrix of the full size)."""
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))  # [B, H, S, D]
+    out = torch.empty_like(qf)
+    for s0 in range(0, qf.shape[2], chunk):
+        sc = torch.matmul(qf[:, :, s0:s0 + chunk], kf.transpose(-1, -2)) * scale
+        out[:, :, s0:s0 + chunk] = torch.matmul(torch.softmax(sc, -1), vf)
+    return out.permute(0, 2, 1, 3)
+
+
+@pytest.mark.parametrize("B,S,H,D", [(1, 4096, 8, 40), (1, 2048, 8, 80), (1, 1024, 8, 160), (2, 4096, 5, 64),
+                                     (1, 16384, 1, 64), (1, 16384, 1, 512), (2, 4096, 1, 512), (1, 1000, 1, 512),
+                                     (1, 4100, 2, 160)])
+def test_attention_head_dims_long_sequences(gpu, B, S, H, D):
+    """Every UNet / VAE head dim (SD1.5 40/80/160, SD2/XL 64, VAE 512) up to
+    S = 16384 (SD2.1 at 1024^2); the d = 512 flash kernel allocates nothing of
+    size S x S (checked with the allocator's peak)."""
+    q, k, v = (rnd(B, S, H, D, dev=gpu) for _ in range(3))
+    scale = D ** -0.5
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    y = hip_ops.attention(q, k, v, scale)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert peak <= y.numel() * 2 + (1 << 20), peak  # the output, nothing S x S
+    assert rel_err(y, _attn_ref_chunked(q, k, v, scale)) < 1.5e-2
+
+
+def test_attention_d512_strided_heads(gpu):
+    """d = 512 over strided [B, S, H, D] views (fused QKV layout) and a ragged key tail."""
+    qkv = rnd(1, 777, 3, 512, dev=gpu)
+    q, k, v = qkv[:, :, 0:1], qkv[:, :, 1:2], qkv[:, :, 2:3]
+    y = hip_ops.attention(q, k, v, 512 ** -0.5)
+    assert rel_err(y, _attn_ref_chunked(q, k, v, 512 ** -0.5)) < 1.5e-2
