@@ -93,7 +93,31 @@ class ControlNetModel(Prepared):
         """cond: NHWC [B, H, W, 3] in [0, 1] -> [B, H/8, W/8, C0] (constant per job)."""
         return self.controlnet_cond_embedding(cond.to(self.conv_in.weight.dtype))
 
+    def features(self, sample, timestep, cond_emb, cross_kv=None, ctx=None):
+        """The ControlNet encoder copy up to (not including) its zero convs:
+        (the 12 skip features, the mid-block output)."""
+        return self._encode(sample, timestep, cond_emb, cross_kv, ctx)
+
+    def merge_skip(self, i, feat, unet_skip, scale: float = 1.0):
+        """UNet skip i + scale * zero_conv_i(feat) in ONE GEMM: the residual add
+        and the conditioning scale ride in the 1x1 conv's epilogue (which also
+        emits the GroupNorm statistics the consuming up-block ResNet needs)."""
+        return self.controlnet_down_blocks[i](feat, residual=unet_skip, out_scale=scale, gn_stats=True)
+
+    def merge_mid(self, feat, unet_h, scale: float = 1.0):
+        return self.controlnet_mid_block(feat, residual=unet_h, out_scale=scale, gn_stats=True)
+
     def forward(self, sample, timestep, cond_emb, cross_kv=None, ctx=None, scale: float = 1.0):
+        """Residual tensors (diffusers ControlNetModel output: down residuals, mid residual)."""
+        skips, h = self._encode(sample, timestep, cond_emb, cross_kv, ctx)
+        downs = [zc(s) for zc, s in zip(self.controlnet_down_blocks, skips)]
+        mid = self.controlnet_mid_block(h)
+        if scale != 1.0:
+            downs = [d * scale for d in downs]
+            mid = mid * scale
+        return downs, mid
+
+    def _encode(self, sample, timestep, cond_emb, cross_kv=None, ctx=None):
         b = sample.shape[0]
         dtype = self.conv_in.weight.dtype
         t = timestep.reshape(-1).float()
@@ -121,9 +145,4 @@ class ControlNetModel(Prepared):
         kvs = [next(kv_iter) for _ in t2.transformer_blocks] if kv_iter else None
         h = t2(h, ctx=ctx, kvs=kvs)
         h = m.resnets[1](h, m.resnets[1].time_emb_proj(temb_s))
-        downs = [zc(s) for zc, s in zip(self.controlnet_down_blocks, skips)]
-        mid = self.controlnet_mid_block(h)
-        if scale != 1.0:
-            downs = [d * scale for d in downs]
-            mid = mid * scale
-        return downs, mid
+        return skips, h

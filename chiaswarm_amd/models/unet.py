@@ -254,8 +254,14 @@ class UNet2DConditionModel(Prepared):
         return temb
 
     def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
-                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None):
-        """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout]."""
+                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None):
+        """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout].
+
+        ``control``: a ControlNet's pre-zero-conv features
+        (``pipelines.controlnet.ControlFeatures``): each skip and the mid-block
+        output are merged as ``skip + scale * zero_conv(feature)`` inside the
+        zero conv's GEMM epilogue (no separate add pass); ``down_residuals`` /
+        ``mid_residual`` (ready-made residuals, diffusers style) are added."""
         b = sample.shape[0]
         dtype = self.conv_in.weight.dtype
         x = sample.to(dtype)
@@ -282,13 +288,17 @@ class UNet2DConditionModel(Prepared):
                 h = blk.downsamplers[0](h)
                 skips.append(h)
 
-        if down_residuals is not None:
+        if control is not None:
+            skips = [control.merge_skip(i, s) for i, s in enumerate(skips)]
+        elif down_residuals is not None:
             skips = [s + r.to(s.dtype) for s, r in zip(skips, down_residuals)]
 
         h = self.mid_block.resnets[0](h, next(tprojs))
         h = run_attn(self.mid_block.attentions[0], h)
         h = self.mid_block.resnets[1](h, next(tprojs))
-        if mid_residual is not None:
+        if control is not None:
+            h = control.merge_mid(h)
+        elif mid_residual is not None:
             h = h + mid_residual.to(h.dtype)
 
         for blk in self.up_blocks:

@@ -19,12 +19,43 @@ from ..runtime.model_cache import cache, find_weights
 from ..utils import stable_seed
 
 
+class ControlFeatures:
+    """One step's ControlNet output, merged into the UNet skips lazily."""
+
+    def __init__(self, model, feats, mid, scale):
+        self.model, self.feats, self.mid, self.scale = model, feats, mid, scale
+
+    def merge_skip(self, i, unet_skip):
+        return self.model.merge_skip(i, self.feats[i], unet_skip, self.scale)
+
+    def merge_mid(self, unet_h):
+        return self.model.merge_mid(self.mid, unet_h, self.scale)
+
+
+class ControlContext:
+    """Per-request ControlNet state: the embedded conditioning image and the
+    ControlNet's cross-attention K/V (both constant over the denoising loop)."""
+
+    def __init__(self, runner, cond_emb, kv, scale):
+        self.runner, self.model = runner, runner.model
+        self.cond_emb, self.kv, self.scale = cond_emb, kv, scale
+
+    def features(self, x_in, t):
+        """Eager per-step evaluation (CPU / reference mode)."""
+        dev = self.cond_emb.device
+        tt = t if torch.is_tensor(t) else torch.tensor([float(t)], device=dev, dtype=torch.float32)
+        with torch.no_grad():
+            feats, mid = self.model.features(x_in[..., :self.model.cfg.in_channels], tt, self.cond_emb,
+                                             cross_kv=self.kv)
+        return ControlFeatures(self.model, feats, mid, self.scale)
+
+
 class ControlNetRunner:
     def __init__(self, model: ControlNetModel, name: str):
         self.model = model
         self.name = name
 
-    def make_fn(self, image, height, width, b, nrep, ctx, scale, dtype):
+    def make_context(self, image, height, width, b, nrep, ctx, scale, dtype) -> ControlContext:
         im = image[0] if isinstance(image, list) else image
         arr = np.asarray(im.convert("RGB").resize((width, height), Image.Resampling.BICUBIC), dtype=np.float32) / 255.0
         dev = self.model.conv_in.weight.device
@@ -33,12 +64,18 @@ class ControlNetRunner:
             cond_emb = self.model.embed_cond(cond)
             kv = self.model.encode_context(ctx)
         scale = float(scale if not isinstance(scale, (list, tuple)) else scale[0])
+        return ControlContext(self, cond_emb, kv, scale)
+
+    def make_fn(self, image, height, width, b, nrep, ctx, scale, dtype):
+        """diffusers-style per-step residuals (down list, mid) — kept for callers
+        that want the residual tensors themselves."""
+        cc = self.make_context(image, height, width, b, nrep, ctx, scale, dtype)
 
         def fn(x_in, t):
-            tt = torch.tensor([float(t)], device=dev, dtype=torch.float32)
+            tt = torch.tensor([float(t)], device=cc.cond_emb.device, dtype=torch.float32)
             with torch.no_grad():
-                downs, mid = self.model(x_in[..., :self.model.cfg.in_channels], tt, cond_emb, cross_kv=kv,
-                                        scale=scale)
+                downs, mid = self.model(x_in[..., :self.model.cfg.in_channels], tt, cc.cond_emb, cross_kv=cc.kv,
+                                        scale=cc.scale)
             return {"down_residuals": downs, "mid_residual": mid}
 
         return fn

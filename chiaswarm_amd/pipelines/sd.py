@@ -203,23 +203,29 @@ class StableDiffusion:
             torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------
-    def _unet_eval(self, x_in, t, cross_kv, added, ctl):
+    def _unet_eval(self, x_in, t, cross_kv, added, cc=None):
+        """One denoiser evaluation.  ``cc``: a ControlNet request context — on
+        the graph path the ControlNet encoder copy, its zero convs (fused with
+        the skip adds) and the UNet are ONE captured hipGraph."""
         share = bool(getattr(self, "_kv_static", False))
-        key = (x_in.shape, added is not None, ctl is not None, len(cross_kv), share)
         if (not self.use_graphs or ops.get_mode() != "hip" or not ops._lib.available()
                 or self.device.type != "cuda"):
-            return self.unet(x_in, torch.tensor([t], device=x_in.device, dtype=torch.float32),
-                             cross_kv=cross_kv, added_cond=added, **(ctl or {}))
+            tt = torch.tensor([t], device=x_in.device, dtype=torch.float32)
+            control = cc.features(x_in, tt) if cc is not None else None
+            return self.unet(x_in, tt, cross_kv=cross_kv, added_cond=added, control=control)
+        key = (x_in.shape, added is not None, len(cross_kv), share,
+               None if cc is None else (id(cc.model), cc.scale, tuple(cc.cond_emb.shape)))
         g = self._graphs.get(key)
         if g is None:
-            g = _UNetGraph(self.unet, x_in, cross_kv, added, ctl, share_kv=share)
+            g = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share) if cc is None else
+                 _ControlUNetGraph(self.unet, x_in, cross_kv, added, cc, share_kv=share))
             self._graphs[key] = g
-        return g.run(x_in, t, cross_kv, added, ctl, req=getattr(self, "_req", None))
+        return g.run(x_in, t, cross_kv, added, cc, req=getattr(self, "_req", None))
 
     @torch.no_grad()
     def denoise(self, latents, sched: Scheduler, cross_kv, guidance, added=None, generator=None,
                 image_latents=None, image_guidance=None, mask=None, masked_latents=None,
-                init_latents=None, noise=None, controlnet_fn=None):
+                init_latents=None, noise=None, control=None):
         """Sampler loop on NHWC fp32 latents.
 
         * guidance > 1 -> CFG batch [uncond, cond] (pix2pix: [cond, uncond-img, uncond]);
@@ -239,8 +245,7 @@ class StableDiffusion:
             x_in = torch.cat(parts, 0) if nrep > 1 else xi
             if image_latents is not None:
                 x_in = torch.cat([x_in, image_latents.to(self.dtype)], dim=-1)
-            ctl = controlnet_fn(x_in, t) if controlnet_fn is not None else None
-            e = self._unet_eval(x_in, t, cross_kv, added, ctl)
+            e = self._unet_eval(x_in, t, cross_kv, added, control)
             coeffs = sched.fused_coeffs()
             if three_way:
                 e_c, e_i, e_u = e.float().chunk(3)
@@ -372,16 +377,17 @@ class StableDiffusion:
         if latents is not None:
             x = latents.to(self.device).float()
 
-        controlnet_fn = None
+        control = None
         if self.controlnet is not None and image is not None:
-            controlnet_fn = self.controlnet.make_fn(image, height, width, b, 2 if cfg else 1,
-                                                    ctx, controlnet_conditioning_scale, self.dtype)
+            control = self.controlnet.make_context(image, height, width, b, 2 if cfg else 1,
+                                                   ctx, controlnet_conditioning_scale, self.dtype)
+            control.req = getattr(self, "_req", None)
         timings["prepare"] = time.perf_counter() - t0 - timings["text_encode"]
         t1 = time.perf_counter()
         with trace_range("denoise"):
             x = self.denoise(x, sched, cross_kv, guidance_scale, added, generator,
                              image_latents=image_latents, image_guidance=img_guid,
-                             mask=mask_t, init_latents=init_latents, noise=noise, controlnet_fn=controlnet_fn)
+                             mask=mask_t, init_latents=init_latents, noise=noise, control=control)
             self._phase_sync()
         timings["denoise"] = time.perf_counter() - t1
         if output_type == "latent":
@@ -409,7 +415,7 @@ class _UNetGraph:
     """hipGraph of one UNet forward at a fixed (batch, H, W): static input
     buffers are refreshed by ``copy_`` before each replay."""
 
-    def __init__(self, unet, x_in, cross_kv, added, ctl, warmup=2, share_kv=False):
+    def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False):
         self.unet = unet
         self.x = x_in.clone()
         self.t = torch.zeros(1, device=x_in.device, dtype=torch.float32)
@@ -417,8 +423,6 @@ class _UNetGraph:
         self.kv = list(cross_kv) if share_kv else [k.clone() for k in cross_kv]
         self._kv_req = None
         self.added = {k: v.clone() for k, v in added.items()} if added else None
-        self.ctl = ({"down_residuals": [r.clone() for r in ctl["down_residuals"]],
-                     "mid_residual": ctl["mid_residual"].clone()} if ctl else None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -430,9 +434,9 @@ class _UNetGraph:
             self.out = self._fwd()
 
     def _fwd(self):
-        return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, **(self.ctl or {}))
+        return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added)
 
-    def run(self, x_in, t, cross_kv, added, ctl, req=None):
+    def run(self, x_in, t, cross_kv, added, cc=None, req=None):
         self.x.copy_(x_in)
         self.t.fill_(float(t))
         # per-request cross-attention K/V: copied into the graph's static buffers
@@ -443,12 +447,38 @@ class _UNetGraph:
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src)
             self._kv_req = req
+            self._new_request(cc)
         if added:
             for k, v in added.items():
                 self.added[k].copy_(v)
-        if ctl:
-            for dst, src in zip(self.ctl["down_residuals"], ctl["down_residuals"]):
-                dst.copy_(src)
-            self.ctl["mid_residual"].copy_(ctl["mid_residual"])
         self.graph.replay()
         return self.out
+
+    def _new_request(self, cc):
+        pass
+
+
+class _ControlUNetGraph(_UNetGraph):
+    """ControlNet encoder copy + zero convs fused into the skip merges + UNet,
+    all in one hipGraph (the reference ran ControlNet and UNet as separate eager
+    modules every step, swarm/diffusion/diffusion_func.py:29-39 -> :96).  The
+    conditioning embedding and the ControlNet's prompt K/V are static buffers
+    refreshed once per request; the conditioning scale is part of the graph key."""
+
+    def __init__(self, unet, x_in, cross_kv, added, cc, warmup=2, share_kv=False):
+        self.cn, self.scale = cc.model, cc.scale
+        self.cond = cc.cond_emb.clone()
+        self.ckv = [k.clone() for k in cc.kv]
+        super().__init__(unet, x_in, cross_kv, added, warmup=warmup, share_kv=share_kv)
+
+    def _fwd(self):
+        from .controlnet import ControlFeatures
+
+        feats, mid = self.cn.features(self.x[..., :self.cn.cfg.in_channels], self.t, self.cond, cross_kv=self.ckv)
+        control = ControlFeatures(self.cn, feats, mid, self.scale)
+        return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, control=control)
+
+    def _new_request(self, cc):
+        self.cond.copy_(cc.cond_emb)
+        for dst, src in zip(self.ckv, cc.kv):
+            dst.copy_(src)

@@ -101,3 +101,28 @@ def test_baseline_config1_sd21_cpu():
     assert r["pipeline_config"]["family"] == "sd21" and r["pipeline_config"]["seed"] == 1
     im = Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"])))
     assert im.size == (64, 64)
+
+
+def test_controlnet_fused_merge_equals_residual_add(tiny):
+    """skip + scale * zero_conv(feature) in the zero conv's epilogue == the
+    diffusers-style residual tensors added to the skips (reference:
+    StableDiffusionControlNetPipeline, swarm/diffusion/diffusion_func.py:29-39)."""
+    import torch
+
+    from chiaswarm_amd.pipelines.controlnet import ControlFeatures, load_controlnet
+
+    runner = load_controlnet("tiny/controlnet-merge", tiny, "cpu")
+    cn, unet = runner.model, tiny.unet
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 8, 8, 4, generator=g)
+    ctx = torch.randn(2, 77, unet.cfg.cross_attention_dim, generator=g)
+    cond = cn.embed_cond(torch.rand(2, 64, 64, 3, generator=g))
+    t = torch.tensor([500.0])
+    kv, ckv = unet.encode_context(ctx), cn.encode_context(ctx)
+    with torch.no_grad():
+        downs, mid = cn(x, t, cond, cross_kv=ckv, scale=0.7)
+        ref = unet(x, t, cross_kv=kv, down_residuals=downs, mid_residual=mid)
+        feats, m = cn.features(x, t, cond, cross_kv=ckv)
+        got = unet(x, t, cross_kv=kv, control=ControlFeatures(cn, feats, m, 0.7))
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)
+    assert not torch.allclose(got, unet(x, t, cross_kv=kv), atol=1e-3)  # the control does something

@@ -50,7 +50,7 @@ def main():
     graphs = {}
     for arm in a.arms.split(","):
         apply_arm(arm)
-        graphs[arm] = _UNetGraph(p.unet, x, kv, None, None)
+        graphs[arm] = _UNetGraph(p.unet, x, kv, None)
     res = {arm: [] for arm in graphs}
     for _ in range(a.rounds):
         for arm, g in graphs.items():

@@ -58,7 +58,7 @@ def main():
         with ops.ops_mode("reference"):
             res["unet_step_reference_ms"] = timeit(lambda: p.unet(x, t, encoder_hidden_states=ctx), a.iters)
         res["unet_step_hip_eager_ms"] = timeit(lambda: p.unet(x, t, cross_kv=kv), a.iters)
-        g = _UNetGraph(p.unet, x, kv, None, None)
+        g = _UNetGraph(p.unet, x, kv, None)
         res["unet_step_hip_graph_ms"] = timeit(lambda: g.run(x, 500.0, kv, None, None), a.iters)
     if not a.only or a.only == "vae":
         z = torch.randn(B, L, L, 4, device=dev)

@@ -66,7 +66,7 @@ def main():
     table = tuning.table()
 
     def capture():
-        return _UNetGraph(p.unet, x, kv, None, None, warmup=1)
+        return _UNetGraph(p.unet, x, kv, None, warmup=1)
 
     def timed(g, rounds=3):
         for _ in range(2):
