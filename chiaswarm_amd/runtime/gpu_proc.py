@@ -118,7 +118,8 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
             except BaseException as e:
                 outbox.put((gpu_index, "__preloaded__", None, f"{e}\n{traceback.format_exc()}"))
             continue
-        _test_hook(job)
+        for j in (job if isinstance(job, list) else [job]):
+            _test_hook(j)
         if isinstance(job, list):  # a coalesced batch (runtime.batcher)
             from .batcher import run_jobs
 

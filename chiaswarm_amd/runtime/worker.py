@@ -169,6 +169,7 @@ class ProcessExecutor:
             futs[j.get("id")] = fut
         self.inbox.put(list(jobs))
         t0 = time.monotonic()
+        why = "failed"
         while True:
             done, _ = await asyncio.wait(set(futs.values()), timeout=2.0)
             if len(done) == len(futs):
@@ -191,7 +192,7 @@ class ProcessExecutor:
                 out.append(_error_result(j.get("id"), RuntimeError(f"worker error: {err}"),
                                          j.get("content_type", "image/jpeg"), False))
             else:
-                out.append(_error_result(j.get("id"), RuntimeError("GPU worker failed"),
+                out.append(_error_result(j.get("id"), RuntimeError(f"GPU worker {why}"),
                                          j.get("content_type", "image/jpeg"), False))
         return out
 

@@ -43,12 +43,19 @@ struct AttnArgs {
                       // KV-cache decode step be captured once in a hipGraph
 };
 
-template <int DP, int QT>
+// DV: the head dim rounded up to 16 (SD1.5's 40 / 80 / 160 live in 64 / 128 / 256
+// wide tiles): the QK^T k-steps and O d-tiles past DV only multiply zeros and
+// are not instantiated (compile-time bounds — MFMAs ignore EXEC, so a runtime
+// skip would have to be a scalar branch the compiler keeps)
+template <int DP, int QT, int DV = DP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   constexpr int CPR = DP / 8;          // 16B chunks per K/V row
   constexpr int KB = 64;               // keys per block
   constexpr int DS = DP / 32;          // k-steps of S = K Q^T over d
   constexpr int DT = DP / 16;          // O^T d-tiles
+  constexpr int DSV = (DV + 31) / 32;  // k-steps / d-tiles that touch a real column
+  constexpr int DTV = (DV + 15) / 16;
+  static_assert(DV <= DP && DV % 16 == 0, "DV: head dim rounded up to 16");
   constexpr int QROWS = QT * 16 * 4;   // query rows per workgroup
   constexpr int TILE = KB * DP;        // elements per K or V tile
   constexpr int LPT = KB * CPR / 256;  // 16B chunks per thread per tile
@@ -140,17 +147,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     // key tiles wholly past kv_end (the tail block: Skv = 77 cross-attention
     // keeps 1 of its 4) skip their QK^T and PV MFMAs (wave-uniform branches)
     const int ktn = DP == 64 ? min(4, (kv_end - kb * KB + 15) >> 4) : 4;
-    // head dims below the padded DP (SD1.5: 40 / 80 / 160 in 64 / 128 / 256)
-    // skip the QK^T k-steps and O d-tiles that would only multiply zeros
-    const int dsn = (a.D + 31) >> 5, dtn = (a.D + 15) >> 4;
     v4f s[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) s[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      if (DP > 64 && ds >= dsn) continue;
+    for (int ds = 0; ds < DSV; ++ds) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         if (kt >= ktn) continue;
@@ -213,8 +216,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
     for (int kp2 = 0; kp2 < 2; ++kp2) {
       if (2 * kp2 >= ktn) continue;  // keys kp2*32 .. +31 all masked: P^T is zero there
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        if (dt >= dtn) continue;
+      for (int dt = 0; dt < DTV; ++dt) {
         // group fg reads rows (keys) kp2*32 + 4*fg + {0..3} and kp2*32 + 16 + 4*fg + {0..3},
         // lane 4q+p of the group addresses row q, columns dt*16 + 4p .. +3
         const int qq = fr >> 2, pp = fr & 3;
@@ -531,11 +533,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   }
 }
 
-template <int DP, int QT>
+template <int DP, int QT, int DV = DP>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
   constexpr int QROWS = QT * 64;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
-  attn_fwd_kernel<DP, QT><<<a.B * a.H * nqb, 256, 0, s>>>(a);
+  attn_fwd_kernel<DP, QT, DV><<<a.B * a.H * nqb, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -606,8 +608,11 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
         return (int)hipGetLastError();
       }
     }
+    if (D <= 48) return launch_attn<64, 2, 48>(a, stream);  // SD1.5 64x64 level, d = 40
     return launch_attn<64, 2>(a, stream);
   }
+  if (D <= 80) return launch_attn<128, 2, 80>(a, stream);  // SD1.5 32x32 level
   if (D <= 128) return launch_attn<128, 2>(a, stream);
+  if (D <= 160) return launch_attn<256, 1, 160>(a, stream);  // SD1.5 16x16 / 8x8 levels
   return launch_attn<256, 1>(a, stream);
 }
