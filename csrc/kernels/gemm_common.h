@@ -12,6 +12,7 @@ enum {
   ACT_LRELU_001 = 9,   // leaky relu 0.01 (torch default)
   ACT_ELU = 10,        // EnCodec
   ACT_GELU_TANH = 11,  // T5 "gelu_new"
+  ACT_PROBE_NO_EPILOGUE = 99,  // profiling only: skip the epilogue (tilebench --probe)
 };
 
 // pointwise epilogue activation (every act except GEGLU, which pairs columns)

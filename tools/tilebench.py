@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="conv|gemm")
+    ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
@@ -59,11 +60,12 @@ def main():
             y = torch.empty(M, no, dtype=torch.bfloat16, device=dev)
             fl = 2.0 * M * N * K
 
-            def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu):
-                ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
-                _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, no, no, 1,
-                          3 if geglu else 0, 1.0, None, tile, split, _p(ws), _s())
-            jobs.append((f"gemm {spec}", fl, run))
+            for probe in ((False, True) if a.probe else (False,)):
+                def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe):
+                    ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
+                    _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, no, no, 1,
+                              99 if probe else (3 if geglu else 0), 1.0, None, tile, split, _p(ws), _s())
+                jobs.append((f"gemm {spec}" + (" noepi" if probe else ""), fl, run))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for name, fl, run in jobs:
         res = {}
