@@ -157,7 +157,28 @@ __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
   return *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + r, args.M - 1) * 2);
 }
 
-template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256>
+// The 8-column output vector a lane owns after the v_permlane16_swap of a pair of
+// row-layout fragments (SW epilogues): fragments f and f+1 hold columns
+// f*16 + fq*4 + r and (f+1)*16 + fq*4 + r of one row; after the swap an even-row
+// lane (fq even) holds columns (f+1)*16 + fq*4 .. +7 and an odd-row lane
+// f*16 + (fq-1)*4 .. +7, in register order [Y, X].  Returns that first column.
+__device__ __forceinline__ int sw_pair(v4f& x, v4f& y, int f, int fq, float (&o)[8]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(y[r]), __float_as_uint(x[r]), false, false);
+    o[r] = __uint_as_float(p[0]);
+    o[4 + r] = __uint_as_float(p[1]);
+  }
+  return (fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4;
+}
+
+// SW: the accumulators are row-layout (the MFMA ran as B * A, C^T in registers):
+// lane = output row i*16 + fr, registers = 4 consecutive output columns
+// j*16 + fq*4 + r.  Lets the common short-K epilogue (bias / per-sample bias /
+// activation incl. GEGLU / scale / residual) store 16-byte row vectors straight
+// from registers — no fp32 LDS round trip, no barrier (the probe measured the
+// LDS epilogue at about half of a K = 320 GEMM's time, tools/tilebench.py --probe).
+template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                               bf16_t* smem, int m0, int n0, int split,
                                               float2 lnrow = make_float2(0.f, 0.f)) {
@@ -175,14 +196,117 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + fr;
+        if constexpr (SW) {
+          const int m = m0 + wm * WTM + i * 16 + fr, n = n0 + wn * WTN + j * 16 + fq * 4;
+          if (m < M) {
+            if (n + 3 < N && (N & 3) == 0) {
+              *reinterpret_cast<float4*>(wp + (size_t)m * N + n) =
+                  make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+            } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-          if (m < M && n < N) wp[(size_t)m * N + n] = acc[i][j][r];
+              for (int r = 0; r < 4; ++r)
+                if (n + r < N) wp[(size_t)m * N + n + r] = acc[i][j][r];
+            }
+          }
+        } else {
+          const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+            if (m < M && n < N) wp[(size_t)m * N + n] = acc[i][j][r];
+          }
         }
       }
     return;
+  }
+  if constexpr (SW && NT % 2 == 0) {
+    // ---- direct row-vector stores (no LDS) for the common case ----
+    const bool geglu = args.act == ACT_GEGLU;
+    constexpr bool geglu_ok = NT % 4 == 0;
+    const bool direct = !args.gn_part && !args.row_part && !args.ln_part && (geglu_ok || !geglu) &&
+                        (N % (geglu ? 16 : 8)) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
+                        (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
+                        (!args.bias2d || ((args.ldb2 % 8) == 0 && ((((size_t)args.bias2d) & 15) == 0))) &&
+                        (!args.res || ((args.ldr % 8) == 0 && ((((size_t)args.res) & 15) == 0)));
+    if (direct) {
+      // Output-fragment pairs outer, row blocks inner: the bias of a pair is read
+      // once into registers (reloading it per row block is forced otherwise, as
+      // the C stores may alias it).
+      const int outN = geglu ? N / 2 : N;
+      const int ob = geglu ? (n0 + wn * WTN) / 2 : n0 + wn * WTN;  // this wave's first output column
+      const float osc = args.out_scale;
+      const int act = args.act;
+      if (geglu) {
+        if constexpr (NT % 4 == 0) {
+#pragma unroll
+          for (int f = 0; f < NT / 2; f += 2) {
+            // packed columns: fragments 2f, 2f+1 = hidden, gate of output fragment f
+            float bq[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int nh = n0 + wn * WTN + (2 * f + q) * 16 + fq * 4;
+              if (args.bias && nh < N) {
+                const uint2 u = *reinterpret_cast<const uint2*>(args.bias + nh);
+                bq[q][0] = __uint_as_float(u.x << 16);
+                bq[q][1] = __uint_as_float(u.x & 0xffff0000u);
+                bq[q][2] = __uint_as_float(u.y << 16);
+                bq[q][3] = __uint_as_float(u.y & 0xffff0000u);
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bq[q][r] = 0.f;
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+              const int m = m0 + wm * WTM + i * 16 + fr;
+              v4f x, y;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                x[r] = (acc[i][2 * f][r] + bq[0][r]) * gelu_f(acc[i][2 * f + 1][r] + bq[1][r]);
+                y[r] = (acc[i][2 * f + 2][r] + bq[2][r]) * gelu_f(acc[i][2 * f + 3][r] + bq[3][r]);
+              }
+              float o[8];
+              const int col = ob + sw_pair(x, y, f, fq, o);
+              if (m >= M || col >= outN) continue;
+              if (osc != 1.0f) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] *= osc;
+              }
+              if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
+              *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < NT; f += 2) {
+          // the 8 columns this lane stores for fragment pair f (same for every row block)
+          const int col = ob + ((fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4);
+          float bb[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) bb[r] = 0.f;
+          if (args.bias && col < outN) add8(bb, args.bias + col, true, 8);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int m = m0 + wm * WTM + i * 16 + fr;
+            float o[8];
+            sw_pair(acc[i][f], acc[i][f + 1], f, fq, o);
+            if (m >= M || col >= outN) continue;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) o[r] += bb[r];
+            if (args.bias2d) add8(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col, true, 8);
+            act8(act, o);
+            if (osc != 1.0f) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] *= osc;
+            }
+            if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
+            *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
+          }
+        }
+      }
+      return;
+    }
   }
   static_assert(WM % EP == 0, "epilogue passes split the wave rows");
   constexpr int PR = BM / EP;                  // tile rows staged per pass
@@ -194,10 +318,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     if (tid < BM) *reinterpret_cast<float2*>(lnst + 2 * tid) = lnrow;
     epi_barrier<RAW>();
   }
-  // this lane's column sums of the folded weight, loaded once (fused LN)
+  // this lane's column sums of the folded weight, loaded once (fused LN; the
+  // row layout loads them per fragment below)
   float lncs[NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) lncs[j] = ln ? args.ln_colsum[min(n0 + wn * WTN + j * 16 + fr, N - 1)] : 0.f;
+  for (int j = 0; j < NT; ++j) lncs[j] = (ln && !SW) ? args.ln_colsum[min(n0 + wn * WTN + j * 16 + fr, N - 1)] : 0.f;
   // acc -> LayerNorm-corrected value (identity without a fused LN)
   auto lnfix = [&](float v, int row, int j) {
     if (!ln) return v;
@@ -208,6 +333,49 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   if (pass) epi_barrier<RAW>();  // the previous band's readers are done with cs
   const bool mine = EP == 1 || (wm * WTM) / PR == pass;
   if (!mine) {
+  } else if (SW && act == ACT_GEGLU) {
+    // row layout: fragment columns outer so each lane's 8 folded-weight column
+    // sums (fused LN) are loaded once per fragment pair and die with it
+#pragma unroll
+    for (int j = 0; j < NT; j += 2) {
+      const int ch = wn * WTN + j * 16 + fq * 4;  // packed hidden column (tile-relative)
+      const int oc = (wn * WTN + j * 16) / 2 + fq * 4;
+      float bh[4], bg[4], ch_s[4], cg_s[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nh = n0 + ch + r;
+        bh[r] = (args.bias && nh < N) ? bf2f(args.bias[nh]) : 0.f;
+        bg[r] = (args.bias && nh + 16 < N) ? bf2f(args.bias[nh + 16]) : 0.f;
+        ch_s[r] = ln ? args.ln_colsum[min(nh, N - 1)] : 0.f;
+        cg_s[r] = ln ? args.ln_colsum[min(nh + 16, N - 1)] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = wm * WTM + i * 16 + fr;
+        const float mu = ln ? lnst[2 * row] : 0.f, rs = ln ? lnst[2 * row + 1] : 1.f;
+        float g[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          g[r] = (rs * (acc[i][j][r] - mu * ch_s[r]) + bh[r]) * gelu_f(rs * (acc[i][j + 1][r] - mu * cg_s[r]) + bg[r]);
+        *reinterpret_cast<float4*>(cs + (row - pr0) * LDC_S + oc) = make_float4(g[0], g[1], g[2], g[3]);
+      }
+    }
+  } else if (SW) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = wn * WTN + j * 16 + fq * 4;
+      float c_s[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c_s[r] = ln ? args.ln_colsum[min(n0 + col + r, N - 1)] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = wm * WTM + i * 16 + fr;
+        const float mu = ln ? lnst[2 * row] : 0.f, rs = ln ? lnst[2 * row + 1] : 1.f;
+        *reinterpret_cast<float4*>(cs + (row - pr0) * LDC_S + col) =
+            make_float4(rs * (acc[i][j][0] - mu * c_s[0]), rs * (acc[i][j][1] - mu * c_s[1]),
+                        rs * (acc[i][j][2] - mu * c_s[2]), rs * (acc[i][j][3] - mu * c_s[3]));
+      }
+    }
   } else if (act == ACT_GEGLU) {
     // packed columns: even 16-tiles = hidden, odd = gate (same output column in the same lane)
 #pragma unroll

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     if (sum == 1234.5f) args.C[threadIdx.x] = f2bf(sum);  // keeps the MFMAs alive
     return;
   }
-  gemm_epilogue<BM, BN, WM, WN, false, EP>(args, acc, smem, m0, n0, split, lnrow);
+  gemm_epilogue<BM, BN, WM, WN, false, EP, 256, true>(args, acc, smem, m0, n0, split, lnrow);
 }
 
 // ---------------------------------------------------------------------------
@@ -417,12 +417,12 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (++c_k == nk) {
       int m0, n0;
       tile_of(c_tile, m0, n0);
-      gemm_epilogue<BM, BN, WM, WN, true>(args, acc, smem + SMEM_MAIN, m0, n0, 0);
+      gemm_epilogue<BM, BN, WM, WN, true, 1, 256, true>(args, acc, smem + SMEM_MAIN, m0, n0, 0);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
