@@ -116,8 +116,9 @@ class CLIPTextModel(Prepared):
         if cfg.projection_dim:
             self.text_projection = nn.Linear(cfg.hidden_size, cfg.projection_dim, bias=False)
 
-    @torch.no_grad()
-    def forward(self, input_ids: torch.Tensor):
+    def _encode(self, input_ids):
+        """(output of the last encoder layer before final_layer_norm, penultimate
+        hidden state, final_layer_norm output)."""
         tm = self.text_model
         x = tm.embeddings(input_ids)
         penult = x
@@ -128,10 +129,25 @@ class CLIPTextModel(Prepared):
             x = layer(x)
         if n == 1:
             penult = x
-        last = tm.final_layer_norm(x)
+        return x, penult, tm.final_layer_norm(x)
+
+    def _pool(self, last, input_ids):
         # pooled = hidden state at the EOS token (highest id in CLIP vocab order)
         eos_pos = (input_ids == self.cfg.eos_token_id).int().argmax(dim=-1)
-        pooled = last[torch.arange(last.shape[0], device=last.device), eos_pos]
+        return last[torch.arange(last.shape[0], device=last.device), eos_pos]
+
+    @torch.no_grad()
+    def encode_pre_ln(self, input_ids: torch.Tensor):
+        """(last encoder layer output BEFORE final_layer_norm, pooled output):
+        transformers' ``hidden_states[-1]`` / ``pooler_output``, the latent x2
+        upscaler's text conditioning."""
+        x, _, last = self._encode(input_ids)
+        return x, self._pool(last, input_ids)
+
+    @torch.no_grad()
+    def forward(self, input_ids: torch.Tensor):
+        _, penult, last = self._encode(input_ids)
+        pooled = self._pool(last, input_ids)
         proj = None
         if self.cfg.projection_dim:
             proj = pooled @ self.text_projection.weight.t().to(pooled.dtype)

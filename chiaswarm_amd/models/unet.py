@@ -95,15 +95,7 @@ X4_UPSCALER = UNetConfig(
     down_block_types=("DownBlock2D",) + ("CrossAttnDownBlock2D",) * 3,
     up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
     num_heads=8, cross_attention_dim=1024, num_class_embeds=1000, sample_size=128)
-# stabilityai/sd-x2-latent-upscaler (geometry approximated with standard blocks:
-# 4 noisy + 4 low-res latent channels, CLIP-L context)
-LATENT_X2 = UNetConfig(
-    in_channels=8, out_channels=4, block_out_channels=(128, 256, 512, 512),
-    down_block_types=("DownBlock2D",) + ("CrossAttnDownBlock2D",) * 3,
-    up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
-    num_heads=(2, 4, 8, 8), cross_attention_dim=768, use_linear_projection=False, sample_size=64)
 TINY_X4 = dataclasses.replace(TINY, in_channels=7, num_class_embeds=1000)
-TINY_X2 = dataclasses.replace(TINY, in_channels=8)
 
 CONFIGS = {"sd15": SD15, "sd21": SD21, "sd21-v": SD21_V, "sdxl": SDXL, "pix2pix": PIX2PIX,
            "sd2-inpaint": INPAINT_SD2, "tiny": TINY}

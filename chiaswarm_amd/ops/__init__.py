@@ -374,14 +374,18 @@ def _ref_group_norm(x, gamma, beta, groups, eps, silu):
         y = y * gamma.to(dt).view(shp) + beta.to(dt).view(shp)
     else:
         y = F.group_norm(xn, groups, gamma.to(dt), beta.to(dt), eps)
-    if silu:
+    if silu == "gelu":
+        y = F.gelu(y)
+    elif silu:
         y = F.silu(y)
     return y.movedim(1, -1).to(x.dtype).contiguous()
 
 
 def group_norm(x, gamma, beta, groups=32, eps=1e-5, silu=False):
-    """GroupNorm over a channels-last tensor [B, ..., C] (+ optional fused SiLU).
-    ``gamma``/``beta`` are [C], or [B, C] for a per-sample affine."""
+    """GroupNorm over a channels-last tensor [B, ..., C] (+ optional fused
+    activation: ``silu=True`` SiLU, ``silu="gelu"`` GELU).  ``gamma``/``beta``
+    are [C], or [B, C] (rows may be strided views) for a per-sample affine
+    (AdaGroupNorm / scale-shift time conditioning)."""
     if use_hip(x):
         from . import hip_ops
 

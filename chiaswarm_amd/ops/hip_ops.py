@@ -321,7 +321,12 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     if gamma.dim() == 2:
         if gamma.shape != (B, C) or beta.shape != (B, C):
             raise ValueError("group_norm: per-sample affine must be [B, C]")
-        gamma, beta, bstride = gamma.contiguous(), beta.contiguous(), C
+        # rows of a wider matrix (e.g. slices of one batched projection) are
+        # read in place when both share the row stride
+        if gamma.stride(1) != 1 or beta.stride(1) != 1 or gamma.stride(0) != beta.stride(0):
+            gamma, beta = gamma.contiguous(), beta.contiguous()
+        bstride = gamma.stride(0)
+    act = 2 if silu == "gelu" else int(bool(silu))
     y = torch.empty_like(x)
     fused = getattr(x, "_csk_gn", None)
     if fused is not None:
@@ -329,11 +334,11 @@ def group_norm(x, gamma, beta, groups, eps, silu):
         if P % seg == 0 and fpart.numel() == (B * P // seg) * C * 2:
             stat = torch.empty(B * groups * 2, dtype=torch.float32, device=x.device)
             _lib.call("csk_group_norm_part", _p(y), _p(x), None, 0, _p(fpart), seg, _p(stat), _p(gamma), _p(beta),
-                      B, P, C, groups, chunk, nchunk, float(eps), int(bool(silu)), bstride, _s())
+                      B, P, C, groups, chunk, nchunk, float(eps), act, bstride, _s())
             return y
     part = torch.empty(B * nchunk * groups * 3 + B * groups * 2, dtype=torch.float32, device=x.device)
     _lib.call("csk_group_norm", _p(y), _p(x), None, 0, _p(part), _p(gamma), _p(beta), B, P, C, groups, chunk, nchunk,
-              float(eps), int(bool(silu)), bstride, _s())
+              float(eps), act, bstride, _s())
     return y
 
 

@@ -2,10 +2,13 @@
 
 * ``LatentUpscaler`` — the ``upscale: true`` option of txt2img/img2img jobs
   (reference: swarm/diffusion/upscale.py:6-32, stabilityai/sd-x2-latent-upscaler,
-  20 steps, guidance 0).  Images are VAE-encoded, the x2 UNet denoises at twice
-  the latent resolution conditioned on the nearest-upsampled low-res latents,
-  and the VAE decodes at 2x.  Unlike the reference (which returned only
-  ``images[0]``) every image is upscaled, as one batch.
+  20 steps, guidance 0).  Images are VAE-encoded; the k-diffusion K-UNet
+  (``models.kunet``) denoises at twice the latent resolution conditioned on the
+  nearest-upsampled low-res latents, the pooled CLIP-L text (mapping network)
+  and the pre-final-LayerNorm CLIP-L hidden states (cross-attention), with the
+  Karras preconditioning (c_noise = log(sigma)/4, x0 = x/(s^2+1) +
+  s/sqrt(s^2+1) F, Euler); the VAE decodes at 2x.  Unlike the reference (which
+  returned only ``images[0]``) every image is upscaled, as one batch.
 * ``X4Upscaler`` — stabilityai/stable-diffusion-x4-upscaler, the third stage
   of DeepFloyd IF (reference: swarm/diffusion/diffusion_func_if.py:36-40,
   :63-65): 7-channel UNet (4 latent + 3 noised low-res RGB) with the noise
@@ -16,6 +19,8 @@ the same fused sampler-step kernel as the SD path.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 from PIL import Image
@@ -25,7 +30,8 @@ from ..models import clip as clip_mod
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
 from ..models.weights import tokenizer_dir
-from ..models.unet import LATENT_X2, TINY_X2, TINY_X4, X4_UPSCALER, UNet2DConditionModel
+from ..models.kunet import LATENT_X2_K, TINY_X2_K, KUNet2DConditionModel
+from ..models.unet import TINY_X4, X4_UPSCALER, UNet2DConditionModel
 from ..models.vae import SD_VAE, TINY_VAE, AutoencoderKL, VAEConfig
 from ..runtime.model_cache import cache, find_weights
 from ..schedulers import get_scheduler
@@ -104,31 +110,63 @@ class LatentUpscaler(_Base):
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         tcfg = clip_mod.TINY_TEXT if tiny else clip_mod.CLIP_L
         with torch.device(self.device):
-            self.unet = UNet2DConditionModel(TINY_X2 if tiny else LATENT_X2).to(self.dtype)
+            self.unet = KUNet2DConditionModel(TINY_X2_K if tiny else LATENT_X2_K).to(self.dtype)
             self.vae = AutoencoderKL(TINY_VAE if tiny else SD_VAE).to(self.dtype)
             self.text_encoder = clip_mod.CLIPTextModel(tcfg).to(self.dtype)
         self._init([self.unet, self.vae, self.text_encoder], seed, weights_dir,
                    [("unet", self.unet), ("vae", self.vae), ("text_encoder", self.text_encoder)])
         self.tokenizer = CLIPTokenizer(tokenizer_dir(weights_dir), 77, vocab_size=tcfg.vocab_size)
-        self._graphs = GraphCache(self._unet_fn)
+        self._graphs = GraphCache(self._kunet_fn)
         self.f = 2 ** (len(self.vae.cfg.block_out_channels) - 1)
 
+    def _kunet_fn(self, x, c, cond, kv):
+        return self.unet(x, c, cond, cross_kv=list(kv))
+
+    def _text(self, prompts):
+        """(cross-attention K/V of the pre-final-LN hidden states, pooled) per prompt."""
+        ids = self.tokenizer(prompts).to(self.device)
+        hidden, pooled = self.text_encoder.encode_pre_ln(ids)
+        return self.unet.encode_context(hidden), pooled
+
     @torch.no_grad()
-    def __call__(self, prompt, images, num_inference_steps=20, guidance_scale=0.0, generator=None, latents=None):
+    def __call__(self, prompt, images, num_inference_steps=20, guidance_scale=0.0, generator=None, latents=None,
+                 negative_prompt=None):
         """images: PIL list (or SD latents via ``latents`` [B, h, w, 4], scaled) -> 2x PIL images."""
         if latents is None:
             x = _to_nhwc(images, self.device)
-            latents = self.vae.encode(x, generator=generator, sample=False) * self.vae.cfg.scaling_factor
+            latents = self.vae.encode(x.to(self.dtype), generator=generator, sample=True) * self.vae.cfg.scaling_factor
         b, h, w, c = latents.shape
         prompts = prompt if isinstance(prompt, list) else [prompt] * b
         cfg = guidance_scale > 1.0
-        kv = self._encode_text(([""] * b + prompts) if cfg else prompts)
-        cond = latents.float().repeat_interleave(2, 1).repeat_interleave(2, 2)  # nearest x2
-        sched = get_scheduler("EulerDiscreteScheduler", use_karras_sigmas=False)
+        negs = negative_prompt if isinstance(negative_prompt, list) else [negative_prompt or ""] * b
+        kv, pooled = self._text((negs + prompts) if cfg else prompts)
+        nb = pooled.shape[0]
+        # low-res noise level 0: inv_noise_level 1 and Fourier(log1p(0)) = [cos 0 | sin 0]
+        half = (self.unet.cfg.time_cond_proj_dim - pooled.shape[-1]) // 2
+        cond_vec = torch.cat([torch.ones(nb, half, device=self.device), torch.zeros(nb, half, device=self.device),
+                              pooled.float()], -1).to(self.dtype)
+        low = latents.float().repeat_interleave(2, 1).repeat_interleave(2, 2)  # nearest x2
+        low = (torch.cat([low, low], 0) if cfg else low).to(self.dtype)
+        sched = get_scheduler("EulerDiscreteScheduler", use_karras_sigmas=False, prediction_type="k_denoiser")
         sched.set_timesteps(num_inference_steps)
         noise = torch.randn((b, c, 2 * h, 2 * w), generator=generator, device=self.device, dtype=torch.float32)
         x = noise.permute(0, 2, 3, 1).contiguous() * sched.init_noise_sigma
-        x = self._denoise(x, sched, kv, guidance_scale, cond, None, generator)
+        c_dev = torch.zeros(nb, device=self.device, dtype=torch.float32)
+        while sched.step_index < sched.n:
+            xi = (x * sched.current_scale()).to(self.dtype)
+            x_in = torch.cat([torch.cat([xi, xi], 0) if cfg else xi, low], -1)
+            c_dev.fill_(math.log(max(sched.eval_sigma(), 1e-10)) * 0.25)
+            e = self._graphs(self.device, x=x_in, c=c_dev, cond=cond_vec, kv=tuple(kv))
+            coeffs = sched.fused_coeffs()
+            if ops.use_hip(x):
+                x = ops.sched_step(e, x, sched, coeffs, guidance_scale if cfg else None, None)
+            else:
+                if cfg:
+                    e_u, e_c = e.float().chunk(2)
+                    eg = e_u + guidance_scale * (e_c - e_u)
+                else:
+                    eg = e.float()
+                x = sched.step(eg, x, generator)
         img = self.vae.decode((x / self.vae.cfg.scaling_factor).to(self.dtype))
         return _to_pil(ops.vae_postprocess(img).cpu())
 

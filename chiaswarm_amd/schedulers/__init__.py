@@ -137,6 +137,8 @@ class Scheduler:
         sv = s * a
         pt = self.prediction_type
         if self.space == "vp":
+            if pt == "k_denoiser":
+                raise ValueError(f"{self.name}: k_denoiser outputs need a k-space sampler (Euler / Heun / DPM2 ...)")
             if pt == "epsilon":
                 return 1.0 / a, -sv / a
             if pt == "v_prediction":
@@ -146,6 +148,8 @@ class Scheduler:
             return 1.0, -s
         if pt == "v_prediction":
             return 1.0 / (s * s + 1.0), -s / math.sqrt(s * s + 1.0)
+        if pt == "k_denoiser":  # Karras preconditioning, sigma_data = 1: x0 = c_skip x + c_out F
+            return 1.0 / (s * s + 1.0), s / math.sqrt(s * s + 1.0)
         return 0.0, 1.0
 
     def coeffs(self, i: int) -> StepCoeffs | None:  # pragma: no cover - overridden

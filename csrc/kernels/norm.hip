@@ -338,7 +338,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const float t = f[j] * sa[u][j] + sb[u][j];
-              f[j] = silu ? silu_f(t) : t;
+              f[j] = silu == 1 ? silu_f(t) : (silu == 2 ? gelu_f(t) : t);  // act: 0 none, 1 SiLU, 2 GELU
             }
             *reinterpret_cast<uint4*>(y + boff + (size_t)pp * C + v * 8) = pack8(f);
           }

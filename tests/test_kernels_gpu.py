@@ -122,6 +122,21 @@ def test_group_norm(gpu, shape, G, silu):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("shape,G", [((2, 32, 32, 384), 12), ((3, 16, 16, 768), 24), ((2, 8, 8, 64), 8)])
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_group_norm_adaptive_strided_affine(gpu, shape, G, act):
+    """AdaGroupNorm (K-UNet): per-sample affine taken in place from row slices
+    of one wider batched projection [B, sum 2C] (row stride > C), + fused GELU."""
+    B, C = shape[0], shape[-1]
+    x = rnd(*shape, dev=gpu, scale=2.0) + 1.0
+    proj = rnd(B, 3 * C + 40, dev=gpu)
+    g, b = proj[:, 40:40 + C], proj[:, 40 + C:40 + 2 * C]
+    assert g.stride(0) == 3 * C + 40
+    y = hip_ops.group_norm(x, g, b, G, 1e-5, act)
+    ref = ops._ref_group_norm(x.float().cpu(), g.float().cpu(), b.float().cpu(), G, 1e-5, act)
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("C", [320, 768, 1024, 1280, 2048])
 def test_layer_norm(gpu, C):
     x = rnd(3, 50, C, dev=gpu, scale=2.0) + 1.0

@@ -44,14 +44,14 @@ def test_ranges_cover_all_images():
 
 
 def test_process_executor_recovers_from_crash_and_hang():
-    ex = ProcessExecutor("cpu", job_timeout_s=20)
+    ex = ProcessExecutor("cpu", job_timeout_s=120)  # generous: a loaded box slows child start-up
     try:
         async def main():
             crashed = await ex.run({"id": "c1", **TINY, "_test": "exit"})
             ok1 = await ex.run({"id": "ok1", **TINY, "seed": 3})
             ex.job_timeout_s = 4
             hung = await ex.run({"id": "h1", **TINY, "_test": "hang"})
-            ex.job_timeout_s = 60
+            ex.job_timeout_s = 120
             ok2 = await ex.run({"id": "ok2", **TINY, "seed": 3})
             return crashed, ok1, hung, ok2
 
