@@ -149,29 +149,39 @@ class KAttentionBlock(nn.Module):
         return out.view(b, hh, ww, c)
 
 
-def _binomial_kernel(c, device, dtype, scale=1.0):
-    k1 = torch.tensor([1.0, 3.0, 3.0, 1.0], device=device) / 8.0 * scale
-    return (k1[:, None] * k1[None, :]).to(dtype).expand(c, 1, 4, 4).contiguous()
+def _binomial_kernel(c, scale=1.0):
+    k1 = torch.tensor([1.0, 3.0, 3.0, 1.0]) / 8.0 * scale
+    return (k1[:, None] * k1[None, :]).expand(c, 1, 4, 4).contiguous()
 
 
 class KDownsample2D(nn.Module):
-    """Depthwise [1,3,3,1]/8 binomial filter, reflect pad 1, stride 2 (no params).
-    A fixed 16-tap depthwise filter: MIOpen's grouped conv, not worth an MFMA tile."""
+    """Depthwise [1,3,3,1]/8 binomial filter, reflect pad 1, stride 2 (no
+    checkpoint params; the filter is a non-persistent buffer so it moves with
+    the model and never needs a host copy inside a captured graph).  A fixed
+    16-tap depthwise filter: MIOpen's grouped conv, not worth an MFMA tile."""
+
+    def __init__(self, channels):
+        super().__init__()
+        self.register_buffer("kernel", _binomial_kernel(channels), persistent=False)
 
     def forward(self, x):
         c = x.shape[-1]
         xn = F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect")
-        y = F.conv2d(xn, _binomial_kernel(c, x.device, x.dtype), stride=2, groups=c)
+        y = F.conv2d(xn, self.kernel.to(x.dtype), stride=2, groups=c)
         return y.permute(0, 2, 3, 1).contiguous()
 
 
 class KUpsample2D(nn.Module):
     """Transposed depthwise binomial filter (x2 gain), reflect pad 1, stride 2."""
 
+    def __init__(self, channels):
+        super().__init__()
+        self.register_buffer("kernel", _binomial_kernel(channels, 2.0), persistent=False)
+
     def forward(self, x):
         c = x.shape[-1]
         xn = F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect")
-        y = F.conv_transpose2d(xn, _binomial_kernel(c, x.device, x.dtype, 2.0), stride=2, padding=3, groups=c)
+        y = F.conv_transpose2d(xn, self.kernel.to(x.dtype), stride=2, padding=3, groups=c)
         return y.permute(0, 2, 3, 1).contiguous()
 
 
@@ -235,7 +245,7 @@ class KUNet2DConditionModel(Prepared):
             cin = ch[max(0, i - 1)]
             rs = [res(cin if j == 0 else ch[i], ch[i], ch[i]) for j in range(cfg.layers_per_block[i])]
             ats = [att(ch[i], i) for _ in rs] if cfg.cross_attn[i] else None
-            self.down_blocks.append(_KBlock(rs, ats, "downsamplers", KDownsample2D() if i < n - 1 else None))
+            self.down_blocks.append(_KBlock(rs, ats, "downsamplers", KDownsample2D(ch[i]) if i < n - 1 else None))
 
         # up (lowest level first): level i takes [h | skip_i] except the first,
         # mid width ch[i], last layer narrows to ch[i-1]
@@ -250,7 +260,7 @@ class KUNet2DConditionModel(Prepared):
                 rs.append(res(cin if j == 0 else ch[i], ch[i], cout if last else ch[i]))
                 ats.append(att(cout if last else ch[i], i))
             self.up_blocks.append(_KBlock(rs, ats if cfg.cross_attn[i] else None, "upsamplers",
-                                          KUpsample2D() if i > 0 else None))
+                                          KUpsample2D(cout) if i > 0 else None))
         self.conv_out = Conv2d(ch[0], cfg.out_channels, 1)
 
     # ------------------------------------------------------------------

@@ -2,7 +2,8 @@
 """Secondary BASELINE.json configs on one MI355X (random weights, synthetic inputs):
 
   sdxl      SDXL-base 1024x1024, 30 steps, batch 1 per GPU (config #3's per-GPU share)
-  controlnet ControlNet-canny on SD1.5 512x512 (config #4)
+  controlnet ControlNet-canny on SD1.5 512x512 (config #4), batch 1 and 4
+  x2up      sd-x2-latent-upscaler K-UNet 512 -> 1024, 20 steps (the ``upscale`` option)
   esrgan    Real-ESRGAN x4 512 -> 2048 (config #5)
   sd21-b1   SD2.1 512x512 50 steps batch 1 (latency)
   audioldm  AudioLDM-S 10 s clip, 25 steps (txt2audio default)
@@ -87,14 +88,25 @@ def main():
         img = Image.fromarray((rng.random((512, 512, 3)) * 255).astype(np.uint8))
         g = torch.Generator(device=dev)
 
-        def run():
-            cond = image_to_canny(img)
-            p(prompt="a house", image=cond, num_inference_steps=30, generator=g.manual_seed(0),
-              scheduler=get_scheduler("DPMSolverMultistepScheduler"))
+        for n in (1, 4):
+            def run(n=n):
+                cond = image_to_canny(img)
+                p(prompt="a house", image=cond, num_inference_steps=30, generator=g.manual_seed(0),
+                  num_images_per_prompt=n, scheduler=get_scheduler("DPMSolverMultistepScheduler"))
 
-        lat = timed(run, a.reps)
-        emit("controlnet-canny-sd15-512-30step", 1, lat)
+            lat = timed(run, a.reps)
+            emit(f"controlnet-canny-sd15-512-30step{'' if n == 1 else '-batch4'}", n, lat)
         del p
+    if "x2up" in todo:
+        from chiaswarm_amd.pipelines.upscale import LatentUpscaler
+
+        up = LatentUpscaler(str(dev))
+        rng = np.random.default_rng(0)
+        ims = [Image.fromarray((rng.random((512, 512, 3)) * 255).astype(np.uint8))]
+        g = torch.Generator(device=dev)
+        lat = timed(lambda: up(["a fox"], ims, num_inference_steps=20, generator=g.manual_seed(0)), a.reps)
+        emit("latent-x2-upscaler-512to1024-20step", 1, lat)
+        del up
     if "audioldm" in todo:
         from chiaswarm_amd.pipelines.audio import AudioLDM
 
