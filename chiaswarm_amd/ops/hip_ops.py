@@ -46,12 +46,23 @@ def set_gn_fine(v: int):
     _lib.call("csk_set_gn_fine", GN_FINE)
 
 
-def _gn_seg(tile, split, rows_per_b, M, code):
+SPLITK_GN_SEG = 64  # gemm_common.h SPLITK_GN_SEG: segment rows of the split-K reduce's GN statistics
+SPLITK_GN = True  # split-K producers emit GN statistics from their reduce (tools/abstep.py arms skgn0 / skgn1)
+
+
+def _gn_seg(tile, split, rows_per_b, M, code, N=8):
     """Rows per fused-GN statistics segment (fine: the epilogue's column pass
     splits each BM-row tile into 256/BN segments of BM*BN/256 rows; else one
-    segment per tile), or 0."""
+    segment per tile; split-K: the reduce kernel's SPLITK_GN_SEG rows), or 0."""
     bm, bn = tuning.TILES.get(tile, (0, 0))
-    if split != 1 or code == 3 or bm == 0 or rows_per_b <= 0 or rows_per_b % bm or M % bm:
+    if code == 3 or bm == 0 or rows_per_b <= 0:
+        return 0
+    if split != 1:
+        if not SPLITK_GN:
+            return 0
+        s = SPLITK_GN_SEG
+        return s if rows_per_b % s == 0 and M % s == 0 and N % 8 == 0 else 0
+    if rows_per_b % bm or M % bm:
         return 0
     seg = bm * bn // 256 if GN_FINE else bm
     band = bm // 2 if (bm > 128 or bn == 160) else bm  # epilogue row band (gemm_common.h epi_passes, WM = 2)
@@ -172,7 +183,7 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
             tile, split = (19 if N <= 1280 else 20), 1
         if ln is None and code == 3:
             row_stats = False
-    seg = _gn_seg(tile, split, gn_rows, M, code) if gn_rows and out.is_contiguous() else 0
+    seg = _gn_seg(tile, split, gn_rows, M, code, N) if gn_rows and out.is_contiguous() else 0
     part = _gn_part(M, N, seg, a2.device) if seg else None
     if ln is None and not row_stats:
         run(tile, split, part)
@@ -270,7 +281,7 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     if kh != kw or dilation != 1:
         key += f":{kw}:{dilation}"
     tile, split = tuning.choose(key, M, Cout, K, run)
-    seg = _gn_seg(tile, split, Ho * Wo, M, code) if gn_stats and ys == Cout else 0
+    seg = _gn_seg(tile, split, Ho * Wo, M, code, Cout) if gn_stats and ys == Cout else 0
     part = _gn_part(M, Cout, seg, x.device) if seg else None
     run(tile, split, part)
     if part is not None:

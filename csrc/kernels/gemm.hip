@@ -289,11 +289,117 @@ __global__ void splitk_reduce8_kernel(const GemmArgs a, int ksplit) {
   }
 }
 
+// Split-K reduce that also emits the consumer GroupNorm's statistics (the
+// partial layout of the GEMM epilogue: gn_part[((m / gn_seg) * N + n) * 2] =
+// (mean, M2) of the final fp32 outputs of a gn_seg-row segment), so a split-K
+// producer no longer forces the separate statistics pass over its output.
+// Workgroup = (segment, 8*VC-column block); thread (cv, r0) finishes rows
+// r0, r0 + RPI, ... of its 8 columns and keeps their running (mean, M2)
+// (Welford); the RPI row groups are merged in LDS (Chan).  The first version
+// walked its rows one dependent load at a time and cost the step 0.36 ms
+// (tools/abstep.py skgn0 / skgn1); the rows' loads now go out together.
+template <int VC>
+__global__ __launch_bounds__(256) void splitk_reduce8_gn_kernel(const GemmArgs a, int ksplit) {
+  constexpr int RPI = 256 / VC, RPT = SPLITK_GN_SEG / RPI;  // row groups, rows per thread
+  static_assert(SPLITK_GN_SEG % RPI == 0, "segment rows split evenly over the row groups");
+  __shared__ float smean[RPI * (8 * VC + 1)], sm2[RPI * (8 * VC + 1)];
+  const int N = a.N;
+  const size_t total = (size_t)a.M * N;
+  const int cv = threadIdx.x % VC, r0 = threadIdx.x / VC;
+  const int n = (blockIdx.y * VC + cv) * 8;
+  const bool live = n < N;
+  float mean[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mean[j] = m2[j] = 0.f;
+  if (live) {
+    // all of this thread's rows' partial sums first (independent loads in flight
+    // together), then the epilogue and the Welford update row by row
+    float f[RPT][8];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const float* w = a.ws + (size_t)(blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI) * N + n;
+      const float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
+      f[q][0] = lo.x; f[q][1] = lo.y; f[q][2] = lo.z; f[q][3] = lo.w;
+      f[q][4] = hi.x; f[q][5] = hi.y; f[q][6] = hi.z; f[q][7] = hi.w;
+    }
+    for (int sidx = 1; sidx < ksplit; ++sidx) {
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const float* w = a.ws + sidx * total + (size_t)(blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI) * N + n;
+        const float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
+        f[q][0] += lo.x; f[q][1] += lo.y; f[q][2] += lo.z; f[q][3] += lo.w;
+        f[q][4] += hi.x; f[q][5] += hi.y; f[q][6] += hi.z; f[q][7] += hi.w;
+      }
+    }
+    float bb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+    if (a.bias) add8(bb, a.bias + n, true, 8);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int m = blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[q][j] += bb[j];
+      if (a.bias2d) add8(f[q], a.bias2d + (size_t)(m / a.rows_per_b) * a.ldb2 + n, true, 8);
+      act8(a.act, f[q]);
+      if (a.out_scale != 1.0f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[q][j] *= a.out_scale;
+      }
+      if (a.res) add8(f[q], a.res + (size_t)m * a.ldr + n, true, 8);
+      *reinterpret_cast<uint4*>(a.C + (size_t)m * a.ldc + n) = pack8(f[q]);
+      const float inv = 1.0f / (float)(q + 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = f[q][j] - mean[j];
+        mean[j] += d * inv;
+        m2[j] += d * (f[q][j] - mean[j]);
+      }
+    }
+  }
+  // merge the RPI row groups of each of the WG's 8*VC columns: 4 lanes per
+  // column (consecutive lanes, shuffle-reduced), RPI/4 groups each; equal counts
+  // (RPT rows per group): mean = average of the group means, M2 = sum of the
+  // group M2 + RPT * sum (mean_g - mean)^2 (exact Chan merge)
+  constexpr int CW = 8 * VC, LS = CW + 1;  // padded row-group stride: the 4 lanes of a column hit 4 banks
+  static_assert(CW * 4 == 256 && RPI % 4 == 0, "4 merge lanes per column");
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    smean[r0 * LS + cv * 8 + j] = mean[j];
+    sm2[r0 * LS + cv * 8 + j] = m2[j];
+  }
+  __syncthreads();
+  const int c = threadIdx.x >> 2, part = threadIdx.x & 3;
+  float sm = 0.f;
+#pragma unroll
+  for (int g = part; g < RPI; g += 4) sm += smean[g * LS + c];
+  sm += __shfl_xor(sm, 1);
+  sm += __shfl_xor(sm, 2);
+  const float mu = sm / (float)RPI;
+  float q = 0.f;
+#pragma unroll
+  for (int g = part; g < RPI; g += 4) {
+    const float d = smean[g * LS + c] - mu;
+    q += sm2[g * LS + c] + (float)RPT * d * d;
+  }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  const int nc = blockIdx.y * CW + c;
+  if (part == 0 && nc < N)
+    *reinterpret_cast<float2*>(a.gn_part + ((size_t)blockIdx.x * N + nc) * 2) = make_float2(mu, q);
+}
+
 static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
   const size_t total = (size_t)a.M * a.N;
   const bool vec = a.N % 8 == 0 && a.ldc % 8 == 0 && (!a.res || a.ldr % 8 == 0) && (!a.bias2d || a.ldb2 % 8 == 0) &&
                    ((size_t)a.C % 16 == 0) && (!a.res || (size_t)a.res % 16 == 0) && (!a.bias || (size_t)a.bias % 16 == 0) &&
                    (!a.bias2d || (size_t)a.bias2d % 16 == 0) && ((size_t)a.ws % 16 == 0);
+  if (a.gn_part) {  // host guarantees the vector layout and gn_seg | M (hip_ops._gn_seg)
+    constexpr int VC = 8;
+    if (!vec || a.gn_seg != SPLITK_GN_SEG || a.M % SPLITK_GN_SEG != 0) return (int)hipErrorInvalidValue;
+    splitk_reduce8_gn_kernel<VC><<<dim3(a.M / SPLITK_GN_SEG, (a.N / 8 + VC - 1) / VC), 256, 0, s>>>(a, ksplit);
+    return (int)hipGetLastError();
+  }
   if (vec) {
     int grid = (int)((total / 8 + 255) / 256);
     if (grid > 8192) grid = 8192;
@@ -310,7 +416,7 @@ template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
-  if (a.gn_part && (ksplit > 1 || a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
+  if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
   if (a.ln_part && tile >= 21) tile = (tile == 21) ? 11 : (tile == 23 ? 18 : 19);  // persistent: no per-tile LN stats
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
@@ -350,6 +456,7 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     }
   }
   if (err || ksplit == 1) return err;
+  if (a.gn_part) a.gn_seg = SPLITK_GN_SEG;  // mirrored by hip_ops._gn_seg
   return splitk_reduce(a, ksplit, s);
 }
 

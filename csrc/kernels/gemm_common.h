@@ -566,6 +566,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 // the column pass busy), 0 = one segment per BM-row tile.  The host mirrors it
 // (hip_ops._gn_seg).
 extern int g_gn_fine;
+// rows per GroupNorm-statistics segment written by the split-K reduce
+// (splitk_reduce8_gn_kernel); the host requires it to divide the rows per sample
+constexpr int SPLITK_GN_SEG = 64;
 template <int BM, int BN, int WM>
 __host__ __forceinline__ int gn_seg_for() {
   constexpr int PR = BM / epi_passes<BM, BN, WM>();  // the epilogue's row band

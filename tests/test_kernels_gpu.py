@@ -326,6 +326,41 @@ def test_fused_group_norm_stats(gpu, tile):
     assert rel_err(yc.cpu(), refc) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [1, 11, 14, 26, 31, 32])
+@pytest.mark.parametrize("split", [2, 4])
+def test_fused_group_norm_stats_split_k(gpu, tile, split):
+    """Split-K producers emit GN statistics from the reduce kernel
+    (splitk_reduce8_gn_kernel, 64-row segments): fused GN == own-stats GN, and
+    the partials match the fp32 segment moments of the output."""
+    from chiaswarm_amd.ops import tuning
+
+    B, H, W, Cin, Cout = 2, 16, 16, 128, 320
+    x = rnd(B, H, W, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(Cout, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    res = rnd(B, H, W, Cout, dev=gpu) + 1.0
+    g, b = rnd(Cout, dev=gpu), rnd(Cout, dev=gpu)
+    key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:3:1:0"
+    t = tuning.table()
+    old = t.get(key)
+    t[key] = [tile, split, 0.0]
+    try:
+        y = hip_ops.conv2d(x, wp, None, 1, 1, res, False, None, gn_stats=True)
+    finally:
+        if old is None:
+            t.pop(key, None)
+        else:
+            t[key] = old
+    part, seg = y._csk_gn
+    assert seg == hip_ops.SPLITK_GN_SEG
+    yv = y.float().reshape(-1, seg, Cout)
+    pm = part.view(-1, Cout, 2)
+    assert torch.allclose(pm[..., 0], yv.mean(1), atol=2e-2)
+    assert rel_err(pm[..., 1], yv.var(1, unbiased=False) * seg) < 2e-2
+    fused = hip_ops.group_norm(y, g, b, 32, 1e-5, True)
+    ref = ops._ref_group_norm(y.float().cpu(), g.float().cpu(), b.float().cpu(), 32, 1e-5, True)
+    assert rel_err(fused.cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("size", [(512, 512), (97, 131)])
 def test_canny_matches_numpy(gpu, size):
     import numpy as np

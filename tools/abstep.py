@@ -27,6 +27,8 @@ def apply_arm(arm):
         _lib.call("csk_set_short_kv_variant", int(arm[3:]))
     elif arm.startswith("attn"):
         hip_ops.ATTN_VARIANT = int(arm[4:])
+    elif arm in ("skgn0", "skgn1"):
+        hip_ops.SPLITK_GN = arm == "skgn1"
     elif arm in ("lnoff", "lnon"):
         ops.LN_FUSE = arm == "lnon"
     elif arm != "base":
