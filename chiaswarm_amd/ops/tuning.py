@@ -31,6 +31,8 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64),
          # one 256x160 workgroup per CU (3-stage, 156 KB LDS): least L2->LDS traffic per output
          25: (256, 160), 26: (128, 160),
+         # 4-stage rings (3 K-steps in flight) for latency-bound low-M / long-K shapes
+         27: (128, 128), 28: (64, 128), 29: (128, 64),
          # 8-wave 256-row phased tiles (gemm8p.hip): half the L2->LDS bytes per FLOP of 128x128
          31: (256, 256), 32: (256, 128)}
 
@@ -91,7 +93,7 @@ def candidates(M, N, K):
     for tile, (bm, bn) in TILES.items():
         if tile in (5, 16) and N > 32:
             continue
-        if tile in (2, 6, 12, 17, 19, 22, 24) and N > 1280:
+        if tile in (2, 6, 12, 17, 19, 22, 24, 29) and N > 1280:
             continue
         persistent = 21 <= tile <= 24
         if (persistent or tile >= 31) and K % 64:

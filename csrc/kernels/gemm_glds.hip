@@ -528,6 +528,12 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     // 128x160, 2-stage (74 KB): two workgroups per CU, 1.66x fewer L2->LDS bytes
     // per output than 128x64 and no padded columns at N = 320 (2 x 160)
     case 26: return launch_glds<128, 160, 2, 2, 2>(a, ksplit, conv, s);
+    // deep rings for the latency-bound low-M / long-K shapes (8x8 and 16x16
+    // levels: M = 512 / 2048 rows, K up to 23040): three K-steps of loads in
+    // flight per workgroup instead of one
+    case 27: return launch_glds<128, 128, 2, 2, 4>(a, ksplit, conv, s);
+    case 28: return launch_glds<64, 128, 2, 2, 4>(a, ksplit, conv, s);
+    case 29: return launch_glds<128, 64, 2, 2, 4>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }
 }

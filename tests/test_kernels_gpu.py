@@ -33,7 +33,7 @@ def test_gemm(gpu, M, N, K, act):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("split", [1, 3])
 def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     from chiaswarm_amd.ops import _lib
@@ -73,7 +73,7 @@ def test_gemm_strided_a_and_geglu(gpu):
     assert rel_err(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 3, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26])
+@pytest.mark.parametrize("tile", [1, 3, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29])
 def test_geglu_every_tile(gpu, tile):
     """GEGLU pairs (hidden, gate) 16-column tiles inside each wave's columns: every
     tile (incl. the persistent ones) must produce the same gated output."""
@@ -288,7 +288,7 @@ def test_persistent_tiles_many_tiles_per_workgroup(gpu, tile):
     assert rel_err(y, refc) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 16, 17, 21, 23, 25, 26])
+@pytest.mark.parametrize("tile", [1, 2, 4, 11, 12, 14, 16, 17, 21, 23, 25, 26, 27, 28, 29])
 def test_fused_group_norm_stats(gpu, tile):
     """GroupNorm fed by conv-epilogue statistics == GroupNorm with its own stats pass."""
     from chiaswarm_amd.ops import tuning
