@@ -124,12 +124,12 @@ def fold_layer_norm(w: torch.Tensor, bias, gamma: torch.Tensor, beta):
     return w2.contiguous(), colsum, b2.to(w.dtype)
 
 
-# Off by default: measured on one MI355X in one process (tools/abstep.py, arms
-# lnon / lnoff) the fused path is 0.27 ms per UNet step SLOWER than LayerNorm
-# kernels + plain GEMMs (14.25 vs 13.98 ms): the row-statistics epilogue of the
-# producers, the per-row merge kernel and the forced split-K=1 tiles cost more
-# than the 3 LN passes they remove.  CSK_LN_FUSE=1 enables it.
-LN_FUSE = os.environ.get("CSK_LN_FUSE", "0") == "1"
+# On by default since the row-layout direct epilogue carries both halves (the
+# producer's per-row sums, the consumer's rstd * (acc - mean * colsum)): one
+# MI355X, one process (tools/abstep.py arms lnoff / lnon) 12.79 -> 12.70 ms per
+# UNet step (profiles/unet_step_ab_lnfuse_r2x.txt).  With the LDS epilogue it
+# had been 0.27-0.6 ms SLOWER than LayerNorm kernels.  CSK_LN_FUSE=0 disables.
+LN_FUSE = os.environ.get("CSK_LN_FUSE", "1") == "1"
 
 
 def row_stats_wanted(x: torch.Tensor) -> bool:

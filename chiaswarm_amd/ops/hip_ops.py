@@ -181,6 +181,8 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
     if ln is not None or row_stats:
         if split > 1:  # the split-K reduce has no LN / row-statistics epilogue
             tile, split = (19 if N <= 1280 else 20), 1
+        if tile in (25, 26):  # 160-column tiles: no LN / row statistics (the library runs tile 11)
+            tile = 11
         if ln is None and code == 3:
             row_stats = False
     seg = _gn_seg(tile, split, gn_rows, M, code, N) if gn_rows and out.is_contiguous() else 0

@@ -149,7 +149,8 @@ __device__ __forceinline__ void act8(int act, float (&f)[8]) {
 // the producer's column-slab partials.  Loaded BEFORE the K loop so the
 // L2/HBM round trip overlaps the operand staging; one float2 in registers
 // (merging the partials here raised every tile's VGPR peak and cost the
-// small tiles a workgroup per CU).
+// small tiles a workgroup per CU; merging them in the epilogue serialised
+// ln_nparts dependent loads per row and cost the UNet step 0.8 ms).
 template <int BM>
 __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
   const int r = threadIdx.x;
@@ -220,10 +221,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     return;
   }
   if constexpr (SW && NT % 2 == 0) {
-    // ---- direct row-vector stores (no LDS) for the common case ----
+    // ---- direct row-vector stores (no fp32 LDS staging) ----
+    // Also covers the fused-LayerNorm consumer (ln_part: rstd * (acc - mean *
+    // colsum) from the merged per-row statistics ln_row) and the row-statistics
+    // producer (row_part: per-row (mean, M2) over this tile's BN columns, the
+    // WN waves' sums combined through a few bytes of LDS).
     const bool geglu = args.act == ACT_GEGLU;
     constexpr bool geglu_ok = NT % 4 == 0;
-    const bool direct = !args.gn_part && !args.row_part && !args.ln_part && (geglu_ok || !geglu) &&
+    const bool lnf = args.ln_part != nullptr;
+    const bool rst = args.row_part != nullptr;
+    const bool direct = !args.gn_part && (!lnf || args.ln_row) && (!rst || !geglu) && (geglu_ok || !geglu) &&
                         (N % (geglu ? 16 : 8)) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
                         (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
                         (!args.bias2d || ((args.ldb2 % 8) == 0 && ((((size_t)args.bias2d) & 15) == 0))) &&
@@ -236,16 +243,31 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       const int ob = geglu ? (n0 + wn * WTN) / 2 : n0 + wn * WTN;  // this wave's first output column
       const float osc = args.out_scale;
       const int act = args.act;
+      float lnm[MT], lnr[MT];  // fused LN: (mean, rstd) of each row block's row
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        lnm[i] = 0.f;
+        lnr[i] = 1.f;
+        if (lnf) {  // independent loads, issued together before the fragment loop
+          const float2 st =
+              *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + wm * WTM + i * 16 + fr, M - 1) * 2);
+          lnm[i] = st.x;
+          lnr[i] = st.y;
+        }
+      }
       if (geglu) {
         if constexpr (NT % 4 == 0) {
 #pragma unroll
           for (int f = 0; f < NT / 2; f += 2) {
             // packed columns: fragments 2f, 2f+1 = hidden, gate of output fragment f
-            float bq[4][4];
+            float bq[4][4], cq[4][4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int nh = n0 + wn * WTN + (2 * f + q) * 16 + fq * 4;
-              if (args.bias && nh < N) {
+              const bool in = nh < N;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) cq[q][r] = (lnf && in) ? args.ln_colsum[nh + r] : 0.f;
+              if (args.bias && in) {
                 const uint2 u = *reinterpret_cast<const uint2*>(args.bias + nh);
                 bq[q][0] = __uint_as_float(u.x << 16);
                 bq[q][1] = __uint_as_float(u.x & 0xffff0000u);
@@ -262,8 +284,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
               v4f x, y;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                x[r] = (acc[i][2 * f][r] + bq[0][r]) * gelu_f(acc[i][2 * f + 1][r] + bq[1][r]);
-                y[r] = (acc[i][2 * f + 2][r] + bq[2][r]) * gelu_f(acc[i][2 * f + 3][r] + bq[3][r]);
+                const float h0 = lnr[i] * (acc[i][2 * f][r] - lnm[i] * cq[0][r]) + bq[0][r];
+                const float g0 = lnr[i] * (acc[i][2 * f + 1][r] - lnm[i] * cq[1][r]) + bq[1][r];
+                const float h1 = lnr[i] * (acc[i][2 * f + 2][r] - lnm[i] * cq[2][r]) + bq[2][r];
+                const float g1 = lnr[i] * (acc[i][2 * f + 3][r] - lnm[i] * cq[3][r]) + bq[3][r];
+                x[r] = h0 * gelu_f(g0);
+                y[r] = h1 * gelu_f(g1);
               }
               float o[8];
               const int col = ob + sw_pair(x, y, f, fq, o);
@@ -278,14 +304,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
           }
         }
       } else {
+        float rs[MT], rq[MT];  // row statistics: sum, sum of squares over this lane's columns
+#pragma unroll
+        for (int i = 0; i < MT; ++i) rs[i] = rq[i] = 0.f;
 #pragma unroll
         for (int f = 0; f < NT; f += 2) {
           // the 8 columns this lane stores for fragment pair f (same for every row block)
           const int col = ob + ((fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4);
-          float bb[8];
+          float bb[8], cs[8];
 #pragma unroll
-          for (int r = 0; r < 8; ++r) bb[r] = 0.f;
-          if (args.bias && col < outN) add8(bb, args.bias + col, true, 8);
+          for (int r = 0; r < 8; ++r) bb[r] = cs[r] = 0.f;
+          if (col < outN) {
+            if (args.bias) add8(bb, args.bias + col, true, 8);
+            if (lnf) {
+              const float4 c0 = *reinterpret_cast<const float4*>(args.ln_colsum + col);
+              const float4 c1 = *reinterpret_cast<const float4*>(args.ln_colsum + col + 4);
+              cs[0] = c0.x; cs[1] = c0.y; cs[2] = c0.z; cs[3] = c0.w;
+              cs[4] = c1.x; cs[5] = c1.y; cs[6] = c1.z; cs[7] = c1.w;
+            }
+          }
 #pragma unroll
           for (int i = 0; i < MT; ++i) {
             const int m = m0 + wm * WTM + i * 16 + fr;
@@ -293,7 +330,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
             sw_pair(acc[i][f], acc[i][f + 1], f, fq, o);
             if (m >= M || col >= outN) continue;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) o[r] += bb[r];
+            for (int r = 0; r < 8; ++r) o[r] = lnr[i] * (o[r] - lnm[i] * cs[r]) + bb[r];
             if (args.bias2d) add8(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col, true, 8);
             act8(act, o);
             if (osc != 1.0f) {
@@ -301,8 +338,49 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
               for (int r = 0; r < 8; ++r) o[r] *= osc;
             }
             if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
+            if (rst) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                rs[i] += o[r];
+                rq[i] = __builtin_fmaf(o[r], o[r], rq[i]);
+              }
+            }
             *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
           }
+        }
+        if (rst) {
+          // the 4 lanes of a row (fq) -> the wave's WTN columns -> the WN waves (LDS)
+          float* red = reinterpret_cast<float*>(smem);  // [WN][BM][2]
+          epi_barrier<RAW>();                            // main-loop LDS reads are done
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            float sv = rs[i], qv = rq[i];
+            sv += __shfl_xor(sv, 16);
+            qv += __shfl_xor(qv, 16);
+            sv += __shfl_xor(sv, 32);
+            qv += __shfl_xor(qv, 32);
+            if (fq == 0) {
+              const int row = wm * WTM + i * 16 + fr;
+              red[(wn * BM + row) * 2] = sv;
+              red[(wn * BM + row) * 2 + 1] = qv;
+            }
+          }
+          epi_barrier<RAW>();
+          const int ncols = min(BN, N - n0);
+          for (int row = tid; row < BM; row += NTHR) {
+            const int m = m0 + row;
+            if (m >= M) continue;
+            float sv = 0.f, qv = 0.f;
+#pragma unroll
+            for (int w = 0; w < WN; ++w) {
+              sv += red[(w * BM + row) * 2];
+              qv += red[(w * BM + row) * 2 + 1];
+            }
+            const float mean = sv / (float)ncols;
+            *reinterpret_cast<float2*>(args.row_part + ((size_t)(n0 / BN) * M + m) * 2) =
+                make_float2(mean, fmaxf(qv - sv * mean, 0.f));
+          }
+          epi_barrier<RAW>();  // persistent kernels reuse this LDS for the next tile
         }
       }
       return;

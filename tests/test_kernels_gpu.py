@@ -405,18 +405,29 @@ def test_conv_bias2d_row_stride(gpu):
 
 
 @pytest.mark.parametrize("N,act", [(960, None), (320, None), (2 * 1280, "geglu")])
-def test_layer_norm_fused_into_gemm(gpu, N, act, monkeypatch):
+@pytest.mark.parametrize("tile", [None, 11, 13, 14, 19, 20, 21, 26, 27])
+def test_layer_norm_fused_into_gemm(gpu, N, act, tile, monkeypatch):
     """Producer GEMM emits per-row statistics; the consumer GEMM applies the
     LayerNorm in its epilogue with gamma/beta folded into its weights
-    (opt-in path, CSK_LN_FUSE=1)."""
+    (opt-in path, CSK_LN_FUSE=1).  ``tile`` forces producer and consumer onto
+    one tile: the row-layout direct epilogue (glds / persistent tiles) and the
+    LDS epilogue (heuristic tiles) both."""
     from types import SimpleNamespace
+
+    from chiaswarm_amd.ops import tuning
 
     monkeypatch.setattr(ops, "LN_FUSE", True)
 
     M, C, Kp = 1000, 320, 640
+    if tile is not None:
+        t = tuning.table()
+        for key in (f"g:{M}:{C}:{Kp}:0", f"g:{M}:{N}:{C}:{3 if act == 'geglu' else 0}"):
+            monkeypatch.setitem(t, key, [tile, 1, 0.0])
     a = rnd(M, Kp, dev=gpu)
     wp_, res = rnd(C, Kp, dev=gpu, scale=Kp ** -0.5), rnd(M, C, dev=gpu, scale=3.0) + 1.5
     x = ops.gemm(a, wp_, None, residual=res, row_stats=True)  # residual stream with an offset
+    xr = ops._ref_gemm(a.float().cpu(), wp_.float().cpu(), None, res.float().cpu(), None)
+    assert rel_err(x.cpu(), xr) < 1e-2
     assert getattr(x, "_csk_rows", None) is not None
     norm = SimpleNamespace(weight=rnd(C, dev=gpu) + 1.0, bias=rnd(C, dev=gpu), eps=1e-5)
     w, b = rnd(N, C, dev=gpu, scale=C ** -0.5), rnd(N, dev=gpu)
