@@ -412,13 +412,20 @@ static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+int g_gn_lds = 0;  // tools/abstep.py arms gnd0 / gnd1: GN statistics in the direct (0) or LDS (1) epilogue
+CSK_API int csk_set_gn_lds(int v) {
+  g_gn_lds = v;
+  return 0;
+}
+
 template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
+  a.gn_lds = g_gn_lds;
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
-  if (a.ln_part && tile >= 21) tile = (tile == 21) ? 11 : (tile == 23 ? 18 : 19);  // persistent: no per-tile LN stats
+  if (a.ln_part && tile >= 21 && tile <= 24) tile = (tile == 21) ? 11 : (tile == 23 ? 18 : 19);  // persistent: no per-tile LN stats (hip_ops.gemm mirrors)
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;

@@ -54,6 +54,7 @@ struct GemmArgs {
   // split-K, no GEGLU.  gn_part[((m0 / BM) * N + n) * 2 + {0, 1}]
   float* gn_part;
   int gn_seg;  // rows per gn_part segment (divides BM; 0 -> BM)
+  int gn_lds;  // 1: GroupNorm statistics through the LDS epilogue even where the direct one can (A/B knob)
   // fused LayerNorm of the INPUT rows (SURVEY K11 folded into K9/K10): the
   // weight was pre-multiplied by gamma (W' = W diag(gamma)), the bias holds
   // b + W beta, and the epilogue applies
@@ -230,7 +231,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     constexpr bool geglu_ok = NT % 4 == 0;
     const bool lnf = args.ln_part != nullptr;
     const bool rst = args.row_part != nullptr;
-    const bool direct = !args.gn_part && (!lnf || args.ln_row) && (!rst || !geglu) && (geglu_ok || !geglu) &&
+    const bool gnp = args.gn_part != nullptr;
+    const int gseg = args.gn_seg > 0 ? args.gn_seg : BM;
+    const bool direct = (!gnp || (!args.gn_lds && !geglu && !rst && gseg % WTM == 0 && BM % gseg == 0)) && (!lnf || args.ln_row) &&
+                        (!rst || !geglu) && (geglu_ok || !geglu) &&
                         (N % (geglu ? 16 : 8)) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
                         (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
                         (!args.bias2d || ((args.ldb2 % 8) == 0 && ((((size_t)args.bias2d) & 15) == 0))) &&
@@ -307,13 +311,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         float rs[MT], rq[MT];  // row statistics: sum, sum of squares over this lane's columns
 #pragma unroll
         for (int i = 0; i < MT; ++i) rs[i] = rq[i] = 0.f;
+        // GroupNorm statistics of the output: per column, (sum, sum^2) over the
+        // wave's WTM rows -> LDS [WM][BN][2] -> (mean, M2) per gn_seg-row segment
+        float* gred = reinterpret_cast<float*>(smem);
+        if (gnp) epi_barrier<RAW>();  // main-loop LDS reads are done
 #pragma unroll
         for (int f = 0; f < NT; f += 2) {
           // the 8 columns this lane stores for fragment pair f (same for every row block)
           const int col = ob + ((fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4);
-          float bb[8], cs[8];
+          float bb[8], cs[8], gs[8], gq[8];
 #pragma unroll
-          for (int r = 0; r < 8; ++r) bb[r] = cs[r] = 0.f;
+          for (int r = 0; r < 8; ++r) bb[r] = cs[r] = gs[r] = gq[r] = 0.f;
           if (col < outN) {
             if (args.bias) add8(bb, args.bias + col, true, 8);
             if (lnf) {
@@ -345,8 +353,51 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
                 rq[i] = __builtin_fmaf(o[r], o[r], rq[i]);
               }
             }
+            if (gnp) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                gs[r] += o[r];
+                gq[r] = __builtin_fmaf(o[r], o[r], gq[r]);
+              }
+            }
             *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
           }
+          if (gnp) {
+            // the 16 lanes of a 16-row group (fr) hold the same 8 columns
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+#pragma unroll
+              for (int x = 1; x < 16; x <<= 1) {
+                gs[r] += __shfl_xor(gs[r], x);
+                gq[r] += __shfl_xor(gq[r], x);
+              }
+            }
+            if (fr == 0 && col < outN) {
+              const int c = col - n0;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                gred[(wm * BN + c + r) * 2] = gs[r];
+                gred[(wm * BN + c + r) * 2 + 1] = gq[r];
+              }
+            }
+          }
+        }
+        if (gnp) {
+          epi_barrier<RAW>();
+          const int nseg = BM / gseg, wps = gseg / WTM;  // segments per tile, waves per segment
+          for (int t = tid; t < BN * nseg; t += NTHR) {
+            const int c = t % BN, sq = t / BN;
+            if (n0 + c >= N) continue;
+            float sv = 0.f, qv = 0.f;
+            for (int w = sq * wps; w < (sq + 1) * wps; ++w) {
+              sv += gred[(w * BN + c) * 2];
+              qv += gred[(w * BN + c) * 2 + 1];
+            }
+            const float mean = sv / (float)gseg;
+            *reinterpret_cast<float2*>(args.gn_part + ((size_t)((m0 + sq * gseg) / gseg) * N + n0 + c) * 2) =
+                make_float2(mean, fmaxf(qv - sv * mean, 0.f));
+          }
+          epi_barrier<RAW>();  // persistent kernels reuse this LDS for the next tile
         }
         if (rst) {
           // the 4 lanes of a row (fq) -> the wave's WTN columns -> the WN waves (LDS)

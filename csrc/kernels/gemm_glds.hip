@@ -495,7 +495,7 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   a.zero = g_zero;
   // GEGLU pairs 16-column (hidden, gate) tiles inside one wave's columns: every
   // tile below has a per-wave width (BN / WN) that is a multiple of 32
-  if (tile >= 21) {  // persistent continuous-ring variants: FAST staging, no split-K
+  if (tile >= 21 && tile <= 24) {  // persistent continuous-ring variants: FAST staging, no split-K
     const bool fast = (conv ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
                       (size_t)(a.K + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
                       (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);

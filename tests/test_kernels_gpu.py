@@ -405,7 +405,7 @@ def test_conv_bias2d_row_stride(gpu):
 
 
 @pytest.mark.parametrize("N,act", [(960, None), (320, None), (2 * 1280, "geglu")])
-@pytest.mark.parametrize("tile", [None, 11, 13, 14, 19, 20, 21, 26, 27])
+@pytest.mark.parametrize("tile", [None, 11, 13, 14, 19, 20, 21, 22, 25, 26, 27, 29, 31, 32])
 def test_layer_norm_fused_into_gemm(gpu, N, act, tile, monkeypatch):
     """Producer GEMM emits per-row statistics; the consumer GEMM applies the
     LayerNorm in its epilogue with gamma/beta folded into its weights
