@@ -256,3 +256,49 @@ def test_kunet_hip_matches_fp32(gpu):
     y = mg(x.to(gpu), c.to(gpu), cond.to(gpu), cross_kv=mg.encode_context(ctx.to(gpu, torch.bfloat16)))
     assert y.shape == ref.shape
     assert rel_err(y.float().cpu(), ref) < 3e-2
+
+
+@torch.no_grad()
+def test_lora_and_textual_inversion_on_graph_path(gpu, tmp_path):
+    """LoRA / textual inversion on a resident GPU pipeline whose denoiser and
+    text encoder replay captured hipGraphs: the LoRA job matches a fresh eager
+    pipeline with the same merge, and the plain job after unload reproduces the
+    plain job before it bit for bit (graphs re-captured on every weight change)."""
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.models.lora import (load_lora, load_textual_inversion, unload_lora,
+                                           unload_textual_inversion)
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    pipe = StableDiffusion("tiny", device=gpu, seed=3)
+    g = torch.Generator().manual_seed(0)
+    sd = {}
+    for name, mod in pipe.unet.named_modules():
+        if name.endswith(("attn1.to_q", "attn2.to_v", "attn1.to_out.0")):
+            o, i = mod.weight.shape
+            sd[f"unet.{name}.lora_A.weight"] = torch.randn(2, i, generator=g) * 0.3
+            sd[f"unet.{name}.lora_B.weight"] = torch.randn(o, 2, generator=g) * 0.3
+    lora = str(tmp_path / "lora.safetensors")
+    save_file(sd, lora)
+    ti = str(tmp_path / "ti.safetensors")
+    save_file({"<toy>": torch.randn(1, pipe.text_encoders[0].cfg.hidden_size, generator=g)}, ti)
+
+    def run(p, prompt="a cat"):
+        gen = torch.Generator(device=gpu).manual_seed(11)
+        return p(prompt=prompt, num_inference_steps=3, height=64, width=64, generator=gen,
+                 output_type="latent").latents.float().cpu()
+
+    plain = run(pipe)
+    run(pipe)  # second call replays the captured graphs
+    load_lora(pipe.unet, lora, 1.0, pipe=pipe)
+    with_lora = run(pipe)
+    unload_lora(pipe.unet, pipe=pipe)
+    load_textual_inversion(pipe, ti)
+    with_ti = run(pipe, "a <toy> cat")
+    unload_textual_inversion(pipe)
+    after = run(pipe)
+    assert torch.equal(plain, after)
+    assert not torch.equal(plain, with_lora) and not torch.equal(plain, with_ti)
+    fresh = StableDiffusion("tiny", device=gpu, seed=3)
+    load_lora(fresh.unet, lora, 1.0, pipe=fresh)
+    assert torch.equal(run(fresh), with_lora)
