@@ -46,6 +46,7 @@ def set_gn_fine(v: int):
     _lib.call("csk_set_gn_fine", GN_FINE)
 
 
+GN_TARGET_WG = 1024  # GroupNorm apply/stats workgroups per call (rows per chunk follow; tools/abstep.py gnwgN)
 SPLITK_GN_SEG = 64  # gemm_common.h SPLITK_GN_SEG: segment rows of the split-K reduce's GN statistics
 SPLITK_GN = True  # split-K producers emit GN statistics from their reduce (tools/abstep.py arms skgn0 / skgn1)
 
@@ -332,7 +333,7 @@ def group_norm(x, gamma, beta, groups, eps, silu):
     # workgroups over the whole tensor (each apply workgroup re-merges the
     # statistics partials in its prologue: fewer, longer workgroups amortise it)
     rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
-    chunk = max(4 * rows, -(-P * B // 1024))
+    chunk = max(4 * rows, -(-P * B // GN_TARGET_WG))
     nchunk = -(-P // chunk)
     chunk = -(-P // nchunk)
     bstride = 0
@@ -375,7 +376,7 @@ def group_norm_cat(a, b, gamma, beta, groups, eps, silu):
     if Ca % 8 or Cb % 8 or gamma.dim() != 1 or C % groups or C > 4096:
         return None
     rows = max(1, 256 // max(1, -(-(C // 8) // (2 if C > 2048 else 1))))
-    chunk = max(4 * rows, -(-P * B // 1024))
+    chunk = max(4 * rows, -(-P * B // GN_TARGET_WG))
     nchunk = -(-P // chunk)
     chunk = -(-P // nchunk)
     y = torch.empty(a.shape[:-1] + (C,), dtype=torch.bfloat16, device=a.device)

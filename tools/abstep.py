@@ -20,6 +20,8 @@ from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
 def apply_arm(arm):
     if arm in ("gnd0", "gnd1"):  # GN statistics in the direct (gnd0) / LDS (gnd1) epilogue
         _lib.call("csk_set_gn_lds", int(arm == "gnd1"))
+    elif arm.startswith("gnwg"):
+        hip_ops.GN_TARGET_WG = int(arm[4:])
     elif arm in ("gnfine", "gntile"):
         hip_ops.set_gn_fine(arm == "gnfine")
     elif arm.startswith("gn"):
