@@ -46,7 +46,7 @@ def set_gn_fine(v: int):
     _lib.call("csk_set_gn_fine", GN_FINE)
 
 
-GN_TARGET_WG = 1024  # GroupNorm apply/stats workgroups per call (rows per chunk follow; tools/abstep.py gnwgN)
+GN_TARGET_WG = 512  # GroupNorm apply/stats workgroups per call (rows per chunk follow); 512: -0.05 ms/step vs 1024 (tools/abstep.py gnwgN, profiles/unet_step_ab_gnwg_r3e.txt)
 SPLITK_GN_SEG = 64  # gemm_common.h SPLITK_GN_SEG: segment rows of the split-K reduce's GN statistics
 SPLITK_GN = True  # split-K producers emit GN statistics from their reduce (tools/abstep.py arms skgn0 / skgn1)
 
