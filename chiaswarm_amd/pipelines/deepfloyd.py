@@ -14,8 +14,8 @@ offload, 288 GB HBM) and every UNet step replays from a hipGraph.
 
 Stage I/II sample with DDPM-family schedulers on the epsilon half of the
 6-channel UNet output (the learned-variance half is dropped: fixed-variance
-sampling) with IF's ``squaredcos_cap_v2`` noise schedule and dynamic
-thresholding of x0 replaced by clamping to [-1, 1].  Geometry and sampler
+sampling) with IF's ``squaredcos_cap_v2`` noise schedule and Imagen dynamic
+thresholding of the x0 prediction (``Scheduler.threshold_x0``).  Geometry and sampler
 details are parity-unpinned (no IF checkpoint in this image).
 """
 from __future__ import annotations
@@ -34,7 +34,10 @@ from ..schedulers import get_scheduler
 from .graphs import GraphCache
 from .upscale import load_x4_upscaler
 
-IF_SCHED = dict(beta_schedule="squaredcos_cap_v2", use_karras_sigmas=False, prediction_type="epsilon")
+# IF-I / IF-II scheduler_config: cosine betas, epsilon half of the learned-range
+# output, Imagen dynamic thresholding (ratio 0.95, sample_max_value 1.5)
+IF_SCHED = dict(beta_schedule="squaredcos_cap_v2", use_karras_sigmas=False, prediction_type="epsilon",
+                thresholding=True, dynamic_thresholding_ratio=0.95, sample_max_value=1.5)
 
 
 def _cos_acp(n=1000):
@@ -109,7 +112,7 @@ class IFCascade:
             out = graphs(self.device, x=x_in, t=t_dev, kv=tuple(kv), temb=temb, **extra)
             e = out[..., :3]
             e_u, e_c = e.float().chunk(2)
-            x = sched.step(e_u + guidance * (e_c - e_u), x, generator).clamp(-1.5, 1.5)
+            x = sched.step(e_u + guidance * (e_c - e_u), x, generator)
         return x.clamp(-1, 1)
 
     @torch.no_grad()

@@ -4,6 +4,8 @@ txt2vid (reference swarm/video/tx2vid.py:17-76): ModelScope text-to-video
 (UNet3D + SD VAE + OpenCLIP-H text encoder), default 25 frames, DPM-Solver++
 Karras, exported at 8 fps; frames stay on the GPU for the whole denoise (the
 video is one [B*F, h, w, 4] latent batch) and are VAE-decoded as one batch.
+Every UNet3D step replays from a shape-keyed hipGraph (``GraphCache``) and the
+CFG combine + DPM-Solver++ update run as the fused ``sched_step`` kernel.
 
 vid2vid (reference swarm/video/pix2pix.py:14-87): instruct-pix2pix applied to
 every frame (<= 100 frames, 512 px), Euler-ancestral Karras, default 15 steps,
@@ -28,7 +30,8 @@ from ..models.tokenizer import CLIPTokenizer
 from ..output.media import frames_to_video, read_video_frames
 from ..output.processor import image_to_buffer, make_result
 from ..runtime.model_cache import cache, find_weights
-from ..schedulers import get_scheduler
+from ..schedulers import batch_randn, get_scheduler
+from .graphs import GraphCache
 
 
 class TextToVideo:
@@ -54,8 +57,12 @@ class TextToVideo:
         for m in (self.unet, self.vae, self.text):
             prepare_model(m)
         self.tok = CLIPTokenizer(tokenizer_dir(w), 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
+        self._graphs = GraphCache(self._step)
         self.config = {"_class_name": "TextToVideoSDPipeline", "_framework": "chiaswarm_amd",
                        "unet": ["chiaswarm_amd", "UNet3DConditionModel"], "weights": w or "random-init"}
+
+    def _step(self, x, t, kv, frames):
+        return self.unet(x, t, frames, list(kv))
 
     @torch.no_grad()
     def __call__(self, prompt="", negative_prompt="", num_frames=25, num_inference_steps=25, guidance_scale=9.0,
@@ -69,15 +76,21 @@ class TextToVideo:
         x = torch.randn((1, 4, num_frames, lh, lw), generator=generator, device=self.device,
                         dtype=torch.float32).permute(0, 2, 3, 4, 1).reshape(num_frames, lh, lw, 4).contiguous()
         x = x * sched.init_noise_sigma
-        while sched.step_index < sched.n:
-            t = sched.current_t()
-            xi = (x * sched.current_scale()).to(self.dtype)
-            e = self.unet(torch.cat([xi, xi], 0), torch.tensor([t], device=self.device), num_frames, kv)
-            e_u, e_c = e.float().chunk(2)
-            x = sched.step(e_u + guidance_scale * (e_c - e_u), x, generator)
-        img = self.vae.decode(x / self.vae.cfg.scaling_factor)
         from .. import ops
 
+        t_dev = torch.zeros(1, device=self.device, dtype=torch.float32)
+        while sched.step_index < sched.n:
+            t_dev.fill_(float(sched.current_t()))
+            xi = (x * sched.current_scale()).to(self.dtype)
+            e = self._graphs(self.device, x=torch.cat([xi, xi], 0), t=t_dev, kv=tuple(kv), frames=num_frames)
+            coeffs = sched.fused_coeffs()
+            if coeffs is not None and ops.use_hip(x):
+                nz = batch_randn(x.shape, generator, x.device) if coeffs.D != 0.0 else None
+                x = ops.sched_step(e, x, sched, coeffs, guidance_scale, nz)
+            else:
+                e_u, e_c = e.float().chunk(2)
+                x = sched.step(e_u + guidance_scale * (e_c - e_u), x, generator)
+        img = self.vae.decode(x / self.vae.cfg.scaling_factor)
         return ops.vae_postprocess(img).cpu().numpy()  # [F, H, W, 3] uint8
 
 

@@ -76,8 +76,13 @@ class Scheduler:
 
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
                  beta_schedule="scaled_linear", prediction_type="epsilon", use_karras_sigmas=True,
-                 steps_offset=1, **_):
+                 steps_offset=1, thresholding=False, dynamic_thresholding_ratio=0.995, sample_max_value=1.0, **_):
         self.T = num_train_timesteps
+        # Imagen dynamic thresholding of the x0 prediction (DeepFloyd IF:
+        # ratio 0.95, max 1.5) -- non-linear in x0, so those steps skip the fused kernel
+        self.thresholding = thresholding
+        self.dyn_ratio = dynamic_thresholding_ratio
+        self.sample_max = sample_max_value
         self.betas = _betas(num_train_timesteps, beta_start, beta_end, beta_schedule)
         self.alphas_cumprod = np.cumprod(1.0 - self.betas)
         self.train_sigmas = np.sqrt((1 - self.alphas_cumprod) / self.alphas_cumprod)
@@ -173,14 +178,27 @@ class Scheduler:
     def fused_coeffs(self) -> StepCoeffs | None:
         """Coefficients for the fused HIP step kernel, or None if this step must
         run through ``step`` (non-linear-form samplers)."""
+        if self.thresholding:
+            return None
         return self.coeffs(self.step_index)
+
+    def threshold_x0(self, x0: torch.Tensor) -> torch.Tensor:
+        """Per-sample dynamic thresholding: s = quantile(|x0|, ratio) clamped to
+        [1, sample_max]; x0 -> clamp(x0, -s, s) / s (identity when disabled)."""
+        if not self.thresholding:
+            return x0
+        b = x0.shape[0]
+        flat = x0.reshape(b, -1).float()
+        s = torch.quantile(flat.abs(), self.dyn_ratio, dim=1).clamp(1.0, self.sample_max)
+        s = s.reshape((b,) + (1,) * (x0.dim() - 1))
+        return (torch.maximum(torch.minimum(x0, s), -s) / s).to(x0.dtype)
 
     # -- generic torch step (CPU path and reference mode) ---------------------
     def step(self, e: torch.Tensor, x: torch.Tensor, generator=None) -> torch.Tensor:
         """One update on fp32 tensors given the (guided) model output ``e``."""
         i = self.step_index
         c = self.coeffs(i)
-        x0 = c.p * x + c.q * e.float()
+        x0 = self.threshold_x0(c.p * x + c.q * e.float())
         out = c.A * x + c.B * x0
         if c.C != 0.0 and self.prev_x0 is not None:
             out = out + c.C * self.prev_x0

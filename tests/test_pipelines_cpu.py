@@ -126,3 +126,17 @@ def test_controlnet_fused_merge_equals_residual_add(tiny):
         got = unet(x, t, cross_kv=kv, control=ControlFeatures(cn, feats, m, 0.7))
     assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)
     assert not torch.allclose(got, unet(x, t, cross_kv=kv), atol=1e-3)  # the control does something
+
+
+def test_txt2vid_tiny_cpu_seeded():
+    """txt2vid (reference swarm/video/tx2vid.py:17-76) on the tiny UNet3D: the
+    eager CPU path gives uint8 frames and honours the seed."""
+    from chiaswarm_amd.pipelines.video import TextToVideo
+
+    p = TextToVideo("tiny-t2v", "cpu", tiny=True)
+    kw = dict(prompt="a boat", num_frames=3, num_inference_steps=2, height=32, width=32)
+    a = p(generator=gen(4), **kw)
+    b = p(generator=gen(4), **kw)
+    assert a.shape == (3, 32, 32, 3) and a.dtype == np.uint8
+    assert np.array_equal(a, b)
+    assert not p._graphs.graphs  # CPU: no graph capture

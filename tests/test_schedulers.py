@@ -225,3 +225,26 @@ def test_no_scheduler_is_an_alias():
     assert not _ALIASES
     for n in scheduler_names():
         assert type(get_scheduler(n)).__name__ == n
+
+
+def test_dynamic_thresholding_matches_imagen_rule():
+    """IF's samplers threshold x0 per sample (diffusers DDPMScheduler
+    _threshold_sample semantics): s = clamp(quantile(|x0|, r), 1, max)."""
+    import torch
+
+    from chiaswarm_amd.schedulers import get_scheduler
+
+    sch = get_scheduler("DDPMScheduler", thresholding=True, dynamic_thresholding_ratio=0.95,
+                        sample_max_value=1.5, use_karras_sigmas=False)
+    assert sch.fused_coeffs() is None  # non-linear: never the fused kernel
+    g = torch.Generator().manual_seed(0)
+    x0 = torch.randn(3, 8, 8, 3, generator=g) * torch.tensor([0.3, 1.2, 9.0]).reshape(3, 1, 1, 1)
+    y = sch.threshold_x0(x0)
+    for b in range(3):
+        s = min(max(torch.quantile(x0[b].abs().flatten(), 0.95).item(), 1.0), 1.5)
+        ref = x0[b].clamp(-s, s) / s
+        assert torch.allclose(y[b], ref, atol=1e-6)
+    assert y[0].equal(x0[0].clamp(-1, 1))  # quantile < 1 -> s = 1: a plain [-1, 1] clip
+    assert y.abs().max() <= 1.0 + 1e-6
+    off = get_scheduler("DDPMScheduler", use_karras_sigmas=False)
+    assert off.threshold_x0(x0) is x0

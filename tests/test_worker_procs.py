@@ -28,6 +28,11 @@ TINY = {"model_name": "tiny/sd", "prompt": "a red fox", "num_inference_steps": 2
 
 @pytest.fixture(autouse=True)
 def sdaas_root(tmp_path, monkeypatch):
+    from chiaswarm_amd.runtime import model_cache
+
+    # the in-process model cache is per process: a "tiny/sd" pipeline another test
+    # left in it (other weights, other SDAAS_ROOT) must not serve this test's jobs
+    monkeypatch.setattr(model_cache, "_CACHE", None)
     monkeypatch.setenv("SDAAS_ROOT", str(tmp_path))
     monkeypatch.setenv("CSK_TEST_HOOKS", "1")  # inherited by spawned children
     return tmp_path
@@ -99,6 +104,7 @@ def test_group_preload_and_split_job_matches_unsplit(sdaas_root):
     finally:
         solo_hive.stop()
     assert ref["pipeline_config"].get("split") is None
+    assert ref["pipeline_config"]["weights"].endswith(os.path.join("tiny", "sd"))
 
     hive = FakeHive(jobs=[dict(job)]).start()
     envs = group_envs(2)
