@@ -66,7 +66,7 @@ def _gn_seg(tile, split, rows_per_b, M, code, N=8):
     if rows_per_b % bm or M % bm:
         return 0
     seg = bm * bn // 256 if GN_FINE else bm
-    band = bm // 2 if (bm > 128 or bn == 160) else bm  # epilogue row band (gemm_common.h epi_passes, WM = 2)
+    band = bm // tuning.EPI_WM.get(tile, 2) if (bm > 128 or bn == 160) else bm  # epilogue row band (epi_passes)
     return min(seg, band)
 
 
@@ -185,7 +185,7 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
             tile, split = (19 if N <= 1280 else 20), 1
         # mirror the library's own tile substitutions: the row-statistics slabs
         # (and the buffer sized for them below) follow the tile that actually runs
-        if tile in (25, 26, 31, 32):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
+        if tile in (25, 26, 31, 32, 33):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
             tile = 11
         elif ln is not None and 21 <= tile <= 24:  # persistent tiles: no per-tile LN statistics
             tile = {21: 11, 23: 18}.get(tile, 19)

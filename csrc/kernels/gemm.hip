@@ -447,7 +447,9 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   int err;
   if (tile >= 31) {
     err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
-    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, 11, ksplit, CONV, s);
+    // fallback keeps the GN-statistics segment the host sized for: tile 33's
+    // 64-row band = tile 26's (128x160, two bands); 31 / 32's 128 = tile 11's
+    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, tile == 33 ? 26 : 11, ksplit, CONV, s);
   } else if (tile >= 11) {
     err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
   } else {

@@ -267,6 +267,200 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
   gemm_epilogue<BM, BN, WM, WN, false, EP, 512>(args, acc, smem, m0, n0, split);
 }
 
+// ---------------------------------------------------------------------------
+// 8-wave LDS-DMA RING kernel, 256 x BN tiles with BN = 160 (tile 33).
+//
+// Why: the UNet's 64x64 level (M = 32768 rows, N = 320 output channels) is
+// bound by the per-CU L2 -> LDS fill rate (~70 GB/s per CU at ~72 KB in
+// flight, MI355X_MICROARCH.md "Indexed rows: gather into LDS").  Its best tile
+// so far, 128x160 at two workgroups per CU, moves (128 + 160) / (128 * 160) =
+// 0.0141 B per FLOP; 256x160 moves 0.0102 (-28 %) and keeps 256 tiles (one
+// per CU, no padded columns at N = 320).  The 4-wave 256x160 tile 25 ran ONE
+// wave per SIMD, so LDS fragment reads, DMA issue and MFMAs of that wave
+// serialised; here 8 waves (2 per SIMD) share the ring: waves 4 (M) x 2 (N),
+// 64 x 80 outputs per wave (4 x 5 fragments, row-layout accumulators for the
+// SW epilogue), a 3-stage ring (3 x 52 KB = 156 KB: two stages, ~104 KB, in
+// flight per CU while the third is consumed) with one raw barrier per K-step
+// and a counted vmcnt, as gemm_glds.hip.
+//
+// DMA split: A = 32 eight-row groups -> 4 per wave; B = 20 groups -> 3 for
+// waves 0-3 and 2 for waves 4-7, so the per-wave vmcnt is wave-dependent (a
+// scalar branch on the SGPR wave id).  FAST staging only (K % 64 == 0, conv
+// Cin % 64 == 0); no fused LN / row statistics / GEGLU (host falls back).
+// ---------------------------------------------------------------------------
+template <int BN, int S, bool CONV>
+__global__ __launch_bounds__(512, 1) void gemm8r_kernel(const GemmArgs args) {
+  constexpr int BM = 256, WM = 4, WN = 2, NW = 8;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MT = WTM / 16, NT = WTN / 16;
+  constexpr int GA = BM / 8, GB = BN / 8;  // eight-row DMA groups
+  static_assert(GA % NW == 0 && WTN % 16 == 0, "tile shape");
+  constexpr int IA = GA / NW;
+  constexpr int IBL = GB / NW, IBX = GB % NW;  // waves < IBX stage one group more
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int SMEM_MAIN = S * STAGE;
+  constexpr int EP = epi_passes<BM, BN, WM>();
+  constexpr int SMEM_EPI = epi_smem_elems<BM, BN, EP>();
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int M = args.M, N = args.N;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int split = blockIdx.y;
+  const int kbeg = split * args.kchunk;
+  const int kend = args.ws ? min(args.K, kbeg + args.kchunk) : args.K;
+  const int nk = (kend - kbeg) / BK;
+  const bool xb = wid < IBX;  // this wave stages IBL + 1 B groups
+
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  const bf16_t* zero = args.zero + lchunk * 8;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  const int Hin = args.up2x ? 2 * args.H : args.H;
+  const int Win = args.up2x ? 2 * args.Wd : args.Wd;
+
+  // A: DMA instruction i of wave w stages group i * NW + w (rows 8 g .. 8 g + 7)
+  const bf16_t* fa[IA];
+  int a_ihb[CONV ? IA : 1], a_iwb[CONV ? IA : 1];
+  size_t a_bbase[CONV ? IA : 1];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int m = m0 + (i * NW + wid) * 8 + lrow;
+    const bool ok = m < M;
+    if constexpr (CONV) {
+      const int mm = ok ? m : 0;
+      const int hw = args.Ho * args.Wo;
+      const int b = mm / hw, r = mm - b * hw;
+      const int oh = r / args.Wo, ow = r - oh * args.Wo;
+      a_ihb[i] = ok ? oh * args.stride - args.pt : -30000;  // invalid row: every tap reads the zero page
+      a_iwb[i] = ow * args.stride - args.pl;
+      a_bbase[i] = (size_t)b * args.H * args.Wd;
+      fa[i] = zero;
+    } else {
+      fa[i] = ok ? args.A + (size_t)m * args.lda + kbeg + lchunk * 8 : zero;
+    }
+  }
+  const bf16_t* fb[IBL + 1];
+#pragma unroll
+  for (int i = 0; i <= IBL; ++i) {
+    const int n = n0 + (i * NW + wid) * 8 + lrow;
+    fb[i] = (n < N && (i < IBL || xb)) ? args.W + (size_t)n * args.ldb + kbeg + lchunk * 8 : zero;
+  }
+  int f_ky = 0, f_kx = 0, f_c = 0;
+  auto set_rows = [&]() {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int ih = a_ihb[i] + f_ky * args.dil, iw = a_iwb[i] + f_kx * args.dil;
+      const bool v = ih >= 0 && ih < Hin && iw >= 0 && iw < Win;
+      const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
+      fa[i] = v ? args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + lchunk * 8 : zero;
+    }
+  };
+  if constexpr (CONV) {
+    const int tap = kbeg / args.Cin;
+    f_c = kbeg - tap * args.Cin;
+    f_ky = tap / args.kw;
+    f_kx = tap - f_ky * args.kw;
+    set_rows();
+  }
+
+  auto issue = [&](int buf) {
+    bf16_t* as = smem + buf * STAGE;
+    bf16_t* bs = as + BM * BK;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (i * NW + wid) * 8 * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IBL; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)fb[i], (lptr_t)(bs + (i * NW + wid) * 8 * BK), 16, 0, 0);
+    if (IBX > 0 && xb)
+      __builtin_amdgcn_global_load_lds((gptr_t)fb[IBL], (lptr_t)(bs + (IBL * NW + wid) * 8 * BK), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i <= IBL; ++i) fb[i] += BK;  // the zero page is large enough for the running offset
+    if constexpr (CONV) {
+      f_c += BK;
+      if (f_c == args.Cin) {
+        f_c = 0;
+        if (++f_kx == args.kw) { f_kx = 0; ++f_ky; }
+        set_rows();
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IA; ++i) fa[i] += BK;
+    }
+  };
+
+  v4f acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+
+  const int fr = lane & 15, fq = lane >> 4;
+  constexpr int LA = IA + IBL;  // loads per stage of a wave without the extra B group
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed once at most min(S-2, nk-1-kt) younger stages are in flight
+    const int younger = min(S - 2, nk - 1 - kt);
+    if constexpr (S == 3) {
+      if (younger >= 1) {
+        if (xb) p8_vmcnt<LA + 1>();
+        else p8_vmcnt<LA>();
+      } else {
+        p8_vmcnt<0>();
+      }
+    } else {
+      static_assert(S == 2, "ring depth");
+      p8_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) issue((kt + S - 1) % S);
+    const bf16_t* as = smem + (kt % S) * STAGE;
+    const bf16_t* bs = as + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v8s af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[i] = *reinterpret_cast<const v8s*>(as + swz(wm * WTM + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, WM, WN, false, EP, 512, true>(args, acc, smem, m0, n0, split);
+}
+
+template <int BN, int S>
+static int launch8r(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
+  GemmArgs a = a0;
+  a.gn_seg = gn_seg_for<256, BN, 4>();
+  const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, ksplit);
+  if (conv)
+    gemm8r_kernel<BN, S, true><<<grid, 512, 0, s>>>(a);
+  else
+    gemm8r_kernel<BN, S, false><<<grid, 512, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
 template <int BN>
 static int launch8p(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   GemmArgs a = a0;
@@ -284,15 +478,18 @@ static int launch8p(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// tile 31: 256x256, tile 32: 256x128.  Returns hipErrorNotSupported when the
-// shape needs a feature this kernel lacks (the caller falls back).
+// tile 31: 256x256, tile 32: 256x128 (phased), tile 33: 256x160 (8-wave 3-stage
+// ring).  Returns hipErrorNotSupported when the shape needs a feature this
+// kernel lacks (the caller falls back).
 int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s) {
   const int span = ksplit > 1 ? a.kchunk : a.K;
   const bool fast = (conv ? (a.Cin % BK == 0) : true) && a.K % BK == 0 && span % BK == 0 &&
                     (size_t)(span + 2 * BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes() &&
                     (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= (size_t)csk_zero_bytes());
   if (!fast || a.ln_part || a.row_part) return (int)hipErrorNotSupported;
+  if (tile == 33 && a.act == ACT_GEGLU) return (int)hipErrorNotSupported;  // 80 columns per wave: no GEGLU pairing
   switch (tile) {
+    case 33: return launch8r<160, 3>(a, ksplit, conv, s);
     case 31: return launch8p<256>(a, ksplit, conv, s);
     case 32: return launch8p<128>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;

@@ -32,7 +32,7 @@ import torch  # noqa: E402
 from chiaswarm_amd import ops  # noqa: E402
 from chiaswarm_amd.ops import _lib, tuning  # noqa: E402
 
-SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 15, 27, 28, 29)
+SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 33, 15, 27, 28, 29)
 
 
 def main():
@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--min-gain-us", type=float, default=6.0)
     ap.add_argument("--keys", default="", help="only keys containing this substring")
     ap.add_argument("--all-tiles", action="store_true", help="every candidate, not the shortlist")
+    ap.add_argument("--only-tiles", default="", help="comma list: try only these tiles (e.g. a new kernel)")
     a = ap.parse_args()
     t_start = time.time()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
@@ -99,7 +100,9 @@ def main():
     changes = []
     for key in keys:
         M, N, K, cur = used[key]
-        cands = [c for c in tuning.candidates(M, N, K) if (a.all_tiles or c[0] in SHORTLIST) and c != tuple(cur)]
+        only = {int(v) for v in a.only_tiles.split(",") if v}
+        cands = [c for c in tuning.candidates(M, N, K) if (a.all_tiles or c[0] in SHORTLIST) and c != tuple(cur)
+                 and (not only or c[0] in only)]
         best_c, best_t = None, base
         for c in cands:
             if time.time() - t_start > a.budget:
