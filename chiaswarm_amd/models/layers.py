@@ -337,11 +337,16 @@ class ResnetBlock2D(nn.Module):
 
     def forward(self, x, temb_proj=None):
         """``temb_proj``: this block's [B, Cout] time projection (already
-        computed by the model's batched time-embedding GEMM)."""
+        computed by the model's batched time-embedding GEMM).  A 1x1 shortcut
+        runs on a side stream, overlapping norm1 / conv1 / norm2."""
+        sc = x
+        with ops.side_branch(x) as br:
+            if self.conv_shortcut is not None:
+                sc = self.conv_shortcut(x)
         h = self.norm1(x, silu=True)
         h = self.conv1(h, bias2d=temb_proj, gn_stats=True)  # norm2's statistics from conv1's epilogue
         h = self.norm2(h, silu=True)
-        sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
+        br.join()
         return self.conv2(h, residual=sc, gn_stats=True)  # block output usually feeds the next GroupNorm
 
     def forward_cat(self, a, b, temb_proj=None):
@@ -357,12 +362,14 @@ class ResnetBlock2D(nn.Module):
                                     self.norm1.eps, silu=True)
         if hn is None:
             return self.forward(ops.cat_channels(a, b), temb_proj)
-        h = self.conv1(hn, bias2d=temb_proj, gn_stats=True)
-        h = self.norm2(h, silu=True)
         w = sc_conv.weight.view(sc_conv.out_channels, sc_conv.in_channels)
         ca = a.shape[-1]
-        sc = ops.gemm(a, w[:, :ca])
-        sc = ops.gemm(b, w[:, ca:], sc_conv.bias, residual=sc)
+        with ops.side_branch(a) as br:  # shortcut GEMMs overlap conv1 / norm2
+            sc = ops.gemm(a, w[:, :ca])
+            sc = ops.gemm(b, w[:, ca:], sc_conv.bias, residual=sc)
+        h = self.conv1(hn, bias2d=temb_proj, gn_stats=True)
+        h = self.norm2(h, silu=True)
+        br.join()
         return self.conv2(h, residual=sc, gn_stats=True)
 
 

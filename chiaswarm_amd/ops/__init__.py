@@ -132,6 +132,47 @@ def fold_layer_norm(w: torch.Tensor, bias, gamma: torch.Tensor, beta):
 LN_FUSE = os.environ.get("CSK_LN_FUSE", "1") == "1"
 
 
+# CSK_SIDE_STREAM=1: ResNet 1x1 shortcuts run on a side HIP stream forked from /
+# joined to the current one (inside a hipGraph capture: a parallel branch) to
+# overlap the memory-bound GroupNorm passes of the main path.  Off: the 14
+# fork/join pairs per UNet step cost more (cross-queue signals) than the overlap
+# gains -- 11.98 vs 11.76 ms/step (tools/abstep.py side0/side1,
+# profiles/unet_step_ab_side_r4g.txt)
+SIDE_STREAM = os.environ.get("CSK_SIDE_STREAM", "0") == "1"
+_SIDE: dict = {}
+
+
+class side_branch:
+    """``with side_branch(x) as br: ...`` runs the block on a side stream of
+    x's device (HIP path only; a no-op context elsewhere); ``br.join()`` makes
+    the current stream wait for it.  The block's outputs are only used after
+    the join, and the side stream waits for everything queued before the fork."""
+
+    def __init__(self, x: torch.Tensor):
+        self.on = SIDE_STREAM and use_hip(x)
+        self.dev = x.device
+
+    def __enter__(self):
+        if self.on:
+            self.main = torch.cuda.current_stream(self.dev)
+            self.side = _SIDE.get(self.dev)
+            if self.side is None:
+                self.side = _SIDE[self.dev] = torch.cuda.Stream(self.dev)
+            self.side.wait_stream(self.main)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
 def row_stats_wanted(x: torch.Tensor) -> bool:
     """Should a producer GEMM emit row statistics for a LayerNorm consumer?"""
     return LN_FUSE and use_hip(x)

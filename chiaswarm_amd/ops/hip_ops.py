@@ -89,6 +89,7 @@ sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
 sig("csk_set_gn_prologue_max", c_int)
 sig("csk_set_gn_lds", c_int)
+sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_gn_fine", c_int)
 sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
@@ -185,7 +186,7 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
             tile, split = (19 if N <= 1280 else 20), 1
         # mirror the library's own tile substitutions: the row-statistics slabs
         # (and the buffer sized for them below) follow the tile that actually runs
-        if tile in (25, 26, 31, 32, 33):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
+        if tile in (25, 26, 31, 32, 33, 34):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
             tile = 11
         elif ln is not None and 21 <= tile <= 24:  # persistent tiles: no per-tile LN statistics
             tile = {21: 11, 23: 18}.get(tile, 19)

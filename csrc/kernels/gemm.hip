@@ -413,6 +413,11 @@ static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
 }
 
 int g_gn_lds = 0;  // tools/abstep.py arms gnd0 / gnd1: GN statistics in the direct (0) or LDS (1) epilogue
+int g_sw_odd = 0;  // tools/abstep.py arms swodd0 / swodd1: 160-wide tiles on the direct (1) or LDS (0) epilogue; direct measured 0.11 ms/step slower
+CSK_API int csk_set_sw_odd(int v) {
+  g_sw_odd = v;
+  return 0;
+}
 CSK_API int csk_set_gn_lds(int v) {
   g_gn_lds = v;
   return 0;
@@ -422,6 +427,7 @@ template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
   a.gn_lds = g_gn_lds;
+  a.sw_odd = g_sw_odd;
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
@@ -448,8 +454,8 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   if (tile >= 31) {
     err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
     // fallback keeps the GN-statistics segment the host sized for: tile 33's
-    // 64-row band = tile 26's (128x160, two bands); 31 / 32's 128 = tile 11's
-    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, tile == 33 ? 26 : 11, ksplit, CONV, s);
+    // / 34's 64-row band = tile 26's (128x160, two bands); 31 / 32's 128 = tile 11's
+    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, tile >= 33 ? 26 : 11, ksplit, CONV, s);
   } else if (tile >= 11) {
     err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
   } else {

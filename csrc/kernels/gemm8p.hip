@@ -268,7 +268,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
 }
 
 // ---------------------------------------------------------------------------
-// 8-wave LDS-DMA RING kernel, 256 x BN tiles with BN = 160 (tile 33).
+// 8-wave LDS-DMA RING kernel, 256 x BN tiles with BN = 160 (tile 33) / 128 (34).
 //
 // Why: the UNet's 64x64 level (M = 32768 rows, N = 320 output channels) is
 // bound by the per-CU L2 -> LDS fill rate (~70 GB/s per CU at ~72 KB in
@@ -478,8 +478,8 @@ static int launch8p(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// tile 31: 256x256, tile 32: 256x128 (phased), tile 33: 256x160 (8-wave 3-stage
-// ring).  Returns hipErrorNotSupported when the shape needs a feature this
+// tile 31: 256x256, tile 32: 256x128 (phased), tiles 33 / 34: 256x160 / 256x128
+// (8-wave 3-stage ring).  Returns hipErrorNotSupported when the shape needs a feature this
 // kernel lacks (the caller falls back).
 int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s) {
   const int span = ksplit > 1 ? a.kchunk : a.K;
@@ -490,6 +490,7 @@ int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStr
   if (tile == 33 && a.act == ACT_GEGLU) return (int)hipErrorNotSupported;  // 80 columns per wave: no GEGLU pairing
   switch (tile) {
     case 33: return launch8r<160, 3>(a, ksplit, conv, s);
+    case 34: return launch8r<128, 3>(a, ksplit, conv, s);  // 64 x 64 per wave: direct row-layout epilogue
     case 31: return launch8p<256>(a, ksplit, conv, s);
     case 32: return launch8p<128>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;

@@ -55,6 +55,7 @@ struct GemmArgs {
   float* gn_part;
   int gn_seg;  // rows per gn_part segment (divides BM; 0 -> BM)
   int gn_lds;  // 1: GroupNorm statistics through the LDS epilogue even where the direct one can (A/B knob)
+  int sw_odd;  // 1: row-layout tiles with an odd fragment count (160 wide) use the direct epilogue (A/B knob)
   // fused LayerNorm of the INPUT rows (SURVEY K11 folded into K9/K10): the
   // weight was pre-multiplied by gamma (W' = W diag(gamma)), the bias holds
   // b + W beta, and the epilogue applies
@@ -221,7 +222,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       }
     return;
   }
-  if constexpr (SW && NT % 2 == 0) {
+  if constexpr (SW) {
     // ---- direct row-vector stores (no fp32 LDS staging) ----
     // Also covers the fused-LayerNorm consumer (ln_part: rstd * (acc - mean *
     // colsum) from the merged per-row statistics ln_row) and the row-statistics
@@ -233,7 +234,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     const bool rst = args.row_part != nullptr;
     const bool gnp = args.gn_part != nullptr;
     const int gseg = args.gn_seg > 0 ? args.gn_seg : BM;
-    const bool direct = (!gnp || (!args.gn_lds && !geglu && !rst && gseg % WTM == 0 && BM % gseg == 0)) && (!lnf || args.ln_row) &&
+    const bool direct = (NT % 2 == 0 || args.sw_odd) && (!gnp || (!args.gn_lds && !geglu && !rst && gseg % WTM == 0 && BM % gseg == 0)) && (!lnf || args.ln_row) &&
                         (!rst || !geglu) && (geglu_ok || !geglu) &&
                         (N % (geglu ? 16 : 8)) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
                         (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
@@ -316,7 +317,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         float* gred = reinterpret_cast<float*>(smem);
         if (gnp) epi_barrier<RAW>();  // main-loop LDS reads are done
 #pragma unroll
-        for (int f = 0; f < NT; f += 2) {
+        for (int f = 0; f + 1 < NT; f += 2) {
           // the 8 columns this lane stores for fragment pair f (same for every row block)
           const int col = ob + ((fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4);
           float bb[8], cs[8], gs[8], gq[8];
@@ -376,6 +377,82 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
               const int c = col - n0;
 #pragma unroll
               for (int r = 0; r < 8; ++r) {
+                gred[(wm * BN + c + r) * 2] = gs[r];
+                gred[(wm * BN + c + r) * 2 + 1] = gq[r];
+              }
+            }
+          }
+        }
+        if constexpr (NT % 2 == 1) {
+          // odd fragment count (80 columns per wave: the 160-wide tiles): the last
+          // fragment unpaired, 4 consecutive columns per lane, 8-byte stores
+          constexpr int f = NT - 1;
+          const int col = ob + f * 16 + fq * 4;
+          float bb[4], cs[4], gs[4], gq[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bb[r] = cs[r] = gs[r] = gq[r] = 0.f;
+          if (col < outN) {
+            if (args.bias) {
+              const uint2 u = *reinterpret_cast<const uint2*>(args.bias + col);
+              bb[0] = __uint_as_float(u.x << 16); bb[1] = __uint_as_float(u.x & 0xffff0000u);
+              bb[2] = __uint_as_float(u.y << 16); bb[3] = __uint_as_float(u.y & 0xffff0000u);
+            }
+            if (lnf) {
+              const float4 c0 = *reinterpret_cast<const float4*>(args.ln_colsum + col);
+              cs[0] = c0.x; cs[1] = c0.y; cs[2] = c0.z; cs[3] = c0.w;
+            }
+          }
+          auto add4 = [](float (&o)[4], const bf16_t* p) {
+            const uint2 u = *reinterpret_cast<const uint2*>(p);
+            o[0] += __uint_as_float(u.x << 16); o[1] += __uint_as_float(u.x & 0xffff0000u);
+            o[2] += __uint_as_float(u.y << 16); o[3] += __uint_as_float(u.y & 0xffff0000u);
+          };
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int m = m0 + wm * WTM + i * 16 + fr;
+            if (m >= M || col >= outN) continue;
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = lnr[i] * (acc[i][f][r] - lnm[i] * cs[r]) + bb[r];
+            if (args.bias2d) add4(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = apply_act(act, o[r]);
+            if (osc != 1.0f) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] *= osc;
+            }
+            if (args.res) add4(o, args.res + (size_t)m * args.ldr + col);
+            if (rst) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                rs[i] += o[r];
+                rq[i] = __builtin_fmaf(o[r], o[r], rq[i]);
+              }
+            }
+            if (gnp) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                gs[r] += o[r];
+                gq[r] = __builtin_fmaf(o[r], o[r], gq[r]);
+              }
+            }
+            const unsigned lo = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+            const unsigned hi = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+            *reinterpret_cast<uint2*>(args.C + (size_t)m * args.ldc + col) = make_uint2(lo, hi);
+          }
+          if (gnp) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+              for (int x = 1; x < 16; x <<= 1) {
+                gs[r] += __shfl_xor(gs[r], x);
+                gq[r] += __shfl_xor(gq[r], x);
+              }
+            }
+            if (fr == 0 && col < outN) {
+              const int c = col - n0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
                 gred[(wm * BN + c + r) * 2] = gs[r];
                 gred[(wm * BN + c + r) * 2 + 1] = gq[r];
               }

@@ -18,7 +18,11 @@ from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
 
 
 def apply_arm(arm):
-    if arm in ("gnd0", "gnd1"):  # GN statistics in the direct (gnd0) / LDS (gnd1) epilogue
+    if arm in ("side0", "side1"):  # ResNet shortcuts on a forked side stream (1) or inline (0)
+        ops.SIDE_STREAM = arm == "side1"
+    elif arm in ("swodd0", "swodd1"):  # 160-wide tiles: LDS (0) / direct row-layout (1) epilogue
+        _lib.call("csk_set_sw_odd", int(arm == "swodd1"))
+    elif arm in ("gnd0", "gnd1"):  # GN statistics in the direct (gnd0) / LDS (gnd1) epilogue
         _lib.call("csk_set_gn_lds", int(arm == "gnd1"))
     elif arm.startswith("gnwg"):
         hip_ops.GN_TARGET_WG = int(arm[4:])
