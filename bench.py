@@ -145,7 +145,8 @@ def main():
             "dtype": "bf16" if on_gpu else "fp32",
             "data": "synthetic prompts, random-init weights (no checkpoints offline)",
             "config": {
-                "model": "SD2.1 (stable-diffusion-2-1-base arch: UNet 865.9M + OpenCLIP-H 340.4M + VAE 83.7M)",
+                "model": ("SD2.1 (stable-diffusion-2-1-base arch: UNet 865.9M + OpenCLIP-H 340.4M + VAE 83.7M)"
+                          if args.family == "sd21" else f"{args.family} (not the headline config)"),
                 "global_batch": args.batch * world,
                 "seq_len": (args.res // 8) ** 2,
                 "parallelism": f"dp{world}",
