@@ -13,6 +13,8 @@ enum {
   ACT_ELU = 10,        // EnCodec
   ACT_GELU_TANH = 11,  // T5 "gelu_new"
   ACT_PROBE_NO_EPILOGUE = 99,  // profiling only: skip the epilogue (tilebench --probe)
+  ACT_PROBE_NO_A = 98,         // profiling only (2-stage conv tiles): skip the A DMA of kx != 0 taps
+                               // (wrong results; times a kx-halo A reuse, tilebench --probe-halo)
 };
 
 // pointwise epilogue activation (every act except GEGLU, which pairs columns)

@@ -145,10 +145,12 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     bf16_t* as = smem + buf * STAGE;
     bf16_t* bs = as + BM * BK;
     if constexpr (FAST) {
+      if (!(CONV && S == 2 && args.act == ACT_PROBE_NO_A && f_kx != 0)) {
 #pragma unroll
-      for (int i = 0; i < IA; ++i) {
-        const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
-        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+        for (int i = 0; i < IA; ++i) {
+          const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
+          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+        }
       }
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     }
   }
   __syncthreads();
-  if (args.act == ACT_PROBE_NO_EPILOGUE) {  // profiling probe: main loop only (tools/tilebench.py --probe)
+  if (args.act == ACT_PROBE_NO_EPILOGUE || args.act == ACT_PROBE_NO_A) {  // profiling probes: main loop only
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < MT; ++i)

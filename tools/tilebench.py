@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="conv|gemm")
     ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
+    ap.add_argument("--gn", action="store_true", help="convs also emitting fused GroupNorm statistics (64-row segments)")
+    ap.add_argument("--swodd", default="", help="comma list of csk_set_sw_odd values to A/B (160-wide tile epilogue)")
+    ap.add_argument("--probe-halo", action="store_true",
+                    help="convs also without epilogue (act 99) and without the kx != 0 A DMA (act 98, 2-stage tiles)")
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
@@ -45,11 +49,28 @@ def main():
             y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
             fl = 2.0 * B * H * W * Cout * 9 * Cin
 
-            def run(tile, split, x=x, wp=wp, y=y, B=B, H=H, W=W, Cin=Cin, Cout=Cout):
-                ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=dev) if split > 1 else None
-                _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1,
-                          H, W, 0, Cin, Cout, 0, 0, 1.0, 1, None, tile, split, _p(ws), _s())
-            jobs.append((f"conv {spec}", fl, run))
+            gpart = torch.empty(B * H * W // 64 * Cout * 2, dtype=torch.float32, device=dev)
+            variants = [(0, False, None)]
+            if a.gn:
+                variants.append((0, True, None))
+            for sw in [int(v) for v in a.swodd.split(",") if v]:
+                variants.append((0, a.gn, sw))
+            if a.probe_halo:
+                variants += [(99, False, None), (98, False, None)]
+            for act, gn, sw in variants:
+                def run(tile, split, x=x, wp=wp, y=y, B=B, H=H, W=W, Cin=Cin, Cout=Cout, act=act, gn=gn, sw=sw,
+                        gpart=gpart):
+                    if sw is not None:
+                        _lib.call("csk_set_sw_odd", sw)
+                    ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=dev) if split > 1 else None
+                    _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1,
+                              H, W, 0, Cin, Cout, 0, act, 1.0, 1, _p(gpart) if gn else None, tile, split, _p(ws),
+                              _s())
+                    if sw is not None:
+                        _lib.call("csk_set_sw_odd", 0)
+                tag = {0: "", 99: " noepi", 98: " noepi-noA"}[act] + (" gn" if gn else "") + \
+                    ("" if sw is None else f" swodd{sw}")
+                jobs.append((f"conv {spec}{tag}", fl, run))
     if a.only != "conv":
         for spec in GEMMS:
             geglu = spec.endswith(":geglu")
