@@ -25,7 +25,9 @@ _LOCK = threading.Lock()
 _LOAD_ERR: Exception | None = None
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libcsk.so")
+# CSK_LIB_PATH: load another build (same-box A/B of two builds: tools/gpu/lib_ab.sh; set
+# CSK_ALLOW_STALE=1 with it, the staleness stamp belongs to the in-tree build)
+LIB_PATH = os.environ.get("CSK_LIB_PATH") or os.path.join(LIB_DIR, "libcsk.so")
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

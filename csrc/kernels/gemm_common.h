@@ -13,9 +13,37 @@ enum {
   ACT_ELU = 10,        // EnCodec
   ACT_GELU_TANH = 11,  // T5 "gelu_new"
   ACT_PROBE_NO_EPILOGUE = 99,  // profiling only: skip the epilogue (tilebench --probe)
+  ACT_PROBE_NO_STORE = 97,     // profiling only: LDS-staged epilogue without its global stores
   ACT_PROBE_NO_A = 98,         // profiling only (2-stage conv tiles): skip the A DMA of kx != 0 taps
                                // (wrong results; times a kx-halo A reuse, tilebench --probe-halo)
 };
+
+// The libm-heavy activations (tanh, ELU's expm1, tanh-GELU: vocoder / EnCodec /
+// T5 paths only) live in ONE out-of-line function per code object.  Inlined
+// into every epilogue site they made the epilogue of each GEMM / conv
+// instantiation ~22 K instructions long (10 activations x 8 unrolled values x
+// every store path); the executed path then ran from a cold instruction cache
+// on every workgroup's single epilogue.  The UNet's activations (none / SiLU /
+// GELU / quick-GELU / ReLU / leaky ReLU) stay inline.
+struct Act8 {
+  float v[8];
+};
+static __device__ __attribute__((noinline)) Act8 act8_exotic(int act, Act8 x) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = x.v[j];
+    float r = v;
+    if (act == ACT_TANH) r = tanhf(v);
+    else if (act == ACT_ELU) r = v > 0.f ? v : expm1f(v);
+    else if (act == ACT_GELU_TANH) r = 0.5f * v * (1.f + tanhf(0.7978845608028654f * (v + 0.044715f * v * v * v)));
+    x.v[j] = r;
+  }
+  return x;
+}
+
+__device__ __forceinline__ bool act_exotic(int act) {
+  return act == ACT_TANH || act == ACT_ELU || act == ACT_GELU_TANH;
+}
 
 // pointwise epilogue activation (every act except GEGLU, which pairs columns)
 __device__ __forceinline__ float apply_act(int act, float v) {
@@ -25,13 +53,16 @@ __device__ __forceinline__ float apply_act(int act, float v) {
     case ACT_QGELU: return qgelu_f(v);
     case ACT_LRELU: return v > 0.f ? v : 0.2f * v;
     case ACT_LRELU_01: return v > 0.f ? v : 0.1f * v;
-    case ACT_TANH: return tanhf(v);
     case ACT_RELU: return fmaxf(v, 0.f);
     case ACT_LRELU_001: return v > 0.f ? v : 0.01f * v;
-    case ACT_ELU: return v > 0.f ? v : expm1f(v);
-    case ACT_GELU_TANH: return 0.5f * v * (1.f + tanhf(0.7978845608028654f * (v + 0.044715f * v * v * v)));
-    default: return v;
+    default: break;
   }
+  if (act_exotic(act)) {
+    Act8 x{};
+    x.v[0] = v;
+    return act8_exotic(act, x).v[0];
+  }
+  return v;
 }
 
 struct GemmArgs {
@@ -85,10 +116,11 @@ constexpr int epi_passes() {
   return (BM > 128 || BN == 160) ? WM : 1;
 }
 
-// epilogue LDS (bf16-element units): fp32 [BM / EP][BN + 4] band + [BM][2] row LN stats
+// epilogue LDS (bf16-element units): fp32 [BM / EP][BN + 4] band + [BM][2] row LN
+// stats + [BM / EP / 16][BN][2] GroupNorm row-slice moments (gn_column_pass)
 template <int BM, int BN, int EP = 1>
 constexpr int epi_smem_elems() {
-  return BM / EP * (BN + 4) * 2 + 4 * BM;
+  return BM / EP * (BN + 4) * 2 + 4 * BM + (BM / EP / 16) * BN * 4;
 }
 
 #define BK 64
@@ -138,11 +170,19 @@ __device__ __forceinline__ void act8(int act, float (&f)[8]) {
     CSK_ACT8(ACT_QGELU)
     CSK_ACT8(ACT_LRELU)
     CSK_ACT8(ACT_LRELU_01)
-    CSK_ACT8(ACT_TANH)
     CSK_ACT8(ACT_RELU)
     CSK_ACT8(ACT_LRELU_001)
-    CSK_ACT8(ACT_ELU)
-    CSK_ACT8(ACT_GELU_TANH)
+    case ACT_TANH:
+    case ACT_ELU:
+    case ACT_GELU_TANH: {
+      Act8 x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x.v[j] = f[j];
+      x = act8_exotic(act, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = x.v[j];
+      break;
+    }
     default: break;
   }
 #undef CSK_ACT8
@@ -704,7 +744,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] += rf[j];
         }
-        *reinterpret_cast<uint4*>(cp) = pack8(f);
+        if (args.act != ACT_PROBE_NO_STORE) *reinterpret_cast<uint4*>(cp) = pack8(f);
         if (args.gn_part) {
           *reinterpret_cast<float4*>(crow) = make_float4(f[0], f[1], f[2], f[3]);
           *reinterpret_cast<float4*>(crow + 4) = make_float4(f[4], f[5], f[6], f[7]);
@@ -746,23 +786,45 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   }
   if (args.gn_part) {
     // column pass: (mean, M2) of each output channel over row segments of
-    // gn_seg rows (a divisor of BM chosen by the host, _gn_seg): thread =
-    // (segment, channel) with consecutive channels in consecutive lanes
-    // (conflict-free LDS reads); two-pass in LDS: exact, no E[x^2]-E[x]^2
-    // cancellation.  The consumer GroupNorm merges the segments.
+    // gn_seg rows (a divisor of BM chosen by the host, _gn_seg).  Each segment
+    // is cut into slices of <= 16 rows: thread = (segment, slice, channel), with
+    // consecutive channels in consecutive lanes (conflict-free LDS reads), loads
+    // its slice into registers at once (16 independent LDS reads in flight, not
+    // 2 x seg dependent ones: that chain was 3-10 us per conv) and takes the
+    // two-pass moments in registers (exact, no E[x^2]-E[x]^2 cancellation); the
+    // slices are then Chan-merged.  The consumer GroupNorm merges the segments.
     const int seg = args.gn_seg > 0 ? args.gn_seg : PR;
+    const int qrows = seg < 16 ? seg : 16, qs = seg / qrows, nsq = PR / seg;
+    float* qpart = lnst + 2 * BM;  // [nsq * qs][BN][2]
     epi_barrier<RAW>();
-    for (int t = tid; t < BN * (PR / seg); t += NTHR) {
+    for (int t = tid; t < BN * nsq * qs; t += NTHR) {
+      const int c = t % BN, sl = t / BN;  // slice sl = sq * qs + qq
+      const int r0 = sl * qrows;
+      float v[16], sm = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        v[r] = r < qrows ? cs[(r0 + r) * LDC_S + c] : 0.f;
+        sm += v[r];
+      }
+      const float mean = sm / (float)qrows;
+      float m2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = r < qrows ? v[r] - mean : 0.f;
+        m2 = __builtin_fmaf(d, d, m2);
+      }
+      *reinterpret_cast<float2*>(qpart + ((size_t)sl * BN + c) * 2) = make_float2(mean, m2);
+    }
+    epi_barrier<RAW>();
+    for (int t = tid; t < BN * nsq; t += NTHR) {
       const int c = t % BN, sq = t / BN;
       const int n = n0 + c, r0 = sq * seg;
       if (n >= N || m0 + pr0 + r0 >= M) continue;
-      float sm = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < seg; ++r) sm += cs[(r0 + r) * LDC_S + c];
-      const float mean = sm / (float)seg;
-      float m2 = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < seg; ++r) { const float d = cs[(r0 + r) * LDC_S + c] - mean; m2 += d * d; }
+      float cnt = 0.f, mean = 0.f, m2 = 0.f;
+      for (int qq = 0; qq < qs; ++qq) {
+        const float2 p = *reinterpret_cast<const float2*>(qpart + ((size_t)(sq * qs + qq) * BN + c) * 2);
+        chan_combine(cnt, mean, m2, (float)qrows, p.x, p.y);
+      }
       *reinterpret_cast<float2*>(args.gn_part + ((size_t)((m0 + pr0 + r0) / seg) * N + n) * 2) =
           make_float2(mean, m2);
     }

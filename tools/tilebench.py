@@ -56,7 +56,7 @@ def main():
             for sw in [int(v) for v in a.swodd.split(",") if v]:
                 variants.append((0, a.gn, sw))
             if a.probe_halo:
-                variants += [(99, False, None), (98, False, None)]
+                variants += [(97, False, None), (99, False, None), (98, False, None)]
             for act, gn, sw in variants:
                 def run(tile, split, x=x, wp=wp, y=y, B=B, H=H, W=W, Cin=Cin, Cout=Cout, act=act, gn=gn, sw=sw,
                         gpart=gpart):
@@ -68,7 +68,7 @@ def main():
                               _s())
                     if sw is not None:
                         _lib.call("csk_set_sw_odd", 0)
-                tag = {0: "", 99: " noepi", 98: " noepi-noA"}[act] + (" gn" if gn else "") + \
+                tag = {0: "", 97: " nostore", 99: " noepi", 98: " noepi-noA"}[act] + (" gn" if gn else "") + \
                     ("" if sw is None else f" swodd{sw}")
                 jobs.append((f"conv {spec}{tag}", fl, run))
     if a.only != "conv":
