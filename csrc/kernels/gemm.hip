@@ -485,9 +485,19 @@ __global__ void ln_rowstats_kernel(const float* __restrict__ part, float* __rest
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    const float2 st = *reinterpret_cast<const float2*>(part + ((size_t)p * M + m) * 2);
-    chan_combine(n, mean, m2, (float)min(pcols, K - p * pcols), st.x, st.y);
+  // up to 16 slabs (K / producer BN: 2-10 in the UNet) loaded in one round trip,
+  // then merged; a load-combine loop serialised one memory latency per slab
+  constexpr int CAP = 16;
+  float2 st[CAP];
+#pragma unroll
+  for (int p = 0; p < CAP; ++p)
+    st[p] = p < nparts ? *reinterpret_cast<const float2*>(part + ((size_t)p * M + m) * 2) : make_float2(0.f, 0.f);
+#pragma unroll
+  for (int p = 0; p < CAP; ++p)
+    if (p < nparts) chan_combine(n, mean, m2, (float)min(pcols, K - p * pcols), st[p].x, st[p].y);
+  for (int p = CAP; p < nparts; ++p) {
+    const float2 s2 = *reinterpret_cast<const float2*>(part + ((size_t)p * M + m) * 2);
+    chan_combine(n, mean, m2, (float)min(pcols, K - p * pcols), s2.x, s2.y);
   }
   *reinterpret_cast<float2*>(out + (size_t)m * 2) = make_float2(mean, rsqrtf(m2 / fmaxf(n, 1.f) + eps));
 }

@@ -11,6 +11,6 @@ for arm in A B A B; do
 done
 for arm in A B; do
   if [ $arm = A ]; then export CSK_LIB_PATH=$OLD CSK_ALLOW_STALE=1; else unset CSK_LIB_PATH CSK_ALLOW_STALE; fi
-  timeout -k 10 200 python tools/tilebench.py --tiles 26,11 --only conv --gn --rounds 3 > gpurun_out/libab_${TAG}_tb_$arm.txt 2>&1 || exit 1
+  timeout -k 10 200 python tools/tilebench.py --tiles 26 --only conv --gn --rounds 2 > gpurun_out/libab_${TAG}_tb_$arm.txt 2>&1 || exit 1
 done
 paste <(grep -v amdgpu gpurun_out/libab_${TAG}_tb_A.txt | cut -c1-75) <(grep -v amdgpu gpurun_out/libab_${TAG}_tb_B.txt | cut -c30-75) | head -20
