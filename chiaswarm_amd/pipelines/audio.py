@@ -111,6 +111,8 @@ class AudioLDM:
         else:
             x = latents.to(self.device).float()
         t_dev = torch.zeros(1, device=self.device, dtype=torch.float32)
+        if self.device.type == "cuda":  # phase timings are GPU-complete, not launch time
+            torch.cuda.synchronize(self.device)
         t1 = time.perf_counter()
         while sched.step_index < sched.n:
             xi = (x * sched.current_scale()).to(self.dtype)
@@ -129,6 +131,8 @@ class AudioLDM:
                 else:
                     e_g = e.float()
                 x = sched.step(e_g, x, generator)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         t2 = time.perf_counter()
         mel = self.vae.decode((x / self.vae.cfg.scaling_factor).to(self.dtype))  # [B, T, 64, 1]
         wav = self.vocoder(mel[..., 0])  # [B, T * hop]
