@@ -89,11 +89,23 @@ class EncoderPool:
                 pass
         self._pool = cf.ThreadPoolExecutor(max_workers=max(1, processes or 2))
 
+    def _submit(self, fn, *args) -> cf.Future:
+        try:
+            return self._pool.submit(fn, *args)
+        except cf.process.BrokenProcessPool:
+            # a worker died (OOM kill, crash): the process pool refuses all further
+            # work and this process may not spawn replacements once the GPU is up,
+            # so the pool degrades to encoder threads instead of failing every job
+            self._pool.shutdown(wait=False)
+            self._pool = cf.ThreadPoolExecutor(max_workers=2)
+            self.kind = "thread"
+            return self._pool.submit(fn, *args)
+
     def submit(self, arrays, content_type: str = "image/jpeg", output_list=("primary",)) -> cf.Future:
-        return self._pool.submit(encode_arrays, list(arrays), content_type, tuple(output_list))
+        return self._submit(encode_arrays, list(arrays), content_type, tuple(output_list))
 
     def submit_artifact(self, arrays, content_type: str = "image/jpeg") -> cf.Future:
-        return self._pool.submit(encode_artifact, list(arrays), content_type)
+        return self._submit(encode_artifact, list(arrays), content_type)
 
     def shutdown(self):
         self._pool.shutdown(wait=True)

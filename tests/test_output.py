@@ -127,3 +127,33 @@ def test_thumbnail_from_image_matches_decoded_bytes():
     assert a.shape == b.shape == (100, 100, 3)
     assert np.abs(a - b).mean() < 3.0
     assert img.size == (1024, 1024)  # the caller's image is not resized in place
+
+
+def test_encoder_pool_survives_a_dead_worker():
+    """A killed encoder process breaks a ProcessPoolExecutor for good; the pool
+    degrades to encoder threads and later jobs still encode."""
+    import os
+    import signal
+    import time
+
+    import numpy as np
+
+    from chiaswarm_amd.output.encoder import EncoderPool
+
+    pool = EncoderPool(1)
+    assert pool.kind == "process"
+    arrs = [np.zeros((32, 32, 3), dtype=np.uint8)]
+    try:
+        first = pool.submit(arrs, "image/png").result(timeout=60)
+        for pid in list(pool._pool._processes):
+            os.kill(pid, signal.SIGKILL)
+        time.sleep(1.0)
+        try:
+            pool.submit(arrs, "image/png").result(timeout=60)  # may be the one that hits the broken pool
+        except Exception:
+            pass
+        again = pool.submit(arrs, "image/png").result(timeout=60)
+        assert pool.kind == "thread"
+        assert again["primary"]["blob"] == first["primary"]["blob"]
+    finally:
+        pool.shutdown()
