@@ -86,7 +86,7 @@ def main():
 
     def job(i):
         g = torch.Generator(device=device).manual_seed(1000 * rank + i)
-        sched = get_scheduler("DPMSolverMultistepScheduler", prediction_type=pipe.family.prediction_type)
+        sched = get_scheduler("DPMSolverMultistepScheduler", **pipe.family.scheduler_kwargs())
         out = pipe(prompt=prompts[i % len(prompts)], negative_prompt="blurry, low quality",
                    num_inference_steps=args.denoise_steps, guidance_scale=args.guidance,
                    num_images_per_prompt=args.batch, height=args.res, width=args.res,

@@ -20,6 +20,11 @@ from .unet import SD15, UNetConfig, _Block
 from .. import ops
 
 
+def _spatial_mean(x):
+    """NHWC [B, H, W, C] -> [B, 1, 1, C] (fp32 accumulation)."""
+    return x.float().mean(dim=(1, 2), keepdim=True).to(x.dtype).contiguous()
+
+
 class CondEmbedding(nn.Module):
     def __init__(self, out_ch=320, channels=(16, 32, 96, 256), cin=3):
         super().__init__()
@@ -39,9 +44,17 @@ class CondEmbedding(nn.Module):
 
 
 class ControlNetModel(Prepared):
-    def __init__(self, cfg: UNetConfig = SD15):
+    """``cond_channels`` / ``cond_in`` / ``bgr`` / ``global_pool``: the
+    checkpoint config's ``conditioning_embedding_out_channels``,
+    ``conditioning_channels``, ``controlnet_conditioning_channel_order`` and
+    ``global_pool_conditions`` (shuffle ControlNets average every residual over
+    the image, diffusers ControlNetModel.forward)."""
+
+    def __init__(self, cfg: UNetConfig = SD15, cond_channels=(16, 32, 96, 256), cond_in: int = 3,
+                 bgr: bool = False, global_pool: bool = False):
         super().__init__()
         self.cfg = cfg
+        self.bgr, self.global_pool = bgr, global_pool
         ch = list(cfg.block_out_channels)
         nb = len(ch)
         heads = cfg.per_block(cfg.num_heads, nb)
@@ -50,7 +63,7 @@ class ControlNetModel(Prepared):
         g, eps = cfg.norm_num_groups, cfg.norm_eps
         self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, padding=1)
         self.time_embedding = TimestepEmbedding(ch[0], temb_dim)
-        self.controlnet_cond_embedding = CondEmbedding(ch[0])
+        self.controlnet_cond_embedding = CondEmbedding(ch[0], tuple(cond_channels), cond_in)
         self.down_blocks = nn.ModuleList()
         zero = [Conv2d(ch[0], ch[0], 1, padding=0)]
         cout = ch[0]
@@ -91,6 +104,8 @@ class ControlNetModel(Prepared):
 
     def embed_cond(self, cond):
         """cond: NHWC [B, H, W, 3] in [0, 1] -> [B, H/8, W/8, C0] (constant per job)."""
+        if self.bgr:
+            cond = cond.flip(-1)
         return self.controlnet_cond_embedding(cond.to(self.conv_in.weight.dtype))
 
     def features(self, sample, timestep, cond_emb, cross_kv=None, ctx=None):
@@ -101,15 +116,23 @@ class ControlNetModel(Prepared):
     def merge_skip(self, i, feat, unet_skip, scale: float = 1.0):
         """UNet skip i + scale * zero_conv_i(feat) in ONE GEMM: the residual add
         and the conditioning scale ride in the 1x1 conv's epilogue (which also
-        emits the GroupNorm statistics the consuming up-block ResNet needs)."""
+        emits the GroupNorm statistics the consuming up-block ResNet needs).
+        Global pooling: mean(zero_conv(f)) = zero_conv(mean(f)) (a 1x1 conv is
+        affine), so the [B, 1, 1, C] residual broadcasts over the skip."""
+        if self.global_pool:
+            return unet_skip + scale * self.controlnet_down_blocks[i](_spatial_mean(feat)).to(unet_skip.dtype)
         return self.controlnet_down_blocks[i](feat, residual=unet_skip, out_scale=scale, gn_stats=True)
 
     def merge_mid(self, feat, unet_h, scale: float = 1.0):
+        if self.global_pool:
+            return unet_h + scale * self.controlnet_mid_block(_spatial_mean(feat)).to(unet_h.dtype)
         return self.controlnet_mid_block(feat, residual=unet_h, out_scale=scale, gn_stats=True)
 
     def forward(self, sample, timestep, cond_emb, cross_kv=None, ctx=None, scale: float = 1.0):
         """Residual tensors (diffusers ControlNetModel output: down residuals, mid residual)."""
         skips, h = self._encode(sample, timestep, cond_emb, cross_kv, ctx)
+        if self.global_pool:
+            skips, h = [_spatial_mean(s) for s in skips], _spatial_mean(h)
         downs = [zc(s) for zc, s in zip(self.controlnet_down_blocks, skips)]
         mid = self.controlnet_mid_block(h)
         if scale != 1.0:

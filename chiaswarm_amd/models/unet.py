@@ -66,6 +66,7 @@ SDXL = UNetConfig(
     cross_attention_dim=2048, addition_embed_type="text_time", sample_size=128)
 PIX2PIX = dataclasses.replace(SD15, in_channels=8)
 INPAINT_SD2 = dataclasses.replace(SD21, in_channels=9)
+INPAINT_SD15 = dataclasses.replace(SD15, in_channels=9)
 # tiny config for CPU plumbing tests (same topology, small widths)
 TINY = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
                   down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
@@ -98,7 +99,7 @@ X4_UPSCALER = UNetConfig(
 TINY_X4 = dataclasses.replace(TINY, in_channels=7, num_class_embeds=1000)
 
 CONFIGS = {"sd15": SD15, "sd21": SD21, "sd21-v": SD21_V, "sdxl": SDXL, "pix2pix": PIX2PIX,
-           "sd2-inpaint": INPAINT_SD2, "tiny": TINY}
+           "sd2-inpaint": INPAINT_SD2, "sd15-inpaint": INPAINT_SD15, "tiny": TINY}
 
 
 class _Block(nn.Module):

@@ -158,11 +158,18 @@ def load_sd_weights(pipe, weights_dir: str) -> bool:
     parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)]
     for i, te in enumerate(pipe.text_encoders):
         parts.append(("text_encoder" if i == 0 else f"text_encoder_{i + 1}", te, None))
+    present = [sub for sub, _, _ in parts if glob.glob(os.path.join(weights_dir, sub, "*.safetensors"))]
+    if not present:
+        return False
+    absent = [sub for sub, _, _ in parts if sub not in present]
+    if absent:
+        # a real UNet beside a random-init VAE / text encoder would produce
+        # plausible-looking garbage while reporting the checkpoint as loaded
+        raise CheckpointMismatch(f"{weights_dir}: no safetensors weights for {absent} (present: {present}); "
+                                 "refusing a partial load")
     reports = {}
     for sub, mod, ren in parts:
         src = os.path.join(weights_dir, sub)
-        if not os.path.isdir(src) or not glob.glob(os.path.join(src, "*.safetensors")):
-            continue
         fp = packed_cache.fingerprint(src, mod)
         path = packed_cache.cache_path(key, "main", sub)
         if use_cache and packed_cache.load(mod, path, fp):

@@ -86,6 +86,10 @@ sig("csk_add", c_void_p, c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_sched_step", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
     c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p)
 sig("csk_vae_post", c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_loop_prologue", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p)
+sig("csk_sched_loop", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64,
+    c_int, c_void_p)
+LOOP_COEF_STRIDE = 12  # elementwise.hip: {p, q, A, B, C, D, s_next, g, g2, -, -, -} per step
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
 sig("csk_set_gn_prologue_max", c_int)
 sig("csk_set_gn_lds", c_int)
@@ -464,6 +468,44 @@ def sched_step(e, x, prev_x0, c, guidance, noise):
               float(c.p), float(c.q), float(c.A), float(c.B), float(c.C), float(c.D),
               float(guidance or 0.0), int(cfg), _s())
     return xn, x0
+
+
+def loop_prologue(counter, cur, t_tab, t_out):
+    """Head of a device-resident sampler step: cur = counter++, t_out = t_tab[cur]
+    (int32 [1] counter / cur, fp32 table, fp32 [1] output; 1-thread kernel)."""
+    if counter.dtype != torch.int32 or cur.dtype != torch.int32 or t_tab.dtype != torch.float32 \
+            or t_out.dtype != torch.float32 or t_tab.numel() < 1:
+        raise TypeError("loop_prologue: int32 counter/cur, fp32 t_tab/t_out")
+    _lib.call("csk_loop_prologue", _p(counter), _p(cur), _p(t_tab), _p(t_out), t_tab.numel(), _s())
+
+
+def sched_loop(e, x, x0prev, noise_tab, cur, coef, x_in, mode):
+    """Tail of a device-resident sampler step (elementwise.hip sched_loop_kernel):
+    CFG combine (mode 0 none, 1 [u, c], 2 pix2pix [c, i, u]) + the linear update
+    with the coefficients of step ``cur`` from the device table ``coef``
+    [n, LOOP_COEF_STRIDE] (guidance scales in the row),
+    x / x0prev updated in place, the next UNet input written into ``x_in``
+    ([nrep * B, H, W, Cin] bf16, channels 0..3 of every replica)."""
+    _bf16(e, "sched_loop.e")
+    _bf16(x_in, "sched_loop.x_in")
+    nrep = mode + 1
+    B, H, W, C = x.shape
+    if C != 4 or x.dtype != torch.float32 or not x.is_contiguous() or not x0prev.is_contiguous() \
+            or x0prev.shape != x.shape or x0prev.dtype != torch.float32:
+        raise ValueError("sched_loop: x / x0prev must be contiguous fp32 [B, H, W, 4]")
+    if e.numel() != nrep * x.numel() or not e.is_contiguous():
+        raise ValueError(f"sched_loop: model output {tuple(e.shape)} vs {nrep} x {tuple(x.shape)}")
+    if x_in.dim() != 4 or x_in.shape[0] != nrep * B or x_in.shape[1:3] != (H, W) or x_in.shape[3] < 4 \
+            or not x_in.is_contiguous():
+        raise ValueError(f"sched_loop: x_in {tuple(x_in.shape)} for {nrep} x {tuple(x.shape)}")
+    if coef.dtype != torch.float32 or coef.dim() != 2 or coef.shape[1] != LOOP_COEF_STRIDE \
+            or cur.dtype != torch.int32:
+        raise ValueError("sched_loop: coef must be fp32 [n, LOOP_COEF_STRIDE], cur int32")
+    if noise_tab is not None and (noise_tab.dtype != torch.float32 or
+                                  noise_tab.numel() != coef.shape[0] * x.numel()):
+        raise ValueError("sched_loop: noise table must be fp32 [n, B, H, W, 4]")
+    _lib.call("csk_sched_loop", _p(e), _p(x), _p(x0prev), _p(noise_tab), _p(cur), _p(coef), _p(x_in),
+              x_in.shape[3], nrep, B * H * W, mode, _s())
 
 
 def vae_postprocess(img):

@@ -28,7 +28,13 @@ def env_rank():
 
 
 def init_distributed(backend: str | None = None, timeout_s: int = 600):
-    """Initialise the process group from torchrun env vars (one rank per GPU)."""
+    """Initialise the process group from torchrun env vars (one rank per GPU).
+
+    With ``SDAAS_STORE_PORT`` set (the worker's GPU children) the rendezvous is
+    the TCPStore the SUPERVISOR hosts (runtime/worker.py), namespaced by the
+    group generation ``SDAAS_GROUP_GEN``: the store outlives any GPU child, so
+    a crashed rank 0 takes no surviving rank's store with it, and a re-formed
+    group (a new generation) never reads a stale key of the old one."""
     rank, local_rank, world = env_rank()
     if world <= 1:
         return rank, local_rank, world
@@ -42,9 +48,34 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600):
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", local_rank)
-    dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    timeout = datetime.timedelta(seconds=timeout_s)
+    if os.environ.get("SDAAS_STORE_PORT"):
+        kw["store"] = group_store(timeout)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kw)
     return rank, local_rank, world
+
+
+def group_store(timeout=datetime.timedelta(seconds=600)):
+    """Client of the supervisor-hosted TCPStore, prefixed by the group generation."""
+    base = dist.TCPStore(os.environ.get("SDAAS_STORE_HOST", "127.0.0.1"), int(os.environ["SDAAS_STORE_PORT"]),
+                         is_master=False, timeout=timeout)
+    return dist.PrefixStore(f"gen{os.environ.get('SDAAS_GROUP_GEN', '0')}/", base)
+
+
+def leave_group():
+    """Drop this process's process group without waiting on its peers (a dead
+    peer would make a graceful destroy block): abort the communicators."""
+    if not dist.is_initialized():
+        return
+    try:
+        from torch.distributed.distributed_c10d import _abort_process_group
+
+        _abort_process_group()
+    except Exception:  # pragma: no cover - older torch / already torn down
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
 
 
 def is_dist():
@@ -169,3 +200,45 @@ def module_checksum(module: torch.nn.Module) -> float:
     for t in _state_tensors(module):
         s += float(t.float().sum().item())
     return s
+
+
+def send_tensor(x: torch.Tensor, dst: int):
+    """Point-to-point transfer (RCCL over xGMI between GPU children; gloo on CPU)."""
+    dist.send(x.contiguous(), dst)
+
+
+def recv_tensor(shape, dtype, src: int, device) -> torch.Tensor:
+    out = torch.empty(tuple(shape), dtype=dtype, device=device)
+    dist.recv(out, src)
+    return out
+
+
+def group_device():
+    """Where this rank's collective tensors live: its GPU under RCCL, host under gloo."""
+    if is_dist() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+# -- split-job image transfer (runtime/worker.py splits a multi-image job over
+#    idle GPUs; every part's uint8 images go to the leader rank over the group)
+def send_images(images: torch.Tensor | None, dst: int, nsfw: bool = False):
+    """Helper side: header [n, H, W, C, nsfw] then the uint8 NHWC payload; ``None``
+    sends an error header (n = -1) so the leader never waits on a failed part."""
+    dev = group_device()
+    if images is None:
+        send_tensor(torch.tensor([-1, 0, 0, 0, 0], dtype=torch.int64, device=dev), dst)
+        return
+    n, h, w, c = images.shape
+    send_tensor(torch.tensor([n, h, w, c, int(bool(nsfw))], dtype=torch.int64, device=dev), dst)
+    send_tensor(images.to(dev, torch.uint8), dst)
+
+
+def recv_images(src: int):
+    """Leader side: (uint8 [n, H, W, C] on the group device, nsfw) or (None, False)
+    when the part failed."""
+    dev = group_device()
+    hdr = recv_tensor((5,), torch.int64, src, dev).tolist()
+    if hdr[0] < 0:
+        return None, False
+    return recv_tensor(tuple(hdr[:4]), torch.uint8, src, dev), bool(hdr[4])

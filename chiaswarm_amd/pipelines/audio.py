@@ -43,11 +43,27 @@ class AudioLDM:
     def __init__(self, device="cpu", tiny=False, seed=0, weights_dir=None):
         self.device = torch.device(device)
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        tcfg, ucfg = (TINY_CLAP, TINY_AUDIOLDM) if tiny else (CLAP_TEXT, AUDIOLDM)
+        vcfg, hcfg = (TINY_AUDIO_VAE, TINY_HIFIGAN) if tiny else (AUDIOLDM_VAE, AUDIOLDM_HIFIGAN)
+        self.sched_config = dict(AUDIOLDM_SCHED)
+        if weights_dir:
+            # every size (cvssp/audioldm-s/-m/-l ...) from its own config files
+            # (the reference: AudioLDMPipeline.from_pretrained, swarm/audio/audioldm.py:19-20)
+            from ..models import hf_config as hc
+
+            c = {s: hc.component_config(weights_dir, s) for s in ("text_encoder", "unet", "vae", "vocoder")}
+            tcfg = hc.clap_text_config(c["text_encoder"]) if c["text_encoder"] else tcfg
+            ucfg = hc.unet_config(c["unet"]) if c["unet"] else ucfg
+            vcfg = hc.vae_config(c["vae"]) if c["vae"] else vcfg
+            hcfg = hc.hifigan_config(c["vocoder"]) if c["vocoder"] else hcfg
+            sk = hc.scheduler_kwargs(hc.component_config(weights_dir, "scheduler", "scheduler_config.json"))
+            if sk:
+                self.sched_config = dict(sk, use_karras_sigmas=False)
         with torch.device(self.device):
-            self.text_encoder = ClapTextEncoder(TINY_CLAP if tiny else CLAP_TEXT).to(self.dtype)
-            self.unet = UNet2DConditionModel(TINY_AUDIOLDM if tiny else AUDIOLDM).to(self.dtype)
-            self.vae = AutoencoderKL(TINY_AUDIO_VAE if tiny else AUDIOLDM_VAE, with_encoder=False).to(self.dtype)
-            self.vocoder = HifiGan(TINY_HIFIGAN if tiny else AUDIOLDM_HIFIGAN).to(self.dtype)
+            self.text_encoder = ClapTextEncoder(tcfg).to(self.dtype)
+            self.unet = UNet2DConditionModel(ucfg).to(self.dtype)
+            self.vae = AutoencoderKL(vcfg, with_encoder=False).to(self.dtype)
+            self.vocoder = HifiGan(hcfg).to(self.dtype)
         mods = [self.text_encoder, self.unet, self.vae, self.vocoder]
         for i, m in enumerate(mods):
             m.eval().requires_grad_(False)
@@ -67,10 +83,17 @@ class AudioLDM:
     def _load(self, d) -> bool:
         from ..models.weights import _VAE_RENAMES, load_component
 
-        reps = [load_component(mod, d, sub, ren)
-                for sub, mod, ren in (("text_encoder", self.text_encoder, HF_RENAMES), ("unet", self.unet, None),
-                                      ("vae", self.vae, _VAE_RENAMES), ("vocoder", self.vocoder, None))]
-        return any(r is not None for r in reps)
+        from ..models.weights import CheckpointMismatch, tokenizer_dir
+
+        subs = (("text_encoder", self.text_encoder, HF_RENAMES), ("unet", self.unet, None),
+                ("vae", self.vae, _VAE_RENAMES), ("vocoder", self.vocoder, None))
+        reps = {sub: load_component(mod, d, sub, ren) for sub, mod, ren in subs}
+        got = [k for k, r in reps.items() if r is not None]
+        if got and len(got) != len(subs):
+            raise CheckpointMismatch(f"{d}: only {got} of text_encoder / unet / vae / vocoder have weights")
+        if got and tokenizer_dir(d) is None:
+            raise CheckpointMismatch(f"{d}: tokenizer files missing beside real text-encoder weights")
+        return bool(got)
 
     # ------------------------------------------------------------------
     def _unet_fn(self, x, t, class_labels):
@@ -101,7 +124,7 @@ class AudioLDM:
         negs = [negs[i % len(negs)] for i in range(b)]
         emb = self.text_encoder(self.tokenizer((negs + prompts) if cfg else prompts)).to(self.dtype)
 
-        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **AUDIOLDM_SCHED)
+        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **self.sched_config)
         sched.set_timesteps(num_inference_steps)
         lh, lw = height // self.vae_scale, voc.model_in_dim // self.vae_scale
         c = self.unet.cfg.in_channels
@@ -156,10 +179,10 @@ def load_audioldm(model_name: str, device: str) -> AudioLDM:
                                         seed=stable_seed(model_name)))
 
 
-def _scheduler_for(scheduler_type):
+def _scheduler_for(scheduler_type, pipe):
     if scheduler_type is None:
         return None
-    return get_scheduler(scheduler_type, **AUDIOLDM_SCHED)
+    return get_scheduler(scheduler_type, **pipe.sched_config)
 
 
 def txt2audio_diffusion_callback(device_identifier, model_name, **kwargs):
@@ -174,7 +197,7 @@ def txt2audio_diffusion_callback(device_identifier, model_name, **kwargs):
     gen = None
     if seed is not None:
         gen = torch.Generator(device=pipe.device).manual_seed(int(seed))
-    audio = pipe(scheduler=_scheduler_for(scheduler_type), generator=kwargs.pop("generator", gen), **kwargs)
+    audio = pipe(scheduler=_scheduler_for(scheduler_type, pipe), generator=kwargs.pop("generator", gen), **kwargs)
     data, ctype = encode_audio(audio[0], pipe.vocoder.cfg.sampling_rate, content_type)
     results = {"primary": make_result(data, None, ctype)}
     return results, dict(pipe.config)

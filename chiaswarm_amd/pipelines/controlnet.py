@@ -83,15 +83,26 @@ class ControlNetRunner:
 
 def load_controlnet(name: str, pipe, device_identifier: str, revision: str = "main") -> ControlNetRunner:
     def make():
-        cfg = pipe.unet.cfg
-        with torch.device(device_identifier):
-            m = ControlNetModel(cfg).to(pipe.dtype).eval().requires_grad_(False)
-        init_random_fast_(m, seed=stable_seed(name))
         w = find_weights(name, revision)
-        if w:
-            from ..models.weights import _read_dir, load_into
+        cfg, kw = pipe.unet.cfg, {}
+        from ..models.hf_config import component_config, controlnet_config
 
-            load_into(m, _read_dir(w))
+        raw = component_config(w, "")
+        if raw is not None:  # the checkpoint's own config.json (diffusers ControlNetModel.from_pretrained)
+            cfg, kw = controlnet_config(raw)
+            ux = pipe.unet.cfg.cross_attention_dim
+            if (tuple(cfg.block_out_channels) != tuple(pipe.unet.cfg.block_out_channels)
+                    or cfg.cross_attention_dim != ux):
+                raise ValueError(f"ControlNet {name} (channels {tuple(cfg.block_out_channels)}, cross-attention "
+                                 f"{cfg.cross_attention_dim}) does not fit the UNet of this model (channels "
+                                 f"{tuple(pipe.unet.cfg.block_out_channels)}, cross-attention {ux})")
+        with torch.device(device_identifier):
+            m = ControlNetModel(cfg, **kw).to(pipe.dtype).eval().requires_grad_(False)
+        init_random_fast_(m, seed=stable_seed(name))
+        if w:
+            from ..models.weights import load_component
+
+            load_component(m, w, "")
         prepare_model(m)
         return ControlNetRunner(m, name)
 

@@ -62,8 +62,11 @@ class IFCascade:
         self._load(weights_dir, stage2_dir)
         for m in mods:
             prepare_model(m)
-        from ..models.weights import tokenizer_dir
+        from ..models.weights import CheckpointMismatch, tokenizer_dir
 
+        if self.weights_source != "random-init" and tokenizer_dir(weights_dir) is None:
+            # real T5 weights fed hash-fallback ids would condition on a random prompt
+            raise CheckpointMismatch(f"{weights_dir}: tokenizer/spiece.model missing beside real T5 weights")
         self.tokenizer = T5Tokenizer(tokenizer_dir(weights_dir), 77, vocab=self.t5.cfg.vocab)
         self.tiny = tiny
         self.acp = _cos_acp()
@@ -74,12 +77,18 @@ class IFCascade:
 
         from ..models.weights import load_component
 
-        n = 0
+        from ..models.weights import CheckpointMismatch
+
+        got = []
         for d, parts in ((d1, (("text_encoder", self.t5), ("unet", self.stage1))), (d2, (("unet", self.stage2),))):
             for sub, m in parts if d else ():
                 if load_component(m, d, sub) is not None:
-                    n += 1
-        if n:
+                    got.append(f"{'stage1' if d is d1 else 'stage2'}/{sub}")
+        if got and len(got) != 3:
+            # stage I with a random stage II (or T5) would still emit an image
+            raise CheckpointMismatch(f"IF cascade: only {got} of stage1/text_encoder, stage1/unet, stage2/unet "
+                                     "have weights; refusing a partial load")
+        if got:
             self.weights_source = str(d1)
 
     def _s1(self, x, t, kv, temb):

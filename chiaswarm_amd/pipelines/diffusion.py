@@ -20,7 +20,7 @@ import torch
 from ..output.processor import OutputProcessor
 from ..runtime.model_cache import cache, find_weights
 from ..schedulers import get_scheduler
-from .sd import StableDiffusion, family_for_model
+from .sd import StableDiffusion, resolve_family
 from ..utils import stable_seed
 
 _DROP = ("supports_xformers", "cross_attention_kwargs", "eta", "callback", "callback_steps", "output_type",
@@ -29,10 +29,11 @@ _DROP = ("supports_xformers", "cross_attention_kwargs", "eta", "callback", "call
 
 def load_sd(model_name: str, device_identifier: str, revision: str = "main", controlnet_name: str | None = None,
             controlnet_revision: str = "main") -> StableDiffusion:
-    fam = family_for_model(model_name)
-
     def make():
-        return StableDiffusion(fam, device=device_identifier, weights_dir=find_weights(model_name, revision),
+        w = find_weights(model_name, revision)
+        # architecture from the checkpoint's own model_index.json / config.json
+        # files (the reference's from_pretrained); name presets only without them
+        return StableDiffusion(resolve_family(model_name, w), device=device_identifier, weights_dir=w,
                                seed=stable_seed(model_name))
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)
@@ -97,6 +98,7 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     # all images from one generator stream (swarm/gpu/device.py:35-41).
     image_range = kwargs.pop("_image_range", None)
     return_images = bool(kwargs.pop("_return_images", False))
+    split = kwargs.pop("_split", None)  # {"role": "leader", "peers": [rank, ...]} | {"role": "helper", "leader": r}
     gen = kwargs.get("generator")
     n_img = int(kwargs.get("num_images_per_prompt", 1) or 1)
     if (isinstance(gen, torch.Generator) and kwargs.get("image") is None
@@ -121,10 +123,16 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
                 unload_textual_inversion(pipe)
             raise
 
-    sched = get_scheduler(scheduler_type, prediction_type=pipe.family.prediction_type)
+    # the named sampler built from the checkpoint's scheduler config (diffusers from_config)
+    sched = get_scheduler(scheduler_type, **pipe.family.scheduler_kwargs())
     load_s = time.perf_counter() - t0
+    helper = split is not None and split.get("role") == "helper"
     try:
-        p = pipe(scheduler=sched, **kwargs)
+        try:
+            p = pipe(scheduler=sched, **dict(kwargs, output_type="uint8_device" if helper else "pil"))
+        except BaseException:
+            _split_failed(split)
+            raise
     finally:
         from ..models.lora import unload_lora, unload_textual_inversion
 
@@ -140,6 +148,16 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
         config["nsfw"] = True
 
     images = p.images
+    if helper:  # a split part: uint8 images straight to the leader's GPU over the process group
+        from ..parallel import comm
+
+        comm.send_images(images, int(split["leader"]), any(bool(x) for x in (p.nsfw_content_detected or [])))
+        return {}, {"_split_ack": int(images.shape[0])}
+    if split is not None and split.get("role") == "leader":
+        images, nsfw_peers = _gather_split_images(images, split)
+        if nsfw_peers:
+            config["nsfw"] = True
+        config["split"] = 1 + len(split.get("peers", []))
     if return_images:  # a split sub-job: the supervisor assembles and encodes the whole job
         import numpy as np
 
@@ -160,6 +178,43 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     return results, config
 
 
+def _split_failed(split):
+    """A split part failed before its transfer: keep the peers from waiting on it
+    (a helper sends an error header; the leader drains what its helpers send)."""
+    if split is None:
+        return
+    from ..parallel import comm
+
+    try:
+        if split.get("role") == "helper":
+            comm.send_images(None, int(split["leader"]))
+        else:
+            for r in split.get("peers", []):
+                comm.recv_images(int(r))
+    except Exception:  # the group itself is gone: the supervisor restarts the parts
+        pass
+
+
+def _gather_split_images(images, split):
+    """Leader: its own PIL images + every helper's uint8 images, in image order
+    (helpers hold the later image ranges, in ``peers`` order)."""
+    from PIL import Image
+
+    from ..parallel import comm
+
+    out, nsfw, failed = list(images), False, []
+    for r in split.get("peers", []):
+        got, flag = comm.recv_images(int(r))
+        if got is None:
+            failed.append(r)
+            continue
+        nsfw = nsfw or flag
+        out.extend(Image.fromarray(a) for a in got.cpu().numpy())
+    if failed:
+        raise RuntimeError(f"split job: the parts on ranks {failed} failed")
+    return out, nsfw
+
+
 def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dict]]:
     """Several compatible txt2img jobs (``runtime.batcher``) as ONE denoising
     batch.  ``jobs``: routed kwargs, each with its own ``generator``.  Each
@@ -171,7 +226,7 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
     model_name = k0["model_name"]
     pipe = load_sd(model_name, device_identifier, k0.get("revision", "main"))
     sched_type = k0.get("scheduler_type", "DPMSolverMultistepScheduler")
-    sched = get_scheduler(sched_type, prediction_type=pipe.family.prediction_type)
+    sched = get_scheduler(sched_type, **pipe.family.scheduler_kwargs())
     steps = int(k0.get("num_inference_steps", 30))
     sched.set_timesteps(steps)
     height = int(k0.get("height") or pipe.family.default_size) // 8 * 8

@@ -46,24 +46,67 @@ class Family:
     pad_with_eos: bool = True
     default_size: int = 512
     prediction_type: str = "epsilon"
+    pipeline_class: str = "StableDiffusionPipeline"
+    # the checkpoint's scheduler_config.json training-schedule fields, applied to
+    # whichever sampler a job names (diffusers ``from_config``)
+    sched_config: dict = dataclasses.field(default_factory=dict)
+    from_config: bool = False  # built from the checkpoint's config files (else a named preset)
+
+    @property
+    def is_xl(self) -> bool:  # SDXL conditioning: pooled text embeds + size/crop time ids
+        return self.unet.addition_embed_type == "text_time"
+
+    @property
+    def is_pix2pix(self) -> bool:  # instruct-pix2pix: 8-channel UNet, 3-way CFG
+        return self.pipeline_class == "StableDiffusionInstructPix2PixPipeline" or (
+            self.unet.in_channels == 8 and self.pipeline_class != "StableDiffusionInpaintPipeline")
+
+    def scheduler_kwargs(self) -> dict:
+        kw = dict(self.sched_config)
+        kw["prediction_type"] = self.prediction_type
+        return kw
+
+    @classmethod
+    def from_spec(cls, name: str, spec) -> "Family":
+        """A family from a parsed diffusers directory (models/hf_config.pipeline_spec)."""
+        from ..models.hf_config import scheduler_kwargs
+
+        sk = scheduler_kwargs(spec.scheduler)
+        pcls = spec.class_name
+        if pcls in ("DiffusionPipeline", "StableDiffusionPipeline") and spec.unet.in_channels == 9:
+            pcls = "StableDiffusionInpaintPipeline"
+        if spec.unet.addition_embed_type == "text_time" and not pcls.startswith("StableDiffusionXL"):
+            pcls = "StableDiffusionXLPipeline"
+        pad0 = spec.tokenizer_pad[0] if spec.tokenizer_pad else None
+        return cls(name=name, unet=spec.unet, vae=spec.vae, text=list(spec.text),
+                   pad_with_eos=pad0 is None or pad0 == "<|endoftext|>",
+                   default_size=int(spec.unet.sample_size) * 2 ** (len(spec.vae.block_out_channels) - 1),
+                   prediction_type=sk.pop("prediction_type", "epsilon"), pipeline_class=pcls, sched_config=sk,
+                   from_config=True)
 
 
+# Named presets: random-init runs (bench, smoke) and directories without config files
 FAMILIES = {
     "sd15": Family("sd15", unet_mod.SD15, vae_mod.SD_VAE, [clip_mod.CLIP_L]),
+    "sd15-inpaint": Family("sd15-inpaint", unet_mod.INPAINT_SD15, vae_mod.SD_VAE, [clip_mod.CLIP_L],
+                           pipeline_class="StableDiffusionInpaintPipeline"),
     "sd21": Family("sd21", unet_mod.SD21, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H], pad_with_eos=False),
     "sd21-v": Family("sd21-v", unet_mod.SD21_V, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H], pad_with_eos=False,
                      default_size=768, prediction_type="v_prediction"),
     "sd2-inpaint": Family("sd2-inpaint", unet_mod.INPAINT_SD2, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H],
-                          pad_with_eos=False),
-    "pix2pix": Family("pix2pix", unet_mod.PIX2PIX, vae_mod.SD_VAE, [clip_mod.CLIP_L]),
+                          pad_with_eos=False, pipeline_class="StableDiffusionInpaintPipeline"),
+    "pix2pix": Family("pix2pix", unet_mod.PIX2PIX, vae_mod.SD_VAE, [clip_mod.CLIP_L],
+                      pipeline_class="StableDiffusionInstructPix2PixPipeline"),
     "sdxl": Family("sdxl", unet_mod.SDXL, vae_mod.SDXL_VAE, [clip_mod.CLIP_L, clip_mod.OPENCLIP_BIGG],
-                   default_size=1024),
+                   default_size=1024, pipeline_class="StableDiffusionXLPipeline"),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
 }
 
 
 def family_for_model(model_name: str) -> str:
-    """Map a hive model name (HF repo id) to an architecture family."""
+    """Map a hive model name (HF repo id) to a preset family — ONLY for
+    directories without ``model_index.json`` (and random-init runs); a real
+    checkpoint is built from its own config files (``resolve_family``)."""
     n = model_name.lower()
     if n.startswith("tiny/") or n == "tiny":
         return "tiny"
@@ -73,9 +116,25 @@ def family_for_model(model_name: str) -> str:
         return "sdxl"
     if "inpaint" in n and ("2-" in n or "2." in n):
         return "sd2-inpaint"
+    if "inpaint" in n:
+        return "sd15-inpaint"
     if "stable-diffusion-2" in n:
         return "sd21" if ("base" in n or "512" in n) else "sd21-v"
     return "sd15"
+
+
+def resolve_family(model_name: str, weights_dir: str | None) -> Family:
+    """The architecture of ``model_name``: parsed from ``weights_dir``'s
+    ``model_index.json`` + component configs when present (the reference's
+    ``from_pretrained``, swarm/diffusion/diffusion_func.py:41-46), else the
+    name-matched preset."""
+    if weights_dir:
+        from ..models.hf_config import pipeline_spec
+
+        spec = pipeline_spec(weights_dir)
+        if spec is not None:
+            return Family.from_spec(model_name, spec)
+    return FAMILIES[family_for_model(model_name)]
 
 
 @dataclasses.dataclass
@@ -93,9 +152,9 @@ class StableDiffusion:
     image, mask_image, strength, image_guidance_scale, controlnet_conditioning_scale,
     eta, cross_attention_kwargs ...)."""
 
-    def __init__(self, family: str, device="cpu", dtype=None, seed=0, weights_dir=None,
+    def __init__(self, family: "str | Family", device="cpu", dtype=None, seed=0, weights_dir=None,
                  with_encoder=True, controlnet=None):
-        self.family = FAMILIES[family]
+        self.family = FAMILIES[family] if isinstance(family, str) else family
         self.device = torch.device(device)
         if dtype is None:
             dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
@@ -120,23 +179,29 @@ class StableDiffusion:
         for name, m in zip(names, [self.unet, self.vae] + self.text_encoders):
             if name not in self.prepared:  # loaded components were packed (or read packed) already
                 prepare_model(m)
-        from ..models.weights import tokenizer_dir
+        from ..models.weights import CheckpointMismatch, tokenizer_dir
 
         # tokenizer/ (+ tokenizer_2/ for SDXL, whose OpenCLIP-bigG tokenizer pads with "!")
-        self.tokenizers = [CLIPTokenizer(tokenizer_dir(weights_dir, "tokenizer" if i == 0 else f"tokenizer_{i + 1}"),
-                                         77, pad_with_eos=fam.pad_with_eos and i == 0, vocab_size=c.vocab_size)
+        tdirs = [tokenizer_dir(weights_dir, "tokenizer" if i == 0 else f"tokenizer_{i + 1}")
+                 for i in range(len(fam.text))]
+        if self.weights_source != "random-init" and None in tdirs:
+            # real text-encoder weights fed hash-fallback token ids = a random prompt
+            raise CheckpointMismatch(f"{weights_dir}: tokenizer files (vocab.json / merges.txt) missing for "
+                                     f"{['tokenizer' if i == 0 else f'tokenizer_{i + 1}' for i, d in enumerate(tdirs) if d is None]}")
+        self.tokenizers = [CLIPTokenizer(tdirs[i], 77, pad_with_eos=fam.pad_with_eos and i == 0,
+                                         vocab_size=c.vocab_size)
                            for i, c in enumerate(fam.text)]
         self.controlnet = controlnet
         self.safety_checker = None
         self.config: dict[str, Any] = {
-            "_class_name": "StableDiffusionPipeline" if family != "sdxl" else "StableDiffusionXLPipeline",
+            "_class_name": fam.pipeline_class,
             "_framework": "chiaswarm_amd",
             "unet": ["chiaswarm_amd", "UNet2DConditionModel"],
             "vae": ["chiaswarm_amd", "AutoencoderKL"],
             "text_encoder": ["chiaswarm_amd", "CLIPTextModel"],
             "tokenizer": ["chiaswarm_amd", "CLIPTokenizer"],
             "scheduler": ["chiaswarm_amd", "DPMSolverMultistepScheduler"],
-            "family": family,
+            "family": fam.name,
             "weights": self.weights_source,
         }
         self._graphs: dict = {}
@@ -160,7 +225,7 @@ class StableDiffusion:
         hs, pooled = [], None
         for i, te in enumerate(self.text_encoders):
             last, penult, pool, proj = te(ids[i])
-            if self.family.name == "sdxl":
+            if self.family.is_xl:
                 hs.append(penult)
                 if proj is not None:
                     pooled = proj
@@ -183,7 +248,7 @@ class StableDiffusion:
             ctx, pooled, kv = self._text_graphs(self.device, ids=ids)
         else:
             ctx, pooled, kv = self._text_fn(ids, with_kv)
-        added = {"text_embeds": pooled} if self.family.name == "sdxl" else None
+        added = {"text_embeds": pooled} if self.family.is_xl else None
         return ctx, added, kv
 
     @torch.no_grad()
@@ -237,6 +302,11 @@ class StableDiffusion:
         three_way = image_guidance is not None
         nrep = 3 if three_way else (2 if cfg else 1)
         x = latents
+        if mask is None and self._loop_ok():
+            table = sched.loop_table()
+            if table is not None and len(table[0]) > 0:
+                return self._denoise_loop(x, sched, table, cross_kv, guidance, added, generator, image_latents,
+                                          image_guidance, nrep, control)
         while sched.step_index < sched.n:
             t = sched.current_t()
             s_in = sched.current_scale()
@@ -269,6 +339,65 @@ class StableDiffusion:
                 x = known * (1 - mask) + x * mask
         return x
 
+    def _loop_ok(self) -> bool:
+        return (LOOP_GRAPHS and self.use_graphs and self.device.type == "cuda" and ops.get_mode() == "hip"
+                and ops._lib.available())
+
+    def _denoise_loop(self, x, sched, table, cross_kv, guidance, added, generator, image_latents,
+                      image_guidance, nrep, control):
+        """Device-resident sampler loop: ONE hipGraph replay per step and no
+        host work in between.  The step graph is [loop_prologue (device step
+        counter -> timestep), UNet (+ ControlNet), sched_loop (CFG + update ->
+        the next step's bf16 UNet input written in place)]; the per-step
+        scalars, the guidance scales and any sampler noise (drawn up front, in
+        the order the eager loop draws it) sit in device tables."""
+        from ..ops import hip_ops
+
+        ts, rows, s0 = table
+        n = len(ts)
+        mode = nrep - 1
+        g, g2 = (float(guidance), float(image_guidance)) if mode == 2 else (float(guidance), 0.0)
+        need_noise = any(r[5] != 0.0 for r in rows)
+        x_first = (x * s0).to(self.dtype)
+        x_in = torch.cat([x_first] * nrep, 0) if nrep > 1 else x_first
+        if image_latents is not None:
+            x_in = torch.cat([x_in, image_latents.to(self.dtype)], dim=-1)
+        share = bool(getattr(self, "_kv_static", False))
+        cap = max(64, -(-n // 64) * 64)
+        key = ("loop", x_in.shape, added is not None, len(cross_kv), share, mode, need_noise,
+               None if control is None else (id(control.model), control.scale, tuple(control.cond_emb.shape)))
+        gph = self._graphs.get(key)
+        if gph is not None and gph.loop_cap < n:
+            gph = None
+        if gph is None:
+            spec = _LoopSpec(tuple(x.shape), mode, cap, need_noise, x.device)
+            gph = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share, loop=spec) if control is None else
+                   _ControlUNetGraph(self.unet, x_in, cross_kv, added, control, share_kv=share, loop=spec))
+            self._graphs[key] = gph
+        L = gph.loop
+        coef = torch.zeros((n, hip_ops.LOOP_COEF_STRIDE), dtype=torch.float32)
+        coef[:, :7] = torch.tensor(rows, dtype=torch.float64).float()
+        coef[:, 7] = g
+        coef[:, 8] = g2
+        L.coef[:n].copy_(coef.to(self.device, non_blocking=False))
+        L.t_tab[:n].copy_(torch.tensor(ts, dtype=torch.float32).to(self.device))
+        if need_noise:
+            for i, r in enumerate(rows):  # the eager loop's draw order: one draw per noisy step
+                if r[5] != 0.0:
+                    L.noise[i].copy_(batch_randn(x.shape, generator, x.device))
+        L.x.copy_(x)
+        if sched.prev_x0 is not None:
+            L.x0prev.copy_(sched.prev_x0)
+        else:
+            L.x0prev.zero_()
+        L.counter.zero_()
+        gph.prepare(x_in, cross_kv, added, control, req=getattr(self, "_req", None))
+        for _ in range(n):
+            gph.graph.replay()
+        sched.step_index = sched.n
+        sched.prev_x0 = L.x0prev.clone()
+        return L.x.clone()
+
     @torch.no_grad()
     def decode(self, latents, to_host=True) -> torch.Tensor:
         """NHWC fp32 latents -> uint8 NHWC images (on the host unless to_host=False)."""
@@ -299,10 +428,9 @@ class StableDiffusion:
         negs = neg if isinstance(neg, list) else [neg] * b
         if len(negs) != b:
             negs = [negs[0]] * b
-        is_pix2pix = self.family.name == "pix2pix"
+        is_pix2pix = self.family.is_pix2pix
         cfg = guidance_scale > 1.0 or is_pix2pix
-        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler",
-                                           prediction_type=self.family.prediction_type)
+        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **self.family.scheduler_kwargs())
         sched.prediction_type = self.family.prediction_type
 
         if image is not None and not isinstance(image, list):
@@ -398,6 +526,9 @@ class StableDiffusion:
         nsfw = [False] * b
         if self.safety_checker is not None:  # on the device, before the D2H copy
             nsfw, imgs = self.safety_checker(imgs)
+        if output_type == "uint8_device":  # a split-job part: sent device-to-device to the leader
+            timings["decode"] = time.perf_counter() - t2
+            return PipelineOutput(imgs, nsfw, x, timings)
         imgs = imgs.cpu()
         timings["decode"] = time.perf_counter() - t2
         pil = [Image.fromarray(a.numpy()) for a in imgs] if output_type == "pil" else imgs
@@ -411,12 +542,37 @@ def _apply_mask(image: Image.Image, mask: Image.Image) -> Image.Image:
     return Image.fromarray(arr)
 
 
+LOOP_GRAPHS = True  # device-resident sampler loop (StableDiffusion._denoise_loop); False: per-step host loop
+
+
+class _LoopSpec:
+    """Static device buffers of a device-resident sampler loop (fixed pointers
+    captured into the step graph): latents / previous x0 (fp32 NHWC), step
+    counter, per-step timestep and coefficient tables sized for ``cap`` steps,
+    optional per-step noise table."""
+
+    def __init__(self, shape, mode, cap, need_noise, device):
+        from ..ops import hip_ops
+
+        self.mode, self.cap = mode, cap
+        self.x = torch.zeros(shape, dtype=torch.float32, device=device)
+        self.x0prev = torch.zeros(shape, dtype=torch.float32, device=device)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
+        self.cur = torch.zeros(1, dtype=torch.int32, device=device)
+        self.t_tab = torch.zeros(cap, dtype=torch.float32, device=device)
+        self.coef = torch.zeros((cap, hip_ops.LOOP_COEF_STRIDE), dtype=torch.float32, device=device)
+        self.noise = torch.zeros((cap,) + tuple(shape), dtype=torch.float32, device=device) if need_noise else None
+
+
 class _UNetGraph:
     """hipGraph of one UNet forward at a fixed (batch, H, W): static input
-    buffers are refreshed by ``copy_`` before each replay."""
+    buffers are refreshed by ``copy_`` before each replay.  With ``loop`` the
+    graph is a whole sampler step (see StableDiffusion._denoise_loop)."""
 
-    def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False):
+    def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False, loop=None):
         self.unet = unet
+        self.loop = loop
+        self.loop_cap = loop.cap if loop is not None else 0
         self.x = x_in.clone()
         self.t = torch.zeros(1, device=x_in.device, dtype=torch.float32)
         # share_kv: the K/V are another graph's static outputs -> capture them directly
@@ -434,11 +590,21 @@ class _UNetGraph:
             self.out = self._fwd()
 
     def _fwd(self):
+        if self.loop is None:
+            return self._unet_fwd()
+        from ..ops import hip_ops
+
+        L = self.loop
+        hip_ops.loop_prologue(L.counter, L.cur, L.t_tab, self.t)
+        e = self._unet_fwd().contiguous()
+        hip_ops.sched_loop(e, L.x, L.x0prev, L.noise, L.cur, L.coef, self.x, L.mode)
+        return e
+
+    def _unet_fwd(self):
         return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added)
 
-    def run(self, x_in, t, cross_kv, added, cc=None, req=None):
+    def prepare(self, x_in, cross_kv, added, cc=None, req=None):
         self.x.copy_(x_in)
-        self.t.fill_(float(t))
         # per-request cross-attention K/V: copied into the graph's static buffers
         # once per request (a no-op when they ARE the text-encoder graph's static
         # outputs, which that graph rewrites in place for every request)
@@ -451,6 +617,10 @@ class _UNetGraph:
         if added:
             for k, v in added.items():
                 self.added[k].copy_(v)
+
+    def run(self, x_in, t, cross_kv, added, cc=None, req=None):
+        self.prepare(x_in, cross_kv, added, cc, req)
+        self.t.fill_(float(t))
         self.graph.replay()
         return self.out
 
@@ -465,13 +635,13 @@ class _ControlUNetGraph(_UNetGraph):
     conditioning embedding and the ControlNet's prompt K/V are static buffers
     refreshed once per request; the conditioning scale is part of the graph key."""
 
-    def __init__(self, unet, x_in, cross_kv, added, cc, warmup=2, share_kv=False):
+    def __init__(self, unet, x_in, cross_kv, added, cc, warmup=2, share_kv=False, loop=None):
         self.cn, self.scale = cc.model, cc.scale
         self.cond = cc.cond_emb.clone()
         self.ckv = [k.clone() for k in cc.kv]
-        super().__init__(unet, x_in, cross_kv, added, warmup=warmup, share_kv=share_kv)
+        super().__init__(unet, x_in, cross_kv, added, warmup=warmup, share_kv=share_kv, loop=loop)
 
-    def _fwd(self):
+    def _unet_fwd(self):
         from .controlnet import ControlFeatures
 
         feats, mid = self.cn.features(self.x[..., :self.cn.cfg.in_channels], self.t, self.cond, cross_kv=self.ckv)

@@ -41,6 +41,16 @@ class TextToVideo:
         ucfg = unet3d.TINY_T2V if tiny else unet3d.T2V
         tcfg = clip_mod.TINY_TEXT if tiny else clip_mod.OPENCLIP_H
         vcfg = vae_mod.TINY_VAE if tiny else vae_mod.SD_VAE
+        w = find_weights(model_name)
+        self.sched_config = {}
+        if w:  # the checkpoint's own configs (the reference: from_pretrained, swarm/video/tx2vid.py:24-30)
+            from ..models import hf_config as hc
+
+            uc, tc, vc = (hc.component_config(w, s) for s in ("unet", "text_encoder", "vae"))
+            ucfg = hc.unet3d_config(uc) if uc else ucfg
+            tcfg = hc.clip_text_config(tc) if tc else tcfg
+            vcfg = hc.vae_config(vc) if vc else vcfg
+            self.sched_config = hc.scheduler_kwargs(hc.component_config(w, "scheduler", "scheduler_config.json"))
         with torch.device(self.device):
             self.unet = unet3d.UNet3DConditionModel(ucfg).to(self.dtype)
             self.vae = vae_mod.AutoencoderKL(vcfg, with_encoder=False).to(self.dtype)
@@ -48,12 +58,17 @@ class TextToVideo:
         for i, m in enumerate((self.unet, self.vae, self.text)):
             m.eval().requires_grad_(False)
             init_random_fast_(m, seed=21 + i)
-        w = find_weights(model_name)
-        from ..models.weights import _VAE_RENAMES, load_component, tokenizer_dir
+        from ..models.weights import _VAE_RENAMES, CheckpointMismatch, load_component, tokenizer_dir
 
+        loaded = []
         if w:
             for sub, m in (("unet", self.unet), ("vae", self.vae), ("text_encoder", self.text)):
-                load_component(m, w, sub, _VAE_RENAMES if sub == "vae" else None)
+                if load_component(m, w, sub, _VAE_RENAMES if sub == "vae" else None) is not None:
+                    loaded.append(sub)
+            if loaded and len(loaded) != 3:
+                raise CheckpointMismatch(f"{w}: only {loaded} of unet / vae / text_encoder have weights")
+            if loaded and tokenizer_dir(w) is None:
+                raise CheckpointMismatch(f"{w}: tokenizer files missing beside real text-encoder weights")
         for m in (self.unet, self.vae, self.text):
             prepare_model(m)
         self.tok = CLIPTokenizer(tokenizer_dir(w), 77, pad_with_eos=False, vocab_size=tcfg.vocab_size)
@@ -67,7 +82,7 @@ class TextToVideo:
     @torch.no_grad()
     def __call__(self, prompt="", negative_prompt="", num_frames=25, num_inference_steps=25, guidance_scale=9.0,
                  height=256, width=256, generator=None, scheduler=None, **_):
-        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler")
+        sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **self.sched_config)
         sched.set_timesteps(num_inference_steps)
         ids = self.tok([negative_prompt or "", prompt]).to(self.device)
         ctx = self.text(ids)[0]
@@ -141,8 +156,7 @@ def model_video_callback(device_identifier, model_name, **kwargs):
                  num_inference_steps=steps, guidance_scale=guidance_scale,
                  image_guidance_scale=image_guidance_scale, generator=generator,
                  height=chunk[0].height, width=chunk[0].width,
-                 scheduler=get_scheduler("EulerAncestralDiscreteScheduler",
-                                         prediction_type=pipe.family.prediction_type))
+                 scheduler=get_scheduler("EulerAncestralDiscreteScheduler", **pipe.family.scheduler_kwargs()))
         out_frames.extend(np.asarray(im.convert("RGB")) for im in r.images)
         nsfw = nsfw or any(r.nsfw_content_detected)
     video, ct = frames_to_video(np.stack(out_frames), max(1, int(round(fps))), "video/mp4")

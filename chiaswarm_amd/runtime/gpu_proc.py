@@ -12,8 +12,18 @@ CPU children — before any GPU work.  The group is used for collective model
 preloads: every child reads 1/N of each checkpoint's bytes and an all_gather
 assembles the rest (parallel/sharded.py).  Job-triggered loads stay local.
 
-This module must not import torch at import time: the child selects its GPU via
-HIP_VISIBLE_DEVICES *before* torch initialises.
+GPU visibility: by default every child sees ALL of the node's GPUs and binds
+its own with ``torch.cuda.set_device(i)`` (LOCAL_RANK = i), so RCCL can see its
+peers and take the P2P / xGMI paths (a child isolated with HIP_VISIBLE_DEVICES
+sees no peer device, which leaves RCCL only host-memory transports);
+``SDAAS_GPU_ISOLATION=1`` restores the one-visible-GPU child.
+
+The process group's rendezvous store lives in the SUPERVISOR (runtime/worker.py)
+so no GPU child's death takes it down; ``__regroup__`` re-forms the group (a new
+store generation) after a child was restarted.
+
+This module must not import torch at import time: an isolated child selects its
+GPU via HIP_VISIBLE_DEVICES *before* torch initialises.
 """
 from __future__ import annotations
 
@@ -21,33 +31,66 @@ import os
 import traceback
 
 
-def _join_group(gpu_index) -> str:
-    """Join the node's process group (RANK / WORLD_SIZE / MASTER_* in the env).
-    Returns a status string; a failure leaves the child working rank-local."""
-    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
-        return "single"
-    os.environ["LOCAL_RANK"] = "0"  # this child sees exactly one GPU (HIP_VISIBLE_DEVICES)
+def _isolated() -> bool:
+    return os.environ.get("SDAAS_GPU_ISOLATION", "0") == "1"
+
+
+def _local_index(gpu_index) -> int:
+    """The torch device index of this child's GPU."""
+    return 0 if (gpu_index == "cpu" or _isolated()) else int(gpu_index)
+
+
+def _join_group(gpu_index) -> dict:
+    """Join the node's process group (RANK / WORLD_SIZE / SDAAS_STORE_* /
+    SDAAS_GROUP_GEN in the env).  Returns the group status the supervisor
+    checks before it issues any collective: {"gen", "rank", "world"} when
+    joined, {"error": ...} on failure (the child then works rank-local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return {"world": 1}
+    os.environ["LOCAL_RANK"] = str(_local_index(gpu_index))
     from ..parallel import comm
 
     backend = "gloo" if gpu_index == "cpu" else os.environ.get("CSK_DIST_BACKEND", "nccl")
     try:
         comm.init_distributed(backend=backend, timeout_s=int(os.environ.get("CSK_DIST_TIMEOUT", "600")))
-        return f"{backend} rank {os.environ.get('RANK')}/{os.environ.get('WORLD_SIZE')}"
+        return {"gen": int(os.environ.get("SDAAS_GROUP_GEN", "0")), "rank": int(os.environ["RANK"]),
+                "world": world, "backend": backend}
     except Exception as e:  # pragma: no cover - depends on the node
         import logging
 
         logging.exception(e)
-        return f"no group ({e})"
+        comm.leave_group()
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
-def _preload(names: list, device_id: str) -> dict:
-    """Collective preload of SD-family models (every child, same list, same order)."""
+def _regroup(gpu_index, spec: dict) -> dict:
+    """Leave the current group (aborting its communicators: a peer may be dead)
+    and join generation ``spec['gen']`` as ``spec['rank']`` of ``spec['world']``."""
+    from ..parallel import comm
+
+    comm.leave_group()
+    os.environ.update({"RANK": str(spec["rank"]), "WORLD_SIZE": str(spec["world"]),
+                       "SDAAS_GROUP_GEN": str(spec["gen"]), "SDAAS_STORE_PORT": str(spec["store_port"])})
+    return _join_group(gpu_index)
+
+
+def _preload(names: list, device_id: str, collective: bool = True) -> dict:
+    """Preload of SD-family models.  ``collective``: every child of the group
+    loads the same list in the same order, reading 1/N of the bytes each
+    (the supervisor sends it only when every child reported the same group)."""
+    import contextlib
+
     from ..parallel import comm
     from ..pipelines.diffusion import load_sd
 
     done = {}
-    with comm.collective_loading():
+    with comm.collective_loading() if collective else contextlib.nullcontext():
         for name in names:
+            if name == "__test_exit__" and os.environ.get("CSK_TEST_HOOKS") == "1":
+                if os.environ.get("RANK") == os.environ.get("CSK_TEST_EXIT_RANK", "1"):
+                    os._exit(3)  # a rank dying inside a collective preload (tests/test_worker_procs.py)
+                continue
             pipe = load_sd(name, device_id)
             done[name] = pipe.config.get("weights", "random-init")
     return done
@@ -68,7 +111,7 @@ def _test_hook(job):
 
 def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
     """Child entry point.  inbox: job dicts (None = stop); outbox: (gpu, job_id, result|None, err)."""
-    if gpu_index != "cpu":
+    if gpu_index != "cpu" and _isolated():
         os.environ["HIP_VISIBLE_DEVICES"] = str(gpu_index)
         os.environ["CUDA_VISIBLE_DEVICES"] = str(gpu_index)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -104,19 +147,29 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         setup_logging(resolve_path(settings.log_filename), settings.log_level, suffix=f"gpu{gpu_index}")
     except Exception:
         pass
+    if gpu_index != "cpu":
+        import torch
+
+        torch.cuda.set_device(_local_index(gpu_index))  # before any allocation: this child's GPU
     group = _join_group(gpu_index)
-    device = Device("cpu" if gpu_index == "cpu" else 0)
-    outbox.put((gpu_index, "__ready__", None, f"{device.descriptor()} [{group}]"))
+    device = Device("cpu" if gpu_index == "cpu" else _local_index(gpu_index))
+    outbox.put((gpu_index, "__ready__", None, {"desc": device.descriptor(), "group": group}))
     while True:
         job = inbox.get()
         if job is None:
             break
         if isinstance(job, dict) and "__preload__" in job:
             try:
-                res = _preload(list(job["__preload__"]), device.identifier())
+                res = _preload(list(job["__preload__"]), device.identifier(), bool(job.get("collective", True)))
                 outbox.put((gpu_index, "__preloaded__", res, None))
             except BaseException as e:
                 outbox.put((gpu_index, "__preloaded__", None, f"{e}\n{traceback.format_exc()}"))
+            continue
+        if isinstance(job, dict) and "__regroup__" in job:
+            try:
+                outbox.put((gpu_index, "__regrouped__", _regroup(gpu_index, job["__regroup__"]), None))
+            except BaseException as e:
+                outbox.put((gpu_index, "__regrouped__", None, f"{e}\n{traceback.format_exc()}"))
             continue
         for j in (job if isinstance(job, list) else [job]):
             _test_hook(j)

@@ -5,18 +5,26 @@ one executor per device -> result queue -> POST results.  Poll cadence, queue
 depth, error backoff and hive endpoints are the reference's.
 
 MI355X-first changes:
-  * ``ProcessExecutor``: one OS process per GPU (HIP_VISIBLE_DEVICES=i), so
-    the eight GPUs of a node do not share a GIL and each keeps its own resident
-    models; results are encoded in the GPU's process.
+  * ``ProcessExecutor``: one OS process per GPU (torch.cuda.set_device(i), all
+    GPUs visible so RCCL sees its peers), so the eight GPUs of a node do not
+    share a GIL and each keeps its own resident models; results are encoded in
+    the GPU's process.
   * per-GPU watchdog: a crashed / hung child is restarted and its in-flight job
     is reported as a NON-fatal error (the hive may retry it), SURVEY §5.3.
-  * the GPU children form one process group (RCCL over xGMI): models listed in
-    ``settings.preload`` are read once across the node — each GPU reads 1/N of
-    the checkpoint bytes, one all_gather per dtype fills every GPU
-    (parallel/sharded.py).  A restarted child leaves the group (rank-local).
+  * the GPU children form one process group (RCCL over xGMI) whose rendezvous
+    store (a TCPStore) lives HERE in the supervisor, so a child's death never
+    takes the store with it.  Collectives are issued only while every child
+    reports the same group generation; a restarted child comes back rank-local
+    and the next idle moment re-forms the group (a new generation).
+  * preload: models listed in ``settings.preload`` are read once across the
+    node — each GPU reads 1/N of the checkpoint bytes, one all_gather per
+    dtype fills every GPU (parallel/sharded.py); a child dying mid-preload
+    restarts every group child (the others may be wedged in the collective).
   * split jobs: a multi-image txt2img job may run on several idle GPUs at once
     (image j always uses seed + j, so the images do not depend on the split);
-    the supervisor assembles the images in order and builds the one envelope.
+    with a healthy group the helpers send their uint8 images device-to-device
+    to the leading GPU (RCCL point-to-point over xGMI), which builds the one
+    envelope; without one the supervisor assembles pickled images.
   * ``ThreadExecutor`` (reference-style, in-process) for CPU plumbing runs and
     tests.
 """
@@ -79,11 +87,14 @@ class ProcessExecutor:
         self.restarts = 0
         self.ready = threading.Event()
         self.ready_info = ""
+        self.group: dict = {}  # the child's process-group status ({"gen", "rank", "world"} when joined)
         self._start()
 
     def _start(self):
         from .gpu_proc import gpu_main
 
+        self.ready.clear()
+        self.group = {}
         self.inbox = self.ctx.Queue()
         self.outbox = self.ctx.Queue()
         self.proc = self.ctx.Process(target=gpu_main, args=(self.gpu_index, self.inbox, self.outbox, self.env),
@@ -102,10 +113,14 @@ class ProcessExecutor:
                 return
             _, jid, result, err = item
             if jid == "__ready__":
-                self.ready_info = str(err)
+                info = err if isinstance(err, dict) else {"desc": str(err), "group": {}}
+                self.group = dict(info.get("group") or {})
+                self.ready_info = f"{info.get('desc')} [{_group_str(self.group)}]"
                 self.ready.set()
-                print(f"Started device {err}")
+                print(f"Started device {self.ready_info}")
                 continue
+            if jid == "__regrouped__" and result is not None:
+                self.group = dict(result)
             fut = self.pending.pop(jid, None)
             if fut is not None and self.loop is not None:
                 self.loop.call_soon_threadsafe(_resolve, fut, (result, err))
@@ -116,21 +131,57 @@ class ProcessExecutor:
         except Exception:
             pass
         self.proc.join(timeout=10)
-        # the process group cannot re-admit a rank: the fresh child works rank-local
+        # a live process group cannot re-admit a rank: the fresh child starts
+        # rank-local and joins the next generation when the supervisor regroups
         self.env["WORLD_SIZE"] = "1"
         self.restarts += 1
+        for jid, fut in list(self.pending.items()):  # control messages die with the child
+            if jid.startswith("__") and self.loop is not None:
+                self.pending.pop(jid, None)
+                self.loop.call_soon_threadsafe(_resolve, fut, (None, "GPU worker restarted"))
         self._start()
 
-    async def preload(self, names, timeout_s: float = 3600.0):
-        """Collective model preload (every executor of the group, same list)."""
+    def kill(self):
+        """Kill the child (its pending run() notices within 2 s and restarts it)."""
+        try:
+            self.proc.kill()
+        except Exception:
+            pass
+
+    async def _control(self, key: str, reply: str, msg: dict, timeout_s: float):
+        """Send a control message and await its reply, watching the child: a
+        child that dies or outlives ``timeout_s`` is restarted and the call
+        raises (a plain wait would block forever on a dead child)."""
         self.loop = asyncio.get_running_loop()
         fut = self.loop.create_future()
-        self.pending["__preloaded__"] = fut
-        self.inbox.put({"__preload__": list(names)})
-        result, err = await asyncio.wait_for(fut, timeout_s)
-        if err:
-            raise RuntimeError(f"{self.name} preload failed: {err}")
-        return result
+        self.pending[reply] = fut
+        self.inbox.put(msg)
+        t0 = time.monotonic()
+        while True:
+            done, _ = await asyncio.wait({fut}, timeout=1.0)
+            if done:
+                result, err = fut.result()
+                if err:
+                    raise RuntimeError(f"{self.name} {key} failed: {err}")
+                return result
+            if not self.proc.is_alive() or time.monotonic() - t0 > timeout_s:
+                why = "died" if not self.proc.is_alive() else "timed out"
+                self.pending.pop(reply, None)
+                self._restart()
+                raise RuntimeError(f"{self.name} {why} during {key}")
+
+    async def preload(self, names, timeout_s: float = 3600.0, collective: bool = True):
+        """Model preload (collective: every executor of the group, same list)."""
+        return await self._control("preload", "__preloaded__",
+                                   {"__preload__": list(names), "collective": collective}, timeout_s)
+
+    async def regroup(self, spec: dict, timeout_s: float = 300.0):
+        """Leave the current process group and join generation ``spec``."""
+        self.env.update({"RANK": str(spec["rank"]), "WORLD_SIZE": str(spec["world"]),
+                         "SDAAS_GROUP_GEN": str(spec["gen"]), "SDAAS_STORE_PORT": str(spec["store_port"])})
+        res = await self._control("regroup", "__regrouped__", {"__regroup__": dict(spec)}, timeout_s)
+        self.group = dict(res or {})
+        return self.group
 
     async def run(self, job):
         from .generator import _error_result
@@ -242,11 +293,47 @@ def _resolve(fut, value):
         fut.set_result(value)
 
 
+def _group_str(g: dict) -> str:
+    if g.get("error"):
+        return f"no group ({g['error']})"
+    if "rank" in g:
+        return f"{g.get('backend', '?')} rank {g['rank']}/{g['world']} gen {g.get('gen', 0)}"
+    return "single"
+
+
+class GroupStore:
+    """The node process group's rendezvous: a TCPStore hosted by the
+    supervisor (is_master), with generations — each (re)formed group uses its
+    own key prefix, so a regroup never reads a dead generation's keys."""
+
+    def __init__(self, host: str = "127.0.0.1"):
+        import datetime
+
+        import torch.distributed as dist
+
+        self.host = host
+        self.store = dist.TCPStore(host, 0, is_master=True, wait_for_workers=False,
+                                   timeout=datetime.timedelta(seconds=600))
+        self.port = self.store.port
+        self.gen = 0
+
+    def next_gen(self) -> int:
+        self.gen += 1
+        return self.gen
+
+
+_STORES: list = []  # keep every hosted store alive for the life of the process
+
+
 class Supervisor:
     def __init__(self, settings=None, executors=None, hive=None):
         self.settings = settings or load_settings()
         self.hive = hive or HiveClient(self.settings)
         self.executors = executors if executors is not None else self._default_executors()
+        self.store = next((s for s in _STORES if any(getattr(e, "env", {}).get("SDAAS_STORE_PORT") == str(s.port)
+                                                       for e in self.executors)), None)
+        self._last_regroup = 0.0
+        self.regroups = 0
         n = max(1, len(self.executors))
         # batching: each device may hold up to max_batch queued jobs (max_batch <= 1:
         # the reference's queue depth of one job per device)
@@ -258,6 +345,10 @@ class Supervisor:
         self.splits = 0
         self.stop = asyncio.Event()
         self.locks = {id(ex): asyncio.Lock() for ex in self.executors}
+        # executors whose device_worker is parked on the work queue: only these
+        # may be claimed as split helpers (their lock has no waiter, so taking it
+        # never suspends; ADVICE r2: probing lk.locked() alone could stall)
+        self.idle: set = set()
 
     def _default_executors(self):
         gpus = visible_gpus(self.settings)
@@ -270,10 +361,45 @@ class Supervisor:
         ensure_built()
         return [ProcessExecutor(g, env=e) for g, e in zip(gpus, group_envs(len(gpus), self.settings))]
 
+    # ------------------------------------------------------------------ process group
+    def group_ok(self) -> bool:
+        """Every executor reports the SAME live group generation with distinct
+        ranks 0..N-1: only then are collectives / point-to-point sends issued
+        (a half-formed group would leave the joined ranks waiting forever)."""
+        gs = [getattr(e, "group", None) or {} for e in self.executors]
+        if len(self.executors) < 2 or not all("rank" in g for g in gs):
+            return False
+        gens = {g.get("gen") for g in gs}
+        return len(gens) == 1 and sorted(g["rank"] for g in gs) == list(range(len(gs))) and \
+            all(g["world"] == len(gs) for g in gs)
+
+    async def regroup(self, timeout_s: float = 300.0) -> bool:
+        """Re-form the process group as a new store generation (after a child
+        restart left it degraded).  Call only while every executor is idle."""
+        if self.store is None or len(self.executors) < 2:
+            return False
+        gen = self.store.next_gen()
+        self._last_regroup = time.monotonic()
+        self.regroups += 1
+        specs = [{"gen": gen, "rank": i, "world": len(self.executors), "store_port": self.store.port}
+                 for i in range(len(self.executors))]
+        res = await asyncio.gather(*(e.regroup(sp, timeout_s) for e, sp in zip(self.executors, specs)),
+                                   return_exceptions=True)
+        ok = self.group_ok()
+        if not ok:
+            logging.error(f"regroup to generation {gen} failed: {res}")
+        return ok
+
+    async def _maybe_regroup(self):
+        if (self.store is not None and not self.group_ok() and self.busy == 0 and self.work_queue.empty()
+                and all(hasattr(e, "regroup") for e in self.executors) and len(self.executors) > 1
+                and time.monotonic() - self._last_regroup > float(os.environ.get("SDAAS_REGROUP_S", "60"))):
+            await self.regroup()
+
     # ------------------------------------------------------------------ split jobs
     async def _claim_helpers(self, job, ex) -> list:
-        """Idle executors for a split (an uncontended asyncio.Lock.acquire never
-        suspends, so check-and-take is atomic on the event loop)."""
+        """Idle executors for a split, claimed synchronously: an executor in
+        ``self.idle`` has no waiter on its lock, so ``acquire`` returns at once."""
         if not getattr(self.settings, "split_jobs", True) or len(self.executors) < 2:
             return []
         n = splittable(job)
@@ -284,7 +410,8 @@ class Supervisor:
             if len(helpers) + 1 >= n:
                 break
             lk = self.locks[id(other)]
-            if other is not ex and not lk.locked():
+            if other is not ex and other in self.idle and not lk.locked():
+                self.idle.discard(other)
                 await lk.acquire()
                 helpers.append(other)
         return helpers
@@ -299,6 +426,8 @@ class Supervisor:
         seed = job.get("seed")
         if seed is None:
             seed = random.SystemRandom().randrange(0, 2 ** 63 - 1)
+        if self.group_ok() and all(hasattr(e, "kill") for e in exs):
+            return await self._run_split_group(job, exs, n, seed)
         subs = []
         for i, (lo, hi) in enumerate(_ranges(n, len(exs))):
             subs.append(dict(job, id=f"{jid}#{i}", seed=seed, num_images_per_prompt=hi - lo,
@@ -337,12 +466,69 @@ class Supervisor:
         return {"id": jid, "artifacts": artifacts, "nsfw": nsfw, "worker_version": __version__,
                 "pipeline_config": cfg}
 
+    async def _run_split_group(self, job, exs, n, seed) -> dict:
+        """Split over the process group: the leader (exs[0]) renders images
+        [0, n0) and receives every helper's uint8 images over RCCL (gloo on
+        CPU children), then encodes the one envelope itself.  A part whose child
+        dies leaves its peers blocked in a transfer, so the other parts' children
+        are killed too (each restarts; the group re-forms when idle)."""
+        from .generator import _error_result
+
+        jid = job.get("id")
+        rngs = _ranges(n, len(exs))
+        ranks = [e.group["rank"] for e in exs]
+        subs = [dict(job, id=jid, seed=seed, num_images_per_prompt=rngs[0][1] - rngs[0][0], _image_range=list(rngs[0]),
+                     _split={"role": "leader", "peers": ranks[1:]})]
+        for i in range(1, len(exs)):
+            lo, hi = rngs[i]
+            subs.append(dict(job, id=f"{jid}#{i}", seed=seed, num_images_per_prompt=hi - lo, _image_range=[lo, hi],
+                             _split={"role": "helper", "leader": ranks[0]}))
+        restarts0 = [e.restarts for e in exs]
+        tasks = [asyncio.ensure_future(e.run(sj)) for e, sj in zip(exs, subs)]
+        pending = set(tasks)
+        while pending:
+            done, pending = await asyncio.wait(pending, return_when=asyncio.FIRST_COMPLETED)
+            if any(e.restarts != r0 for e, r0 in zip(exs, restarts0)):
+                for e, t in zip(exs, tasks):  # a part crashed: its peers may wait on it forever
+                    if not t.done():
+                        e.kill()
+        results = [t.result() for t in tasks]
+        lead = results[0]
+        helper_ok = all("_split_ack" in (r.get("pipeline_config") or {}) for r in results[1:])
+        if lead.get("artifacts") and helper_ok and "error" not in (lead.get("pipeline_config") or {}):
+            self.splits += 1
+            lead["pipeline_config"]["seed"] = seed
+            return lead
+        bad = next((r for r in results if "error" in (r.get("pipeline_config") or {})), lead)
+        return dict(bad, id=jid) if bad.get("pipeline_config") else \
+            _error_result(jid, RuntimeError("split job failed"), job.get("content_type", "image/jpeg"), False)
+
     async def preload(self, names):
-        """Every executor loads the same models together (sharded reads + all_gather)."""
+        """Every executor loads the same models: collectively (sharded reads +
+        all_gather) while the group is healthy, otherwise each on its own.  A
+        child dying mid-collective restarts every group child (the survivors may
+        be blocked in the collective) and the preload is abandoned."""
         names = [n for n in names if n]
-        if not names:
+        exs = [ex for ex in self.executors if hasattr(ex, "preload")]
+        if not names or not exs:
             return []
-        return await asyncio.gather(*(ex.preload(names) for ex in self.executors if hasattr(ex, "preload")))
+        collective = self.group_ok()
+        if not collective and any(getattr(e, "group", {}).get("error") for e in exs):
+            logging.warning("process group incomplete: " + "; ".join(getattr(e, "ready_info", "") for e in exs))
+        tasks = [asyncio.ensure_future(ex.preload(names, collective=collective)) for ex in exs]
+        pending = set(tasks)
+        killed = False
+        while pending:
+            done, pending = await asyncio.wait(pending, return_when=asyncio.FIRST_COMPLETED)
+            if collective and not killed and any(t.exception() is not None for t in done):
+                killed = True
+                for ex, t in zip(exs, tasks):  # peers of a dead rank are stuck in the all_gather
+                    if not t.done():
+                        ex.kill()
+        failed = [t.exception() for t in tasks if t.exception() is not None]
+        if failed:
+            raise RuntimeError(f"preload failed on {len(failed)} device(s): {failed[0]}")
+        return [t.result() for t in tasks]
 
     def _drain_compatible(self, first) -> list:
         """Take queued jobs that can share ``first``'s UNet batch (cheap raw-job
@@ -365,7 +551,11 @@ class Supervisor:
     async def device_worker(self, ex):
         lock = self.locks[id(ex)]
         while True:
-            job = await self.work_queue.get()
+            self.idle.add(ex)
+            try:
+                job = await self.work_queue.get()
+            finally:
+                self.idle.discard(ex)
             batch = self._drain_compatible(job)
             self.busy += len(batch)
             helpers = []
@@ -418,6 +608,7 @@ class Supervisor:
         polls = 0
         try:
             while not self.stop.is_set():
+                await self._maybe_regroup()
                 while (self.work_queue.full() or
                        self.busy + self.work_queue.qsize() >= len(self.executors) * self.batch_jobs) \
                         and not self.stop.is_set():
@@ -439,19 +630,17 @@ class Supervisor:
                 t.cancel()
 
 
-def group_envs(n: int, settings=None, port: int | None = None) -> list:
-    """Per-child process-group environment (RANK, WORLD_SIZE, MASTER_*)."""
+def group_envs(n: int, settings=None, store: GroupStore | None = None) -> list:
+    """Per-child process-group environment (RANK, WORLD_SIZE and the
+    supervisor-hosted store's port / generation); hosts the store if none given."""
     if n <= 1 or (settings is not None and not getattr(settings, "distributed", True)):
         return [{} for _ in range(n)]
-    if port is None:
-        import socket
-
-        sk = socket.socket()
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-        sk.close()
-    return [{"RANK": str(i), "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
-             "HSA_ENABLE_IPC_MODE_LEGACY": "0"} for i in range(n)]
+    if store is None:
+        store = GroupStore()
+        _STORES.append(store)
+    return [{"RANK": str(i), "WORLD_SIZE": str(n), "SDAAS_STORE_HOST": store.host, "SDAAS_STORE_PORT": str(store.port),
+             "SDAAS_GROUP_GEN": str(store.gen), "MASTER_ADDR": store.host, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+            for i in range(n)]
 
 
 def startup(settings=None, require_gpu=True):

@@ -72,12 +72,21 @@ class Scheduler:
     name = "base"
     order = 1
     space = "vp"
+    default_spacing = "linspace"
     karras_full_range = False  # DPM-Solver: Karras over the whole training sigma range  # "vp": sample lives in x_t = a x0 + s eps; "k": x = x0 + sigma eps
 
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
                  beta_schedule="scaled_linear", prediction_type="epsilon", use_karras_sigmas=True,
-                 steps_offset=1, thresholding=False, dynamic_thresholding_ratio=0.995, sample_max_value=1.0, **_):
+                 steps_offset=1, thresholding=False, dynamic_thresholding_ratio=0.995, sample_max_value=1.0,
+                 timestep_spacing=None, clip_sample=False, clip_sample_range=1.0, **_):
         self.T = num_train_timesteps
+        # the checkpoint's scheduler_config.json fields (models/hf_config.scheduler_kwargs)
+        timestep_spacing = timestep_spacing or self.default_spacing  # diffusers: each class's own default
+        if timestep_spacing not in ("linspace", "leading", "trailing"):
+            raise ValueError(f"timestep_spacing={timestep_spacing!r} is not supported")
+        self.timestep_spacing = timestep_spacing
+        self.clip_sample = bool(clip_sample)
+        self.clip_sample_range = float(clip_sample_range)
         # Imagen dynamic thresholding of the x0 prediction (DeepFloyd IF:
         # ratio 0.95, max 1.5) -- non-linear in x0, so those steps skip the fused kernel
         self.thresholding = thresholding
@@ -103,9 +112,22 @@ class Scheduler:
         w = np.clip((lo - log_sigma) / (lo - hi), 0, 1)
         return float((1 - w) * low + w * high)
 
+    def _spaced_timesteps(self, n):
+        """Decreasing inference timesteps per ``timestep_spacing`` (diffusers
+        semantics): "linspace" n points over [0, T-1] (the DPM-Solver form:
+        n + 1 rounded points, last dropped), "leading" multiples of T // n
+        plus ``steps_offset``, "trailing" from T - 1 down in steps of T / n."""
+        if self.timestep_spacing == "leading":
+            ts = (np.arange(0, n) * (self.T // n)).round()[::-1].astype(np.float64) + self.steps_offset
+        elif self.timestep_spacing == "trailing":
+            ts = np.round(np.arange(self.T, 0, -self.T / n)).astype(np.float64) - 1
+        else:
+            ts = np.linspace(0, self.T - 1, n + 1).round()[::-1][:-1]
+        return np.clip(ts, 0, self.T - 1).copy()
+
     def _ladder(self, n):
         """Decreasing sigma ladder of length n (+ final sigma appended by caller)."""
-        ts = np.linspace(0, self.T - 1, n + 1).round()[::-1][:-1].copy()
+        ts = self._spaced_timesteps(n)
         sig = np.interp(ts, np.arange(self.T), self.train_sigmas)
         if self.use_karras:
             if self.karras_full_range:
@@ -178,13 +200,37 @@ class Scheduler:
     def fused_coeffs(self) -> StepCoeffs | None:
         """Coefficients for the fused HIP step kernel, or None if this step must
         run through ``step`` (non-linear-form samplers)."""
-        if self.thresholding:
+        if self.thresholding or self.clip_sample:
             return None
         return self.coeffs(self.step_index)
+
+    def loop_table(self):
+        """The remaining steps as a device-loop table, or None when a step is
+        not the plain linear form (thresholding, two evaluations per step, a
+        sampler-specific ``step``): ``(timesteps, rows, s_first)`` with one
+        ``[p, q, A, B, C, D, s_next]`` row per step from ``step_index`` on and
+        the input scale of the first evaluation.  Every row is a pure function
+        of its step index, so the table is exactly what ``fused_coeffs`` would
+        return step by step."""
+        cls = type(self)
+        if (self.thresholding or self.clip_sample or cls.step is not Scheduler.step or cls.current_t is not Scheduler.current_t
+                or cls.current_scale is not Scheduler.current_scale
+                or cls.fused_coeffs is not Scheduler.fused_coeffs or self.num_evals != self.n):
+            return None
+        rows = []
+        for i in range(self.step_index, self.n):
+            c = self.coeffs(i)
+            if c is None:
+                return None
+            rows.append([c.p, c.q, c.A, c.B, c.C, c.D, c.s_next])
+        ts = [float(t) for t in self.timesteps[self.step_index:self.n]]
+        return ts, rows, self.current_scale()
 
     def threshold_x0(self, x0: torch.Tensor) -> torch.Tensor:
         """Per-sample dynamic thresholding: s = quantile(|x0|, ratio) clamped to
         [1, sample_max]; x0 -> clamp(x0, -s, s) / s (identity when disabled)."""
+        if self.clip_sample and not self.thresholding:
+            return x0.clamp(-self.clip_sample_range, self.clip_sample_range)
         if not self.thresholding:
             return x0
         b = x0.shape[0]
@@ -305,10 +351,10 @@ class DDIMScheduler(Scheduler):
 
     name = "DDIMScheduler"
 
+    default_spacing = "leading"
+
     def _ladder(self, n):
-        ratio = self.T // n
-        ts = (np.arange(0, n) * ratio).round()[::-1].astype(np.float64) + self.steps_offset
-        ts = np.clip(ts, 0, self.T - 1)
+        ts = self._spaced_timesteps(n)
         sig = self.train_sigmas[ts.astype(int)]
         return ts, sig
 

@@ -118,6 +118,110 @@ CSK_API int csk_sched_step(void* xn, void* x0o, const void* e, const void* x, co
 }
 
 // --------------------------------------------------------------------------
+// Device-resident sampler loop (one hipGraph replay per denoising step, no
+// host work between replays).  The per-step scalars live in a device table
+// indexed by a device step counter:
+//   loop_prologue (1 thread, head of the step graph): cur = counter++,
+//     t_out = t_tab[cur]  -> the UNet's timestep input;
+//   sched_loop (tail of the step graph): coefficients coef[cur] =
+//     {p, q, A, B, C, D, s_next, g, g2, -, -, -} (g / g2: the request's guidance
+//     scales, so one captured graph serves every guidance value), CFG combine (none / 2-way [u, c] /
+//     3-way pix2pix [c, i, u]), x0 = p x + q e, x' = A x + B x0 + C x0prev +
+//     D noise[cur], x and x0prev updated in place, and the NEXT UNet input
+//     written directly: x_in[r] = bf16(s_next x') for every CFG replica r,
+//     channels [0, 4) of a Cin-channel pixel (extra image-latent channels of
+//     pix2pix / 9-channel inpaint stay as set up once per request).
+// Replaces per step: x * s_in, bf16 cast, torch.cat of the CFG copies, the
+// static-input copy, t.fill_ and the separate step launch.
+// --------------------------------------------------------------------------
+__global__ void loop_prologue_kernel(int* __restrict__ counter, int* __restrict__ cur,
+                                     const float* __restrict__ t_tab, float* __restrict__ t_out, int n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int i = *counter;
+    i = i < 0 ? 0 : (i >= n ? n - 1 : i);  // clamp: never index past the table
+    *cur = i;
+    *t_out = t_tab[i];
+    *counter = i + 1;
+  }
+}
+
+CSK_API int csk_loop_prologue(void* counter, void* cur, const void* t_tab, void* t_out, int n, hipStream_t stream) {
+  if (n <= 0) return (int)hipErrorInvalidValue;
+  loop_prologue_kernel<<<1, 64, 0, stream>>>((int*)counter, (int*)cur, (const float*)t_tab, (float*)t_out, n);
+  CSK_CHECK_LAUNCH();
+}
+
+#define LOOP_COEF_STRIDE 12
+__global__ void sched_loop_kernel(const bf16_t* __restrict__ e, float* __restrict__ x, float* __restrict__ x0prev,
+                                  const float* __restrict__ noise_tab, const int* __restrict__ cur,
+                                  const float* __restrict__ coef, bf16_t* __restrict__ xin, int cin, int nrep,
+                                  size_t npix, int mode) {
+  const int idx = *cur;
+  const float* c = coef + (size_t)idx * LOOP_COEF_STRIDE;
+  const float p = c[0], q = c[1], A = c[2], B = c[3], C = c[4], D = c[5], s = c[6], g = c[7], g2 = c[8];
+  const float* nz = (noise_tab != nullptr && D != 0.f) ? noise_tab + (size_t)idx * npix * 4 : nullptr;
+  const size_t n = npix * 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < npix; i += (size_t)gridDim.x * blockDim.x) {
+    float4 xv = reinterpret_cast<const float4*>(x)[i];
+    float4 pv = reinterpret_cast<const float4*>(x0prev)[i];
+    uint2 e0 = reinterpret_cast<const uint2*>(e)[i];
+    float ev[4] = {__uint_as_float(e0.x << 16), __uint_as_float(e0.x & 0xffff0000u), __uint_as_float(e0.y << 16),
+                   __uint_as_float(e0.y & 0xffff0000u)};
+    if (mode >= 1) {
+      uint2 e1 = reinterpret_cast<const uint2*>(e + n)[i];
+      float cv[4] = {__uint_as_float(e1.x << 16), __uint_as_float(e1.x & 0xffff0000u), __uint_as_float(e1.y << 16),
+                     __uint_as_float(e1.y & 0xffff0000u)};
+      if (mode == 1) {  // [u, c]: e = u + g (c - u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ev[j] = ev[j] + g * (cv[j] - ev[j]);
+      } else {  // [c, i, u]: e = u + g (c - i) + g2 (i - u)
+        uint2 e2 = reinterpret_cast<const uint2*>(e + 2 * n)[i];
+        float uv[4] = {__uint_as_float(e2.x << 16), __uint_as_float(e2.x & 0xffff0000u),
+                       __uint_as_float(e2.y << 16), __uint_as_float(e2.y & 0xffff0000u)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ev[j] = uv[j] + g * (ev[j] - cv[j]) + g2 * (cv[j] - uv[j]);
+      }
+    }
+    float nv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (nz != nullptr) {
+      float4 t = reinterpret_cast<const float4*>(nz)[i];
+      nv[0] = t.x; nv[1] = t.y; nv[2] = t.z; nv[3] = t.w;
+    }
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    const float ps[4] = {pv.x, pv.y, pv.z, pv.w};
+    float o[4], z[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      z[j] = p * xs[j] + q * ev[j];
+      o[j] = A * xs[j] + B * z[j] + C * ps[j] + D * nv[j];
+    }
+    reinterpret_cast<float4*>(x)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(x0prev)[i] = make_float4(z[0], z[1], z[2], z[3]);
+    const u32 lo = pack2(s * o[0], s * o[1]), hi = pack2(s * o[2], s * o[3]);
+    for (int r = 0; r < nrep; ++r) {
+      bf16_t* dst = xin + ((size_t)r * npix + i) * cin;
+      if ((cin & 3) == 0) {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+      } else {
+        dst[0] = (bf16_t)(lo & 0xffffu); dst[1] = (bf16_t)(lo >> 16);
+        dst[2] = (bf16_t)(hi & 0xffffu); dst[3] = (bf16_t)(hi >> 16);
+      }
+    }
+  }
+}
+
+CSK_API int csk_sched_loop(const void* e, void* x, void* x0prev, const void* noise_tab, const void* cur,
+                           const void* coef, void* xin, int cin, int nrep, long long npix, int mode,
+                           hipStream_t stream) {
+  if (cin < 4 || nrep < 1 || nrep > 3 || npix <= 0 || mode < 0 || mode > 2 || (mode > 0 && mode + 1 != nrep))
+    return (int)hipErrorInvalidValue;
+  sched_loop_kernel<<<ew_grid((size_t)npix / 2 + 1), 256, 0, stream>>>(
+      (const bf16_t*)e, (float*)x, (float*)x0prev, (const float*)noise_tab, (const int*)cur, (const float*)coef,
+      (bf16_t*)xin, cin, nrep, (size_t)npix, mode);
+  CSK_CHECK_LAUNCH();
+}
+
+// --------------------------------------------------------------------------
 // VAE post-process: NHWC bf16 [-1,1], C channels (3) -> uint8 NHWC.
 // --------------------------------------------------------------------------
 __global__ void vae_post_kernel(const bf16_t* __restrict__ x, unsigned char* __restrict__ y, size_t n) {

@@ -72,6 +72,9 @@ def test_packed_cache_round_trip(tmp_path, monkeypatch):
     for sub, m in (("unet", src.unet), ("vae", src.vae), ("text_encoder", src.text_encoders[0])):
         os.makedirs(d / sub)
         save_file({k: v.contiguous() for k, v in m.state_dict().items()}, str(d / sub / "m.safetensors"))
+    from test_checkpoints import _train_bpe
+
+    _train_bpe(str(d / "tokenizer"))  # real weights need their tokenizer (strict loads)
     a = StableDiffusion("tiny", device="cpu", seed=1, weights_dir=str(d))
     assert all(not isinstance(r, str) for r in a.load_reports.values())
     calls = []

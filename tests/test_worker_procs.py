@@ -83,6 +83,9 @@ def _save_tiny_model(root):
     for sub, m in (("unet", pipe.unet), ("vae", pipe.vae), ("text_encoder", pipe.text_encoders[0])):
         os.makedirs(d / sub, exist_ok=True)
         save_file({k: v.contiguous() for k, v in m.state_dict().items()}, str(d / sub / "model.safetensors"))
+    from tests.test_checkpoints import _train_bpe
+
+    _train_bpe(str(d / "tokenizer"))  # real weights need their tokenizer (strict loads)
     return d
 
 
@@ -123,6 +126,7 @@ def test_group_preload_and_split_job_matches_unsplit(sdaas_root):
         sup = asyncio.run(main())
         assert all(e.ready.wait(5) for e in exs)
         assert all("gloo rank" in e.ready_info for e in exs), [e.ready_info for e in exs]
+        assert sup.group_ok() and sup.store is not None  # the rendezvous lives in the supervisor
         assert sup.splits == 1
         res = hive.results[0]
         assert res["id"] == "multi" and res["pipeline_config"]["split"] == 2
@@ -134,5 +138,79 @@ def test_group_preload_and_split_job_matches_unsplit(sdaas_root):
         assert d.mean() < 0.5 and d.max() <= 24  # same seeds per image; only batch-size summation order differs
     finally:
         hive.stop()
+        for e in exs:
+            e.close()
+
+
+def test_rank0_crash_survivors_restart_and_regroup(sdaas_root):
+    """World 3 (gloo): rank 0's child dies in the middle of a job.  The store is
+    the supervisor's, so the survivors keep serving; the restarted child serves
+    rank-local; the idle supervisor re-forms the group (generation 1) and a
+    split job then runs over it again (images sent rank-to-rank)."""
+    _save_tiny_model(sdaas_root)
+    exs = [ProcessExecutor("cpu", env=e, job_timeout_s=300) for e in group_envs(3)]
+    try:
+        s = Settings()
+        s.max_batch = 1
+
+        async def main():
+            sup = Supervisor(s, executors=exs, hive=FakeHive(jobs=[]))
+            for e in exs:
+                await asyncio.get_running_loop().run_in_executor(None, e.ready.wait, 120)
+            assert sup.group_ok()
+            crashed = await exs[0].run({"id": "c", **TINY, "_test": "exit"})
+            assert "crashed" in crashed["pipeline_config"]["error"] and exs[0].restarts == 1
+            await asyncio.get_running_loop().run_in_executor(None, exs[0].ready.wait, 120)
+            assert not sup.group_ok()  # the fresh child is rank-local: no collectives now
+            later = await asyncio.gather(*(e.run({"id": f"j{i}", **TINY, "seed": 5}) for i, e in enumerate(exs)))
+            for r in later:
+                assert "error" not in r["pipeline_config"], r["pipeline_config"]
+            imgs = [_img(r) for r in later]
+            assert all(np.array_equal(imgs[0], im) for im in imgs[1:])
+            assert await sup.regroup()
+            assert all(e.group["gen"] == 1 for e in exs)
+            job = {"id": "multi", **TINY, "seed": 99, "num_images_per_prompt": 3, "content_type": "image/png"}
+            res = await sup._run_split(job, list(exs))
+            return sup, res
+
+        sup, res = asyncio.run(main())
+        assert sup.splits == 1 and res["id"] == "multi"
+        assert res["pipeline_config"]["split"] == 3 and res["pipeline_config"]["seed"] == 99
+        assert _img(res).shape[:2] == (128, 128)  # 3 images -> 2x2 grid of 64x64
+    finally:
+        for e in exs:
+            e.close()
+
+
+def test_rank_dying_mid_preload_does_not_wedge_the_node(sdaas_root):
+    """A child that dies inside a collective preload: the supervisor kills any
+    peer still blocked in the all_gather, reports the preload as failed within
+    seconds (not after the 3600 s preload timeout), and every child serves jobs."""
+    import time
+
+    _save_tiny_model(sdaas_root)
+    exs = [ProcessExecutor("cpu", env=e, job_timeout_s=300) for e in group_envs(2)]
+    try:
+        s = Settings()
+        s.max_batch = 1
+
+        async def main():
+            sup = Supervisor(s, executors=exs, hive=FakeHive(jobs=[]))
+            for e in exs:
+                await asyncio.get_running_loop().run_in_executor(None, e.ready.wait, 120)
+            t0 = time.monotonic()
+            with pytest.raises(RuntimeError, match="preload failed"):
+                await sup.preload(["__test_exit__", "tiny/sd"])
+            dt = time.monotonic() - t0
+            return dt, await asyncio.gather(*(e.run({"id": f"p{i}", **TINY, "seed": 2}) for i, e in enumerate(exs)))
+
+        dt, res = asyncio.run(main())
+        assert dt < 120
+        # the dead rank is restarted; its peer was either killed out of the wedged
+        # all_gather (restarted too) or saw the broken group itself and returned
+        assert exs[1].restarts == 1
+        for r in res:
+            assert "error" not in r["pipeline_config"], r["pipeline_config"]
+    finally:
         for e in exs:
             e.close()
