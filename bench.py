@@ -11,10 +11,16 @@ CFG batch), 50 DPM-Solver++(2M) Karras denoising steps of the full SD2.1 UNet
 (865.9M params) on the CFG batch of 8 latents 64x64, VAE decode 512x512, uint8
 D2H, and JPEG/base64/sha256 result-envelope encoding (in encoder processes,
 overlapped with the next job, joined before the clock stops).  Data-parallel over GPUs
-(one process per GPU, weak scaling: 4 images per GPU per step); weights are
-random-init on every rank and distributed with a sharded RCCL all_gather
-(outside the timed region); each rank's final latents are all-gathered to
-every rank over xGMI (split-job assembly, inside the timed region).
+(one process per GPU, weak scaling: 4 images per GPU per step; each rank's
+job is an independent request, exactly the reference's one-job-per-GPU node
+model, so no collective runs inside the timed region).
+
+Model load (outside the timed region, reported as ``model_load_s``): the
+random-init weights are written ONCE as a diffusers-layout safetensors
+directory (rank 0, /dev/shm), then every rank loads them through the
+production loader: with N > 1 ranks each reads only 1/N of the checkpoint
+bytes and one RCCL ``all_gather`` per dtype over xGMI assembles the rest
+(parallel/sharded.py); ``load_bytes_read_per_rank`` reports the share read.
 
 ``--impl reference`` runs the same models with plain PyTorch ops (hipBLASLt
 GEMMs, MIOpen channels-last convs, SDPA) = the diffusers-style eager baseline
@@ -72,14 +78,10 @@ def main():
     if args.impl == "hip" and on_gpu:
         ops._lib.load()  # fail loudly: the HIP path must be the one measured
 
-    t_load = time.perf_counter()
     pipe = StableDiffusion(args.family, device=device, seed=1234)
     if args.no_graphs:
         pipe.use_graphs = False
-    # sharded RCCL distribution of the (random-init) weights to every GPU
-    for m in [pipe.unet, pipe.vae] + pipe.text_encoders:
-        comm.allgather_module(m)
-    load_s = time.perf_counter() - t_load
+    load_s, load_bytes = load_through_checkpoint(pipe, rank, world)
 
     prompts = ["a photograph of an astronaut riding a horse", "a watercolor fox in a snowy forest",
                "a cyberpunk city street at night, neon", "a bowl of ramen, studio lighting"]
@@ -91,11 +93,9 @@ def main():
                    num_inference_steps=args.denoise_steps, guidance_scale=args.guidance,
                    num_images_per_prompt=args.batch, height=args.res, width=args.res,
                    generator=g, scheduler=sched, output_type="uint8")
-        gathered = comm.all_gather_tensor(out.latents.contiguous())  # split-job assembly over xGMI
-
         # JPEG/base64/sha256 envelope encoding in the encoder processes, overlapped
         # with the next job (joined before the clock stops)
-        return pool.submit(list(out.images.numpy()), "image/jpeg"), out.timings, gathered.shape
+        return pool.submit(list(out.images.numpy()), "image/jpeg"), out.timings, out.latents.shape
 
     futs = []
     for i in range(args.warmup):
@@ -160,11 +160,60 @@ def main():
             "p50_job_latency_ms": round(1000 * p50, 1),
             "phase_ms_median": phase,
             "model_load_s": round(load_s, 2),
+            "load_bytes_read_per_rank": load_bytes,
+            "load_path": "safetensors dir -> sharded byte-range reads + RCCL all_gather" if world > 1 else
+                         "safetensors dir -> local read",
         }
         print(json.dumps(rec), flush=True)
     pool.shutdown()
     if comm.is_dist():
         torch.distributed.destroy_process_group()
+
+
+def load_through_checkpoint(pipe, rank, world):
+    """Write the pipeline's weights once as safetensors (rank 0, /dev/shm), then
+    load them on every rank through models/weights.load_component inside
+    ``collective_loading`` (sharded reads + all_gather with N > 1).  Returns
+    (seconds, bytes this rank read from the files)."""
+    import shutil
+    import tempfile
+
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.models.layers import prepare_model
+    from chiaswarm_amd.models.weights import _VAE_RENAMES, load_component
+    from chiaswarm_amd.parallel import comm, sharded
+
+    parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)] + \
+        [("text_encoder" if i == 0 else f"text_encoder_{i + 1}", m, None) for i, m in enumerate(pipe.text_encoders)]
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    root = os.path.join(base, f"chiaswarm_bench_{os.getuid()}_{os.environ.get('MASTER_PORT', os.getpid())}")
+    if rank == 0:
+        for sub, m, _ in parts:
+            os.makedirs(os.path.join(root, sub), exist_ok=True)
+            save_file({k: v.detach().contiguous().cpu() for k, v in m.state_dict().items()},
+                      os.path.join(root, sub, "model.safetensors"))
+    comm.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nbytes = 0
+    with comm.collective_loading():
+        for sub, m, ren in parts:
+            load_component(m, root, sub, ren)
+            if comm.collective_load_active() and sharded.LAST_READER is not None:
+                nbytes += sharded.LAST_READER.read_bytes
+            else:
+                nbytes += sum(os.path.getsize(f) for f in sharded.safetensors_files(os.path.join(root, sub)))
+            prepare_model(m)  # re-pack for the kernels (fused QKV, NHWC conv weights ...)
+    pipe.invalidate_graphs()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    load_s = comm.max_over_ranks(time.perf_counter() - t0)
+    comm.barrier()
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+    return load_s, nbytes
 
 
 if __name__ == "__main__":

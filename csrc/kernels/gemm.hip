@@ -451,11 +451,23 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else tile = 4;
   }
   int err;
-  if (tile >= 31) {
+  if (tile >= 31 && tile <= 34) {  // 8-wave phased / ring tiles (gemm8p.hip); 40+: gemm_glds.hip
     err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
-    // fallback keeps the GN-statistics segment the host sized for: tile 33's
-    // / 34's 64-row band = tile 26's (128x160, two bands); 31 / 32's 128 = tile 11's
-    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, tile >= 33 ? 26 : 11, ksplit, CONV, s);
+    if (err == (int)hipErrorNotSupported) {
+      // the fallback must write the GN-statistics segments the host sized gn_part
+      // for (hip_ops._gn_seg of the REQUESTED tile): 33 / 34 (64-row band) ->
+      // tile 26 (128x160, two bands); 31 / 32 -> tile 11 only when its segment
+      // matches (fine segments: 31 / 32 write 128 rows, tile 11 64 -> an
+      // out-of-bounds gn_part write).  A mismatch fails loudly instead.
+      const int fb = tile >= 33 ? 26 : 11;
+      if (a.gn_part && ksplit == 1) {
+        const int want = tile >= 33 ? (tile == 33 ? gn_seg_for<256, 160, 4>() : gn_seg_for<256, 128, 4>())
+                                    : 128;  // launch8p: min(BN or 256, one 128-row band)
+        const int got = fb == 26 ? gn_seg_for<128, 160, 2>() : gn_seg_for<128, 128, 2>();
+        if (want != got) return (int)hipErrorInvalidValue;
+      }
+      err = csk_gemm_glds_launch(a, fb, ksplit, CONV, s);
+    }
   } else if (tile >= 11) {
     err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
   } else {

@@ -1,0 +1,133 @@
+#!/usr/bin/env python
+"""Exact per-call kernel time of one SD2.1 UNet step (CFG batch 8, 64x64):
+every libcsk call is followed by a 1-element int32 fill, so in a rocprofv3
+kernel trace the separator kernels split the dispatch stream into calls; the
+calls' shapes are recorded on the host in the same order.  No host syncs, so
+the kernels run back to back as in the hipGraph (durations are device time).
+
+    rocprofv3 --kernel-trace -d OUT -o cp -- python tools/callprof.py --record OUT/calls.json
+    python tools/callprof.py --db OUT/.../cp_results.db --calls OUT/calls.json
+"""
+import argparse
+import collections
+import glob
+import json
+import os
+import sqlite3
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def record(path, batch, iters):
+    import torch
+
+    from chiaswarm_amd.models import unet as unet_mod
+    from chiaswarm_amd.models.layers import init_random_fast_, prepare_model
+    from chiaswarm_amd.ops import _lib
+    from stepshapes import flops_of
+
+    _lib.load()
+    dev = torch.device("cuda", 0)
+    with torch.device(dev):
+        m = unet_mod.UNet2DConditionModel(unet_mod.SD21).to(torch.bfloat16).eval().requires_grad_(False)
+    init_random_fast_(m, seed=0)
+    prepare_model(m)
+    x = torch.randn(batch, 64, 64, 4, device=dev).to(torch.bfloat16)
+    ctx = torch.randn(batch, 77, 1024, device=dev).to(torch.bfloat16)
+    kv = m.encode_context(ctx)
+    t = torch.tensor([500.0], device=dev)
+    with torch.no_grad():
+        for _ in range(2):
+            m(x, t, cross_kv=kv)
+    torch.cuda.synchronize()
+    sep = torch.zeros(1, dtype=torch.int32, device=dev)
+    orig = _lib.call
+    seq = []
+
+    def wrapped(name, *args):
+        orig(name, *args)
+        sep.fill_(len(seq))
+        label, fl, tile = flops_of(name, args)
+        seq.append([label, fl, tile])
+
+    _lib.call = wrapped
+    with torch.no_grad():
+        for _ in range(iters):
+            m(x, t, cross_kv=kv)
+    torch.cuda.synchronize()
+    _lib.call = orig
+    with open(path, "w") as f:
+        json.dump({"iters": iters, "calls": seq}, f)
+    print(f"recorded {len(seq)} calls")
+
+
+def analyse(db, calls_path, out_json=""):
+    with open(calls_path) as f:
+        meta = json.load(f)
+    calls = meta["calls"]
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    name_col = "name" if "name" in cols else "kernel_name"
+    rows = c.execute(f"select {name_col}, start, end from kernels order by start").fetchall()
+    is_sep = [("FillFunctor<int>" in r[0]) for r in rows]
+    sep_idx = [i for i, s in enumerate(is_sep) if s]
+    n = len(calls)
+    if len(sep_idx) < n:
+        raise SystemExit(f"{len(sep_idx)} separators for {n} calls")
+    sep_idx = sep_idx[-n:]  # the recorded calls are the last n separated groups
+    agg = collections.OrderedDict()
+    per_kernel = collections.defaultdict(float)
+    prev = sep_idx[0] - 1
+    # the group of call k: the kernels between separator k-1 and separator k
+    first = sep_idx[0]
+    j = first - 1
+    while j >= 0 and not is_sep[j]:
+        j -= 1
+    bounds = [j] + sep_idx
+    total = 0.0
+    for k in range(n):
+        ks = [r for r in rows[bounds[k] + 1:bounds[k + 1]] if "FillFunctor<int>" not in r[0]]
+        us = sum(e - s for _, s, e in ks) / 1e3
+        total += us
+        label, fl, tile = calls[k]
+        key = (label, tile)
+        a = agg.setdefault(key, [0, 0.0, fl, collections.Counter()])
+        a[0] += 1
+        a[1] += us
+        for nm, s, e in ks:
+            a[3][nm.split("(")[0][:60]] += 1
+            per_kernel[nm.split("(")[0][:70]] += (e - s) / 1e3
+    iters = meta.get("iters", 1)
+    print(f"{n} calls over {iters} step(s): {total / iters / 1e3:.3f} ms device time per step")
+    out = []
+    for (label, tile), (cnt, us, fl, kn) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        tf = fl * cnt / (us * 1e-6) / 1e12 if fl and us else 0.0
+        print(f"{us / iters:9.1f} us {cnt // iters:3d}x {us / cnt:8.1f} us {tf:7.1f} TF/s  tile {tile}  {label}  "
+              f"[{', '.join(f'{k}' for k in kn)}]")
+        out.append({"op": label, "tile": tile, "calls_per_step": cnt // iters, "us_each": round(us / cnt, 2),
+                    "us_per_step": round(us / iters, 1), "tflops": round(tf, 1), "kernels": list(kn)})
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump({"ms_per_step": total / iters / 1e3, "rows": out}, f, indent=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--record", default="")
+    ap.add_argument("--db", default="")
+    ap.add_argument("--calls", default="")
+    ap.add_argument("--json", default="")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=2)
+    a = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if a.record:
+        record(a.record, a.batch, a.iters)
+    if a.db:
+        dbs = glob.glob(a.db) or [a.db]
+        analyse(dbs[0], a.calls, a.json)
+
+
+if __name__ == "__main__":
+    main()
