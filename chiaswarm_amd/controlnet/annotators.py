@@ -2,8 +2,7 @@
 which calls controlnet_aux / transformers detectors):
 
   scribble  -> HED (ControlNetHED_Apache2) + scribble post-process (nms, blur, threshold)
-  softedge  -> HED soft edge map (the reference's PiDiNet is a drop-in alternative
-               checkpoint for the same control type)
+  softedge  -> PiDiNet (table5_pidinet: pixel-difference convs folded into plain convs)
   lineart   -> "informative drawings" generator (sk_model / sk_model2 coarse)
   mlsd      -> M-LSD large (MobileNetV2 encoder + line-segment decoder)
   depth     -> DPT-Large (ViT-L/16 + reassemble/fusion neck + depth head)
@@ -37,6 +36,7 @@ from PIL import Image
 _CACHE: dict = {}
 _FILES = {
     "hed": ["ControlNetHED.pth", "hed.safetensors"],
+    "pidinet": ["table5_pidinet.pth", "pidinet.safetensors"],
     "lineart": ["sk_model.pth", "lineart.safetensors"],
     "lineart_coarse": ["sk_model2.pth", "lineart_coarse.safetensors"],
     "mlsd": ["mlsd_large_512_fp32.pth", "mlsd.safetensors"],
@@ -184,6 +184,146 @@ def hed(image: Image.Image, scribble=False, res=512) -> Image.Image:
         out = _nms(out, 127, 3.0)
         out = ndimage.gaussian_filter(out.astype(np.float32), sigma=3.0)
         out = np.where(out > 4, 255, 0).astype(np.uint8)
+    return Image.fromarray(_hwc3(out)).resize(image.size, Image.Resampling.BILINEAR)
+
+
+# ---------------------------------------------------------------------------
+# PiDiNet (pixel-difference network, table5_pidinet.pth: inplane 60, carv4, dil 24, sa)
+# ---------------------------------------------------------------------------
+_AD_PERM = [3, 0, 1, 6, 4, 2, 7, 8, 5]  # clockwise neighbour of each 3x3 tap
+_RD_OUTER = [0, 2, 4, 10, 14, 20, 22, 24]  # 5x5 taps two pixels out along the 8 directions
+_RD_INNER = [6, 7, 8, 11, 13, 16, 17, 18]  # ... and one pixel out
+
+
+class PDConv(nn.Module):
+    """A pixel-difference convolution stored as its raw 3x3 weight (checkpoint
+    layout) and run as the equivalent plain convolution: 'cd' central
+    differences fold into the centre tap, 'ad' angular differences into a
+    rotated copy, 'rd' radial differences into a 5x5 kernel; 'cv' is vanilla."""
+
+    def __init__(self, kind, cin, cout, groups=1):
+        super().__init__()
+        self.kind, self.groups = kind, groups
+        self.weight = nn.Parameter(torch.empty(cout, cin // groups, 3, 3))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+
+    def effective(self):
+        w = self.weight
+        o, i = w.shape[:2]
+        if self.kind == "cd":
+            return w - F.pad(w.sum((2, 3), keepdim=True), (1, 1, 1, 1)), 1
+        if self.kind == "ad":
+            f = w.reshape(o, i, 9)
+            return (f - f[:, :, _AD_PERM]).reshape(o, i, 3, 3), 1
+        if self.kind == "rd":
+            f = w.reshape(o, i, 9)[:, :, 1:]
+            b = w.new_zeros(o, i, 25)
+            b[:, :, _RD_OUTER] = f
+            b[:, :, _RD_INNER] = -f
+            return b.reshape(o, i, 5, 5), 2
+        return w, 1
+
+    def forward(self, x):
+        w, pad = self.effective()
+        return F.conv2d(x, w, None, 1, pad, 1, self.groups)
+
+
+class PDCBlock(nn.Module):
+    def __init__(self, kind, cin, cout, stride=1):
+        super().__init__()
+        self.stride = stride
+        if stride > 1:
+            self.shortcut = nn.Conv2d(cin, cout, 1)
+        self.conv1 = PDConv(kind, cin, cin, groups=cin)
+        self.conv2 = nn.Conv2d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        if self.stride > 1:
+            x = F.max_pool2d(x, 2, 2)
+        y = self.conv2(F.relu(self.conv1(x)))
+        return y + (self.shortcut(x) if self.stride > 1 else x)
+
+
+class _CDCM(nn.Module):
+    """Compact dilation convolution module: 1x1 then four dilated 3x3s, summed."""
+
+    def __init__(self, cin, c):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, c, 1)
+        for j, d in enumerate((5, 7, 9, 11)):
+            setattr(self, f"conv2_{j + 1}", nn.Conv2d(c, c, 3, padding=d, dilation=d, bias=False))
+
+    def forward(self, x):
+        x = self.conv1(F.relu(x))
+        return self.conv2_1(x) + self.conv2_2(x) + self.conv2_3(x) + self.conv2_4(x)
+
+
+class _CSAM(nn.Module):
+    """Compact spatial attention: a sigmoid gate from 1x1 (to 4) + 3x3 (to 1)."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.conv1 = nn.Conv2d(c, 4, 1)
+        self.conv2 = nn.Conv2d(4, 1, 3, padding=1, bias=False)
+
+    def forward(self, x):
+        return x * torch.sigmoid(self.conv2(self.conv1(F.relu(x))))
+
+
+class _MapReduce(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, 1, 1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class PiDiNet(nn.Module):
+    """Four stages of pixel-difference blocks (C, 2C, 4C, 4C channels), per-stage
+    CDCM + CSAM + 1-channel side output upsampled to full size, fused by a
+    1x1 classifier; returns the sigmoid side maps and the fused map last."""
+
+    def __init__(self, inplane=60, pdcs=("cd", "ad", "rd", "cv") * 4, dil=24):
+        super().__init__()
+        self.init_block = PDConv(pdcs[0], 3, inplane)
+        planes = [inplane, 2 * inplane, 4 * inplane, 4 * inplane]
+        cin, idx = inplane, 1
+        for s in range(4):
+            for j in range(4 if s else 3):
+                stride = 2 if (s and j == 0) else 1
+                setattr(self, f"block{s + 1}_{j + 1}", PDCBlock(pdcs[idx], cin, planes[s], stride))
+                cin, idx = planes[s], idx + 1
+        self.dilations = nn.ModuleList([_CDCM(p, dil) for p in planes])
+        self.attentions = nn.ModuleList([_CSAM(dil) for _ in planes])
+        self.conv_reduces = nn.ModuleList([_MapReduce(dil) for _ in planes])
+        self.classifier = nn.Conv2d(4, 1, 1)
+
+    def stage_blocks(self, s):
+        return [getattr(self, f"block{s + 1}_{j + 1}") for j in range(4 if s else 3)]
+
+    def forward(self, x):
+        H, W = x.shape[2:]
+        h = self.init_block(x)
+        side = []
+        for s in range(4):
+            for b in self.stage_blocks(s):
+                h = b(h)
+            e = self.conv_reduces[s](self.attentions[s](self.dilations[s](h)))
+            side.append(F.interpolate(e, size=(H, W), mode="bilinear", align_corners=False))
+        side.append(self.classifier(torch.cat(side, 1)))
+        return [torch.sigmoid(e) for e in side]
+
+
+@torch.no_grad()
+def pidinet(image: Image.Image, res=512, apply_filter=False) -> Image.Image:
+    """controlnet_aux PidiNetDetector: BGR in [0, 1], fused (last) map x 255."""
+    m = _build("pidinet", PiDiNet)
+    img = np.asarray(_resize_short(image.convert("RGB"), res))[:, :, ::-1].astype(np.float32) / 255.0
+    edge = m(_to_tensor(img, m))[-1][0, 0].float().cpu().numpy()
+    if apply_filter:
+        edge = (edge > 0.5).astype(np.float32)
+    out = (edge * 255.0).clip(0, 255).astype(np.uint8)
     return Image.fromarray(_hwc3(out)).resize(image.size, Image.Resampling.BILINEAR)
 
 
@@ -565,13 +705,15 @@ class _DPTHead(nn.Module):
 
 
 class DPTDepth(nn.Module):
-    out_indices = (5, 11, 17, 23)
+    """Defaults are Intel/dpt-large (ViT-L/16 at 384, taps after layers 5/11/17/23)."""
 
-    def __init__(self):
+    def __init__(self, c=1024, heads=16, mlp=4096, n=24, patch=16, image=384, out_indices=(5, 11, 17, 23),
+                 neck_sizes=(256, 512, 1024, 1024), factors=(4, 2, 1, 0.5), fusion=256):
         super().__init__()
-        self.dpt = _DPTViT()
-        self.neck = _DPTNeck(1024)
-        self.head = _DPTHead()
+        self.out_indices, self.patch = tuple(out_indices), patch
+        self.dpt = _DPTViT(c, heads, mlp, n, patch, image)
+        self.neck = _DPTNeck(c, neck_sizes, factors, fusion)
+        self.head = _DPTHead(fusion)
 
     def forward(self, x):
         h = self.dpt.embeddings(x)
@@ -580,7 +722,7 @@ class DPTDepth(nn.Module):
             h = layer(h)
             if i in self.out_indices:
                 hs.append(h)
-        gh, gw = x.shape[2] // 16, x.shape[3] // 16
+        gh, gw = x.shape[2] // self.patch, x.shape[3] // self.patch
         return self.head.head(self.neck(hs, gh, gw))[:, 0]
 
 
@@ -676,16 +818,11 @@ class _ConvModule(nn.Module):
         return F.relu(self.batch_norm(self.conv(x)))
 
 
-class _PPMStage(nn.Module):
-    def __init__(self, scale, cin, c):
-        super().__init__()
-        self.scale = scale
-        self.layers = nn.ModuleList([nn.AdaptiveAvgPool2d(scale), _ConvModule(cin, c)])
+class _PPMStage(nn.Sequential):
+    """Pool + 1x1 ConvModule; children named "0"/"1" (psp_modules.<i>.1.conv.weight)."""
 
-    def forward(self, x):
-        for layer in self.layers:
-            x = layer(x)
-        return x
+    def __init__(self, scale, cin, c):
+        super().__init__(nn.AdaptiveAvgPool2d(scale), _ConvModule(cin, c))
 
 
 class UperHead(nn.Module):
@@ -712,10 +849,12 @@ class UperHead(nn.Module):
 
 
 class UperNetConvNext(nn.Module):
-    def __init__(self):
+    """Defaults are openmmlab/upernet-convnext-small (ADE20K, 150 classes)."""
+
+    def __init__(self, dims=(96, 192, 384, 768), depths=(3, 3, 27, 3), c=512, num_classes=150, scales=(1, 2, 3, 6)):
         super().__init__()
-        self.backbone = ConvNextBackbone()
-        self.decode_head = UperHead()
+        self.backbone = ConvNextBackbone(dims, depths)
+        self.decode_head = UperHead(tuple(dims), c, num_classes, scales)
 
     def forward(self, x):
         return self.decode_head(self.backbone(x))

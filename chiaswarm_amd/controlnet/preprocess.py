@@ -8,7 +8,7 @@ Dispatch on ``parameters.controlnet.type`` when ``preprocess`` is true:
   shuffle  -> content shuffle (random smooth flow warp, seeded)
   scribble / softedge / lineart / mlsd / depth / seg / openpose / normalbae
            -> neural annotators (controlnet/annotators.py: HED, informative-
-              drawings lineart, M-LSD, DPT-Large, UperNet-ConvNeXt, OpenPose
+              drawings lineart, PiDiNet, M-LSD, DPT-Large, UperNet-ConvNeXt, OpenPose
               body, NormalBae NNET), resident per process
   a type listed in UNAVAILABLE (none today) -> ValueError -> fatal job error,
               like an incompatible model
@@ -39,7 +39,7 @@ def preprocess_image(image: Image.Image, controlnet: dict) -> Image.Image:
         if t == "scribble":
             return an.hed(image, scribble=True)
         if t == "softedge":
-            return an.hed(image)
+            return an.pidinet(image)
         if t == "lineart":
             return an.lineart(image, coarse=bool(controlnet.get("coarse", False)))
         if t == "mlsd":

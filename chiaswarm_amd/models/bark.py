@@ -63,6 +63,38 @@ class GPTConfig:
     n_codes_given: int = 1
 
 
+def bark_configs_from_hf(raw: dict):
+    """GPT + EnCodec geometry from a transformers ``BarkConfig`` dict
+    (``semantic_config`` / ``coarse_acoustics_config`` / ``fine_acoustics_config``
+    / ``codec_config``) — the config.json beside suno/bark's safetensors."""
+    def gpt(c, causal=True):
+        g = GPTConfig(int(c["input_vocab_size"]), int(c["output_vocab_size"]), int(c["num_layers"]),
+                      int(c["num_heads"]), int(c["hidden_size"]), int(c["block_size"]), bool(c.get("bias", False)),
+                      causal)
+        if not causal:
+            g.n_codes_total, g.n_codes_given = int(c.get("n_codes_total", 8)), int(c.get("n_codes_given", 1))
+        return g
+
+    cc = raw.get("codec_config") or {}
+    fine = gpt(raw["fine_acoustics_config"], causal=False)
+    codec = EncodecConfig(dim=int(cc.get("hidden_size", 128)), n_filters=int(cc.get("num_filters", 32)),
+                          ratios=tuple(cc.get("upsampling_ratios", (8, 5, 4, 2))), n_q=fine.n_codes_total,
+                          bins=int(cc.get("codebook_size", 1024)), lstm_layers=int(cc.get("num_lstm_layers", 2)),
+                          compress=int(cc.get("compress", 2)), kernel=int(cc.get("kernel_size", 7)),
+                          residual_kernel=int(cc.get("residual_kernel_size", 3)),
+                          last_kernel=int(cc.get("last_kernel_size", 7)))
+    unsupported = [k for k, ok in (("num_residual_layers", cc.get("num_residual_layers", 1) == 1),
+                                   ("use_causal_conv", cc.get("use_causal_conv", True)),
+                                   ("pad_mode", cc.get("pad_mode", "reflect") == "reflect"),
+                                   ("use_conv_shortcut", cc.get("use_conv_shortcut", True)),
+                                   ("audio_channels", cc.get("audio_channels", 1) == 1)) if not ok]
+    if unsupported:
+        from .hf_config import UnsupportedConfig
+
+        raise UnsupportedConfig(f"bark codec_config: unsupported {', '.join(unsupported)}")
+    return gpt(raw["semantic_config"]), gpt(raw["coarse_acoustics_config"]), fine, codec
+
+
 def bark_configs(size: str = "large"):
     dims = {"large": (24, 16, 1024), "small": (12, 12, 768), "tiny": (2, 2, 64)}[size]
     ln, nh, ne = dims
@@ -109,9 +141,10 @@ class _Attn(nn.Module):
 class _Block(nn.Module):
     def __init__(self, c: GPTConfig):
         super().__init__()
-        self.layernorm_1 = LayerNorm(c.n_embd, elementwise_affine=True, bias=c.bias)
+        ln_bias = c.bias or not c.causal  # the fine (non-causal) model always has LayerNorm biases
+        self.layernorm_1 = LayerNorm(c.n_embd, elementwise_affine=True, bias=ln_bias)
         self.attn = _Attn(c)
-        self.layernorm_2 = LayerNorm(c.n_embd, elementwise_affine=True, bias=c.bias)
+        self.layernorm_2 = LayerNorm(c.n_embd, elementwise_affine=True, bias=ln_bias)
         self.mlp = nn.Module()
         self.mlp.in_proj = Linear(c.n_embd, 4 * c.n_embd, bias=c.bias)
         self.mlp.out_proj = Linear(4 * c.n_embd, c.n_embd, bias=c.bias)
@@ -208,7 +241,7 @@ class BarkFineGPT(nn.Module):
         self.input_embeds_layers = nn.ModuleList([nn.Embedding(c.in_vocab, c.n_embd) for _ in range(c.n_codes_total)])
         self.position_embeds_layer = nn.Embedding(c.block_size, c.n_embd)
         self.layers = nn.ModuleList([_Block(c) for _ in range(c.n_layer)])
-        self.layernorm_final = LayerNorm(c.n_embd, bias=c.bias)
+        self.layernorm_final = LayerNorm(c.n_embd, bias=True)
         self.lm_heads = nn.ModuleList([Linear(c.n_embd, c.out_vocab, bias=False)
                                        for _ in range(c.n_codes_given, c.n_codes_total)])
 
@@ -237,6 +270,7 @@ class EncodecConfig:
     compress: int = 2
     kernel: int = 7
     residual_kernel: int = 3
+    last_kernel: int = 7
 
     @property
     def hop(self):
@@ -313,7 +347,7 @@ class EncodecDecoder(nn.Module):
             c = scale * cfg.n_filters
             layers += [nn.ELU(), _CausalConvT(c, c // 2, r), _ResBlock(c // 2, cfg.compress, cfg.residual_kernel)]
             scale //= 2
-        layers += [nn.ELU(), _CausalConv(cfg.n_filters, 1, cfg.kernel)]
+        layers += [nn.ELU(), _CausalConv(cfg.n_filters, 1, cfg.last_kernel)]
         self.layers = nn.ModuleList(layers)
 
     @torch.no_grad()
@@ -363,12 +397,23 @@ class Bark:
     def __init__(self, device="cpu", size="large", seed=0, weights_dir=None):
         self.device = torch.device(device)
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-        sc, cc, fc = bark_configs(size)
+        import os
+
+        raw = None
+        if weights_dir and os.path.exists(os.path.join(weights_dir, "config.json")):
+            from .hf_config import read_json
+
+            raw = read_json(os.path.join(weights_dir, "config.json"))
+        if raw and "semantic_config" in raw:
+            sc, cc, fc, ec = bark_configs_from_hf(raw)
+        else:
+            sc, cc, fc = bark_configs(size)
+            ec = TINY_ENCODEC if size == "tiny" else EncodecConfig()
         with torch.device(self.device):
             self.semantic = BarkCausalGPT(sc).to(self.dtype)
             self.coarse = BarkCausalGPT(cc).to(self.dtype)
             self.fine = BarkFineGPT(fc).to(self.dtype)
-            self.codec = EncodecDecoder(TINY_ENCODEC if size == "tiny" else EncodecConfig()).to(self.dtype)
+            self.codec = EncodecDecoder(ec).to(self.dtype)
         self.codec.layers[1].float()  # LSTM in fp32
         mods = [self.semantic, self.coarse, self.fine, self.codec]
         for i, m in enumerate(mods):
@@ -383,28 +428,44 @@ class Bark:
             prepare_model(m)
         from .wordpiece import WordPiece
 
-        import os
-
         tdir = weights_dir if weights_dir and os.path.exists(os.path.join(weights_dir, "vocab.txt")) else None
         self.tokenizer = WordPiece(tdir, vocab_size=119_547, lower=False)
 
     def _load(self, d) -> bool:
+        """transformers ``BarkModel`` safetensors: the three GPTs (strict), the
+        EnCodec decoder (weight norm folded; the encoder is not needed to
+        synthesise) and the first n_q quantizer codebooks."""
         import os
 
-        from .weights import _read_dir, load_into
+        from .weights import CheckpointMismatch, _read_dir, load_into
 
-        n = 0
-        if os.path.isdir(d):
-            sd = fold_weight_norm(_read_dir(d))
-            for pre, mod in (("semantic.", self.semantic), ("coarse_acoustics.", self.coarse),
-                             ("fine_acoustics.", self.fine)):
-                n += load_into(mod, {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)})
-            cb = [sd.get(f"codec_model.quantizer.layers.{i}.codebook.embed") for i in range(self.codec.cfg.n_q)]
-            if all(c is not None for c in cb):
-                with torch.no_grad():
-                    self.codec.codebooks.copy_(torch.stack(cb))
-                n += 1
-        return n > 0
+        if not os.path.isdir(d):
+            return False
+        sd = fold_weight_norm(_read_dir(d))
+        if not sd:
+            return False
+        fine = self.fine.cfg
+        for i in range(fine.n_codes_total - fine.n_codes_given):
+            # the fine model ties lm_heads[i] to input_embeds_layers[i + n_codes_given];
+            # safetensors exports keep only one of each tied pair
+            a, b = f"fine_acoustics.lm_heads.{i}.weight", f"fine_acoustics.input_embeds_layers.{i + fine.n_codes_given}.weight"
+            if a in sd and b not in sd:
+                sd[b] = sd[a]
+            elif b in sd and a not in sd:
+                sd[a] = sd[b]
+        for pre, mod in (("semantic.", self.semantic), ("coarse_acoustics.", self.coarse),
+                         ("fine_acoustics.", self.fine)):
+            # "<layer>.attn.bias" is transformers' causal-mask buffer, not a parameter
+            load_into(mod, {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre) and not k.endswith(".attn.bias")},
+                      name=pre[:-1])
+        pre = "codec_model.decoder."
+        dec = {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)}
+        cb = [sd.get(f"codec_model.quantizer.layers.{i}.codebook.embed") for i in range(self.codec.cfg.n_q)]
+        if any(c is None for c in cb):
+            raise CheckpointMismatch(f"bark: {d} lacks codec_model.quantizer codebooks 0..{self.codec.cfg.n_q - 1}")
+        dec["codebooks"] = torch.stack(cb)
+        load_into(self.codec, dec, name="codec_model.decoder")
+        return True
 
     # -- stage 1 -----------------------------------------------------------
     @torch.no_grad()

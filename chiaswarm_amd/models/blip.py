@@ -88,6 +88,49 @@ def convert_hf_blip(sd: dict) -> dict:
     return out
 
 
+def _convert_text_stack(rest: str, dst: str, v, out: dict, k: str):
+    """One BERT-stack key (after its ``embeddings.`` / ``encoder.layer.`` prefix
+    was split off by the caller) -> this package's names under ``dst``."""
+    if rest.startswith("embeddings."):
+        r = rest.removeprefix("embeddings.")
+        out[dst + r.replace("LayerNorm.", "emb_ln.")] = v
+        return
+    if rest.startswith("encoder.layer."):
+        n, tail = rest.removeprefix("encoder.layer.").split(".", 1)
+        for a, b in _HF_TEXT.items():
+            if tail.startswith(a + "."):
+                out[f"{dst}layers.{n}.{b}.{tail[len(a) + 1:]}"] = v
+                return
+    out[k] = v  # surfaces as an unexpected key
+
+
+def convert_hf_blip_vqa(sd: dict) -> dict:
+    """transformers ``BlipForQuestionAnswering`` state dict -> ``BlipVQA`` keys:
+    ``text_encoder.*`` (BERT over the question, cross-attending to the image)
+    -> ``encoder.*``; ``text_decoder.bert.*`` -> ``decoder.*``; the LM head as in
+    the captioner; the vision tower shared with ``convert_hf_blip``."""
+    out, vis = {}, {}
+    for k, v in sd.items():
+        if k.startswith("text_encoder."):
+            r = k.removeprefix("text_encoder.")
+            if r.startswith("pooler."):
+                continue  # add_pooling_layer=False in the reference model; harmless if present
+            _convert_text_stack(r, "encoder.", v, out, k)
+        elif k.startswith("text_decoder.cls.predictions.decoder."):
+            continue
+        elif k == "text_decoder.cls.predictions.bias":
+            out["head_bias"] = v
+        elif k.startswith("text_decoder.cls.predictions.transform."):
+            r = k.removeprefix("text_decoder.cls.predictions.transform.")
+            out[("head_transform." if r.startswith("dense.") else "head_ln.") + r.split(".", 1)[1]] = v
+        elif k.startswith("text_decoder.bert."):
+            _convert_text_stack(k.removeprefix("text_decoder.bert."), "decoder.", v, out, k)
+        else:
+            vis[k] = v
+    out.update(convert_hf_blip(vis))
+    return out
+
+
 @dataclasses.dataclass
 class BlipConfig:
     image_size: int = 384
@@ -104,6 +147,23 @@ class BlipConfig:
     pad_id: int = 0
 
 
+    patch: int = 16
+    cross_dim: int | None = None  # text_config.encoder_hidden_size (None: vision_dim)
+    cls_id: int = 101
+
+    @classmethod
+    def from_hf(cls, cfg: dict) -> "BlipConfig":
+        """A transformers ``BlipConfig`` config.json (text_config / vision_config)."""
+        t, v = cfg.get("text_config") or {}, cfg.get("vision_config") or {}
+        return cls(image_size=v.get("image_size", 384), vision_dim=v.get("hidden_size", 768),
+                   vision_depth=v.get("num_hidden_layers", 12), vision_heads=v.get("num_attention_heads", 12),
+                   text_dim=t.get("hidden_size", 768), text_depth=t.get("num_hidden_layers", 12),
+                   text_heads=t.get("num_attention_heads", 12), vocab=t.get("vocab_size", 30524),
+                   max_pos=t.get("max_position_embeddings", 512), bos_id=t.get("bos_token_id", 30522),
+                   sep_id=t.get("sep_token_id", 102), pad_id=t.get("pad_token_id", 0),
+                   patch=v.get("patch_size", 16), cross_dim=t.get("encoder_hidden_size"))
+
+
 BLIP_BASE = BlipConfig()
 BLIP_LARGE = BlipConfig(vision_dim=1024, vision_depth=24, vision_heads=16)
 TINY_BLIP = BlipConfig(image_size=64, vision_dim=64, vision_depth=2, vision_heads=2, text_dim=64, text_depth=2,
@@ -117,7 +177,7 @@ class BlipCaptioner(nn.Module):
     def __init__(self, cfg: BlipConfig = BLIP_BASE):
         super().__init__()
         self.cfg = cfg
-        self.vision_model = ViT(cfg.image_size, 16, cfg.vision_dim, cfg.vision_depth, cfg.vision_heads,
+        self.vision_model = ViT(cfg.image_size, cfg.patch, cfg.vision_dim, cfg.vision_depth, cfg.vision_heads,
                                 4 * cfg.vision_dim)
         self.word_embeddings = nn.Embedding(cfg.vocab, cfg.text_dim)
         self.position_embeddings = nn.Embedding(cfg.max_pos, cfg.text_dim)
@@ -165,3 +225,70 @@ class BlipCaptioner(nn.Module):
             ids.append(nxt)
             out.append(nxt)
         return list(prefix_ids) + out
+
+
+class _TextStack(nn.Module):
+    """BERT embeddings + post-LN layers with cross-attention (BlipTextModel)."""
+
+    def __init__(self, cfg: BlipConfig, cross_dim: int):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(cfg.vocab, cfg.text_dim)
+        self.position_embeddings = nn.Embedding(cfg.max_pos, cfg.text_dim)
+        self.emb_ln = LayerNorm(cfg.text_dim, eps=1e-12)
+        self.layers = nn.ModuleList([PostLNBlock(cfg.text_dim, cfg.text_heads, 4 * cfg.text_dim, cross_dim=cross_dim)
+                                     for _ in range(cfg.text_depth)])
+
+    def run(self, ids: list[int], kvs, causal: bool):
+        dev = self.word_embeddings.weight.device
+        t = torch.tensor([ids], device=dev)
+        x = self.emb_ln(self.word_embeddings(t) + self.position_embeddings.weight[: t.shape[1]][None])
+        for blk, kv in zip(self.layers, kvs):
+            x = blk.ln1(blk.attn(x, residual=x, causal=causal))
+            x = blk.ln_x(blk.cross(x, kv=kv, residual=x))
+            x = blk.ln2(blk.fc2(blk.fc1(x, act="gelu"), residual=x))
+        return x
+
+
+class BlipVQA(nn.Module):
+    """BLIP visual question answering (transformers ``BlipForQuestionAnswering``,
+    the VQA branch of swarm/captioning/caption_image.py:21-29): the question is
+    encoded by a bidirectional BERT that cross-attends to the image, and the
+    answer is decoded greedily from [DEC] by a causal BERT that cross-attends
+    to the question encoding."""
+
+    def __init__(self, cfg: BlipConfig = BLIP_BASE):
+        super().__init__()
+        self.cfg = cfg
+        xd = cfg.cross_dim or cfg.vision_dim
+        self.vision_model = ViT(cfg.image_size, cfg.patch, cfg.vision_dim, cfg.vision_depth, cfg.vision_heads,
+                                4 * cfg.vision_dim)
+        self.encoder = _TextStack(cfg, xd)
+        self.decoder = _TextStack(cfg, xd)
+        self.head_transform = Linear(cfg.text_dim, cfg.text_dim)
+        self.head_ln = LayerNorm(cfg.text_dim, eps=1e-12)
+        self.head_bias = nn.Parameter(torch.zeros(cfg.vocab))
+
+    preprocess = BlipCaptioner.preprocess
+
+    @torch.no_grad()
+    def answer(self, image: Image.Image, question_ids: list[int], max_length: int = 20) -> list[int]:
+        """Greedy answer tokens (transformers ``generate`` defaults: at most
+        ``max_length`` tokens including [DEC], stop at [SEP]).  ``question_ids``:
+        the BERT-tokenised question WITH [CLS] ... [SEP]."""
+        dev = self.head_bias.device
+        dt = self.encoder.word_embeddings.weight.dtype
+        vis = self.vision_model(self.preprocess(image).to(dev).to(dt))
+        q = self.encoder.run(list(question_ids), [blk.cross.kv_of(vis) for blk in self.encoder.layers], causal=False)
+        kvs = [blk.cross.kv_of(q) for blk in self.decoder.layers]
+        ids = [self.cfg.bos_id]
+        out = []
+        for _ in range(max(0, max_length - 1)):
+            x = self.decoder.run(ids, kvs, causal=True)
+            h = self.head_ln(self.head_transform(x[:, -1:], act="gelu"))
+            logits = h.float() @ self.decoder.word_embeddings.weight.float().t() + self.head_bias.float()
+            nxt = int(logits[0, -1].argmax())
+            if nxt == self.cfg.sep_id:
+                break
+            ids.append(nxt)
+            out.append(nxt)
+        return out

@@ -24,11 +24,115 @@ import os
 import sys
 
 
-def _noop(_=None) -> int:
-    import time
+class BrokenEncoderPool(RuntimeError):
+    """No encoder process is alive to take (or finish) a task."""
 
-    time.sleep(0.05)  # keep each worker busy so every submit below starts a new one
-    return os.getpid()
+
+def _worker_main(inq, outq):
+    """Encoder process: run (task id, fn, args) items until a None arrives."""
+    while True:
+        item = inq.get()
+        if item is None:
+            return
+        tid, fn, args = item
+        try:
+            outq.put((tid, True, fn(*args)))
+        except BaseException as e:  # reported on the task's future
+            outq.put((tid, False, e))
+
+
+class _ProcessPool:
+    """A fixed set of spawned encoder processes, all started at construction
+    (this process may not spawn once it has initialised the GPU, so nothing is
+    ever respawned), each with its own task queue; tasks go round-robin to live
+    workers.  A monitor thread fails the pending tasks of a worker that died
+    (``BrokenEncoderPool``) and takes it out of rotation.  Only public
+    multiprocessing / concurrent.futures APIs are used."""
+
+    def __init__(self, n: int, ctx):
+        import threading
+
+        self.outq = ctx.Queue()
+        self.workers = []  # [process, task queue, pending task ids]
+        for _ in range(n):
+            inq = ctx.Queue()
+            proc = ctx.Process(target=_worker_main, args=(inq, self.outq), daemon=True)
+            proc.start()
+            self.workers.append([proc, inq, set()])
+        self.futs: dict = {}
+        self.lock = threading.Lock()
+        self.next_id = 0
+        self.rr = 0
+        self.closed = False
+        self.reader = threading.Thread(target=self._read, daemon=True)
+        self.reader.start()
+        self.monitor = threading.Thread(target=self._watch, daemon=True)
+        self.monitor.start()
+
+    def pids(self) -> list:
+        return [w[0].pid for w in self.workers]
+
+    def alive(self) -> int:
+        return sum(1 for w in self.workers if w[0].is_alive())
+
+    def submit(self, fn, *args) -> cf.Future:
+        fut: cf.Future = cf.Future()
+        with self.lock:
+            live = [i for i, w in enumerate(self.workers) if w[0].is_alive()]
+            if self.closed or not live:
+                raise BrokenEncoderPool("no live encoder process")
+            wi = live[self.rr % len(live)]
+            self.rr += 1
+            tid = self.next_id
+            self.next_id += 1
+            self.futs[tid] = (fut, wi)
+            self.workers[wi][2].add(tid)
+            self.workers[wi][1].put((tid, fn, args))
+        return fut
+
+    def _read(self):
+        while True:
+            try:
+                item = self.outq.get()
+            except (EOFError, OSError):
+                return
+            if item is None:
+                return
+            tid, ok, value = item
+            with self.lock:
+                fut, wi = self.futs.pop(tid, (None, None))
+                if wi is not None:
+                    self.workers[wi][2].discard(tid)
+            if fut is not None and not fut.done():
+                (fut.set_result if ok else fut.set_exception)(value)
+
+    def _watch(self):
+        import time
+
+        while not self.closed:
+            time.sleep(0.25)
+            with self.lock:
+                dead = [(wi, w) for wi, w in enumerate(self.workers) if not w[0].is_alive() and w[2]]
+                lost = []
+                for wi, w in dead:
+                    for tid in list(w[2]):
+                        fut, _ = self.futs.pop(tid, (None, None))
+                        if fut is not None:
+                            lost.append(fut)
+                    w[2].clear()
+            for fut in lost:
+                if not fut.done():
+                    fut.set_exception(BrokenEncoderPool("the encoder process running this task died"))
+
+    def shutdown(self, wait: bool = True):
+        self.closed = True
+        for proc, inq, _ in self.workers:
+            if proc.is_alive():
+                inq.put(None)
+        if wait:
+            for proc, _, _ in self.workers:
+                proc.join(timeout=30)
+        self.outq.put(None)
 
 
 def encode_arrays(arrays, content_type: str = "image/jpeg", output_list=("primary",)) -> dict:
@@ -72,30 +176,27 @@ class EncoderPool:
         if processes is None:
             processes = int(os.environ.get("CSK_ENCODER_PROCS", "2"))
         self.kind = "thread"
-        self._pool: cf.Executor
+        self._pool: cf.Executor | _ProcessPool
         if processes > 0 and not _gpu_initialised():
             try:
-                self._pool = cf.ProcessPoolExecutor(max_workers=processes, mp_context=mp.get_context("spawn"))
-                # start every worker now, while this process has not touched the GPU
-                # (the executor only spawns on submit; a later spawn would exec from
-                # a GPU process)
-                list(self._pool.map(_noop, range(processes)))
-                procs = getattr(self._pool, "_processes", None)
-                while procs is not None and len(procs) < processes and hasattr(self._pool, "_spawn_process"):
-                    self._pool._spawn_process()
+                # every worker starts now, while this process has not touched the GPU
+                self._pool = _ProcessPool(processes, mp.get_context("spawn"))
                 self.kind = "process"
                 return
             except Exception:
                 pass
         self._pool = cf.ThreadPoolExecutor(max_workers=max(1, processes or 2))
 
+    def pids(self) -> list:
+        return self._pool.pids() if isinstance(self._pool, _ProcessPool) else []
+
     def _submit(self, fn, *args) -> cf.Future:
         try:
             return self._pool.submit(fn, *args)
-        except cf.process.BrokenProcessPool:
-            # a worker died (OOM kill, crash): the process pool refuses all further
-            # work and this process may not spawn replacements once the GPU is up,
-            # so the pool degrades to encoder threads instead of failing every job
+        except BrokenEncoderPool:
+            # every worker died (OOM kill, crash) and this process may not spawn
+            # replacements once the GPU is up: degrade to encoder threads instead
+            # of failing every job
             self._pool.shutdown(wait=False)
             self._pool = cf.ThreadPoolExecutor(max_workers=2)
             self.kind = "thread"

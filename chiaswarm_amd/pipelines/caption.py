@@ -1,59 +1,106 @@
 """``workflow: img2txt`` (reference: swarm/captioning/caption_image.py:6-40).
 
 Same contract: returns a text artifact ``{"caption": ...}`` and
-``pipeline_config.caption``; errors are swallowed into the artifact (the
-reference catches everything inside the callback and returns
-``pipeline_config.error``).  ``parameters.processor_type/model_type`` name the
-transformers classes in the reference; here they select the BLIP size.
+``pipeline_config.caption``; runtime errors are swallowed into the artifact
+(the reference catches everything inside the callback and returns
+``pipeline_config.error``).
+
+``parameters.processor_type`` / ``parameters.model_type`` name transformers
+classes in the reference (resolved by reflection, :11-13).  Here they select
+the implementation:
+
+* ``BlipForConditionalGeneration`` (+ ``BlipProcessor`` / ``AutoProcessor``):
+  image captioning, conditional on the prompt when one is given;
+* ``BlipForQuestionAnswering``: visual question answering — the prompt is the
+  question (the reference's "conditional image captioning and VQA" branch,
+  :21-23);
+
+any other class is refused with a ``ValueError`` that names it (a fatal job
+error: retrying cannot help).  Model geometry comes from the checkpoint's
+``config.json`` (a transformers ``BlipConfig``), name heuristics only without one.
 """
 from __future__ import annotations
 
 import torch
 
-from ..models.blip import BLIP_BASE, BLIP_LARGE, TINY_BLIP, BlipCaptioner
+from ..models.blip import BLIP_BASE, BLIP_LARGE, TINY_BLIP, BlipCaptioner, BlipConfig, BlipVQA
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.wordpiece import WordPiece
 from ..output.processor import make_text_result
 from ..runtime.model_cache import cache, find_weights
 
+MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa"}
+PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", None}
 
-def load_captioner(model_name: str, device: str):
+
+def resolve_task(params: dict | None, model_name: str) -> str:
+    """'caption' | 'vqa' from the hive's class names; ValueError for anything else."""
+    params = params or {}
+    mt, pt = params.get("model_type"), params.get("processor_type")
+    if pt not in PROCESSOR_TYPES:
+        raise ValueError(f"img2txt: processor_type {pt!r} is not supported (supported: BlipProcessor, AutoProcessor)")
+    if mt is None:
+        return "vqa" if "vqa" in model_name.lower() else "caption"
+    if mt not in MODEL_TYPES:
+        raise ValueError(f"img2txt: model_type {mt!r} is not supported "
+                         f"(supported: {', '.join(sorted(MODEL_TYPES))})")
+    return MODEL_TYPES[mt]
+
+
+def _config(model_name: str, w: str | None) -> BlipConfig:
+    from ..models.hf_config import component_config
+
+    raw = component_config(w, "") if w else None
+    if raw is not None and ("text_config" in raw or "vision_config" in raw):
+        return BlipConfig.from_hf(raw)
+    n = model_name.lower()
+    return TINY_BLIP if n.startswith("tiny") else (BLIP_LARGE if "large" in n else BLIP_BASE)
+
+
+def load_captioner(model_name: str, device: str, task: str = "caption"):
     def make():
-        n = model_name.lower()
-        cfg = TINY_BLIP if n.startswith("tiny") else (BLIP_LARGE if "large" in n else BLIP_BASE)
-        dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
-        with torch.device(device):
-            m = BlipCaptioner(cfg).to(dt).eval().requires_grad_(False)
-        init_random_fast_(m, seed=11)
         w = find_weights(model_name)
+        cfg = _config(model_name, w)
+        dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+        cls = BlipVQA if task == "vqa" else BlipCaptioner
+        with torch.device(device):
+            m = cls(cfg).to(dt).eval().requires_grad_(False)
+        init_random_fast_(m, seed=11)
         m.weights_source = "random-init"
         if w:
-            from ..models.blip import convert_hf_blip
+            from ..models.blip import convert_hf_blip, convert_hf_blip_vqa
             from ..models.weights import _read_dir, load_into
 
             sd = _read_dir(w)
             if sd:
-                m.load_report = load_into(m, convert_hf_blip(sd), name=model_name)
+                conv = convert_hf_blip_vqa if task == "vqa" else convert_hf_blip
+                m.load_report = load_into(m, conv(sd), name=model_name)
                 m.weights_source = w
         prepare_model(m)
         return m, WordPiece(w, cfg.vocab)
 
-    return cache().get(("blip", model_name, device), make)
+    return cache().get(("blip", task, model_name, device), make)
 
 
 def caption_callback(device_identifier, model_name, **kwargs):
     config, results = {}, {}
+    task = resolve_task(kwargs.pop("parameters", None), model_name)  # unsupported classes: fatal ValueError
     try:
-        print("Image captioning...")
-        kwargs.pop("parameters", None)
-        model, tok = load_captioner(model_name, device_identifier)
+        print("Image captioning..." if task == "caption" else "Visual question answering...")
+        model, tok = load_captioner(model_name, device_identifier, task)
         image = kwargs["image"]
         prompt = kwargs.get("prompt") or ""
-        prefix = tok.encode(prompt) if prompt else []
-        mnt = kwargs.get("max_new_tokens")
-        ids = model.generate(image, prefix, max_new_tokens=None if mnt is None else int(mnt),
-                             max_length=int(kwargs.get("max_length", 20)))
-        caption = tok.decode(ids)
+        if task == "vqa":
+            if not prompt:
+                raise ValueError("img2txt VQA: a question (prompt) is required")
+            qids = [model.cfg.cls_id] + tok.encode(prompt) + [model.cfg.sep_id]  # BertTokenizer [CLS] q [SEP]
+            caption = tok.decode(model.answer(image, qids, max_length=int(kwargs.get("max_length", 20))))
+        else:
+            prefix = tok.encode(prompt) if prompt else []
+            mnt = kwargs.get("max_new_tokens")
+            ids = model.generate(image, prefix, max_new_tokens=None if mnt is None else int(mnt),
+                                 max_length=int(kwargs.get("max_length", 20)))
+            caption = tok.decode(ids)
         results["primary"] = make_text_result(caption)
         config["caption"] = caption
         return results, config

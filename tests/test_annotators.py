@@ -146,3 +146,47 @@ def test_openpose_paf_grouping_one_arm():
     assert len(subset) == 1 and subset[0][-1] == 4
     canvas = an._draw_pose(H, W, cands, subset)
     assert canvas.shape == (H, W, 3) and canvas.any()
+
+
+def test_pidinet_pixel_difference_convs_match_definitions():
+    """cd: sum_i w_i (x_i - x_c); rd: sum_{i>0} w_i (x_outer_i - x_inner_i) over
+    the 8 directions; the folded plain-conv forms reproduce both."""
+    torch.manual_seed(0)
+    x = torch.randn(1, 2, 9, 9)
+    cd = an.PDConv("cd", 2, 3)
+    pat = torch.nn.functional.unfold(x, 3, padding=1).view(1, 2, 9, 81)  # [b, c, tap, pix]
+    ref = torch.einsum("oct,bctp->bop", cd.weight.view(3, 2, 9), pat - pat[:, :, 4:5]).view(1, 3, 9, 9)
+    assert torch.allclose(cd(x), ref, atol=1e-5)
+    rd = an.PDConv("rd", 2, 3)
+    p5 = torch.nn.functional.unfold(x, 5, padding=2).view(1, 2, 25, 81)
+    diff = p5[:, :, an._RD_OUTER] - p5[:, :, an._RD_INNER]
+    ref = torch.einsum("oct,bctp->bop", rd.weight.view(3, 2, 9)[:, :, 1:], diff).view(1, 3, 9, 9)
+    assert torch.allclose(rd(x), ref, atol=1e-5)
+    ad = an.PDConv("ad", 2, 3)
+    ref = torch.einsum("oct,bctp->bop", ad.weight.view(3, 2, 9),
+                       pat - pat[:, :, [1, 2, 5, 0, 4, 8, 3, 6, 7]]).view(1, 3, 9, 9)
+    assert torch.allclose(ad(x), ref, atol=1e-5)
+
+
+def test_pidinet_checkpoint_layout_and_outputs():
+    """table5_pidinet.pth names (module.-prefixed, under 'state_dict') load
+    without missing keys; 4 side maps + fused map at input size, in [0, 1]."""
+    m = an.PiDiNet().eval()
+    sd = m.state_dict()
+    for k, shape in (("init_block.weight", (60, 3, 3, 3)), ("block1_1.conv1.weight", (60, 1, 3, 3)),
+                     ("block2_1.shortcut.weight", (120, 60, 1, 1)), ("block4_4.conv2.weight", (240, 240, 1, 1)),
+                     ("dilations.3.conv2_4.weight", (24, 24, 3, 3)), ("attentions.0.conv1.bias", (4,)),
+                     ("conv_reduces.2.conv.weight", (1, 24, 1, 1)), ("classifier.bias", (1,))):
+        assert tuple(sd[k].shape) == shape, k
+    assert m.block3_2.conv1.kind == "ad" and m.block4_3.conv1.kind == "rd" and m.init_block.kind == "cd"
+    wrapped = {"state_dict": {"module." + k: torch.randn_like(v) for k, v in sd.items()}}
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "table5_pidinet.pth")
+        torch.save(wrapped, p)
+        flat = an.load_checkpoint(p)
+    missing, unexpected = m.load_state_dict(flat, strict=True)
+    with torch.no_grad():
+        outs = m(torch.rand(1, 3, 64, 48))
+    assert len(outs) == 5 and all(o.shape == (1, 1, 64, 48) for o in outs)
+    assert all(((o >= 0) & (o <= 1)).all() for o in outs)

@@ -154,6 +154,68 @@ def test_blip_captioner_parity_vs_transformers(tmp_path):
     assert got == ref_body[: len(got)] and len(got) >= len(prefix)
 
 
+def test_blip_vqa_parity_vs_transformers(tmp_path):
+    """BlipForQuestionAnswering: question encoder (bidirectional, cross-attends to
+    the image) + answer decoder (causal, cross-attends to the question): strict
+    load of the transformers state dict, question encoding and greedy answer
+    tokens equal to transformers' generate."""
+    from PIL import Image
+    from transformers import BlipConfig, BlipForQuestionAnswering
+
+    from chiaswarm_amd.models.blip import BlipConfig as OurCfg
+    from chiaswarm_amd.models.blip import BlipVQA, convert_hf_blip_vqa
+    from chiaswarm_amd.models.weights import _read_dir
+
+    raw = dict(text_config=dict(vocab_size=1000, hidden_size=64, num_hidden_layers=2, num_attention_heads=2,
+                                intermediate_size=256, encoder_hidden_size=64, bos_token_id=998, sep_token_id=999,
+                                pad_token_id=0, eos_token_id=999),
+               vision_config=dict(hidden_size=64, num_hidden_layers=2, num_attention_heads=2, intermediate_size=256,
+                                  image_size=64, patch_size=16))
+    hcfg = BlipConfig(**raw)
+    torch.manual_seed(0)
+    hf = BlipForQuestionAnswering(hcfg).eval()
+    with torch.no_grad():
+        hf.text_decoder.cls.predictions.bias.normal_(0, 0.5)
+    _save(hf.state_dict(), str(tmp_path))
+    cfg = OurCfg.from_hf(raw)
+    assert cfg.vision_dim == 64 and cfg.bos_id == 998 and cfg.sep_id == 999
+    ours = BlipVQA(cfg).eval()
+    rep = load_into(ours, convert_hf_blip_vqa(_read_dir(str(tmp_path))))
+    assert rep.complete, rep.summary()
+    img = Image.fromarray((torch.rand(64, 64, 3) * 255).byte().numpy())
+    pix = ours.preprocess(img).permute(0, 3, 1, 2)
+    q = [101, 17, 42, 300, 102]
+    with torch.no_grad():
+        vis = hf.vision_model(pixel_values=pix)[0]
+        ref_q = hf.text_encoder(input_ids=torch.tensor([q]), encoder_hidden_states=vis,
+                                encoder_attention_mask=torch.ones(vis.shape[:-1], dtype=torch.long))[0]
+        got_vis = ours.vision_model(ours.preprocess(img))
+        got_q = ours.encoder.run(q, [blk.cross.kv_of(got_vis) for blk in ours.encoder.layers], causal=False)
+    torch.testing.assert_close(got_q, ref_q, atol=3e-4, rtol=1e-4)
+    with torch.no_grad():
+        ref = hf.generate(input_ids=torch.tensor([q]), pixel_values=pix, max_length=10, do_sample=False,
+                          num_beams=1)[0].tolist()
+    got = ours.answer(img, q, max_length=10)
+    ref_body = [t for t in ref[1:] if t != 999]  # transformers: [DEC] + answer (+ [SEP])
+    assert got == ref_body
+
+
+def test_img2txt_class_names(tmp_path):
+    """processor_type / model_type pick captioning or VQA; any other class is a
+    fatal error naming it (the reference instantiated the named class)."""
+    from chiaswarm_amd.pipelines.caption import resolve_task
+
+    assert resolve_task({"processor_type": "BlipProcessor", "model_type": "BlipForConditionalGeneration"},
+                        "Salesforce/blip-image-captioning-base") == "caption"
+    assert resolve_task({"processor_type": "BlipProcessor", "model_type": "BlipForQuestionAnswering"},
+                        "Salesforce/blip-vqa-base") == "vqa"
+    assert resolve_task(None, "Salesforce/blip-vqa-base") == "vqa"
+    with pytest.raises(ValueError, match="GitForCausalLM"):
+        resolve_task({"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"}, "microsoft/git-base")
+    with pytest.raises(ValueError, match="ViltProcessor"):
+        resolve_task({"processor_type": "ViltProcessor", "model_type": "BlipForQuestionAnswering"}, "x")
+
+
 # --------------------------------------------------------------------------- CLAP
 def test_clap_text_parity_vs_transformers(tmp_path):
     from transformers import ClapTextConfig, ClapTextModelWithProjection

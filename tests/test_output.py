@@ -130,8 +130,9 @@ def test_thumbnail_from_image_matches_decoded_bytes():
 
 
 def test_encoder_pool_survives_a_dead_worker():
-    """A killed encoder process breaks a ProcessPoolExecutor for good; the pool
-    degrades to encoder threads and later jobs still encode."""
+    """A killed encoder process: its pending task fails, no replacement is ever
+    spawned (the GPU process may not exec), and once no encoder process is left
+    the pool degrades to encoder threads; later jobs still encode."""
     import os
     import signal
     import time
@@ -145,7 +146,7 @@ def test_encoder_pool_survives_a_dead_worker():
     arrs = [np.zeros((32, 32, 3), dtype=np.uint8)]
     try:
         first = pool.submit(arrs, "image/png").result(timeout=60)
-        for pid in list(pool._pool._processes):
+        for pid in pool.pids():
             os.kill(pid, signal.SIGKILL)
         time.sleep(1.0)
         try:

@@ -140,3 +140,32 @@ def test_txt2vid_tiny_cpu_seeded():
     assert a.shape == (3, 32, 32, 3) and a.dtype == np.uint8
     assert np.array_equal(a, b)
     assert not p._graphs.graphs  # CPU: no graph capture
+
+
+def test_img2txt_vqa_and_unsupported_class_envelopes(monkeypatch):
+    """img2txt through the real router / generator: BLIP VQA answers the prompt
+    (text artifact + pipeline_config.caption); an unsupported transformers class
+    comes back fatal, naming the class."""
+    import base64
+    import io
+    import json
+
+    from PIL import Image
+
+    import chiaswarm_amd.jobs.inputs as inputs
+
+    img = Image.new("RGB", (64, 64), (10, 200, 30))
+    monkeypatch.setattr(inputs, "get_image", lambda *a, **k: img)
+    monkeypatch.setattr("chiaswarm_amd.jobs.router.get_image", lambda *a, **k: img, raising=False)
+    buf = io.BytesIO()
+    img.save(buf, "PNG")
+    job = {"id": "v1", "model_name": "tiny/blip-vqa", "workflow": "img2txt", "prompt": "what color is it?",
+           "start_image_uri": "http://x/img.png",
+           "parameters": {"processor_type": "BlipProcessor", "model_type": "BlipForQuestionAnswering"}}
+    r = synchronous_do_work_function(dict(job), Device("cpu"))
+    assert "fatal_error" not in r and "error" not in r["pipeline_config"], r["pipeline_config"]
+    blob = json.loads(base64.b64decode(r["artifacts"]["primary"]["blob"]))
+    assert blob["caption"] == r["pipeline_config"]["caption"]
+    bad = dict(job, id="v2", parameters={"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"})
+    r2 = synchronous_do_work_function(bad, Device("cpu"))
+    assert r2.get("fatal_error") is True and "GitForCausalLM" in r2["pipeline_config"]["error"]
