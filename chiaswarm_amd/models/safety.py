@@ -48,7 +48,7 @@ class SafetyChecker(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.vision_model = ViT(cfg.image_size, cfg.patch, cfg.dim, cfg.depth, cfg.heads, cfg.mlp, eps=1e-5,
-                                act="quick_gelu", pre_norm=True)
+                                act="quick_gelu", pre_norm=True, patch_bias=False)
         self.visual_projection = Linear(cfg.dim, cfg.proj, bias=False)
         self.concept_embeds = nn.Parameter(torch.zeros(17, cfg.proj))
         self.special_care_embeds = nn.Parameter(torch.zeros(3, cfg.proj))
@@ -71,23 +71,42 @@ class SafetyChecker(nn.Module):
         std = torch.tensor(STD, device=x.device)[None, :, None, None]
         return ((x - mean) / std).permute(0, 2, 3, 1).contiguous()
 
+    def image_embeds(self, x: torch.Tensor) -> torch.Tensor:
+        """Normalised NHWC pixels -> projected CLS embedding (CLIPVisionModelWithProjection.image_embeds)."""
+        return self.visual_projection(self.vision_model(x)[:, 0])
+
+    def flags(self, emb: torch.Tensor) -> torch.Tensor:
+        """Per-image NSFW decision from projected embeddings [B, proj]; scores are
+        rounded to 3 decimals before the > 0 test, as diffusers does."""
+        emb = F.normalize(emb.float(), dim=-1)
+        special = emb @ F.normalize(self.special_care_embeds.float(), dim=-1).t()
+        concept = emb @ F.normalize(self.concept_embeds.float(), dim=-1).t()
+        special_scores = torch.round((special - self.special_care_embeds_weights.float()) * 1000) / 1000
+        adj = (special_scores > 0).any(dim=1, keepdim=True).float() * 0.01
+        concept_scores = torch.round((concept - self.concept_embeds_weights.float() + adj) * 1000) / 1000
+        return (concept_scores > 0).any(dim=1)
+
     @torch.no_grad()
     def forward(self, images_u8: torch.Tensor):
         """Returns (nsfw flags list[bool], images with flagged ones blacked out)."""
         dt = self.visual_projection.weight.dtype
         x = self.preprocess(images_u8.to(self.visual_projection.weight.device)).to(dt)
-        pooled = self.vision_model(x)[:, 0]
-        emb = F.normalize(self.visual_projection(pooled).float(), dim=-1)
-        special = emb @ F.normalize(self.special_care_embeds.float(), dim=-1).t()
-        concept = emb @ F.normalize(self.concept_embeds.float(), dim=-1).t()
-        special_scores = special - self.special_care_embeds_weights.float()
-        adj = (special_scores > 0).any(dim=1, keepdim=True).float() * 0.01
-        concept_scores = concept - self.concept_embeds_weights.float() + adj
-        flags = (concept_scores > 0).any(dim=1)
+        flags = self.flags(self.image_embeds(x))
         out = images_u8.clone()
         if bool(flags.any()):
             out[flags.to(out.device)] = 0
         return [bool(f) for f in flags.cpu()], out
+
+
+_HF_RENAMES = {"vision_model.embeddings.patch_embedding.": "vision_model.patch_embedding.",
+               "vision_model.embeddings.class_embedding": "vision_model.class_embedding",
+               "vision_model.embeddings.position_embedding.weight": "vision_model.position_embedding",
+               "vision_model.pre_layrnorm.": "vision_model.pre_ln.",
+               "vision_model.post_layernorm.": "vision_model.post_ln.",
+               "vision_model.encoder.layers.": "vision_model.layers.",
+               ".self_attn.q_proj.": ".attn.q.", ".self_attn.k_proj.": ".attn.k.",
+               ".self_attn.v_proj.": ".attn.v.", ".self_attn.out_proj.": ".attn.o.",
+               ".layer_norm1.": ".ln1.", ".layer_norm2.": ".ln2.", ".mlp.fc1.": ".fc1.", ".mlp.fc2.": ".fc2."}
 
 
 def load_safety_checker(device, weights_dir=None, tiny=False) -> SafetyChecker:
@@ -102,15 +121,6 @@ def load_safety_checker(device, weights_dir=None, tiny=False) -> SafetyChecker:
     if weights_dir:
         from .weights import _read_dir, load_into
 
-        renames = {"vision_model.embeddings.patch_embedding.": "vision_model.patch_embedding.",
-                   "vision_model.embeddings.class_embedding": "vision_model.class_embedding",
-                   "vision_model.embeddings.position_embedding.weight": "vision_model.position_embedding",
-                   "vision_model.pre_layrnorm.": "vision_model.pre_ln.",
-                   "vision_model.post_layernorm.": "vision_model.post_ln.",
-                   "vision_model.encoder.layers.": "vision_model.layers.",
-                   ".self_attn.q_proj.": ".attn.q.", ".self_attn.k_proj.": ".attn.k.",
-                   ".self_attn.v_proj.": ".attn.v.", ".self_attn.out_proj.": ".attn.o.",
-                   ".layer_norm1.": ".ln1.", ".layer_norm2.": ".ln2.", ".mlp.fc1.": ".fc1.", ".mlp.fc2.": ".fc2."}
         # StableDiffusionSafetyChecker nests CLIPVisionModel: vision_model.vision_model.*
-        load_into(m, _read_dir(weights_dir), renames, prefix_strip="vision_model.")
+        load_into(m, _read_dir(weights_dir), _HF_RENAMES, prefix_strip="vision_model.")
     return prepare_model(m)

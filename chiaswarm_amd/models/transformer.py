@@ -110,12 +110,13 @@ class ViT(nn.Module):
     """Patch-embedding vision transformer (pre-LN), NHWC image input."""
 
     def __init__(self, image_size=384, patch=16, dim=768, depth=12, heads=12, mlp=3072, eps=1e-5,
-                 act="gelu", pre_norm=False):
+                 act="gelu", pre_norm=False, patch_bias=True):
         super().__init__()
         self.patch, self.image_size = patch, image_size
         from .layers import Conv2d
 
-        self.patch_embedding = Conv2d(3, dim, patch, stride=patch, padding=0)
+        # CLIP's patch embedding has no bias, BLIP's has one
+        self.patch_embedding = Conv2d(3, dim, patch, stride=patch, padding=0, bias=patch_bias)
         self.class_embedding = nn.Parameter(torch.zeros(dim))
         self.position_embedding = nn.Parameter(torch.zeros(1 + (image_size // patch) ** 2, dim))
         self.pre_ln = LayerNorm(dim, eps=eps) if pre_norm else None
