@@ -26,8 +26,12 @@ _LOAD_ERR: Exception | None = None
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
 # CSK_LIB_PATH: load another build (same-box A/B of two builds: tools/gpu/lib_ab.sh; set
-# CSK_ALLOW_STALE=1 with it, the staleness stamp belongs to the in-tree build)
-LIB_PATH = os.environ.get("CSK_LIB_PATH") or os.path.join(LIB_DIR, "libcsk.so")
+# CSK_ALLOW_STALE=1 with it, the staleness stamp belongs to the in-tree build).
+# CSK_DEBUG=1: the bounds-checking build (python -m chiaswarm_amd._build --debug)
+DEBUG = os.environ.get("CSK_DEBUG", "") not in ("", "0")
+LIB_PATH = os.environ.get("CSK_LIB_PATH") or os.path.join(LIB_DIR, "libcsk_debug.so" if DEBUG else "libcsk.so")
+# translation units that export csk_debug_read_<tu> / csk_debug_clear_<tu> in debug builds
+DEBUG_TUS = ("gemm", "gemm_glds", "gemm8p", "attention", "attention_wide")
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -60,7 +64,7 @@ def check_fresh():
         return
     from .. import _build
 
-    want = _build.source_digest()
+    want = _build.source_digest(DEBUG)
     try:
         with open(LIB_PATH + ".src") as f:
             have = f.read().strip()
@@ -83,7 +87,7 @@ def ensure_built():
         pass
     from .. import _build
 
-    _build.build(verbose=False)
+    _build.build(verbose=False, debug=DEBUG)
 
 
 def load():
@@ -112,6 +116,31 @@ def load():
                 raise RuntimeError(f"csk_init failed with hipError {err}")
         _LIB = lib
         return lib
+
+
+def debug_records(clear: bool = True) -> list:
+    """Bounds violations recorded by a CSK_DEBUG build since the last clear:
+    [(tu, count, site, block_x, thread, value, limit, block_y)].  Call after a
+    synchronise.  Empty for release builds (no records are compiled in)."""
+    lib = load()
+    out = []
+    for tu in DEBUG_TUS:
+        rd = getattr(lib, f"csk_debug_read_{tu}", None)
+        if rd is None:
+            continue
+        buf = (ctypes.c_uint * 8)()
+        rd.argtypes = [c_void_p]
+        rd.restype = c_int
+        if rd(ctypes.cast(buf, c_void_p)) != 0:
+            raise RuntimeError(f"csk_debug_read_{tu} failed")
+        if buf[0]:
+            val = buf[4] | (buf[5] << 32)
+            if val >= 1 << 63:
+                val -= 1 << 64
+            out.append((tu, buf[0], buf[1], buf[2], buf[3], val, buf[6], buf[7]))
+            if clear:
+                getattr(lib, f"csk_debug_clear_{tu}")()
+    return out
 
 
 def available() -> bool:

@@ -58,8 +58,6 @@ def _gn_seg(tile, split, rows_per_b, M, code, N=8):
     bm, bn = tuning.TILES.get(tile, (0, 0))
     if code == 3 or bm == 0 or rows_per_b <= 0:
         return 0
-    if tile in tuning.BSTAT_KMAX:  # B-stationary: one segment per 32-row wave band (direct epilogue)
-        return 32 if rows_per_b % 32 == 0 and M % 64 == 0 else 0
     if split != 1:
         if not SPLITK_GN:
             return 0
@@ -187,8 +185,6 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
                   M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
-    if tile in tuning.BSTAT_KMAX and (split > 1 or not tuning.bstat_ok(tile, M, N, K, code)):
-        tile, split = 19, 1  # a table entry from another shape class: the tiled kernel
     if ln is not None or row_stats:
         if split > 1:  # the split-K reduce has no LN / row-statistics epilogue
             tile, split = (19 if N <= 1280 else 20), 1

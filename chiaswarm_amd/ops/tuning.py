@@ -36,17 +36,7 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # 8-wave 256-row phased tiles (gemm8p.hip): half the L2->LDS bytes per FLOP of 128x128
          31: (256, 256), 32: (256, 128),
          # 8-wave 256x160 3-stage ring (gemm8p.hip gemm8r_kernel): 0.0102 B/FLOP, 256 tiles at the 64x64 level
-         33: (256, 160), 34: (256, 128),
-         # B-stationary persistent (gemm_glds.hip gemm_bstat_kernel): weight slice resident
-         # in LDS, A streamed; GEMM only, M % 64 == N % BN == 0, K <= 320 (40) / 640 (41)
-         40: (64, 160), 41: (64, 64)}
-BSTAT_KMAX = {40: 320, 41: 640}
-
-
-def bstat_ok(tile, M, N, K, code) -> bool:
-    """Shapes the B-stationary tiles accept (gemm_glds.hip launch_bstat)."""
-    bm, bn = TILES[tile]
-    return (M % bm == 0 and N % bn == 0 and K % 64 == 0 and K <= BSTAT_KMAX[tile] and code != 3)
+         33: (256, 160), 34: (256, 128)}
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
 # cannot exceed that band (hip_ops._gn_seg mirrors gemm_common.h gn_seg_for)

@@ -123,9 +123,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
   auto store_kv = [&](int buf) {
     bf16_t* ks = smem + buf * 2 * TILE;
     bf16_t* vs = ks + TILE;
+    CSK_DCHECK(buf >= 0 && buf < 2, 20, buf, 2);  // the 2-buffer K/V ring
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      CSK_DCHECK(kv_off<CPR>(row, c) + 8 <= TILE, 21, kv_off<CPR>(row, c), TILE);
       *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
       *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
     }
@@ -274,8 +276,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
 //          T13) is corrected by one wave-uniform subtract pass.
 //   ONES : the row sum l rides on the PV MFMAs as an extra all-ones V^T tile
 //          (4 MFMAs per block instead of 32 adds + 2 shuffles per query tile).
-template <int QT, bool PRE, bool ONES>
-__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a) {
+//
+// PROBE (profiling builds of the same loop, variants 11/12/14/18; results are
+// wrong by design): 1 = no exp (P = S), 2 = no K/V global loads (LDS keeps its
+// first blocks), 4 = no PV MFMAs (P kept alive), 8 = no QK^T MFMAs.
+template <int QT, bool PRE, bool ONES, int PROBE = 0, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs a) {
   constexpr int DP = 64;
   constexpr int CPR = DP / 8;
   constexpr int KB = 64;
@@ -340,10 +346,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 
   uint4 rk[LPT], rv[LPT];
   auto load_kv = [&](int kb) {
+    if constexpr ((PROBE & 2) != 0) {
+      if (kb >= 2) return;
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
       const int key = min(kb * KB + row, Skv - 1), d = c * 8;  // clamped rows are masked later
+      CSK_DCHECK(key >= 0, 22, key, Skv);  // Skv >= 1 whenever a block is loaded
       uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (d < a.D) {
         vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
@@ -356,9 +366,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   auto store_kv = [&](int buf) {
     bf16_t* ks = smem + buf * 2 * TILE;
     bf16_t* vs = ks + TILE;
+    CSK_DCHECK(buf >= 0 && buf < 3, 20, buf, 3);  // the 3-buffer K/V ring
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      CSK_DCHECK(kv_off<CPR>(row, c) + 8 <= TILE, 21, kv_off<CPR>(row, c), TILE);
       *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
       *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
     }
@@ -371,6 +383,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     for (int qt = 0; qt < QT; ++qt) {
       mu[qt] = (PRE && mrow[qt] > -1e29f) ? mrow[qt] : 0.f;
       cinit[qt] = v4f{-mu[qt], -mu[qt], -mu[qt], -mu[qt]};
+    }
+    if constexpr ((PROBE & 8) != 0) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[kt][qt] = cinit[qt] + (float)kt;
+      return;
     }
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -446,10 +465,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) sc[kt][qt][r] -= shift;
         }
+        if constexpr ((PROBE & 1) == 0) {
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+          for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) sc[kt][qt][r] = __builtin_amdgcn_exp2f(sc[kt][qt][r]);
+            for (int r = 0; r < 4; ++r) sc[kt][qt][r] = __builtin_amdgcn_exp2f(sc[kt][qt][r]);
+        }
       } else {
         const float mref = mrow[qt];
 #pragma unroll
@@ -477,8 +498,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       }
     }
     const bf16_t* vs = smem + cur * 2 * TILE + TILE;
+    if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
-    for (int kp2 = 0; kp2 < 2; ++kp2) {
+      for (int kp2 = 0; kp2 < 2; ++kp2)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) asm volatile("" ::"v"(pf[kp2][qt]));
+    }
+#pragma unroll
+    for (int kp2 = 0; kp2 < ((PROBE & 4) ? 0 : 2); ++kp2) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int qq = fr >> 2, pp = fr & 3;
@@ -586,6 +613,21 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
         attn_fwd_pipe_kernel<3, true, true><<<grid3, 256, 0, stream>>>(a);
         return (int)hipGetLastError();
       }
+      if (variant == 9) {  // 3 workgroups per CU (12 waves): registers capped at 168
+        attn_fwd_pipe_kernel<2, true, true, 0, 3><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
+        return (int)hipGetLastError();
+      }
+      if (variant >= 11 && variant <= 18) {  // profiling probes (wrong results by design)
+        const dim3 gp(B * H * ((Sq + 127) / 128));
+        switch (variant) {
+          case 11: attn_fwd_pipe_kernel<2, true, true, 1><<<gp, 256, 0, stream>>>(a); break;
+          case 12: attn_fwd_pipe_kernel<2, true, true, 2><<<gp, 256, 0, stream>>>(a); break;
+          case 14: attn_fwd_pipe_kernel<2, true, true, 4><<<gp, 256, 0, stream>>>(a); break;
+          case 18: attn_fwd_pipe_kernel<2, true, true, 8><<<gp, 256, 0, stream>>>(a); break;
+          default: return (int)hipErrorInvalidValue;
+        }
+        return (int)hipGetLastError();
+      }
       if (variant == 7) {  // 16 query rows per wave (QT = 1): twice the workgroups for short sequences
         const dim3 grid1(B * H * ((Sq + 63) / 64));
         attn_fwd_pipe_kernel<1, true, true><<<grid1, 256, 0, stream>>>(a);
@@ -616,3 +658,5 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   if (D <= 160) return launch_attn<256, 1, 160>(a, stream);  // SD1.5 16x16 / 8x8 levels
   return launch_attn<256, 1>(a, stream);
 }
+
+CSK_DEBUG_EXPORT(attention)

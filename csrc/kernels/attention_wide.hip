@@ -29,6 +29,8 @@ struct AttnWideArgs {
   int B, H, Sq, Skv, D;
   float scale_log2;
   const bf16_t* zero;
+  const bf16_t* k_end;  // one past the last K / V element (CSK_DEBUG checks)
+  const bf16_t* v_end;
 };
 
 template <int CPR>
@@ -43,8 +45,6 @@ __global__ __launch_bounds__(256, 1) void attn_wide_kernel(const AttnWideArgs a)
   constexpr int TILE = KB * DP;
   constexpr int QROWS = QT * 16 * 4;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // K0 V0 K1 V1 (128 KB)
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,8 +92,13 @@ __global__ __launch_bounds__(256, 1) void attn_wide_kernel(const AttnWideArgs a)
       const bool ok = key < Skv && (dfull || d < a.D);
       const bf16_t* sk = ok ? kp + (size_t)key * a.sks + d : a.zero + lane * 8;
       const bf16_t* sv = ok ? vp + (size_t)key * a.svs + d : a.zero + lane * 8;
-      __builtin_amdgcn_global_load_lds((gptr_t)sk, (lptr_t)(ks + row * DP), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gptr_t)sv, (lptr_t)(vs + row * DP), 16, 0, 0);
+      CSK_DCHECK((sk >= a.k && sk + 8 <= a.k_end) || (sk >= a.zero && sk + 8 <= a.zero + ZERO_BYTES / 2), SITE_WIDE_KV,
+                 key, Skv);
+      CSK_DCHECK((sv >= a.v && sv + 8 <= a.v_end) || (sv >= a.zero && sv + 8 <= a.zero + ZERO_BYTES / 2), SITE_WIDE_KV,
+                 key, Skv);
+      CSK_DCHECK(buf * 2 * TILE + TILE + row * DP + 512 <= 4 * TILE, SITE_WIDE_KV + 100, row, buf);
+      __builtin_amdgcn_global_load_lds((csk_gptr_t)sk, (csk_lptr_t)(ks + row * DP), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((csk_gptr_t)sv, (csk_lptr_t)(vs + row * DP), 16, 0, 0);
     }
   };
 
@@ -212,8 +217,12 @@ CSK_API int csk_attention_wide(void* o, const void* q, const void* k, const void
   a.B = B; a.H = H; a.Sq = Sq; a.Skv = Skv; a.D = D;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.zero = zero;
+  a.k_end = a.k + (B - 1) * a.skb + (long long)(Skv - 1) * a.sks + (H - 1) * a.skh + D;
+  a.v_end = a.v + (B - 1) * a.svb + (long long)(Skv - 1) * a.svs + (H - 1) * a.svh + D;
   if (Sq <= 0 || B * H == 0) return 0;
   // QT = 1: 16 query rows per wave (QT = 2 needs ~640 registers: spills)
   attn_wide_kernel<1><<<(unsigned)((long long)B * H * ((Sq + 63) / 64)), 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
+
+CSK_DEBUG_EXPORT(attention_wide)

@@ -120,3 +120,42 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 #define CSK_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// ---- CSK_DEBUG builds (python -m chiaswarm_amd._build --debug -> libcsk_debug.so) ----
+// Device-side checks record the FIRST violation per translation unit into a
+// device record {count, site, block.x, thread, value lo, value hi, limit,
+// block.y} instead of trapping (a trap would take the GPU down with it); the
+// host reads it after a synchronise (csk_debug_read_<tu>) and the GPU test
+// suite fails any test that left a record (tests/conftest.py).  Release builds
+// compile every check away.
+#ifdef CSK_DEBUG
+static __device__ unsigned int csk_dbg_rec[8];
+static __device__ __noinline__ void csk_dbg_fail(int site, long long v, long long lim) {
+  if (atomicAdd(&csk_dbg_rec[0], 1u) == 0u) {
+    csk_dbg_rec[1] = (unsigned)site;
+    csk_dbg_rec[2] = blockIdx.x;
+    csk_dbg_rec[3] = threadIdx.x;
+    csk_dbg_rec[4] = (unsigned)(v & 0xffffffffll);
+    csk_dbg_rec[5] = (unsigned)(v >> 32);
+    csk_dbg_rec[6] = (unsigned)lim;
+    csk_dbg_rec[7] = blockIdx.y;
+  }
+}
+#define CSK_DCHECK(cond, site, v, lim) \
+  do {                                 \
+    if (!(cond)) csk_dbg_fail((site), (long long)(v), (long long)(lim)); \
+  } while (0)
+#define CSK_DEBUG_EXPORT(tu)                                                                              \
+  CSK_API int csk_debug_read_##tu(unsigned* out) {                                                      \
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(csk_dbg_rec), sizeof(csk_dbg_rec), 0, hipMemcpyDeviceToHost); \
+  }                                                                                                     \
+  CSK_API int csk_debug_clear_##tu() {                                                                  \
+    const unsigned z[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                                     \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(csk_dbg_rec), z, sizeof(z), 0, hipMemcpyHostToDevice);     \
+  }
+#else
+#define CSK_DCHECK(cond, site, v, lim) \
+  do {                                 \
+  } while (0)
+#define CSK_DEBUG_EXPORT(tu)
+#endif

@@ -540,6 +540,8 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   a.ln_part = (const float*)ln_part; a.ln_colsum = (const float*)ln_colsum;
   a.ln_nparts = ln_nparts; a.ln_pcols = ln_pcols; a.ln_eps = ln_eps;
   a.row_part = (float*)row_part;
+  a.a_end = a.A + (size_t)(M > 0 ? M - 1 : 0) * lda + K;
+  a.w_end = a.W + (size_t)(N > 0 ? N - 1 : 0) * ldb + K;
   if (M == 0 || N == 0) return 0;
   if (ln_part) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
@@ -579,6 +581,8 @@ CSK_API int csk_conv2d_ex(void* Y, const void* X, const void* Wp, const void* bi
   a.ldb2 = b2s > 0 ? b2s : Cout;
   a.ws = (float*)ws;
   a.gn_part = (float*)gn_part;
+  a.a_end = a.A + ((size_t)B * H * W - 1) * xs + Cin;
+  a.w_end = a.W + (size_t)(Cout - 1) * a.ldb + a.K;
   if (a.M == 0) return 0;
   return dispatch<true>(a, tile, ksplit, stream);
 }
@@ -590,3 +594,5 @@ CSK_API int csk_conv2d(void* Y, const void* X, const void* Wp, const void* bias,
   return csk_conv2d_ex(Y, X, Wp, bias, bias2d, 0, res, B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, up2x, xs, ys,
                        rs, act, out_scale, dil, gn_part, tile, ksplit, ws, stream);
 }
+
+CSK_DEBUG_EXPORT(gemm)

@@ -64,8 +64,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
   const int lrow = lane >> 3;
   const int lchunk = (lane & 7) ^ lrow;  // swizzled source chunk for this lane's lane-linear LDS slot
   const bf16_t* zero = args.zero + lchunk * 8;
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
 
   // ---- per-lane DMA source state: DMA instruction i of wave w stages rows (i*8 + w)*8 .. +8 ----
   // B (and GEMM A) rows of one lane are 64 rows apart: ONE running pointer plus a
@@ -132,13 +130,12 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
         const bf16_t* src = CONV ? fa[CONV ? i : 0] + f_c : fa0 + i * astride;
-        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+        dma16<SITE_8P_A>(args, src, as + (i * 8 + wid) * 8 * BK, smem, SMEM_MAIN);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < IA; ++i)
-        __builtin_amdgcn_global_load_lds((gptr_t)(fa0 + min(i, a_cnt - 1) * astride),
-                                         (lptr_t)(as + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+        dma16<SITE_8P_A>(args, fa0 + min(i, a_cnt - 1) * astride, as + (i * 8 + wid) * 8 * BK, smem, SMEM_MAIN);
     }
     if constexpr (CONV) {
       f_c += BK;
@@ -156,12 +153,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(const GemmArgs args) {
     if (b_full) {
 #pragma unroll
       for (int i = 0; i < IB; ++i)
-        __builtin_amdgcn_global_load_lds((gptr_t)(fb + i * bstride), (lptr_t)(bs + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+        dma16<SITE_8P_B>(args, fb + i * bstride, bs + (i * 8 + wid) * 8 * BK, smem, SMEM_MAIN);
     } else {
 #pragma unroll
       for (int i = 0; i < IB; ++i)
-        __builtin_amdgcn_global_load_lds((gptr_t)(fb + min(i, b_cnt - 1) * bstride),
-                                         (lptr_t)(bs + (i * 8 + wid) * 8 * BK), 16, 0, 0);
+        dma16<SITE_8P_B>(args, fb + min(i, b_cnt - 1) * bstride, bs + (i * 8 + wid) * 8 * BK, smem, SMEM_MAIN);
     }
     fb += BK;
   };
@@ -320,8 +316,6 @@ __global__ __launch_bounds__(512, 1) void gemm8r_kernel(const GemmArgs args) {
   const int lrow = lane >> 3;
   const int lchunk = (lane & 7) ^ lrow;
   const bf16_t* zero = args.zero + lchunk * 8;
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
 
@@ -376,13 +370,11 @@ __global__ __launch_bounds__(512, 1) void gemm8r_kernel(const GemmArgs args) {
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (i * NW + wid) * 8 * BK), 16, 0, 0);
+      dma16<SITE_8R_A>(args, src, as + (i * NW + wid) * 8 * BK, smem, SMEM_MAIN);
     }
 #pragma unroll
-    for (int i = 0; i < IBL; ++i)
-      __builtin_amdgcn_global_load_lds((gptr_t)fb[i], (lptr_t)(bs + (i * NW + wid) * 8 * BK), 16, 0, 0);
-    if (IBX > 0 && xb)
-      __builtin_amdgcn_global_load_lds((gptr_t)fb[IBL], (lptr_t)(bs + (IBL * NW + wid) * 8 * BK), 16, 0, 0);
+    for (int i = 0; i < IBL; ++i) dma16<SITE_8R_B>(args, fb[i], bs + (i * NW + wid) * 8 * BK, smem, SMEM_MAIN);
+    if (IBX > 0 && xb) dma16<SITE_8R_B>(args, fb[IBL], bs + (IBL * NW + wid) * 8 * BK, smem, SMEM_MAIN);
 #pragma unroll
     for (int i = 0; i <= IBL; ++i) fb[i] += BK;  // the zero page is large enough for the running offset
     if constexpr (CONV) {
@@ -496,3 +488,5 @@ int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStr
     default: return (int)hipErrorInvalidValue;
   }
 }
+
+CSK_DEBUG_EXPORT(gemm8p)

@@ -105,7 +105,35 @@ struct GemmArgs {
   // row_part[((n0 / BN) * M + m) * 2 + {mean, M2}] over the tile's columns.
   // No split-K, no GEGLU.
   float* row_part;
+  // one past the last element an LDS-DMA may read from A / W (CSK_DEBUG checks)
+  const bf16_t* a_end;
+  const bf16_t* w_end;
 };
+
+#define ZERO_BYTES (128 * 1024)  // the LDS-DMA zero page (gemm_glds.hip: csk_init)
+
+// Debug-check sites (CSK_DEBUG record field 1); +100: the LDS destination
+enum DmaSite { SITE_GLDS_A = 1, SITE_GLDS_B, SITE_PERSIST_A, SITE_PERSIST_B,
+               SITE_8P_A, SITE_8P_B, SITE_8R_A, SITE_8R_B, SITE_WIDE_KV };
+
+typedef __attribute__((address_space(1))) const void* csk_gptr_t;
+typedef __attribute__((address_space(3))) void* csk_lptr_t;
+
+// One 16-byte-per-lane LDS-DMA (a wave writes 1 KB at dst).  CSK_DEBUG builds
+// check each lane's source against the operand extents (A, W or the zero page)
+// and the wave's destination against the workgroup's LDS array.
+template <int SITE>
+__device__ __forceinline__ void dma16(const GemmArgs& args, const bf16_t* src, bf16_t* dst, const bf16_t* lds,
+                                      int lds_elems) {
+#ifdef CSK_DEBUG
+  const bool ok = (src >= args.A && src + 8 <= args.a_end) || (src >= args.W && src + 8 <= args.w_end) ||
+                  (src >= args.zero && src + 8 <= args.zero + ZERO_BYTES / 2);
+  CSK_DCHECK(ok, SITE, src - args.A, args.a_end - args.A);
+  const long long off = dst - lds;
+  CSK_DCHECK(off >= 0 && off + 512 <= lds_elems, SITE + 100, off, lds_elems);
+#endif
+  __builtin_amdgcn_global_load_lds((csk_gptr_t)src, (csk_lptr_t)dst, 16, 0, 0);
+}
 
 // Epilogue passes: tiles taller than 128 rows, and the 160-column tiles, stage
 // their fp32 accumulators one wave-row band at a time (a 256x160 tile would need

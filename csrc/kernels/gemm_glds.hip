@@ -24,7 +24,6 @@
 #include "gemm_common.h"
 
 static bf16_t* g_zero = nullptr;
-#define ZERO_BYTES (128 * 1024)
 
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
@@ -110,8 +109,6 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
 
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
 
   // ---- FAST path state: per-row running source pointers, uniform tap / channel offset ----
   const bf16_t* fa[IA];
@@ -149,12 +146,12 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
 #pragma unroll
         for (int i = 0; i < IA; ++i) {
           const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
-          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+          dma16<SITE_GLDS_A>(args, src, as + (wid * IA + i) * 8 * BK, smem, SMEM);
         }
       }
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
-        __builtin_amdgcn_global_load_lds((gptr_t)fb[i], (lptr_t)(bs + (wid * IB + i) * 8 * BK), 16, 0, 0);
+        dma16<SITE_GLDS_B>(args, fb[i], bs + (wid * IB + i) * 8 * BK, smem, SMEM);
         fb[i] += BK;
       }
       if constexpr (CONV) {
@@ -184,12 +181,12 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
       } else {
         if (kin && a_ok[i]) src = a_ptr[i] + (size_t)kt * BK;
       }
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+      dma16<SITE_GLDS_A>(args, src, as + (wid * IA + i) * 8 * BK, smem, SMEM);
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const bf16_t* src = (kin && b_ok[i]) ? b_ptr[i] + (size_t)kt * BK : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(bs + (wid * IB + i) * 8 * BK), 16, 0, 0);
+      dma16<SITE_GLDS_B>(args, src, bs + (wid * IB + i) * 8 * BK, smem, SMEM);
     }
     if constexpr (CONV) {
       c_ci += BK;
@@ -290,8 +287,6 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
   const bf16_t* zero = args.zero;
   const int Hin = args.up2x ? 2 * args.H : args.H;
   const int Win = args.up2x ? 2 * args.Wd : args.Wd;
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
 
   auto tile_of = [&](int i, int& m0, int& n0) {
     const int t = xcd_remap(blockIdx.x + i * gridDim.x, ntiles);
@@ -353,11 +348,11 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
+      dma16<SITE_PERSIST_A>(args, src, as + (wid * IA + i) * 8 * BK, smem, SMEM_MAIN);
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      __builtin_amdgcn_global_load_lds((gptr_t)fb[i], (lptr_t)(bs + (wid * IB + i) * 8 * BK), 16, 0, 0);
+      dma16<SITE_PERSIST_B>(args, fb[i], bs + (wid * IB + i) * 8 * BK, smem, SMEM_MAIN);
       fb[i] += BK;
     }
     if constexpr (CONV) {
@@ -435,168 +430,6 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArg
   }
 }
 
-// ---------------------------------------------------------------------------
-// B-stationary persistent GEMM for the short-K, large-M projections (the UNet's
-// 64x64 / 32x32-level linear layers: M = 8192..32768 rows, K = 320 / 640).
-// Those are bound by the L2->LDS fill (~70 GB/s per CU), and a BM x BN tile
-// moves A * N / BN + B * M / BM bytes: with 128x64 tiles a K = 320, N = 320
-// GEMM re-reads A five times and B 256 times (156 MB for 21 MB of input).
-// Here each workgroup keeps ONE [BN x K] weight slice resident in LDS for its
-// whole life (loaded once, 100 KB at K = 320 / BN = 160) and streams its
-// M-tiles' A operand through an S-stage LDS-DMA ring that runs continuously
-// across tiles (the next tile's A is in flight during this tile's epilogue):
-// A is read N / BN times (twice at N = 320), B once per workgroup (68 MB in all).
-// Grid: column blocks x row groups, the row group's workgroups on one XCD
-// (xcd_remap), so the second read of an A tile hits that XCD's L2.
-// Epilogue: the direct row-layout one (bias, per-sample bias, activation,
-// scale, residual, fused-LN consumer, LN row statistics / GroupNorm statistics
-// of the output), raw barriers so the ring keeps flowing.
-// ---------------------------------------------------------------------------
-template <int BM, int BN, int S, int KMAX>
-__global__ __launch_bounds__(256, 1) void gemm_bstat_kernel(const GemmArgs args0) {
-  constexpr int WM = 2, WN = 2;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int MT = WTM / 16, NT = WTN / 16;
-  constexpr int IA = BM / 32;            // A LDS-DMA instructions per wave per stage (8 rows each)
-  constexpr int ASTAGE = BM * BK;
-  constexpr int BSLICE = BN * KMAX;      // [K / 64][BN][64] swizzled weight slice
-  constexpr int SMEM_EPI = 4 * (WM > WN ? WM : WN) * (BN > BM ? BN : BM) + 64;  // GN / row-stat reductions (fp32)
-  __shared__ __attribute__((aligned(16))) bf16_t smem[BSLICE + S * ASTAGE + SMEM_EPI];
-  bf16_t* bsl = smem;
-  bf16_t* ring = smem + BSLICE;
-  bf16_t* epi = ring + S * ASTAGE;
-  GemmArgs args = args0;
-  args.sw_odd = 1;  // odd fragment counts (BN / WN = 80) use the direct epilogue: no fp32 staging LDS here
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int M = args.M, N = args.N, K = args.K;
-  const int nk = K / BK;
-  const int nbn = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  const int ngroups = gridDim.x / nbn;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = t % nbn, rg = t / nbn;
-  if (rg >= ngroups) return;  // (grid is a multiple of nbn; defensive)
-  const int n0 = cb * BN;
-  const int my_tiles = rg < tiles_m ? (tiles_m - 1 - rg) / ngroups + 1 : 0;
-  const int total = my_tiles * nk;
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;
-  const bf16_t* zero = args.zero;
-  typedef __attribute__((address_space(1))) const void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
-
-  // ---- the weight slice: K / 64 chunks of [BN][64], issued first (oldest in vmcnt order) ----
-  {
-    constexpr int IB = BN / 32;  // per wave per chunk
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int n = n0 + (wid * IB + i) * 8 + lrow;
-      const bf16_t* src = n < N ? args.W + (size_t)n * args.ldb + lchunk * 8 : zero + lchunk * 8;
-      const int step = n < N ? BK : 0;
-      for (int kc = 0; kc < nk; ++kc)
-        __builtin_amdgcn_global_load_lds((gptr_t)(src + (size_t)kc * step),
-                                         (lptr_t)(bsl + kc * BN * BK + (wid * IB + i) * 8 * BK), 16, 0, 0);
-    }
-  }
-
-  // ---- A ring: continuous over (tile, K-step) ----
-  const bf16_t* fa[IA];
-  int is_tile = 0, is_k = 0;
-  auto begin_tile = [&](int i) {
-    const int m0 = (rg + i * ngroups) * BM;
-#pragma unroll
-    for (int r = 0; r < IA; ++r) {
-      const int m = m0 + (wid * IA + r) * 8 + lrow;
-      fa[r] = m < M ? args.A + (size_t)m * args.lda + lchunk * 8 : zero + lchunk * 8;
-    }
-  };
-  auto issue = [&](int buf) {
-    bf16_t* as = ring + buf * ASTAGE;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      __builtin_amdgcn_global_load_lds((gptr_t)fa[i], (lptr_t)(as + (wid * IA + i) * 8 * BK), 16, 0, 0);
-      fa[i] += BK;
-    }
-    if (++is_k == nk) {
-      is_k = 0;
-      if (++is_tile < my_tiles) begin_tile(is_tile);
-    }
-  };
-
-  v4f acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  if (my_tiles > 0) begin_tile(0);
-#pragma unroll
-  for (int st = 0; st < S - 1; ++st)
-    if (st < total) issue(st);
-
-  // every wave's epilogue issues at least EMIN vector-memory instructions (its C
-  // stores: M % BM == N % BN == 0 is required, so none is skipped) AFTER the A
-  // stages that were in flight when it ran; vmcnt counts loads, LDS-DMA and
-  // stores together in issue order, so a stage issued before an epilogue has at
-  // least EMIN more younger operations than the stage count says
-  constexpr int EMIN = MT * (NT / 2) + MT * (NT % 2);
-  const int fr = lane & 15, fq = lane >> 4;
-  int c_tile = 0, c_k = 0;
-  int epi_g = -(1 << 20);  // the K-step after whose MFMAs the latest epilogue ran
-  for (int g = 0; g < total; ++g) {
-    // A stage g has landed once at most min(S-2, total-1-g) younger stages (plus
-    // the younger epilogue's stores, see EMIN) are in flight; the older weight
-    // slice has landed too
-    const int younger = min(S - 2, total - 1 - g);
-    const bool past_epi = g > epi_g && g <= epi_g + S - 1;  // stage g was issued before that epilogue
-    switch (younger + (past_epi ? 8 : 0)) {
-      case 0: vmcnt_wait<0>(); break;
-      case 1: vmcnt_wait<IA>(); break;
-      case 2: vmcnt_wait<2 * IA>(); break;
-      case 3: vmcnt_wait<3 * IA>(); break;
-      case 4: vmcnt_wait<4 * IA>(); break;
-      case 8: vmcnt_wait<EMIN>(); break;
-      case 9: vmcnt_wait<IA + EMIN>(); break;
-      case 10: vmcnt_wait<2 * IA + EMIN>(); break;
-      case 11: vmcnt_wait<3 * IA + EMIN>(); break;
-      case 12: vmcnt_wait<4 * IA + EMIN>(); break;
-      default: vmcnt_wait<0>(); break;  // (S <= 6: not reached)
-    }
-    __builtin_amdgcn_s_barrier();
-    if (g + S - 1 < total) issue((g + S - 1) % S);
-    const bf16_t* as = ring + (g % S) * ASTAGE;
-    const bf16_t* bs = bsl + c_k * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v8s af[MT], bfr[NT];
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-        af[i] = *reinterpret_cast<const v8s*>(as + swz(wm * WTM + i * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-        bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (++c_k == nk) {
-      const int m0 = (rg + c_tile * ngroups) * BM;
-      gemm_epilogue<BM, BN, WM, WN, true, 1, 256, true>(args, acc, epi, m0, n0, 0);
-      epi_g = g;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-      c_k = 0;
-      ++c_tile;
-    }
-  }
-}
-
 static int g_num_cus = 0;
 
 static int num_cus() {
@@ -607,30 +440,6 @@ static int num_cus() {
       g_num_cus = 256;
   }
   return g_num_cus;
-}
-
-// grid of the B-stationary kernel: column blocks x row groups, about one
-// workgroup per CU (never more row groups than M-tiles)
-int csk_bstat_grid(int M, int N, int BM, int BN) {
-  const int nbn = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  int groups = num_cus() / nbn;
-  if (groups < 1) groups = 1;
-  if (groups > tiles_m) groups = tiles_m;
-  return nbn * groups;
-}
-
-template <int BM, int BN, int S, int KMAX>
-static int launch_bstat(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
-  // GEMM only, whole K resident (K <= KMAX, K % 64 == 0), no split-K / GEGLU,
-  // 16-byte vectors in the direct epilogue
-  static_assert(S <= 6, "the wait switch covers S - 2 <= 4 younger stages");
-  if (conv || ksplit > 1 || a0.K > KMAX || a0.K % BK || a0.act == ACT_GEGLU || a0.M % BM || a0.N % BN ||
-      a0.ldc % 8 || a0.lda % 8 || a0.ldb % 8 || a0.act == ACT_PROBE_NO_EPILOGUE)
-    return (int)hipErrorInvalidValue;
-  GemmArgs a = a0;
-  a.gn_seg = BM / 2;  // one segment per wave-row band (WM = 2): the direct epilogue's GN statistics
-  gemm_bstat_kernel<BM, BN, S, KMAX><<<csk_bstat_grid(a.M, a.N, BM, BN), 256, 0, s>>>(a);
-  return (int)hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN, int S>
@@ -726,11 +535,8 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     case 27: return launch_glds<128, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 28: return launch_glds<64, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 29: return launch_glds<128, 64, 2, 2, 4>(a, ksplit, conv, s);
-    // B-stationary persistent (weight slice resident in LDS, A streamed): short-K
-    // large-M projections.  40: K <= 320, N % 160-ish (2 column blocks at N = 320);
-    // 41: K <= 640, 64-wide slices
-    case 40: return launch_bstat<64, 160, 6, 320>(a, ksplit, conv, s);
-    case 41: return launch_bstat<64, 64, 6, 640>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
+
+CSK_DEBUG_EXPORT(gemm_glds)

@@ -23,3 +23,21 @@ def gpu():
 
     _lib.load()  # the HIP path must load on a GPU box: fail loudly otherwise
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _csk_debug_records(request):
+    """With CSK_DEBUG=1 (libcsk_debug.so), every GPU test must leave no
+    device-side bounds record (csrc/kernels/common.h CSK_DCHECK)."""
+    yield
+    if "gpu" not in request.keywords:
+        return
+    from chiaswarm_amd.ops import _lib
+
+    if not _lib.DEBUG or _lib._LIB is None:
+        return
+    import torch
+
+    torch.cuda.synchronize()
+    recs = _lib.debug_records()
+    assert not recs, f"CSK_DEBUG bounds violations (tu, count, site, block, thread, value, limit, block_y): {recs}"

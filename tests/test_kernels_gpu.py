@@ -603,50 +603,3 @@ def test_ring_256x160_gn_stats_and_fallback(gpu, cin, tile):
     got = part.reshape(-1, Cout, 2)
     assert torch.allclose(got[..., 0], want[..., 0], atol=2e-2, rtol=2e-2)
     assert torch.allclose(got[..., 1], want[..., 1], atol=0.5, rtol=2e-2)
-
-
-@pytest.mark.parametrize("tile,N,K", [(40, 320, 320), (40, 960, 320), (41, 640, 640), (41, 320, 640)])
-def test_bstat_tiles_epilogues(gpu, tile, N, K, monkeypatch):
-    """B-stationary persistent tiles (weight slice resident in LDS, A streamed
-    through a continuous ring, several M-tiles per workgroup): bias + SiLU +
-    residual, GroupNorm statistics of the output, LayerNorm row statistics
-    (producer) and the fused-LN consumer, each against fp32 PyTorch."""
-    from types import SimpleNamespace
-
-    from chiaswarm_amd.ops import _lib, tuning
-    from chiaswarm_amd.ops.hip_ops import _p, _s
-
-    M = 4096
-    a, w, b, r = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=K ** -0.5), rnd(N, dev=gpu), rnd(M, N, dev=gpu)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-    _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M, N, K, K, K, N, N, 1, 2, 1.0, None, tile, 1,
-              None, _s())
-    ref = ops._ref_gemm(a.float(), w.float(), b.float(), r.float(), "silu")
-    assert rel_err(out, ref) < 1e-2
-    # a shape the tile rejects fails loudly (never a silent wrong launch)
-    with pytest.raises(RuntimeError):
-        _lib.call("csk_gemm", _p(out), _p(a), _p(w), _p(b), None, _p(r), M - 8, N, K, K, K, N, N, 1, 2, 1.0, None,
-                  tile, 1, None, _s())
-    # GroupNorm statistics of the output (32-row segments), 2 samples of 2048 rows
-    t = tuning.table()
-    monkeypatch.setitem(t, f"g:{M}:{N}:{K}:0", [tile, 1, 0.0])
-    y = hip_ops.gemm(a, w, b, residual=r, gn_rows=M // 2)
-    assert getattr(y, "_csk_gn", None) is not None and y._csk_gn[1] == 32
-    g2, b2 = rnd(N, dev=gpu), rnd(N, dev=gpu)
-    y3 = y.view(2, M // 2, N)
-    y3._csk_gn = y._csk_gn
-    fused = hip_ops.group_norm(y3, g2, b2, 32, 1e-5, True)
-    refg = ops._ref_group_norm(y3.float().cpu(), g2.float().cpu(), b2.float().cpu(), 32, 1e-5, True)
-    assert rel_err(fused.cpu(), refg) < 1e-2
-    # LayerNorm row statistics (producer) -> fused-LN consumer on the same tile
-    monkeypatch.setattr(ops, "LN_FUSE", True)
-    x = ops.gemm(a, w, None, residual=r, row_stats=True)
-    assert getattr(x, "_csk_rows", None) is not None and x._csk_rows[1] == N // tuning.TILES[tile][1]
-    norm = SimpleNamespace(weight=rnd(N, dev=gpu) + 1.0, bias=rnd(N, dev=gpu), eps=1e-5)
-    wc, bc = rnd(N, N, dev=gpu, scale=N ** -0.5), rnd(N, dev=gpu)
-    if N <= tuning.BSTAT_KMAX[tile]:
-        monkeypatch.setitem(t, f"g:{M}:{N}:{N}:0", [tile, 1, 0.0])
-    yl = ops.layer_norm_gemm(x, norm, wc, bc, ops.fold_layer_norm(wc, bc, norm.weight, norm.bias))
-    xn = F.layer_norm(x.float(), (N,), norm.weight.float(), norm.bias.float(), 1e-5)
-    refl = ops._ref_gemm(xn.cpu(), wc.float().cpu(), bc.float().cpu(), None, None)
-    assert rel_err(yl.cpu(), refl) < 1.5e-2

@@ -1,5 +1,9 @@
 """Model-level parity on the GPU: full-size SD2.1 UNet / VAE / OpenCLIP-H with
-the HIP kernels vs the same modules in plain-PyTorch reference mode."""
+the HIP kernels (bf16) vs an fp32 copy of the SAME bf16-rounded weights run
+through the plain-PyTorch reference ops in fp32 (fp32 activations end to end),
+so the bound measures the kernels' bf16 error, not a bf16 baseline's."""
+import copy
+
 import pytest
 import torch
 
@@ -10,9 +14,12 @@ from chiaswarm_amd.models.layers import init_random_fast_, prepare_model
 pytestmark = pytest.mark.gpu
 
 
-def rel_err(y, ref):
+def rel_err(y, ref, name=""):
     y, ref = y.float(), ref.float()
-    return ((y - ref).norm() / (ref.norm() + 1e-12)).item()
+    e = ((y - ref).norm() / (ref.norm() + 1e-12)).item()
+    if name:
+        print(f"[parity] {name}: rel_err {e:.3e} (HIP bf16 vs fp32 twin)")
+    return e
 
 
 def _build(cls, cfg, dev):
@@ -22,38 +29,49 @@ def _build(cls, cfg, dev):
     return prepare_model(m)
 
 
+def _fp32_twin(m):
+    """The same (bf16-valued) weights held in fp32; run under reference mode."""
+    return copy.deepcopy(m).float()
+
+
 @torch.no_grad()
-def test_unet_sd21_parity(gpu):
+def test_unet_sd21_parity_vs_fp32(gpu):
     m = _build(unet.UNet2DConditionModel, unet.SD21, gpu)
     x = torch.randn(2, 32, 32, 4, device=gpu).bfloat16()
     ctx = torch.randn(2, 77, 1024, device=gpu).bfloat16()
     t = torch.tensor([500.0], device=gpu)
+    m32 = _fp32_twin(m)
     with ops.ops_mode("reference"):
-        ref = m(x, t, encoder_hidden_states=ctx)
+        ref = m32(x.float(), t, encoder_hidden_states=ctx.float())
+    assert ref.dtype == torch.float32
+    del m32
     kv = m.encode_context(ctx)
     y = m(x, t, cross_kv=kv)
     assert torch.isfinite(y).all()
-    assert rel_err(y, ref) < 5e-2
+    assert rel_err(y, ref, "unet_sd21") <= 2e-2
 
 
 @torch.no_grad()
-def test_vae_decoder_parity(gpu):
+def test_vae_decoder_parity_vs_fp32(gpu):
     m = _build(vae.AutoencoderKL, vae.SD_VAE, gpu)
     z = torch.randn(1, 32, 32, 4, device=gpu)
+    m32 = _fp32_twin(m)
     with ops.ops_mode("reference"):
-        ref = m.decode(z)
+        ref = m32.decode(z)
     y = m.decode(z)
-    assert rel_err(y, ref) < 5e-2
+    assert rel_err(y, ref, "vae_decoder") <= 2e-2
 
 
 @torch.no_grad()
-def test_text_encoder_parity(gpu):
+def test_text_encoder_parity_vs_fp32(gpu):
     m = _build(clip.CLIPTextModel, clip.OPENCLIP_H, gpu)
     ids = torch.randint(0, 49000, (2, 77), device=gpu)
+    m32 = _fp32_twin(m)
     with ops.ops_mode("reference"):
-        ref = m(ids)[0]
+        ref = m32(ids)[0]
+    assert ref.dtype == torch.float32
     y = m(ids)[0]
-    assert rel_err(y, ref) < 5e-2
+    assert rel_err(y, ref, "openclip_h") <= 2e-2
 
 
 @torch.no_grad()
@@ -102,6 +120,7 @@ def test_unet_up_blocks_read_skip_concats_in_place(gpu):
     hip_ops.GN_CAT_STATS[:] = [0, 0]
     y = m(x, t, encoder_hidden_states=ctx)
     assert hip_ops.GN_CAT_STATS[0] > 0, hip_ops.GN_CAT_STATS
+    m32 = _fp32_twin(m)
     with ops.ops_mode("reference"):
-        ref = m(x, t, encoder_hidden_states=ctx)
-    assert rel_err(y, ref) < 5e-2
+        ref = m32(x, t, encoder_hidden_states=ctx.float())
+    assert rel_err(y, ref, "unet_sd21_gn_cat") <= 2e-2

@@ -28,7 +28,9 @@ def main():
         agpr = re.match(r":\s+(\d+)", b).group(1)
         v = re.search(r"\.vgpr_count:\s+(\d+)", b).group(1)
         lds = re.search(r"\.group_segment_fixed_size:\s+(\d+)", b).group(1)
-        print(f"{name[:70]:70s} vgpr {v:>4s} agpr {agpr:>4s} lds {lds:>6s}")
+        scr = re.search(r"\.private_segment_fixed_size:\s+(\d+)", b)
+        scr = scr.group(1) if scr else "?"
+        print(f"{name[:70]:70s} vgpr {v:>4s} agpr {agpr:>4s} lds {lds:>6s} scratch {scr:>5s}")
 
 
 if __name__ == "__main__":
