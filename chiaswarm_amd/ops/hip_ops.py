@@ -92,6 +92,7 @@ sig("csk_sched_loop", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p
 LOOP_COEF_STRIDE = 12  # elementwise.hip: {p, q, A, B, C, D, s_next, g, g2, -, -, -} per step
 sig("csk_pad_channels", c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p)
 sig("csk_set_gn_prologue_max", c_int)
+sig("csk_debug_selftest", c_int, c_void_p)  # CSK_DEBUG builds: one deliberate record (tests)
 sig("csk_set_gn_lds", c_int)
 sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)

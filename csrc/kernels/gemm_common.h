@@ -353,14 +353,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
                 for (int r = 0; r < 4; ++r) bq[q][r] = 0.f;
               }
             }
-            uint4 rv[MT];  // residual vectors up front (see the non-GEGLU loop below)
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-              const int m = min(m0 + wm * WTM + i * 16 + fr, M - 1);
-              const int col = ob + ((fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4);
-              rv[i] = (args.res && col < outN) ? *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + col)
-                                               : make_uint4(0, 0, 0, 0);
-            }
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
               const int m = m0 + wm * WTM + i * 16 + fr;
@@ -381,12 +373,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
 #pragma unroll
                 for (int r = 0; r < 8; ++r) o[r] *= osc;
               }
-              if (args.res) {
-                float g[8];
-                unpack8(rv[i], g);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] += g[r];
-              }
+              if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
               *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
             }
           }
@@ -406,21 +393,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
           float bb[8], cs[8], gs[8], gq[8];
 #pragma unroll
           for (int r = 0; r < 8; ++r) bb[r] = cs[r] = gs[r] = gq[r] = 0.f;
-          // residual / per-sample-bias row vectors of every row block, loaded
-          // together up front: C may alias them, so a load inside the store loop
-          // would wait for the previous row block's store (MT serialized round
-          // trips per fragment pair)
-          uint4 rv[MT], b2v[MT];
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            const int m = min(m0 + wm * WTM + i * 16 + fr, M - 1);
-            const bool cin = col < outN;
-            rv[i] = (args.res && cin) ? *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + col)
-                                      : make_uint4(0, 0, 0, 0);
-            b2v[i] = (args.bias2d && cin)
-                         ? *reinterpret_cast<const uint4*>(args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col)
-                         : make_uint4(0, 0, 0, 0);
-          }
           if (col < outN) {
             if (args.bias) add8(bb, args.bias + col, true, 8);
             if (lnf) {
@@ -438,23 +410,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
             if (m >= M || col >= outN) continue;
 #pragma unroll
             for (int r = 0; r < 8; ++r) o[r] = lnr[i] * (o[r] - lnm[i] * cs[r]) + bb[r];
-            if (args.bias2d) {
-              float g[8];
-              unpack8(b2v[i], g);
-#pragma unroll
-              for (int r = 0; r < 8; ++r) o[r] += g[r];
-            }
+            if (args.bias2d) add8(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col, true, 8);
             act8(act, o);
             if (osc != 1.0f) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) o[r] *= osc;
             }
-            if (args.res) {
-              float g[8];
-              unpack8(rv[i], g);
-#pragma unroll
-              for (int r = 0; r < 8; ++r) o[r] += g[r];
-            }
+            if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
             if (rst) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) {
@@ -746,20 +708,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
         bf16_t* cp = args.C + (size_t)m * args.ldc + n;
         const bf16_t* rp = args.res ? args.res + (size_t)m * args.ldr + n : nullptr;
         const size_t cstep = (size_t)RPI * args.ldc, rstep = (size_t)RPI * args.ldr;
-        // this thread's residual rows, loaded together before the first store (the
-        // stores may alias them: a load per row would wait for the previous store)
-        constexpr int IT = (PR + RPI - 1) / RPI;
-        uint4 rv[IT];
-        if (rp) {
-#pragma unroll
-          for (int k = 0; k < IT; ++k)
-            rv[k] = (r0 + k * RPI < PR && m + k * RPI < M) ? *reinterpret_cast<const uint4*>(rp + k * rstep)
-                                                            : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-          const int row = r0 + k * RPI;
-          if (row >= PR || m >= M) break;
+        for (int row = r0; row < PR && m < M; row += RPI, m += RPI) {
           const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
           const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
           float f[8] = {lo.x + bb[0], lo.y + bb[1], lo.z + bb[2], lo.w + bb[3],
@@ -771,13 +720,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
           }
           if (rp) {
             float rf[8];
-            unpack8(rv[k], rf);
+            unpack8(*reinterpret_cast<const uint4*>(rp), rf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] += rf[j];
+            rp += rstep;
           }
           *reinterpret_cast<uint4*>(cp) = pack8(f);
           cp += cstep;
-          m += RPI;
         }
       }
       continue;  // next band: nothing else to do without GN / row statistics
@@ -788,32 +737,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
   const int on0 = act == ACT_GEGLU ? n0 / 2 : n0;
   const int vpr = BNo / 8;
   // PR * vpr is a multiple of NTHR for every tile, so each wave runs the same
-  // number of iterations and the row-statistics shuffles below see all lanes.
-  // Residual vectors (non-GEGLU: vpr = BN / 8) are loaded for every iteration up
-  // front: the C stores may alias them, so a load per iteration would wait for
-  // the previous iteration's store.
-  constexpr int GIT = (PR * (BN / 8) + NTHR - 1) / NTHR;
-  uint4 grv[GIT];
-  const bool gpre = args.res != nullptr && act != ACT_GEGLU && (N % 8) == 0 && (args.ldr % 8) == 0 &&
-                    ((((size_t)args.res) & 15) == 0);
-  if (gpre) {
-#pragma unroll
-    for (int k = 0; k < GIT; ++k) {
-      const int v = tid + k * NTHR;
-      const int row = v / vpr, cv = v - row * vpr;
-      const int m = m0 + pr0 + row, n = on0 + cv * 8;
-      grv[k] = (v < PR * vpr && m < M && n + 8 <= outN)
-                   ? *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n)
-                   : make_uint4(0, 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < GIT; ++k) {
-    const int v = tid + k * NTHR;
-    if (act == ACT_GEGLU ? false : v >= PR * vpr) break;
-    if (act == ACT_GEGLU && k > 0) break;  // GEGLU: the runtime-strided loop below
-    for (int vv = v; vv < (act == ACT_GEGLU ? PR * vpr : v + 1); vv += NTHR) {
-    const int row = vv / vpr, cv = vv - row * vpr;  // row within the band
+  // number of iterations and the row-statistics shuffles below see all lanes
+  for (int v = tid; v < PR * vpr; v += NTHR) {
+    const int row = v / vpr, cv = v - row * vpr;  // row within the band
     const int m = m0 + pr0 + row, n = on0 + cv * 8;
     const bool live = m < M && n < outN;
     float f[8];
@@ -842,7 +768,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       if (full && ((((size_t)cp) & 15) == 0)) {
         if (args.res) {
           float rf[8];
-          unpack8(gpre ? grv[k] : *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n), rf);
+          unpack8(*reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + n), rf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] += rf[j];
         }
@@ -885,7 +811,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       if (cv == 0 && m < M)
         *reinterpret_cast<float2*>(args.row_part + ((size_t)(n0 / BN) * M + m) * 2) = make_float2(mean, q);
     }
-    }  // vv
   }
   if (args.gn_part) {
     // column pass: (mean, M2) of each output channel over row segments of

@@ -539,4 +539,20 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   }
 }
 
+// CSK_DEBUG positive control: one wave records a deliberate violation (site 99,
+// value v, limit 3) so a test can prove the record path works end to end
+#ifdef CSK_DEBUG
+__global__ void csk_debug_selftest_kernel(int v) { CSK_DCHECK(v < 0, 99, v, 3); }
+#endif
+CSK_API int csk_debug_selftest(int v, hipStream_t s) {
+#ifdef CSK_DEBUG
+  csk_debug_selftest_kernel<<<1, 64, 0, s>>>(v);
+  return (int)hipGetLastError();
+#else
+  (void)v;
+  (void)s;
+  return (int)hipErrorNotSupported;
+#endif
+}
+
 CSK_DEBUG_EXPORT(gemm_glds)

@@ -408,10 +408,10 @@ def test_conv_bias2d_row_stride(gpu):
 @pytest.mark.parametrize("tile", [None, 11, 13, 14, 19, 20, 21, 22, 25, 26, 27, 29, 31, 32, 33, 34])
 def test_layer_norm_fused_into_gemm(gpu, N, act, tile, monkeypatch):
     """Producer GEMM emits per-row statistics; the consumer GEMM applies the
-    LayerNorm in its epilogue with gamma/beta folded into its weights
-    (opt-in path, CSK_LN_FUSE=1).  ``tile`` forces producer and consumer onto
-    one tile: the row-layout direct epilogue (glds / persistent tiles) and the
-    LDS epilogue (heuristic tiles) both."""
+    LayerNorm in its epilogue with gamma/beta folded into its weights.
+    ``tile`` forces producer and consumer onto one tile: the row-layout direct
+    epilogue (glds / persistent tiles) and the LDS epilogue (heuristic tiles)
+    both."""
     from types import SimpleNamespace
 
     from chiaswarm_amd.ops import tuning
@@ -603,3 +603,25 @@ def test_ring_256x160_gn_stats_and_fallback(gpu, cin, tile):
     got = part.reshape(-1, Cout, 2)
     assert torch.allclose(got[..., 0], want[..., 0], atol=2e-2, rtol=2e-2)
     assert torch.allclose(got[..., 1], want[..., 1], atol=0.5, rtol=2e-2)
+
+
+def test_debug_build_records_violations(gpu):
+    """CSK_DEBUG=1 (libcsk_debug.so): a deliberate violation from the self-test
+    kernel lands in the device record with its site / value / limit and is
+    cleared on read; release builds export no record at all."""
+    from chiaswarm_amd.ops import _lib
+
+    lib = _lib.load()
+    if not _lib.DEBUG:
+        assert not hasattr(lib, "csk_debug_read_gemm_glds")
+        pytest.skip("release build (run with CSK_DEBUG=1 for the debug library)")
+    assert _lib.LIB_PATH.endswith("libcsk_debug.so")
+    torch.cuda.synchronize()
+    assert _lib.debug_records() == []
+    _lib.call("csk_debug_selftest", 7, _lib.stream_ptr())
+    torch.cuda.synchronize()
+    recs = _lib.debug_records()
+    assert len(recs) == 1 and recs[0][0] == "gemm_glds", recs
+    tu, count, site, bx, tid, val, lim, by = recs[0]
+    assert count == 64 and site == 99 and val == 7 and lim == 3, recs  # one wave, every lane fails
+    assert _lib.debug_records() == []  # cleared

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--keys", default="", help="only keys containing this substring")
     ap.add_argument("--all-tiles", action="store_true", help="every candidate, not the shortlist")
     ap.add_argument("--only-tiles", default="", help="comma list: try only these tiles (e.g. a new kernel)")
+    ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG doubles the images: 8 = 4 images, 2 = 1)")
+    ap.add_argument("--latent", type=int, default=64, help="latent side (64 = 512 px)")
     a = ap.parse_args()
     t_start = time.time()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
@@ -51,8 +53,8 @@ def main():
     _lib.load()
     dev = torch.device("cuda", 0)
     p = StableDiffusion("sd21", device=dev, seed=0)
-    x = torch.randn(8, 64, 64, 4, device=dev).bfloat16()
-    ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
+    x = torch.randn(a.batch, a.latent, a.latent, 4, device=dev).bfloat16()
+    ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
 
     used = {}
