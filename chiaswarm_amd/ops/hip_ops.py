@@ -96,6 +96,7 @@ sig("csk_debug_selftest", c_int, c_void_p)  # CSK_DEBUG builds: one deliberate r
 sig("csk_set_gn_lds", c_int)
 sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
+sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_gn_fine", c_int)
 sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
 

@@ -560,6 +560,154 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
   }
 }
 
+// Short-KV attention (Skv <= 128, D <= 64, no mask: the UNet's cross-attention
+// over 77 text tokens): the whole K and V (<= 128 x 64 each, 32 KB) are staged
+// into LDS ONCE per workgroup, then each wave walks ROWS / 64 query tiles of 16
+// rows with no further barrier.  Every key is present, so the softmax is exact
+// in one pass (row max, exp2, sum) — no online rescale.  The pipelined kernel
+// spent most of its time here in per-block prologue / epilogue for a 2-block
+// key loop, and re-loaded K / V for every 64 query rows.
+template <int ROWS>
+__global__ __launch_bounds__(256) void attn_shortkv_kernel(const AttnArgs a) {
+  constexpr int DP = 64, CPR = 8, KMAX = 128, DT = 4;
+  constexpr int TILE = KMAX * DP;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE];  // K, V: [128][64] each
+  bf16_t* ks = smem;
+  bf16_t* vs = smem + TILE;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int Skv = a.Skv;
+  const int nkt = (Skv + 15) / 16;  // 16-key tiles holding a real key
+  const int nqb = (a.Sq + ROWS - 1) / ROWS;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = wg / nqb, qb = wg % nqb;
+  const int b = bh / a.H, h = bh % a.H;
+  const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
+  const bf16_t* kp = a.k + b * a.skb + h * a.skh;
+  const bf16_t* vp = a.v + b * a.svb + h * a.svh;
+  const float sl2 = a.scale_log2;
+
+  // K / V -> LDS (rows >= Skv and columns >= D zero: their P and V^T entries vanish)
+  for (int id = tid; id < KMAX * CPR; id += 256) {
+    const int row = id / CPR, c = id % CPR, d = c * 8;
+    uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (row < Skv && d < a.D) {
+      vk = *reinterpret_cast<const uint4*>(kp + row * a.sks + d);
+      vv = *reinterpret_cast<const uint4*>(vp + row * a.svs + d);
+    }
+    CSK_DCHECK(kv_off<CPR>(row, c) + 8 <= TILE, 23, row, TILE);
+    *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = vk;
+    *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = vv;
+  }
+  __syncthreads();
+
+  // Q rows of tile t (lane: query q0 + fr, d chunk ds * 32 + 8 * fg), loaded one
+  // tile ahead so the next tile's global loads overlap this tile's MFMAs
+  auto load_q = [&](int t, uint4 (&v)[2]) {
+    const int qi = qb * ROWS + t * 16 + fr;
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      const int d = ds * 32 + 8 * fg;
+      v[ds] = (t < ROWS / 16 && qi < a.Sq && d < a.D) ? *reinterpret_cast<const uint4*>(qp + qi * a.sqs + d)
+                                                     : make_uint4(0, 0, 0, 0);
+    }
+  };
+  uint4 qnext[2];
+  load_q(wid, qnext);
+  for (int t = wid; t < ROWS / 16; t += 4) {
+    const int q0 = qb * ROWS + t * 16;
+    if (q0 >= a.Sq) break;
+    // Q fragments (B operand), pre-scaled into log2 units
+    uint4 qraw[2] = {qnext[0], qnext[1]};
+    if (ROWS > 64) load_q(t + 4, qnext);
+    v8s qf[2];
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      float f[8];
+      unpack8(qraw[ds], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[ds] = __builtin_bit_cast(v8s, pack8(f));
+    }
+    // S^T = K Q^T: lane (fr, fg) holds keys kt*16 + 4fg + r of query q0 + fr
+    v4f s[8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+      if (kt < nkt) {
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds) {
+          const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 16 + fr, ds * 4 + fg));
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], s[kt], 0, 0, 0);
+        }
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (kt * 16 + 4 * fg + r >= Skv) s[kt][r] = -INFINITY;
+          mx = fmaxf(mx, s[kt][r]);
+        }
+      }
+    }
+    mx = max_rowgroups(mx);
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = kt < nkt ? __builtin_amdgcn_exp2f(s[kt][r] - mx) : 0.f;
+        s[kt][r] = p;
+        l += p;
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    // O^T = V^T P^T over 32-key groups (P^T straight from the S^T registers)
+    v4f o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kp2 = 0; kp2 < 4; ++kp2) {
+      if (2 * kp2 < nkt) {
+        const u32 w0 = pack2(s[2 * kp2][0], s[2 * kp2][1]);
+        const u32 w1 = pack2(s[2 * kp2][2], s[2 * kp2][3]);
+        const u32 w2 = pack2(s[2 * kp2 + 1][0], s[2 * kp2 + 1][1]);
+        const u32 w3 = pack2(s[2 * kp2 + 1][2], s[2 * kp2 + 1][3]);
+        const v8s pf = __builtin_bit_cast(v8s, make_uint4(w0, w1, w2, w3));
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int qq = fr >> 2, pp = fr & 3;
+          const int col = dt * 16 + 4 * pp;
+          const int r0 = kp2 * 32 + 4 * fg + qq, r1 = r0 + 16;
+          v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r0, col >> 3) + (col & 7)));
+          v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r1, col >> 3) + (col & 7)));
+          v8s vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        }
+      }
+    }
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    const int qi = q0 + fr;
+    if (qi < a.Sq) {
+      bf16_t* op = a.o + b * a.sob + h * a.soh + qi * a.sos;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int d = dt * 16 + 4 * fg;
+        if (d >= a.D) continue;
+        uint2 w;
+        w.x = pack2(o[dt][0] * inv, o[dt][1] * inv);
+        w.y = pack2(o[dt][2] * inv, o[dt][3] * inv);
+        *reinterpret_cast<uint2*>(op + d) = w;
+      }
+    }
+  }
+}
+
 template <int DP, int QT, int DV = DP>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
   constexpr int QROWS = QT * 64;
@@ -569,10 +717,15 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
 }
 
 // Short-KV (Skv <= 128, D <= 64: UNet cross-attention over 77 text tokens)
-// kernel choice for variant 0: 0 = plain loop, 128-row workgroups; 1 = plain,
-// 64-row workgroups (twice the grid: the loop is only 2 key blocks long, so
-// per-workgroup latency, not MFMA work, sets the time); 2 = pipelined QT=1.
-static int g_short_kv_variant = 2;
+// kernel choice for variant 0: 1 = plain, 64-row workgroups; 2 = pipelined
+// QT=1; 3 = K/V-resident one-pass kernel (attn_shortkv_kernel, no mask / no
+// device-side length: otherwise 2).
+static int g_short_kv_variant = 3;
+static int g_short_kv_rows = 0;  // attn_shortkv_kernel query rows per workgroup: 0 = auto, 64 / 128 / 256
+CSK_API int csk_set_short_kv_rows(int r) {
+  g_short_kv_rows = r;
+  return 0;
+}
 CSK_API int csk_set_short_kv_variant(int v) {
   g_short_kv_variant = v;
   return 0;
@@ -644,8 +797,24 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
       return (int)hipGetLastError();
     }
     if (variant == 0 && Skv <= 128) {
+      if (g_short_kv_variant == 3 && !causal && !kv_len && Skv >= 1) {
+        // auto: 128 query rows per workgroup (2 tiles per wave) when that still
+        // gives >= 512 workgroups, else 64 (one tile per wave); 128 measured best
+        // at S = 4096 / 1024 (20.6 / 12.8 us vs 24.0 / 16.8 for the pipelined
+        // kernel, 22.1 / 16.7 at 256 rows: profiles/attn_shortkv_r3j.txt)
+        int rows = g_short_kv_rows;
+        if (rows == 0) rows = (long long)B * H * ((Sq + 127) / 128) >= 512 ? 128 : 64;
+        if (rows == 256) {
+          attn_shortkv_kernel<256><<<dim3(B * H * ((Sq + 255) / 256)), 256, 0, stream>>>(a);
+        } else if (rows == 128) {
+          attn_shortkv_kernel<128><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
+        } else {
+          attn_shortkv_kernel<64><<<dim3(B * H * ((Sq + 63) / 64)), 256, 0, stream>>>(a);
+        }
+        return (int)hipGetLastError();
+      }
       if (g_short_kv_variant == 1) return launch_attn<64, 1>(a, stream);
-      if (g_short_kv_variant == 2) {
+      if (g_short_kv_variant >= 2) {  // (3 with a mask or device-side length)
         attn_fwd_pipe_kernel<1, true, true><<<dim3(B * H * ((Sq + 63) / 64)), 256, 0, stream>>>(a);
         return (int)hipGetLastError();
       }

@@ -187,6 +187,26 @@ def test_attention_variants(gpu, variant, B, Sq, Skv, H, D, causal):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 1 / math.sqrt(D), causal)) < 1.5e-2
 
 
+@pytest.mark.parametrize("short_kv", [1, 2, 3])
+@pytest.mark.parametrize("B,Sq,Skv,H,D", [(2, 4096, 77, 5, 64), (2, 1024, 77, 10, 64), (2, 64, 77, 20, 64),
+                                          (1, 300, 128, 3, 64), (1, 1000, 1, 2, 64), (2, 333, 77, 8, 40),
+                                          (1, 70, 17, 4, 64)])
+def test_attention_short_kv_kernels(gpu, short_kv, B, Sq, Skv, H, D):
+    """Cross-attention shapes (Skv <= 128): the K/V-resident one-pass kernel (3)
+    and the earlier plain (1) / pipelined (2) choices, incl. ragged query tails,
+    a single key, head dim 40 and fused-projection (strided) K / V."""
+    q = rnd(B, Sq, H, D, dev=gpu)
+    kv = rnd(B, Skv, 2, H, D, dev=gpu, scale=2.0)
+    k, v = kv[:, :, 0], kv[:, :, 1]
+    _lib_call = __import__("chiaswarm_amd.ops._lib", fromlist=["call"]).call
+    _lib_call("csk_set_short_kv_variant", short_kv)
+    try:
+        y = hip_ops.attention(q, k, v, 1 / math.sqrt(D))
+    finally:
+        _lib_call("csk_set_short_kv_variant", 3)
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 1 / math.sqrt(D), False)) < 1.5e-2
+
+
 def test_attention_fused_qkv_strides(gpu):
     B, S, H, D = 2, 333, 10, 64
     qkv = rnd(B, S, 3, H, D, dev=gpu)
