@@ -375,6 +375,49 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
   }
 }
 
+// The same merge with one WORKGROUP per (b, g), for the large partial counts of
+// VAE maps (512^2 and 1024^2 images: 8K-64K entries per group, where the
+// one-wave kernel's tail loop serialised a memory round trip per 64 entries):
+// 256 threads, 8 loads in flight each, block-reduced sums.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // red is reused by the next call
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void gn_finalize_part_wg_kernel(const float* __restrict__ part,
+                                                                  float* __restrict__ stat, int B, int C, int G,
+                                                                  int nseg, int seg_rows, float eps,
+                                                                  const float* __restrict__ part2, int C1) {
+  __shared__ float red[4];
+  const int bg = blockIdx.x;
+  const int b = bg / G, g = bg - b * G, Cg = C / G;
+  const int ne = nseg * Cg;
+  const float fn = (float)seg_rows;
+  float sm = 0.f;
+#pragma unroll 8
+  for (int e = threadIdx.x; e < ne; e += 256) {
+    const float2 mq = load_part(part, part2, b * nseg + e / Cg, g * Cg + e % Cg, C, C1);
+    sm += mq.x;
+  }
+  const float mean = block_sum256(sm, red) / (float)ne;  // every entry holds seg_rows rows
+  float sq = 0.f;
+#pragma unroll 8
+  for (int e = threadIdx.x; e < ne; e += 256) {
+    const float2 mq = load_part(part, part2, b * nseg + e / Cg, g * Cg + e % Cg, C, C1);
+    const float d = mq.x - mean;
+    sq += __builtin_fmaf(fn * d, d, mq.y);
+  }
+  const float m2 = block_sum256(sq, red);
+  if (threadIdx.x == 0) {
+    stat[bg * 2] = mean;
+    stat[bg * 2 + 1] = rsqrtf(m2 / fmaxf(fn * (float)ne, 1.f) + eps);
+  }
+}
+
 // stat: B*G*2 floats of workspace
 // x2 / C1: optional second input (channel concat [x | x2], x has C1 channels)
 // part2: optional partials of x2's channels (then `part` holds only x's), so a
@@ -397,8 +440,12 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
         silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1, (const float*)part2);
     CSK_CHECK_LAUNCH();
   }
-  gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
-      (const float*)part, st, B, C, G, nseg, seg_rows, eps, (const float*)part2, C1);
+  if (nseg * (C / G) > 1024)  // large VAE maps (> one round trip of the wave kernel): a workgroup per group
+    gn_finalize_part_wg_kernel<<<B * G, 256, 0, stream>>>((const float*)part, st, B, C, G, nseg, seg_rows, eps,
+                                                          (const float*)part2, C1);
+  else
+    gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
+        (const float*)part, st, B, C, G, nseg, seg_rows, eps, (const float*)part2, C1);
   gn_apply_kernel<0><<<dim3(nchunk, B), GN_THREADS, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, st,
                                                                  (const bf16_t*)gamma, (const bf16_t*)beta, P, C, G,
                                                                  chunk, silu, affine_bstride, 0, 0, eps,

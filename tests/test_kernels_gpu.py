@@ -346,6 +346,24 @@ def test_fused_group_norm_stats(gpu, tile):
     assert rel_err(yc.cpu(), refc) < 1e-2
 
 
+@pytest.mark.parametrize("H,C", [(256, 128), (256, 256)])
+def test_fused_group_norm_stats_large_vae_maps(gpu, H, C):
+    """VAE-sized maps: thousands of epilogue partials per group take the
+    workgroup-per-group finalize (norm.hip gn_finalize_part_wg_kernel)."""
+    x = rnd(1, H, H, C, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(C, C, 3, 3, dev=gpu, scale=(9 * C) ** -0.5))
+    y = hip_ops.conv2d(x, wp, None, 1, 1, None, False, None, gn_stats=True)
+    assert getattr(y, "_csk_gn", None) is not None
+    part, seg = y._csk_gn
+    assert (H * H // seg) * (C // 32) > 1024  # the large-map finalize path
+    g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
+    fused = hip_ops.group_norm(y, g, b, 32, 1e-6, True)
+    plain = hip_ops.group_norm(y.clone(), g, b, 32, 1e-6, True)
+    ref = ops._ref_group_norm(y.float().cpu(), g.float().cpu(), b.float().cpu(), 32, 1e-6, True)
+    assert rel_err(fused.cpu(), ref) < 1e-2
+    assert rel_err(fused, plain) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [1, 11, 14, 26, 31, 32, 33, 34])
 @pytest.mark.parametrize("split", [2, 4])
 def test_fused_group_norm_stats_split_k(gpu, tile, split):
