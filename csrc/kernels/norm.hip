@@ -294,25 +294,53 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
   }
   const GnLayout L(C, tid);
   if (L.r >= L.R) return;
+  // per-channel scale / shift of this thread's (up to two) 8-channel columns:
+  // gamma / beta as one 16-byte load each, the (mean, rstd) of the <= 2 groups
+  // an 8-channel vector touches when Cg >= 4 (24 scalar loads per thread before
+  // the first pixel otherwise)
   float sa[2][8], sb[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int v = L.cv + u * L.NVT;
+    const int v = min(L.cv + u * L.NVT, L.NV - 1);
+    const int c0 = v * 8;
+    float gf[8], bfv[8];
+    if (((((size_t)(gamma + c0)) | ((size_t)(beta + c0))) & 15) == 0) {
+      unpack8(*reinterpret_cast<const uint4*>(gamma + c0), gf);
+      unpack8(*reinterpret_cast<const uint4*>(beta + c0), bfv);
+    } else {  // a strided per-sample affine view
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gf[j] = bf2f(gamma[c0 + j]);
+        bfv[j] = bf2f(beta[c0 + j]);
+      }
+    }
+    const int g0 = c0 / Cg;
+    float2 s0, s1;
+    if (Cg >= 4) {
+      const int g1 = min(g0 + 1, G - 1);
+      if constexpr (MODE == 0) {
+        s0 = *reinterpret_cast<const float2*>(stat + (b * G + g0) * 2);
+        s1 = *reinterpret_cast<const float2*>(stat + (b * G + g1) * 2);
+      } else {
+        s0 = make_float2(gst[2 * g0], gst[2 * g0 + 1]);
+        s1 = make_float2(gst[2 * g1], gst[2 * g1 + 1]);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = min(v * 8 + j, C - 1);
+      const int c = c0 + j;
       const int g = c / Cg;
-      float mean, rstd;
-      if constexpr (MODE == 0) {
-        mean = stat[(b * G + g) * 2];
-        rstd = stat[(b * G + g) * 2 + 1];
+      float2 st;
+      if (Cg >= 4) {
+        st = g == g0 ? s0 : s1;
+      } else if constexpr (MODE == 0) {
+        st = *reinterpret_cast<const float2*>(stat + (b * G + g) * 2);
       } else {
-        mean = gst[2 * g];
-        rstd = gst[2 * g + 1];
+        st = make_float2(gst[2 * g], gst[2 * g + 1]);
       }
-      const float a = bf2f(gamma[c]) * rstd;
+      const float a = gf[j] * st.y;
       sa[u][j] = a;
-      sb[u][j] = bf2f(beta[c]) - mean * a;
+      sb[u][j] = bfv[j] - st.x * a;
     }
   }
   const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
@@ -379,6 +407,12 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(const floa
 // VAE maps (512^2 and 1024^2 images: 8K-64K entries per group, where the
 // one-wave kernel's tail loop serialised a memory round trip per 64 entries):
 // 256 threads, 8 loads in flight each, block-reduced sums.
+static int g_gn_wg_min = 1024;  // partials per group above which the finalize runs a workgroup per group
+CSK_API int csk_set_gn_finalize_wg(int n) {
+  g_gn_wg_min = n;
+  return 0;
+}
+
 __device__ __forceinline__ float block_sum256(float v, float* red) {
   v = wave_sum(v);
   const int w = threadIdx.x >> 6;
@@ -440,7 +474,7 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
         silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1, (const float*)part2);
     CSK_CHECK_LAUNCH();
   }
-  if (nseg * (C / G) > 1024)  // large VAE maps (> one round trip of the wave kernel): a workgroup per group
+  if (nseg * (C / G) > g_gn_wg_min)  // large VAE maps (> one round trip of the wave kernel): a workgroup per group
     gn_finalize_part_wg_kernel<<<B * G, 256, 0, stream>>>((const float*)part, st, B, C, G, nseg, seg_rows, eps,
                                                           (const float*)part2, C1);
   else
