@@ -259,12 +259,16 @@ class BasicTransformerBlock(nn.Module):
             folds[name] = f
         return f[1]
 
-    def forward(self, x, ctx=None, kv=None, row_stats=None):
+    def forward(self, x, ctx=None, kv=None, row_stats=None, dup=False):
         """On the HIP path every LayerNorm runs inside the GEMM that consumes it
         (``ops.layer_norm_gemm``): each producer GEMM (proj_in, the attention
         out-projections, the FF down-projection) emits per-row statistics of its
         output, so the three LN kernels per block disappear.  ``row_stats``: emit
-        them for whatever consumes this block's output (default: on HIP)."""
+        them for whatever consumes this block's output (default: on HIP).
+        ``dup``: ``x`` is one CFG half (UNet2DConditionModel.forward cfg_dup):
+        self-attention and the cross-attention query run on it, and the query and
+        residual are duplicated for the cross-attention (whose context differs
+        between the halves)."""
         hip = ops.row_stats_wanted(x)
         if row_stats is None:
             row_stats = hip
@@ -277,6 +281,8 @@ class BasicTransformerBlock(nn.Module):
         fus = ops.ln_fusable(x)
         q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
                                 self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None)
+        if dup:
+            q, x = torch.cat([q, q], 0), torch.cat([x, x], 0)
         x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
         g = ff.net[0]
         g.ensure()
@@ -306,7 +312,10 @@ class Transformer2D(nn.Module):
     def cross_modules(self):
         return [blk.attn2 for blk in self.transformer_blocks]
 
-    def forward(self, x, ctx=None, kvs=None):
+    def forward(self, x, ctx=None, kvs=None, dup=False):
+        """``dup``: ``x`` is one CFG half; the first block's cross-attention
+        doubles the batch (BasicTransformerBlock.forward) and the output is the
+        full batch."""
         b, hh, ww, c = x.shape
         h = self.norm(x)
         hip = ops.row_stats_wanted(x)
@@ -317,6 +326,10 @@ class Transformer2D(nn.Module):
             h._csk_rows = rows
         nb = len(self.transformer_blocks)
         for i, blk in enumerate(self.transformer_blocks):
+            if dup and i == 0:
+                h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb, dup=True)
+                x, b = torch.cat([x, x], 0), 2 * b
+                continue
             h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb)
         if isinstance(self.proj_out, Linear):
             return ops.gemm(h.view(b, hh, ww, c), self.proj_out.weight, self.proj_out.bias, residual=x,

@@ -247,14 +247,25 @@ class UNet2DConditionModel(Prepared):
         return temb
 
     def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
-                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None):
+                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None,
+                cfg_dup=False):
         """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout].
 
         ``control``: a ControlNet's pre-zero-conv features
         (``pipelines.controlnet.ControlFeatures``): each skip and the mid-block
         output are merged as ``skip + scale * zero_conv(feature)`` inside the
         zero conv's GEMM epilogue (no separate add pass); ``down_residuals`` /
-        ``mid_residual`` (ready-made residuals, diffusers style) are added."""
+        ``mid_residual`` (ready-made residuals, diffusers style) are added.
+
+        ``cfg_dup``: the caller guarantees ``sample[:B/2] == sample[B/2:]`` and a
+        per-sample-identical time embedding (classifier-free guidance duplicates
+        the latents; the reference's ``torch.cat([latents] * 2)`` in diffusers'
+        pipelines behind swarm/diffusion/diffusion_func.py:96).  Everything up to
+        the first cross-attention — conv_in, the first ResNet, the first
+        transformer's GroupNorm / proj_in / self-attention and its cross-attention
+        query projection — is then bit-identical for both halves, so it runs once
+        at half batch and is duplicated where the halves start to differ
+        (common-subexpression elimination, not an approximation)."""
         b = sample.shape[0]
         dtype = self.conv_in.weight.dtype
         x = sample.to(dtype)
@@ -262,24 +273,38 @@ class UNet2DConditionModel(Prepared):
         tprojs = iter(self._temb_projs(temb))
         kv_iter = iter(cross_kv) if cross_kv is not None else None
         ctx = encoder_hidden_states
+        half = b // 2 if (cfg_dup and b % 2 == 0 and ops.use_hip(x)) else 0
 
-        def run_attn(t, h):
+        def run_attn(t, h, dup=False):
             kvs = None
             if kv_iter is not None:
                 kvs = [next(kv_iter) for _ in t.transformer_blocks]
+            if dup:
+                return t(h, ctx=ctx, kvs=kvs, dup=True)
             return t(h, ctx=ctx, kvs=kvs)
 
-        h = self.conv_in(x)
-        skips = [h]
+        def dup2(t):  # [B/2, ...] -> [B, ...] (both CFG halves)
+            return torch.cat([t, t], 0)
+
+        if half:
+            h = self.conv_in(x[:half])
+            skips = [dup2(h)]
+        else:
+            h = self.conv_in(x)
+            skips = [h]
         for blk in self.down_blocks:
             for j, r in enumerate(blk.resnets):
-                h = r(h, next(tprojs))
+                tp = next(tprojs)
+                h = r(h, tp[:half] if half else tp)
                 if blk.attentions is not None:
-                    h = run_attn(blk.attentions[j], h)
-                skips.append(h)
+                    h = run_attn(blk.attentions[j], h, dup=bool(half))
+                    half = 0
+                skips.append(dup2(h) if half else h)
             if blk.downsamplers is not None:
                 h = blk.downsamplers[0](h)
-                skips.append(h)
+                skips.append(dup2(h) if half else h)
+        if half:  # no cross-attention in the down path
+            h = dup2(h)
 
         if control is not None:
             skips = [control.merge_skip(i, s) for i, s in enumerate(skips)]

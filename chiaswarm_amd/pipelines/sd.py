@@ -19,6 +19,7 @@ MI355X design:
 from __future__ import annotations
 
 import dataclasses
+import os
 import math
 import time
 from typing import Any
@@ -268,7 +269,7 @@ class StableDiffusion:
             torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------
-    def _unet_eval(self, x_in, t, cross_kv, added, cc=None):
+    def _unet_eval(self, x_in, t, cross_kv, added, cc=None, dup=False):
         """One denoiser evaluation.  ``cc``: a ControlNet request context — on
         the graph path the ControlNet encoder copy, its zero convs (fused with
         the skip adds) and the UNet are ONE captured hipGraph."""
@@ -277,12 +278,13 @@ class StableDiffusion:
                 or self.device.type != "cuda"):
             tt = torch.tensor([t], device=x_in.device, dtype=torch.float32)
             control = cc.features(x_in, tt) if cc is not None else None
-            return self.unet(x_in, tt, cross_kv=cross_kv, added_cond=added, control=control)
-        key = (x_in.shape, added is not None, len(cross_kv), share,
+            return self.unet(x_in, tt, cross_kv=cross_kv, added_cond=added, control=control,
+                             cfg_dup=dup and cc is None)
+        key = (x_in.shape, added is not None, len(cross_kv), share, dup,
                None if cc is None else (id(cc.model), cc.scale, tuple(cc.cond_emb.shape)))
         g = self._graphs.get(key)
         if g is None:
-            g = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share) if cc is None else
+            g = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share, cfg_dup=dup) if cc is None else
                  _ControlUNetGraph(self.unet, x_in, cross_kv, added, cc, share_kv=share))
             self._graphs[key] = g
         return g.run(x_in, t, cross_kv, added, cc, req=getattr(self, "_req", None))
@@ -315,7 +317,8 @@ class StableDiffusion:
             x_in = torch.cat(parts, 0) if nrep > 1 else xi
             if image_latents is not None:
                 x_in = torch.cat([x_in, image_latents.to(self.dtype)], dim=-1)
-            e = self._unet_eval(x_in, t, cross_kv, added, control)
+            e = self._unet_eval(x_in, t, cross_kv, added, control,
+                                dup=_cfg_dup(self.unet, nrep, image_latents, added))
             coeffs = sched.fused_coeffs()
             if three_way:
                 e_c, e_i, e_u = e.float().chunk(3)
@@ -371,7 +374,8 @@ class StableDiffusion:
             gph = None
         if gph is None:
             spec = _LoopSpec(tuple(x.shape), mode, cap, need_noise, x.device)
-            gph = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share, loop=spec) if control is None else
+            gph = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share, loop=spec,
+                              cfg_dup=_cfg_dup(self.unet, nrep, image_latents, added)) if control is None else
                    _ControlUNetGraph(self.unet, x_in, cross_kv, added, control, share_kv=share, loop=spec))
             self._graphs[key] = gph
         L = gph.loop
@@ -542,6 +546,17 @@ def _apply_mask(image: Image.Image, mask: Image.Image) -> Image.Image:
     return Image.fromarray(arr)
 
 
+def _cfg_dup(unet, nrep, image_latents, added) -> bool:
+    """True when the UNet input's two CFG halves are identical copies with the
+    same time embedding (plain 2-way CFG on a conditional UNet: no per-half
+    image latents, no per-half added conditioning such as SDXL's pooled text
+    embeds), so UNet2DConditionModel.forward may share the prefix up to the
+    first cross-attention (``CFG_SHARE_PREFIX``)."""
+    return (CFG_SHARE_PREFIX and nrep == 2 and image_latents is None and added is None
+            and hasattr(unet, "down_blocks"))
+
+
+CFG_SHARE_PREFIX = os.environ.get("CSK_CFG_SHARE", "1") != "0"
 LOOP_GRAPHS = True  # device-resident sampler loop (StableDiffusion._denoise_loop); False: per-step host loop
 
 
@@ -569,9 +584,10 @@ class _UNetGraph:
     buffers are refreshed by ``copy_`` before each replay.  With ``loop`` the
     graph is a whole sampler step (see StableDiffusion._denoise_loop)."""
 
-    def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False, loop=None):
+    def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False, loop=None, cfg_dup=False):
         self.unet = unet
         self.loop = loop
+        self.cfg_dup = cfg_dup  # x_in's two halves are identical CFG copies (UNet forward cfg_dup)
         self.loop_cap = loop.cap if loop is not None else 0
         self.x = x_in.clone()
         self.t = torch.zeros(1, device=x_in.device, dtype=torch.float32)
@@ -601,6 +617,8 @@ class _UNetGraph:
         return e
 
     def _unet_fwd(self):
+        if self.cfg_dup:
+            return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, cfg_dup=True)
         return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added)
 
     def prepare(self, x_in, cross_kv, added, cc=None, req=None):

@@ -52,6 +52,30 @@ def test_unet_sd21_parity_vs_fp32(gpu):
 
 
 @torch.no_grad()
+def test_unet_cfg_shared_prefix(gpu):
+    """cfg_dup: the prefix up to the first cross-attention runs once at half
+    batch; the output must match the fp32 twin and the unshared HIP forward."""
+    m = _build(unet.UNet2DConditionModel, unet.SD21, gpu)
+    xh = torch.randn(2, 32, 32, 4, device=gpu).bfloat16()
+    x = torch.cat([xh, xh])
+    ctx = torch.randn(4, 77, 1024, device=gpu).bfloat16()
+    t = torch.tensor([500.0], device=gpu)
+    m32 = _fp32_twin(m)
+    with ops.ops_mode("reference"):
+        ref = m32(x.float(), t, encoder_hidden_states=ctx.float())
+    del m32
+    kv = m.encode_context(ctx)
+    y_full = m(x, t, cross_kv=kv)
+    y = m(x, t, cross_kv=kv, cfg_dup=True)
+    assert y.shape == y_full.shape
+    assert rel_err(y, ref, "unet_sd21_cfg_dup") <= 2e-2
+    # two bf16 runs with different tilings each sit ~1.2e-2 from fp32 (random
+    # weights amplify rounding-order differences), so against each other the
+    # bound is the sum of theirs, not a bit-level one
+    assert rel_err(y, y_full, "cfg_dup vs full") <= 3e-2
+
+
+@torch.no_grad()
 def test_vae_decoder_parity_vs_fp32(gpu):
     m = _build(vae.AutoencoderKL, vae.SD_VAE, gpu)
     z = torch.randn(1, 32, 32, 4, device=gpu)

@@ -44,6 +44,8 @@ def apply_arm(arm):
         hip_ops.SPLITK_GN = arm == "skgn1"
     elif arm in ("lnoff", "lnon"):
         ops.LN_FUSE = arm == "lnon"
+    elif arm in ("dup0", "dup1"):  # CFG-shared prefix off / on (UNet forward cfg_dup)
+        pass
     elif arm != "base":
         raise SystemExit(f"unknown arm {arm}")
 
@@ -59,13 +61,14 @@ def main():
     ops._lib.load()
     dev = torch.device("cuda", 0)
     p = StableDiffusion("sd21", device=dev, seed=0)
-    x = torch.randn(8, 64, 64, 4, device=dev).bfloat16()
+    x = torch.randn(4, 64, 64, 4, device=dev).bfloat16()
+    x = torch.cat([x, x])  # identical CFG halves, as in the product loop
     ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
     graphs = {}
     for arm in a.arms.split(","):
         apply_arm(arm)
-        graphs[arm] = _UNetGraph(p.unet, x, kv, None)
+        graphs[arm] = _UNetGraph(p.unet, x, kv, None, cfg_dup=arm != "dup0")
     res = {arm: [] for arm in graphs}
     for _ in range(a.rounds):
         for arm, g in graphs.items():

@@ -19,7 +19,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def record(path, batch, iters):
+def record(path, batch, iters, dup=True):
     import torch
 
     from chiaswarm_amd.models import unet as unet_mod
@@ -33,13 +33,15 @@ def record(path, batch, iters):
         m = unet_mod.UNet2DConditionModel(unet_mod.SD21).to(torch.bfloat16).eval().requires_grad_(False)
     init_random_fast_(m, seed=0)
     prepare_model(m)
-    x = torch.randn(batch, 64, 64, 4, device=dev).to(torch.bfloat16)
+    x = torch.randn(batch // 2 if dup else batch, 64, 64, 4, device=dev).to(torch.bfloat16)
+    if dup:  # identical CFG halves and the shared prefix, as in the product loop
+        x = torch.cat([x, x])
     ctx = torch.randn(batch, 77, 1024, device=dev).to(torch.bfloat16)
     kv = m.encode_context(ctx)
     t = torch.tensor([500.0], device=dev)
     with torch.no_grad():
         for _ in range(2):
-            m(x, t, cross_kv=kv)
+            m(x, t, cross_kv=kv, cfg_dup=dup)
     torch.cuda.synchronize()
     sep = torch.zeros(1, dtype=torch.int32, device=dev)
     orig = _lib.call
@@ -54,7 +56,7 @@ def record(path, batch, iters):
     _lib.call = wrapped
     with torch.no_grad():
         for _ in range(iters):
-            m(x, t, cross_kv=kv)
+            m(x, t, cross_kv=kv, cfg_dup=dup)
     torch.cuda.synchronize()
     _lib.call = orig
     with open(path, "w") as f:
@@ -120,10 +122,11 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--no-cfg-dup", action="store_true")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if a.record:
-        record(a.record, a.batch, a.iters)
+        record(a.record, a.batch, a.iters, not a.no_cfg_dup)
     if a.db:
         dbs = glob.glob(a.db) or [a.db]
         analyse(dbs[0], a.calls, a.json)

@@ -42,10 +42,13 @@ def main():
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--min-gain-us", type=float, default=6.0)
     ap.add_argument("--keys", default="", help="only keys containing this substring")
+    ap.add_argument("--missing", action="store_true", help="only keys the table has no entry for (new shapes)")
     ap.add_argument("--all-tiles", action="store_true", help="every candidate, not the shortlist")
     ap.add_argument("--only-tiles", default="", help="comma list: try only these tiles (e.g. a new kernel)")
     ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG doubles the images: 8 = 4 images, 2 = 1)")
     ap.add_argument("--latent", type=int, default=64, help="latent side (64 = 512 px)")
+    ap.add_argument("--no-cfg-dup", action="store_true",
+                    help="tune the unshared step (default: the product's CFG-shared prefix, identical halves)")
     a = ap.parse_args()
     t_start = time.time()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
@@ -53,7 +56,8 @@ def main():
     _lib.load()
     dev = torch.device("cuda", 0)
     p = StableDiffusion("sd21", device=dev, seed=0)
-    x = torch.randn(a.batch, a.latent, a.latent, 4, device=dev).bfloat16()
+    x = torch.randn(a.batch // 2, a.latent, a.latent, 4, device=dev).bfloat16()
+    x = torch.cat([x, x])  # CFG halves are identical copies in the product loop
     ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
 
@@ -67,9 +71,10 @@ def main():
 
     tuning.choose = spy
     table = tuning.table()
+    present0 = set(table)  # keys present before the first capture
 
     def capture():
-        return _UNetGraph(p.unet, x, kv, None, warmup=1)
+        return _UNetGraph(p.unet, x, kv, None, warmup=1, cfg_dup=not a.no_cfg_dup)
 
     def timed(g, rounds=3):
         for _ in range(2):
@@ -93,6 +98,8 @@ def main():
     keys = sorted(used, key=lambda k: used[k][0])  # smallest M first
     if a.keys:
         keys = [k for k in keys if a.keys in k]
+    if a.missing:
+        keys = [k for k in keys if k not in present0]
 
     def save():
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
