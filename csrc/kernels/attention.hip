@@ -183,6 +183,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
             if (key >= kv_end || (a.causal && key > qi)) s[kt][qt][r] = -INFINITY;
           }
       }
+      mfma_fence4(s[0][qt], s[1][qt], s[2][qt], s[3][qt]);
       float mx = vmax3(s[0][qt][0], s[0][qt][1], s[0][qt][2]);
       mx = vmax3(mx, s[0][qt][3], s[1][qt][0]);
       mx = vmax3(mx, s[1][qt][1], s[1][qt][2]);
@@ -438,6 +439,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
           }
       }
       // 16 scores -> 8 v_max3, then the 4 row groups via permlane swaps
+      mfma_fence4(sc[0][qt], sc[1][qt], sc[2][qt], sc[3][qt]);
       float mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
       mx = vmax3(mx, sc[0][qt][3], sc[1][qt][0]);
       mx = vmax3(mx, sc[1][qt][1], sc[1][qt][2]);
@@ -557,6 +559,259 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
       w.y = pack2(oacc[dt][qt][2] * inv, oacc[dt][qt][3] * inv);
       *reinterpret_cast<uint2*>(op + qi * a.sos + d) = w;
     }
+  }
+}
+
+// 32x32x16 variant of the pipelined kernel (D <= 64): S^T = K Q^T and
+// O^T = V^T P^T on v_mfma_f32_32x32x16_bf16.  At D = 64 the softmax is
+// VALU-issue bound: a 16x16x32 MFMA (16 cycles) blocks vector issue for 8 of
+// its cycles and leaves room for ~2 VALU instructions, a 32x32x16 one (32
+// cycles) for ~5 (MI355X_MICROARCH.md 'vector-instruction ISSUE cost'), so the
+// same exp / max / convert / sum work per score hides under the MFMAs with
+// 1.5x the slack.  Layout (cdna_hip_programming.md §3 'An accumulator tile as
+// the next MFMA's operand'): the S^T accumulator puts query r = lane & 31 on
+// the lane and keys (i & 3) + 8 (i >> 2) + 4 (lane >> 5) of the 32-key tile in
+// register i, so registers 8s..8s+7 (bf16 pairs) ARE the P^T fragment of PV
+// k-step s, and the matching V^T fragment (keys 16s + 4h + 0..3 and +8) is two
+// ds_read_b64_tr_b16 of the row-major V tile.  Row max: in-lane over 32 scores
+// + one permlane32 swap; row sum: in-lane partials, the two lane halves added
+// at the end.  Q pre-scaled, the QK^T chain starts from -max (PRE), lazy
+// rescale (T13, threshold 2^8), same 3-buffer register-staged K/V ring and
+// one-barrier-per-block software pipeline (QK^T of block kb+1 issued before
+// the softmax of block kb) as attn_fwd_pipe_kernel.
+// QB: 32-query tiles per wave (128 or 256 query rows per workgroup).
+template <int QB>
+__global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
+  constexpr int DP = 64, CPR = DP / 8, KB = 64;
+  constexpr int QROWS = QB * 32 * 4;
+  constexpr int TILE = KB * DP;
+  constexpr int LPT = KB * CPR / 256;
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TILE];  // (K, V) x 3
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
+  const int nqb = (a.Sq + QROWS - 1) / QROWS;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = wg / nqb, qb = wg % nqb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qb * QROWS + wid * QB * 32;
+  const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
+  const bf16_t* kp = a.k + b * a.skb + h * a.skh;
+  const bf16_t* vp = a.v + b * a.svb + h * a.svh;
+  const float sl2 = a.scale_log2;
+
+  // Q^T fragments (B operand): lane holds Q[q0 + qt*32 + r][ds*16 + 8*hh .. +7] * scale*log2(e)
+  v8s qf[QB][4];
+#pragma unroll
+  for (int qt = 0; qt < QB; ++qt)
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      const int qi = q0 + qt * 32 + r, d = ds * 16 + 8 * hh;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qi < a.Sq && d < a.D) v = *reinterpret_cast<const uint4*>(qp + qi * a.sqs + d);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[qt][ds] = __builtin_bit_cast(v8s, pack8(f));
+    }
+  v16f oacc[2][QB];  // O^T d-tile dt: query r, d = dt*32 + (i & 3) + 8 (i >> 2) + 4 hh
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < QB; ++qt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][qt][i] = 0.f;
+  float mrow[QB], lrow[QB];  // running max (log2 units); this lane's partial row sum
+#pragma unroll
+  for (int qt = 0; qt < QB; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
+
+  int kv_end = Skv;
+  if (a.causal) {
+    const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (Skv - a.Sq);
+    kv_end = min(Skv, qlast + 1);
+  }
+  const int nkb = (kv_end + KB - 1) / KB;
+
+  uint4 rk[LPT], rv[LPT];
+  auto load_kv = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      const int key = min(kb * KB + row, Skv - 1), d = c * 8;  // clamped rows are masked later
+      CSK_DCHECK(key >= 0, 24, key, Skv);
+      uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (d < a.D) {
+        vk = *reinterpret_cast<const uint4*>(kp + key * a.sks + d);
+        vv = *reinterpret_cast<const uint4*>(vp + key * a.svs + d);
+      }
+      rk[i] = vk;
+      rv[i] = vv;
+    }
+  };
+  auto store_kv = [&](int buf) {
+    bf16_t* ks = smem + buf * 2 * TILE;
+    bf16_t* vs = ks + TILE;
+    CSK_DCHECK(buf >= 0 && buf < 3, 25, buf, 3);
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+      *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
+      *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
+    }
+  };
+  // scores of one 64-key block: s[kt][qt] = S^T of keys kt*32.. (issued with offset -mu)
+  auto qk = [&](int buf, v16f (&s)[2][QB], float (&mu)[QB]) {
+    const bf16_t* ks = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int qt = 0; qt < QB; ++qt) mu[qt] = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int qt = 0; qt < QB; ++qt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 32 + r, 2 * ds + hh));
+#pragma unroll
+        for (int qt = 0; qt < QB; ++qt)
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qt][ds], s[kt][qt], 0, 0, 0);
+      }
+    }
+  };
+
+  if (nkb > 0) { load_kv(0); store_kv(0); }
+  if (nkb > 1) { load_kv(1); store_kv(1); }
+  __syncthreads();
+  v16f s_a[2][QB], s_b[2][QB];
+  float mu_a[QB], mu_b[QB];
+  auto block = [&](int kb, v16f (&sc)[2][QB], float (&muc)[QB], v16f (&sn)[2][QB], float (&mun)[QB]) {
+    const int cur = kb % NBUF;
+    if (kb + 2 < nkb) load_kv(kb + 2);
+    if (kb + 1 < nkb) qk((kb + 1) % NBUF, sn, mun);  // matrix cores busy while the softmax below runs
+
+    const int kbase = kb * KB;
+    const bool masked = a.causal || (kbase + KB > kv_end);
+    v8s pf[2][2][QB];  // [key tile][PV k-step][query tile]
+#pragma unroll
+    for (int qt = 0; qt < QB; ++qt) {
+      if (masked) {
+        const int qi = q0 + qt * 32 + r + (Skv - a.Sq);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kbase + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (key >= kv_end || (a.causal && key > qi)) sc[kt][qt][i] = -INFINITY;
+          }
+      }
+      mfma_fence16(sc[0][qt], sc[1][qt]);
+      float mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) mx = vmax3(mx, sc[0][qt][i], sc[0][qt][i + 1]);
+      mx = vmax3(mx, sc[0][qt][15], sc[1][qt][0]);
+#pragma unroll
+      for (int i = 1; i < 15; i += 2) mx = vmax3(mx, sc[1][qt][i], sc[1][qt][i + 1]);
+      mx = vmax3(mx, sc[1][qt][15], sc[1][qt][15]);
+      {  // the other 32 keys of this query live in lane ^ 32
+        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = vmax3(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[1]));
+      }
+      const float mb = mx + muc[qt];  // block max, log2 units
+      if (mb > mrow[qt] + 8.f) {
+        const float mnew = fmaxf(mrow[qt], mb);
+        const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
+        mrow[qt] = mnew;
+        lrow[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) oacc[dt][qt] *= alpha;
+      }
+      const float shift = mrow[qt] - muc[qt];  // 0 unless the max moved since the block was issued
+      if (__any(shift != 0.f)) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sc[kt][qt][i] -= shift;
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
+      // 4 independent single-instruction add chains (no v_pk_add_f32 beside MFMAs)
+      float l4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        l4[c] = vadd(sc[0][qt][c], sc[0][qt][c + 4]);
+        l4[c] = vadd(l4[c], vadd(sc[0][qt][c + 8], sc[0][qt][c + 12]));
+        l4[c] = vadd(l4[c], vadd(sc[1][qt][c], sc[1][qt][c + 4]));
+        l4[c] = vadd(l4[c], vadd(sc[1][qt][c + 8], sc[1][qt][c + 12]));
+      }
+      lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int o = 8 * st;
+          const u32 w0 = pack2(sc[kt][qt][o + 0], sc[kt][qt][o + 1]);
+          const u32 w1 = pack2(sc[kt][qt][o + 2], sc[kt][qt][o + 3]);
+          const u32 w2 = pack2(sc[kt][qt][o + 4], sc[kt][qt][o + 5]);
+          const u32 w3 = pack2(sc[kt][qt][o + 6], sc[kt][qt][o + 7]);
+          pf[kt][st][qt] = __builtin_bit_cast(v8s, make_uint4(w0, w1, w2, w3));
+        }
+    }
+    const bf16_t* vs = smem + cur * 2 * TILE + TILE;
+    // V^T fragment of PV k-step (kt, st), d-tile dt: lane 4q+p of 16-lane group g
+    // addresses key row kt*32 + 16 st + 4 (g >> 1) + q (+8 for elements 4..7),
+    // columns dt*32 + 16 (g & 1) + 4p .. +3; lane i of the group receives column i
+    const int qq = fr >> 2, pp = fr & 3;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = dt * 32 + 16 * (fg & 1) + 4 * pp;
+          const int r0 = kt * 32 + 16 * st + 4 * (fg >> 1) + qq, r1 = r0 + 8;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r0, col >> 3) + (col & 7)));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r1, col >> 3) + (col & 7)));
+          const v8s vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int qt = 0; qt < QB; ++qt)
+            oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
+        }
+    if (kb + 2 < nkb) store_kv((kb + 2) % 3);
+    __syncthreads();
+  };
+  if (nkb > 0) qk(0, s_a, mu_a);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    block(kb, s_a, mu_a, s_b, mu_b);
+    if (kb + 1 < nkb) block(kb + 1, s_b, mu_b, s_a, mu_a);
+  }
+
+  bf16_t* op = a.o + b * a.sob + h * a.soh;
+#pragma unroll
+  for (int qt = 0; qt < QB; ++qt) {
+    float l = lrow[qt];
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    const int qi = q0 + qt * 32 + r;
+    if (qi >= a.Sq) continue;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        if (d >= a.D) continue;
+        uint2 w;
+        w.x = pack2(oacc[dt][qt][4 * g] * inv, oacc[dt][qt][4 * g + 1] * inv);
+        w.y = pack2(oacc[dt][qt][4 * g + 2] * inv, oacc[dt][qt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(op + qi * a.sos + d) = w;
+      }
   }
 }
 
@@ -731,6 +986,14 @@ CSK_API int csk_set_short_kv_variant(int v) {
   return 0;
 }
 
+// Default for D = 64, Skv > 128 (the UNet self-attention): the 32x32x16 kernel
+// (attn32_kernel, 1) or the 16x16x32 pipelined one (0; A/B knob)
+static int g_attn32 = 1;
+CSK_API int csk_set_attn32(int on) {
+  g_attn32 = on;
+  return 0;
+}
+
 // variant: 0 = default choice, 1 = plain double-buffered loop, 2 = pipelined (D <= 64),
 // 3 = pipelined + PRE, 4 = pipelined + ONES, 5 = pipelined + PRE + ONES
 extern "C" int csk_attention_wide(void* o, const void* q, const void* k, const void* v, const long long* strides,
@@ -756,6 +1019,14 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   const long long wg4 = (long long)B * H * ((Sq + 255) / 256);
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
+    if (variant == 0 && g_attn32 && D == 64 && Skv > 128) variant = 20;
+    if (variant == 20 || variant == 21) {  // 32x32x16 MFMA kernel, 128 / 256 query rows per workgroup
+      if (variant == 20)
+        attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
+      else
+        attn32_kernel<2><<<dim3(B * H * ((Sq + 255) / 256)), 256, 0, stream>>>(a);
+      return (int)hipGetLastError();
+    }
     if (variant >= 2 || (variant == 0 && Skv > 128)) {
       // PRE+ONES: 279 vs 283 (PRE) vs 306 us (plain) at B8 S4096 H5, same box; for
       // short grids (< 1024 workgroups of 128 rows: S1024 H10) 64-row workgroups

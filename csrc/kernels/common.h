@@ -77,6 +77,18 @@ __device__ __forceinline__ float vadd(float a, float b) {
   asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// MFMA result -> inline-asm reader: hipcc pads no wait states for an asm
+// statement (cdna_hip_programming.md §5.7 item 2), and the softmax's vmax3
+// reads score accumulators straight out of the matrix cores.  This nop
+// statement names the accumulators ("+v": ordered after the MFMAs that write
+// them, before any reader) and covers the XDL write -> read distance: 12 states
+// for the 8-pass 16x16x32, 18 for the 16-pass 32x32x16.
+__device__ __forceinline__ void mfma_fence4(v4f& a, v4f& b, v4f& c, v4f& d) {
+  asm volatile("s_nop 7\n\ts_nop 3" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void mfma_fence16(v16f& a, v16f& b) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
 // max over lanes {l, l^16, l^32, l^48} (the four 16-lane row groups of a
 // 16x16 MFMA fragment) with two permlane swaps: no LDS round trip (the
 // ds_bpermute that __shfl_xor lowers to sat in the softmax's critical chain)

@@ -23,6 +23,10 @@ GEMMS = ["32768,320,320", "32768,960,320", "32768,2560,320:geglu", "32768,320,12
          "8192,5120,640:geglu", "8192,640,2560", "2048,1280,1280", "2048,10240,1280:geglu", "2048,1280,5120"]
 
 
+def tiles_persistent(a):
+    return any(21 <= int(t) <= 24 for t in a.tiles.split(","))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="11,26,31,32")
@@ -31,6 +35,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="conv|gemm")
     ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
+    ap.add_argument("--res", action="store_true", help="GEMMs also with a residual input (epilogue load)")
+    ap.add_argument("--gemms", default="", help="comma-free list 'M,N,K;M,N,K' overriding the GEMM shapes")
     ap.add_argument("--gn", action="store_true", help="convs also emitting fused GroupNorm statistics (64-row segments)")
     ap.add_argument("--swodd", default="", help="comma list of csk_set_sw_odd values to A/B (160-wide tile epilogue)")
     ap.add_argument("--probe-halo", action="store_true",
@@ -72,7 +78,7 @@ def main():
                     ("" if sw is None else f" swodd{sw}")
                 jobs.append((f"conv {spec}{tag}", fl, run))
     if a.only != "conv":
-        for spec in GEMMS:
+        for spec in (a.gemms.split(";") if a.gemms else GEMMS):
             geglu = spec.endswith(":geglu")
             M, N, K = map(int, spec.split(":")[0].split(","))
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -81,12 +87,16 @@ def main():
             y = torch.empty(M, no, dtype=torch.bfloat16, device=dev)
             fl = 2.0 * M * N * K
 
-            for probe in ((False, True) if a.probe else (False,)):
-                def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe):
+            r = torch.randn(M, no, device=dev).to(torch.bfloat16)
+            variants = [(False, False)] + ([(True, False)] if a.probe else []) + ([(False, True)] if a.res else [])
+            for probe, res in variants:
+                if probe and tiles_persistent(a):
+                    continue  # the persistent kernels have no probe exit (act 99 would run the epilogue)
+                def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe, res=res, r=r):
                     ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
-                    _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, None, M, N, K, K, K, no, no, 1,
-                              99 if probe else (3 if geglu else 0), 1.0, None, tile, split, _p(ws), _s())
-                jobs.append((f"gemm {spec}" + (" noepi" if probe else ""), fl, run))
+                    _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, _p(r) if res else None, M, N, K, K, K, no,
+                              no, 1, 99 if probe else (3 if geglu else 0), 1.0, None, tile, split, _p(ws), _s())
+                jobs.append((f"gemm {spec}" + (" noepi" if probe else "") + (" res" if res else ""), fl, run))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for name, fl, run in jobs:
         res = {}
