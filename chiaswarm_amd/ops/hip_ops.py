@@ -98,6 +98,7 @@ sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
+sig("csk_set_ln_in_kernel", c_int)
 sig("csk_set_gn_finalize_wg", c_int)
 sig("csk_set_gn_fine", c_int)
 sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)

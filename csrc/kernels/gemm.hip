@@ -520,6 +520,12 @@ CSK_API int csk_set_gn_fine(int v) {
   return 0;
 }
 
+static int g_ln_in_kernel = 1;  // A/B knob: 0 = ln_rowstats_kernel in front of every fused-LN consumer
+CSK_API int csk_set_ln_in_kernel(int v) {
+  g_ln_in_kernel = v;
+  return 0;
+}
+
 CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
                         int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act,
                         float out_scale, void* gn_part, const void* ln_part, const void* ln_colsum, int ln_nparts,
@@ -543,7 +549,10 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   a.a_end = a.A + (size_t)(M > 0 ? M - 1 : 0) * lda + K;
   a.w_end = a.W + (size_t)(N > 0 ? N - 1 : 0) * ldb + K;
   if (M == 0 || N == 0) return 0;
-  if (ln_part) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
+  // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
+  // ln_merge_tile); the others read them from a merge kernel launched first
+  const bool in_kernel = tile >= 11 && tile <= 29 && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
+  if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
     if (!rows) return (int)hipErrorInvalidValue;
     ln_rowstats_kernel<<<(M + 255) / 256, 256, 0, stream>>>((const float*)ln_part, rows, M, K, ln_nparts, ln_pcols,

@@ -230,6 +230,67 @@ __device__ __forceinline__ float2 ln_row_stats(const GemmArgs& args, int m0) {
   return *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + r, args.M - 1) * 2);
 }
 
+// Fused-LN row statistics merged INSIDE the consumer GEMM (no ln_rowstats
+// launch in front of it): the 256 threads load the producer's column-slab
+// partials of the tile's BM rows (NPH = 256 / BM threads per row, each merging
+// every NPH-th slab, <= 8 in one round trip), combine them (Chan) through a
+// [NPH][BM][3] + [BM][2] float scratch, and every lane keeps the (mean, rstd)
+// of its MT epilogue rows in registers (threads < BM also their own row, for
+// the LDS epilogue).  Called right after the prologue DMA issue with the LAST
+// ring stage as scratch: the DMA first writes that stage after the main loop's
+// first barrier, which every wave reaches only after its scratch reads retired
+// (lgkmcnt(0) below).  Raw barriers: __syncthreads' vmcnt(0) would also wait for
+// the ring prologue.
+template <int BM, int MT, int WTM>
+__device__ __forceinline__ void ln_merge_tile(const GemmArgs& args, int m0, int wm, float* scratch,
+                                              float2 (&lane_rows)[MT], float2& own) {
+  constexpr int NPH = 256 / BM, CAP = 8;
+  const int t = threadIdx.x, r = t % BM, ph = t / BM;
+  const int M = args.M, K = args.K, np = args.ln_nparts, pc = args.ln_pcols;
+  const int m = min(m0 + r, M - 1);
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  float2 st[CAP];
+#pragma unroll
+  for (int j = 0; j < CAP; ++j) {
+    const int p = ph + j * NPH;
+    st[j] = p < np ? *reinterpret_cast<const float2*>(args.ln_part + ((size_t)p * M + m) * 2) : make_float2(0.f, 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < CAP; ++j) {
+    const int p = ph + j * NPH;
+    if (p < np) chan_combine(n, mean, m2, (float)min(pc, K - p * pc), st[j].x, st[j].y);
+  }
+  for (int p = ph + CAP * NPH; p < np; p += NPH) {
+    const float2 s2 = *reinterpret_cast<const float2*>(args.ln_part + ((size_t)p * M + m) * 2);
+    chan_combine(n, mean, m2, (float)min(pc, K - p * pc), s2.x, s2.y);
+  }
+  float* part = scratch;              // [NPH][BM][3]
+  float* rows = scratch + NPH * BM * 3;  // [BM][2] (mean, rstd)
+  part[(ph * BM + r) * 3 + 0] = n;
+  part[(ph * BM + r) * 3 + 1] = mean;
+  part[(ph * BM + r) * 3 + 2] = m2;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (t < BM) {
+    float nn = part[t * 3], mm = part[t * 3 + 1], qq = part[t * 3 + 2];
+#pragma unroll
+    for (int q = 1; q < NPH; ++q) chan_combine(nn, mm, qq, part[(q * BM + t) * 3], part[(q * BM + t) * 3 + 1],
+                                                part[(q * BM + t) * 3 + 2]);
+    rows[t * 2] = mm;
+    rows[t * 2 + 1] = rsqrtf(qq / fmaxf(nn, 1.f) + args.ln_eps);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  own = t < BM ? make_float2(rows[t * 2], rows[t * 2 + 1]) : make_float2(0.f, 0.f);
+  const int fr = t & 15;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int lr = wm * WTM + i * 16 + fr;
+    lane_rows[i] = make_float2(rows[lr * 2], rows[lr * 2 + 1]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // The 8-column output vector a lane owns after the v_permlane16_swap of a pair of
 // row-layout fragments (SW epilogues): fragments f and f+1 hold columns
 // f*16 + fq*4 + r and (f+1)*16 + fq*4 + r of one row; after the swap an even-row
@@ -251,10 +312,14 @@ __device__ __forceinline__ int sw_pair(v4f& x, v4f& y, int f, int fq, float (&o)
 // activation incl. GEGLU / scale / residual) store 16-byte row vectors straight
 // from registers — no fp32 LDS round trip, no barrier (the probe measured the
 // LDS epilogue at about half of a K = 320 GEMM's time, tools/tilebench.py --probe).
+// ln_lane / ln_in: per-lane (mean, rstd) of the MT epilogue rows merged in the
+// kernel prologue (ln_merge_tile); a reference to a fixed-size array so the
+// values stay in registers (a pointer that may be null made hipcc keep the
+// array in scratch)
 template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false>
-__device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
-                                              bf16_t* smem, int m0, int n0, int split,
-                                              float2 lnrow = make_float2(0.f, 0.f)) {
+__device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
+                                                 bf16_t* smem, int m0, int n0, int split, float2 lnrow,
+                                                 const float2 (&ln_lane)[BM / WM / 16], bool ln_in) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int LDC_S = BN + 4;
@@ -304,7 +369,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     const bool rst = args.row_part != nullptr;
     const bool gnp = args.gn_part != nullptr;
     const int gseg = args.gn_seg > 0 ? args.gn_seg : BM;
-    const bool direct = (NT % 2 == 0 || args.sw_odd) && (!gnp || (!args.gn_lds && !geglu && !rst && gseg % WTM == 0 && BM % gseg == 0)) && (!lnf || args.ln_row) &&
+    const bool direct = (NT % 2 == 0 || args.sw_odd) && (!gnp || (!args.gn_lds && !geglu && !rst && gseg % WTM == 0 && BM % gseg == 0)) && (!lnf || args.ln_row || ln_in) &&
                         (!rst || !geglu) && (geglu_ok || !geglu) &&
                         (N % (geglu ? 16 : 8)) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
                         (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
@@ -323,7 +388,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
       for (int i = 0; i < MT; ++i) {
         lnm[i] = 0.f;
         lnr[i] = 1.f;
-        if (lnf) {  // independent loads, issued together before the fragment loop
+      }
+      if (lnf && ln_in) {  // merged in the kernel prologue (ln_merge_tile)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          lnm[i] = ln_lane[i].x;
+          lnr[i] = ln_lane[i].y;
+        }
+      } else if (lnf) {  // independent loads, issued together before the fragment loop
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
           const float2 st =
               *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + wm * WTM + i * 16 + fr, M - 1) * 2);
           lnm[i] = st.x;
@@ -858,6 +932,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[B
     }
   }
   }  // passes
+}
+
+template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
+                                              bf16_t* smem, int m0, int n0, int split,
+                                              float2 lnrow = make_float2(0.f, 0.f)) {
+  float2 none[BM / WM / 16];
+#pragma unroll
+  for (int i = 0; i < BM / WM / 16; ++i) none[i] = make_float2(0.f, 1.f);
+  gemm_epilogue_ln<BM, BN, WM, WN, RAW, EP, NTHR, SW>(args, acc, smem, m0, n0, split, lnrow, none, false);
 }
 
 // GN statistics granularity: 1 = fine segments (BM*BN/256 rows, every thread of

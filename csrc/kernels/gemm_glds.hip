@@ -203,7 +203,20 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s, s);
-  const float2 lnrow = ln_row_stats<BM>(args, m0);  // fused-LN row stats while the first stages land
+  // fused-LN row stats while the first stages land: merged here from the
+  // producer's partials (no ln_rowstats launch), or precomputed per row
+  float2 lnrow = make_float2(0.f, 0.f);
+  float2 lnlane[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) lnlane[i] = make_float2(0.f, 1.f);
+  bool lnl = false;
+  if constexpr (!CONV) {
+    if (args.ln_part && !args.ln_row) {
+      ln_merge_tile<BM, MT, WTM>(args, m0, wm, reinterpret_cast<float*>(smem + (S - 1) * STAGE), lnlane, lnrow);
+      lnl = true;
+    }
+  }
+  if (!lnl) lnrow = ln_row_stats<BM>(args, m0);
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
@@ -249,7 +262,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     if (sum == 1234.5f) args.C[threadIdx.x] = f2bf(sum);  // keeps the MFMAs alive
     return;
   }
-  gemm_epilogue<BM, BN, WM, WN, false, EP, 256, true>(args, acc, smem, m0, n0, split, lnrow);
+  gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true>(args, acc, smem, m0, n0, split, lnrow, lnlane, lnl);
 }
 
 // ---------------------------------------------------------------------------

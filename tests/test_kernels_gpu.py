@@ -442,19 +442,30 @@ def test_conv_bias2d_row_stride(gpu):
     assert rel_err(y.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("ink", [1, 0])
 @pytest.mark.parametrize("N,act", [(960, None), (320, None), (2 * 1280, "geglu")])
 @pytest.mark.parametrize("tile", [None, 11, 13, 14, 19, 20, 21, 22, 25, 26, 27, 29, 31, 32, 33, 34])
-def test_layer_norm_fused_into_gemm(gpu, N, act, tile, monkeypatch):
+def test_layer_norm_fused_into_gemm(gpu, N, act, tile, ink, monkeypatch):
     """Producer GEMM emits per-row statistics; the consumer GEMM applies the
     LayerNorm in its epilogue with gamma/beta folded into its weights.
     ``tile`` forces producer and consumer onto one tile: the row-layout direct
     epilogue (glds / persistent tiles) and the LDS epilogue (heuristic tiles)
-    both."""
+    both.  ``ink``: the consumer merges the producer's row partials in its own
+    prologue (1, LDS-DMA tiles) or reads them from the merge kernel (0)."""
     from types import SimpleNamespace
 
-    from chiaswarm_amd.ops import tuning
+    from chiaswarm_amd.ops import _lib, tuning
 
     monkeypatch.setattr(ops, "LN_FUSE", True)
+    _lib.call("csk_set_ln_in_kernel", ink)
+    try:
+        _ln_fused_case(gpu, N, act, tile, monkeypatch, tuning)
+    finally:
+        _lib.call("csk_set_ln_in_kernel", 1)
+
+
+def _ln_fused_case(gpu, N, act, tile, monkeypatch, tuning):
+    from types import SimpleNamespace
 
     M, C, Kp = 1000, 320, 640
     if tile is not None:
