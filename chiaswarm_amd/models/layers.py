@@ -282,7 +282,7 @@ class BasicTransformerBlock(nn.Module):
         q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
                                 self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None)
         if dup:
-            q, x = torch.cat([q, q], 0), torch.cat([x, x], 0)
+            q, x = ops.dup2(q), ops.dup2(x)
         x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
         g = ff.net[0]
         g.ensure()
@@ -328,7 +328,7 @@ class Transformer2D(nn.Module):
         for i, blk in enumerate(self.transformer_blocks):
             if dup and i == 0:
                 h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb, dup=True)
-                x, b = torch.cat([x, x], 0), 2 * b
+                x, b = ops.dup2(x), 2 * b
                 continue
             h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb)
         if isinstance(self.proj_out, Linear):

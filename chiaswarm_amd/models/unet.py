@@ -283,8 +283,7 @@ class UNet2DConditionModel(Prepared):
                 return t(h, ctx=ctx, kvs=kvs, dup=True)
             return t(h, ctx=ctx, kvs=kvs)
 
-        def dup2(t):  # [B/2, ...] -> [B, ...] (both CFG halves)
-            return torch.cat([t, t], 0)
+        dup2 = ops.dup2  # [B/2, ...] -> [B, ...] (both CFG halves)
 
         if half:
             h = self.conv_in(x[:half])

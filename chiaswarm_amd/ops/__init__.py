@@ -511,6 +511,15 @@ def canny(gray: torch.Tensor, low: float = 100.0, high: float = 200.0) -> torch.
 # ----------------------------------------------------------------------------
 # Elementwise
 # ----------------------------------------------------------------------------
+def dup2(x):
+    """[x; x] along the batch dim (one kernel on the HIP path)."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.dup2(x)
+    return torch.cat([x, x], 0)
+
+
 def silu(x):
     if use_hip(x):
         from . import hip_ops

@@ -98,6 +98,7 @@ sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
+sig("csk_dup2", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_set_ln_in_kernel", c_int)
 sig("csk_set_gn_finalize_wg", c_int)
 sig("csk_set_gn_fine", c_int)
@@ -445,6 +446,18 @@ def silu(x):
     x = x.contiguous()
     y = torch.empty_like(x)
     _lib.call("csk_silu", _p(y), _p(x), x.numel(), _s())
+    return y
+
+
+def dup2(x):
+    """[x; x] along dim 0 (CFG-shared prefix -> both guidance halves) in one pass."""
+    x = x.contiguous()
+    y = torch.empty((2 * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    if x.dtype != torch.bfloat16 or x.numel() % 8 or x.data_ptr() % 16:
+        y[: x.shape[0]].copy_(x)
+        y[x.shape[0]:].copy_(x)
+        return y
+    _lib.call("csk_dup2", _p(y), _p(x), x.numel(), _s())
     return y
 
 

@@ -50,6 +50,33 @@ __global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict_
   }
 }
 
+// y = [x; x] (a CFG-shared prefix result duplicated for both guidance halves):
+// one read of x, two 16-byte stores per vector, 4 vectors in flight per thread
+// (torch.cat ran at ~2 TB/s on these 10 MB tensors)
+__global__ void dup2_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, size_t nvec) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < nvec) v[u] = x[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < nvec) {
+        y[i + u * stride] = v[u];
+        y[nvec + i + u * stride] = v[u];
+      }
+  }
+}
+
+CSK_API int csk_dup2(void* y, const void* x, long long n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n % 8 != 0 || (((size_t)x) & 15) != 0 || (((size_t)y) & 15) != 0) return (int)hipErrorInvalidValue;
+  const size_t nv = n / 8;
+  dup2_kernel<<<ew_grid((nv + 3) / 4), 256, 0, stream>>>((const uint4*)x, (uint4*)y, nv);
+  CSK_CHECK_LAUNCH();
+}
+
 CSK_API int csk_add(void* y, const void* a, const void* b, long long n, hipStream_t stream) {
   if (n <= 0) return 0;
   const size_t nv = n / 8;

@@ -674,3 +674,12 @@ def test_debug_build_records_violations(gpu):
     tu, count, site, bx, tid, val, lim, by = recs[0]
     assert count == 64 and site == 99 and val == 7 and lim == 3, recs  # one wave, every lane fails
     assert _lib.debug_records() == []  # cleared
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 320), (1, 4096, 320), (3, 5, 8)])
+def test_dup2_batch(gpu, shape):
+    """[x; x] in one kernel (the CFG-shared UNet prefix duplication)."""
+    x = rnd(*shape, dev=gpu)
+    y = hip_ops.dup2(x)
+    assert y.shape == (2 * shape[0],) + tuple(shape[1:])
+    assert torch.equal(y[: shape[0]], x) and torch.equal(y[shape[0]:], x)
