@@ -202,6 +202,20 @@ class UNet2DConditionModel(Prepared):
         proj = ops.gemm(ops.silu(temb), self._temb_w, self._temb_b)
         return list(torch.split(proj, self._temb_splits, dim=-1))
 
+    @torch.no_grad()
+    def temb_table(self, ts: torch.Tensor) -> torch.Tensor:
+        """[n, sum Cout] batched ResNet time projections for every timestep of
+        ``ts`` (fp32 [n]) — the whole time-embedding chain (sinusoid, MLP, SiLU,
+        projection GEMM) for a request's schedule in one pass, so the sampler
+        loop's step graph only gathers its row (``forward(temb_proj=...)``)."""
+        dtype = self.conv_in.weight.dtype
+        ts = ts.reshape(-1).float()
+        temb = self.time_embed(ts, ts.numel(), dtype)
+        w = getattr(self, "_temb_w", None)
+        if w is None or w.device != temb.device or w.dtype != dtype:
+            self.prepare_self()
+        return ops.gemm(ops.silu(temb), self._temb_w, self._temb_b)
+
     def cross_attention_modules(self):
         mods = []
         for blk in list(self.down_blocks) + [self.mid_block] + list(self.up_blocks):
@@ -248,7 +262,7 @@ class UNet2DConditionModel(Prepared):
 
     def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
                 added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None,
-                cfg_dup=False):
+                cfg_dup=False, temb_proj=None):
         """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout].
 
         ``control``: a ControlNet's pre-zero-conv features
@@ -265,12 +279,20 @@ class UNet2DConditionModel(Prepared):
         transformer's GroupNorm / proj_in / self-attention and its cross-attention
         query projection — is then bit-identical for both halves, so it runs once
         at half batch and is duplicated where the halves start to differ
-        (common-subexpression elimination, not an approximation)."""
+        (common-subexpression elimination, not an approximation).
+
+        ``temb_proj``: precomputed [B, sum Cout] ResNet time projections (a row
+        of ``temb_table``); ``timestep`` is then unused."""
         b = sample.shape[0]
         dtype = self.conv_in.weight.dtype
         x = sample.to(dtype)
-        temb = self.time_embed(timestep, b, dtype, added_cond, class_labels)
-        tprojs = iter(self._temb_projs(temb))
+        if temb_proj is not None:
+            if getattr(self, "_temb_splits", None) is None:
+                self.prepare_self()
+            tprojs = iter(torch.split(temb_proj, self._temb_splits, dim=-1))
+        else:
+            temb = self.time_embed(timestep, b, dtype, added_cond, class_labels)
+            tprojs = iter(self._temb_projs(temb))
         kv_iter = iter(cross_kv) if cross_kv is not None else None
         ctx = encoder_hidden_states
         half = b // 2 if (cfg_dup and b % 2 == 0 and ops.use_hip(x)) else 0

@@ -99,6 +99,7 @@ sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
 sig("csk_dup2", c_void_p, c_void_p, c_int64, c_void_p)
+sig("csk_row_bcast", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
 sig("csk_set_ln_in_kernel", c_int)
 sig("csk_set_gn_finalize_wg", c_int)
 sig("csk_set_gn_fine", c_int)
@@ -447,6 +448,16 @@ def silu(x):
     y = torch.empty_like(x)
     _lib.call("csk_silu", _p(y), _p(x), x.numel(), _s())
     return y
+
+
+def row_bcast(dst, tab, cur):
+    """dst[r] = tab[cur[0]] for every row r (bf16 [rows, W] <- [n, W], int32 device index)."""
+    _bf16(dst, "row_bcast.dst")
+    _bf16(tab, "row_bcast.tab")
+    if dst.dim() != 2 or tab.dim() != 2 or dst.shape[1] != tab.shape[1] or not dst.is_contiguous() \
+            or not tab.is_contiguous() or cur.dtype != torch.int32:
+        raise ValueError("row_bcast: contiguous bf16 [rows, W] / [n, W], int32 cur")
+    _lib.call("csk_row_bcast", _p(dst), _p(tab), _p(cur), dst.shape[0], dst.shape[1], tab.shape[0], _s())
 
 
 def dup2(x):

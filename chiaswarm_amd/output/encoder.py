@@ -94,7 +94,7 @@ class _ProcessPool:
         while True:
             try:
                 item = self.outq.get()
-            except (EOFError, OSError):
+            except Exception:  # noqa: BLE001 - queue torn down (EOF / OSError, or interpreter exit)
                 return
             if item is None:
                 return
@@ -133,6 +133,8 @@ class _ProcessPool:
             for proc, _, _ in self.workers:
                 proc.join(timeout=30)
         self.outq.put(None)
+        if wait:  # let the reader drain and return before interpreter teardown
+            self.reader.join(timeout=5)
 
 
 def encode_arrays(arrays, content_type: str = "image/jpeg", output_list=("primary",)) -> dict:

@@ -395,6 +395,8 @@ class StableDiffusion:
         else:
             L.x0prev.zero_()
         L.counter.zero_()
+        if hasattr(gph, "fill_temb"):
+            gph.fill_temb(L.t_tab[:n])
         gph.prepare(x_in, cross_kv, added, control, req=getattr(self, "_req", None))
         for _ in range(n):
             gph.graph.replay()
@@ -557,6 +559,7 @@ def _cfg_dup(unet, nrep, image_latents, added) -> bool:
 
 
 CFG_SHARE_PREFIX = os.environ.get("CSK_CFG_SHARE", "1") != "0"
+TEMB_TABLE = os.environ.get("CSK_TEMB_TABLE", "1") != "0"  # per-request time-projection table in the loop graph
 LOOP_GRAPHS = True  # device-resident sampler loop (StableDiffusion._denoise_loop); False: per-step host loop
 
 
@@ -584,6 +587,8 @@ class _UNetGraph:
     buffers are refreshed by ``copy_`` before each replay.  With ``loop`` the
     graph is a whole sampler step (see StableDiffusion._denoise_loop)."""
 
+    _temb_ok = True  # the step's UNet forward may take precomputed time projections
+
     def __init__(self, unet, x_in, cross_kv, added, warmup=2, share_kv=False, loop=None, cfg_dup=False):
         self.unet = unet
         self.loop = loop
@@ -595,6 +600,14 @@ class _UNetGraph:
         self.kv = list(cross_kv) if share_kv else [k.clone() for k in cross_kv]
         self._kv_req = None
         self.added = {k: v.clone() for k, v in added.items()} if added else None
+        # device-resident loop: the ResNet time projections of every step come
+        # from a per-request table (UNet2DConditionModel.temb_table) gathered by
+        # the step's device index, not recomputed (5 small kernels) every step
+        self.temb_tab = self.temb_row = None
+        if loop is not None and added is None and hasattr(unet, "temb_table") and TEMB_TABLE and self._temb_ok:
+            width = sum(unet._resnets()[i].out_channels for i in range(len(unet._resnets())))
+            self.temb_tab = torch.zeros((loop.cap, width), dtype=x_in.dtype, device=x_in.device)
+            self.temb_row = torch.zeros((x_in.shape[0], width), dtype=x_in.dtype, device=x_in.device)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -617,9 +630,20 @@ class _UNetGraph:
         return e
 
     def _unet_fwd(self):
+        kw = {}
+        if self.temb_tab is not None:
+            from ..ops import hip_ops
+
+            hip_ops.row_bcast(self.temb_row, self.temb_tab, self.loop.cur)
+            kw["temb_proj"] = self.temb_row
         if self.cfg_dup:
-            return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, cfg_dup=True)
-        return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added)
+            kw["cfg_dup"] = True
+        return self.unet(self.x, self.t, cross_kv=self.kv, added_cond=self.added, **kw)
+
+    def fill_temb(self, t_tab):
+        """Per-request time-projection table for the step timesteps ``t_tab``."""
+        if self.temb_tab is not None:
+            self.temb_tab[: t_tab.numel()].copy_(self.unet.temb_table(t_tab))
 
     def prepare(self, x_in, cross_kv, added, cc=None, req=None):
         self.x.copy_(x_in)
@@ -652,6 +676,8 @@ class _ControlUNetGraph(_UNetGraph):
     modules every step, swarm/diffusion/diffusion_func.py:29-39 -> :96).  The
     conditioning embedding and the ControlNet's prompt K/V are static buffers
     refreshed once per request; the conditioning scale is part of the graph key."""
+
+    _temb_ok = False  # the ControlNet copy embeds the timestep itself
 
     def __init__(self, unet, x_in, cross_kv, added, cc, warmup=2, share_kv=False, loop=None):
         self.cn, self.scale = cc.model, cc.scale

@@ -50,6 +50,27 @@ __global__ void add_kernel(const uint4* __restrict__ a, const uint4* __restrict_
   }
 }
 
+// dst[r][:] = tab[*cur][:] for r < rows (bf16, width % 8 == 0): the step's row of
+// a per-request table (the ResNet time projections of every timestep, computed
+// once per job) broadcast to the batch inside the step graph
+__global__ void row_bcast_kernel(uint4* __restrict__ dst, const uint4* __restrict__ tab, const int* __restrict__ cur,
+                                 int rows, int wv, int n) {
+  const int c = min(max(*cur, 0), n - 1);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rows * wv; i += gridDim.x * blockDim.x) {
+    const int r = i / wv, v = i - r * wv;
+    dst[(size_t)r * wv + v] = tab[(size_t)c * wv + v];
+  }
+}
+
+CSK_API int csk_row_bcast(void* dst, const void* tab, const void* cur, int rows, int width, int n,
+                          hipStream_t stream) {
+  if (width % 8 != 0 || rows <= 0 || n <= 0) return (int)hipErrorInvalidValue;
+  const int wv = width / 8;
+  row_bcast_kernel<<<min((rows * wv + 255) / 256, 1024), 256, 0, stream>>>((uint4*)dst, (const uint4*)tab,
+                                                                            (const int*)cur, rows, wv, n);
+  CSK_CHECK_LAUNCH();
+}
+
 // y = [x; x] (a CFG-shared prefix result duplicated for both guidance halves):
 // one read of x, two 16-byte stores per vector, 4 vectors in flight per thread
 // (torch.cat ran at ~2 TB/s on these 10 MB tensors)

@@ -683,3 +683,12 @@ def test_dup2_batch(gpu, shape):
     y = hip_ops.dup2(x)
     assert y.shape == (2 * shape[0],) + tuple(shape[1:])
     assert torch.equal(y[: shape[0]], x) and torch.equal(y[shape[0]:], x)
+
+
+def test_row_bcast(gpu):
+    """The sampler-loop step graph's gather of its time-projection row."""
+    tab = rnd(7, 20160, dev=gpu)
+    dst = torch.empty(8, 20160, dtype=torch.bfloat16, device=gpu)
+    for i in (0, 3, 6):
+        hip_ops.row_bcast(dst, tab, torch.tensor([i], dtype=torch.int32, device=gpu))
+        assert torch.equal(dst, tab[i].expand(8, -1))
