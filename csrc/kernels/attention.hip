@@ -562,6 +562,19 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
   }
 }
 
+// [64][64] bf16 K / V tile image of attn32_kernel: 16-byte chunk c of row r at
+// slot c ^ f(r), f(r) = bits (r1, r2, r3) -> (4, 2, 1).  Conflict-free for the
+// kernel's three access patterns (tools/attn32_swizzle.py checks them against
+// the gfx950 lane groups): the K-fragment ds_read_b128 (lanes 0-31 = 32
+// consecutive rows, one chunk: rows r and r + 8 share a lane group), the V^T
+// ds_read_b64_tr_b16 (4 rows x 4 chunks per 32-lane half) and the row-wise
+// ds_write_b128 staging.  The plain (r & 7) swizzle of kv_off is 2-way on the
+// first two (SQ_LDS_BANK_CONFLICT 2.3 cycles per LDS instruction).
+__device__ __forceinline__ int kv_off32(int row, int chunk) {
+  const int f = ((row & 2) << 1) | ((row & 4) >> 1) | ((row & 8) >> 3);
+  return row * 64 + ((chunk ^ f) << 3);
+}
+
 // 32x32x16 variant of the pipelined kernel (D <= 64): S^T = K Q^T and
 // O^T = V^T P^T on v_mfma_f32_32x32x16_bf16.  At D = 64 the softmax is
 // VALU-issue bound: a 16x16x32 MFMA (16 cycles) blocks vector issue for 8 of
@@ -579,8 +592,12 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
 // rescale (T13, threshold 2^8), same 3-buffer register-staged K/V ring and
 // one-barrier-per-block software pipeline (QK^T of block kb+1 issued before
 // the softmax of block kb) as attn_fwd_pipe_kernel.
-// QB: 32-query tiles per wave (128 or 256 query rows per workgroup).
-template <int QB>
+// QB: 32-query tiles per wave (QB = 2, 256 rows per workgroup at one wave per
+// SIMD, was 1.6x slower and spills; only QB = 1 is instantiated).
+// PROBE (profiling builds, wrong results by design; variants 31/32/34/38):
+// 1 = no exp, 2 = no K/V global loads past the first two blocks, 4 = no PV
+// MFMAs, 8 = no QK^T MFMAs
+template <int QB, int PROBE = 0>
 __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
   constexpr int DP = 64, CPR = DP / 8, KB = 64;
   constexpr int QROWS = QB * 32 * 4;
@@ -639,6 +656,9 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 
   uint4 rk[LPT], rv[LPT];
   auto load_kv = [&](int kb) {
+    if constexpr ((PROBE & 2) != 0) {
+      if (kb >= 2) return;
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
@@ -660,8 +680,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
-      *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = rk[i];
-      *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = rv[i];
+      *reinterpret_cast<uint4*>(ks + kv_off32(row, c)) = rk[i];
+      *reinterpret_cast<uint4*>(vs + kv_off32(row, c)) = rv[i];
     }
   };
   // scores of one 64-key block: s[kt][qt] = S^T of keys kt*32.. (issued with offset -mu)
@@ -676,8 +696,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off<CPR>(kt * 32 + r, 2 * ds + hh));
+      for (int ds = 0; ds < ((PROBE & 8) ? 0 : 4); ++ds) {
+        const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off32(kt * 32 + r, 2 * ds + hh));
 #pragma unroll
         for (int qt = 0; qt < QB; ++qt)
           s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qt][ds], s[kt][qt], 0, 0, 0);
@@ -738,10 +758,12 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
           for (int i = 0; i < 16; ++i) sc[kt][qt][i] -= shift;
       }
+      if constexpr ((PROBE & 1) == 0) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
+          for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
+      }
       // 4 independent single-instruction add chains (no v_pk_add_f32 beside MFMAs)
       float l4[4];
 #pragma unroll
@@ -777,12 +799,17 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         for (int dt = 0; dt < 2; ++dt) {
           const int col = dt * 32 + 16 * (fg & 1) + 4 * pp;
           const int r0 = kt * 32 + 16 * st + 4 * (fg >> 1) + qq, r1 = r0 + 8;
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r0, col >> 3) + (col & 7)));
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off<CPR>(r1, col >> 3) + (col & 7)));
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off32(r0, col >> 3) + (col & 7)));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + kv_off32(r1, col >> 3) + (col & 7)));
           const v8s vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-          for (int qt = 0; qt < QB; ++qt)
-            oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
+          for (int qt = 0; qt < QB; ++qt) {
+            if constexpr ((PROBE & 4) != 0) {
+              asm volatile("" ::"v"(vf), "v"(pf[kt][st][qt]));
+            } else {
+              oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
+            }
+          }
         }
     if (kb + 2 < nkb) store_kv((kb + 2) % 3);
     __syncthreads();
@@ -1020,11 +1047,19 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
     if (variant == 0 && g_attn32 && D == 64 && Skv > 128) variant = 20;
-    if (variant == 20 || variant == 21) {  // 32x32x16 MFMA kernel, 128 / 256 query rows per workgroup
-      if (variant == 20)
-        attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
-      else
-        attn32_kernel<2><<<dim3(B * H * ((Sq + 255) / 256)), 256, 0, stream>>>(a);
+    if (variant >= 31 && variant <= 38) {  // attn32 profiling probes (wrong results by design)
+      const dim3 g1(B * H * ((Sq + 127) / 128));
+      switch (variant) {
+        case 31: attn32_kernel<1, 1><<<g1, 256, 0, stream>>>(a); break;
+        case 32: attn32_kernel<1, 2><<<g1, 256, 0, stream>>>(a); break;
+        case 34: attn32_kernel<1, 4><<<g1, 256, 0, stream>>>(a); break;
+        case 38: attn32_kernel<1, 8><<<g1, 256, 0, stream>>>(a); break;
+        default: return (int)hipErrorInvalidValue;
+      }
+      return (int)hipGetLastError();
+    }
+    if (variant == 20) {  // 32x32x16 MFMA kernel, 128 query rows per workgroup
+      attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
       return (int)hipGetLastError();
     }
     if (variant >= 2 || (variant == 0 && Skv > 128)) {

@@ -173,7 +173,7 @@ def test_attention(gpu, B, Sq, Skv, H, D, causal):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, scale, causal)) < 1.5e-2
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 20, 21])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 20])
 @pytest.mark.parametrize("B,Sq,Skv,H,D,causal", [(2, 1024, 1024, 5, 64, False), (1, 300, 517, 3, 64, False),
                                                   (1, 333, 333, 2, 40, True), (2, 4096, 77, 5, 64, False)])
 def test_attention_variants(gpu, variant, B, Sq, Skv, H, D, causal):
@@ -215,7 +215,7 @@ def test_attention_fused_qkv_strides(gpu):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 20, 21])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 20])
 def test_attention_spike_rescale(gpu, variant):
     # forces the online-softmax rescale: growing logits appear in later KV blocks,
     # including consecutive blocks (the pipelined kernels issue block kb+1's
@@ -235,7 +235,7 @@ def test_attention_spike_rescale(gpu, variant):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
-@pytest.mark.parametrize("variant", [2, 3, 5, 20, 21])
+@pytest.mark.parametrize("variant", [2, 3, 5, 20])
 def test_attention_far_negative_logits(gpu, variant):
     # every score far below 0 (softmax is shift-invariant): the running-max offset
     # must follow the logits down, not start from 0
