@@ -20,7 +20,7 @@ import threading
 
 import torch
 
-SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "tune_gfx950.json")
+SHIPPED = os.environ.get("CSK_TUNE_FILE") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "tune_gfx950.json")
 _TABLE: dict | None = None
 _LOCK = threading.Lock()
 TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6: (128, 64),

@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--only", default="", help="conv|gemm")
     ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
     ap.add_argument("--res", action="store_true", help="GEMMs also with a residual input (epilogue load)")
-    ap.add_argument("--gemms", default="", help="comma-free list 'M,N,K;M,N,K' overriding the GEMM shapes")
+    ap.add_argument("--gemms", default="", help="';'-separated 'M,N,K' list overriding the GEMM shapes")
+    ap.add_argument("--convs", default="", help="';'-separated 'B,H,W,Cin,Cout' list overriding the conv shapes")
     ap.add_argument("--gn", action="store_true", help="convs also emitting fused GroupNorm statistics (64-row segments)")
     ap.add_argument("--swodd", default="", help="comma list of csk_set_sw_odd values to A/B (160-wide tile epilogue)")
     ap.add_argument("--probe-halo", action="store_true",
@@ -48,7 +49,7 @@ def main():
     splits = [int(s) for s in a.splits.split(",")]
     jobs = []
     if a.only != "gemm":
-        for spec in CONVS:
+        for spec in (a.convs.split(";") if a.convs else CONVS):
             B, H, W, Cin, Cout = map(int, spec.split(","))
             x = (torch.randn(B, H, W, Cin, device=dev)).to(torch.bfloat16)
             wp = ops.pack_conv_weight((torch.randn(Cout, Cin, 3, 3, device=dev) * (9 * Cin) ** -0.5).to(torch.bfloat16))
