@@ -50,13 +50,15 @@ def main():
     jobs = []
     if a.only != "gemm":
         for spec in (a.convs.split(";") if a.convs else CONVS):
-            B, H, W, Cin, Cout = map(int, spec.split(","))
+            up = int(spec.endswith("u"))  # "B,H,W,Cin,Cout u": nearest-x2 upsample fused into the conv input
+            B, H, W, Cin, Cout = map(int, spec.rstrip("u").split(","))
+            Ho, Wo = H << up, W << up
             x = (torch.randn(B, H, W, Cin, device=dev)).to(torch.bfloat16)
             wp = ops.pack_conv_weight((torch.randn(Cout, Cin, 3, 3, device=dev) * (9 * Cin) ** -0.5).to(torch.bfloat16))
-            y = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
-            fl = 2.0 * B * H * W * Cout * 9 * Cin
+            y = torch.empty(B, Ho, Wo, Cout, dtype=torch.bfloat16, device=dev)
+            fl = 2.0 * B * Ho * Wo * Cout * 9 * Cin
 
-            gpart = torch.empty(B * H * W // 64 * Cout * 2, dtype=torch.float32, device=dev)
+            gpart = torch.empty(B * Ho * Wo // 64 * Cout * 2, dtype=torch.float32, device=dev)
             variants = [(0, False, None)]
             if a.gn:
                 variants.append((0, True, None))
@@ -66,12 +68,12 @@ def main():
                 variants += [(97, False, None), (99, False, None), (98, False, None)]
             for act, gn, sw in variants:
                 def run(tile, split, x=x, wp=wp, y=y, B=B, H=H, W=W, Cin=Cin, Cout=Cout, act=act, gn=gn, sw=sw,
-                        gpart=gpart):
+                        gpart=gpart, up=up, Ho=Ho, Wo=Wo):
                     if sw is not None:
                         _lib.call("csk_set_sw_odd", sw)
-                    ws = torch.empty(split * B * H * W * Cout, dtype=torch.float32, device=dev) if split > 1 else None
+                    ws = torch.empty(split * B * Ho * Wo * Cout, dtype=torch.float32, device=dev) if split > 1 else None
                     _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1,
-                              H, W, 0, Cin, Cout, 0, act, 1.0, 1, _p(gpart) if gn else None, tile, split, _p(ws),
+                              Ho, Wo, up, Cin, Cout, 0, act, 1.0, 1, _p(gpart) if gn else None, tile, split, _p(ws),
                               _s())
                     if sw is not None:
                         _lib.call("csk_set_sw_odd", 0)
