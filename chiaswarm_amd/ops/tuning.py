@@ -105,8 +105,10 @@ def candidates(M, N, K):
         if (persistent or tile >= 31) and K % 64:
             continue
         ntiles = -(-M // bm) * -(-N // bn)
-        for split in (1, 2, 4, 8):
+        for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)
             if split > 1 and (ntiles >= 512 or K // 64 < 4 * split or persistent):
+                continue
+            if split == 16 and ntiles > 64:
                 continue
             out.append((tile, split))
     return out
