@@ -295,7 +295,7 @@ class UNet2DConditionModel(Prepared):
             tprojs = iter(self._temb_projs(temb))
         kv_iter = iter(cross_kv) if cross_kv is not None else None
         ctx = encoder_hidden_states
-        half = b // 2 if (cfg_dup and b % 2 == 0 and ops.use_hip(x)) else 0
+        half = b // 2 if (cfg_dup and b % 2 == 0) else 0
 
         def run_attn(t, h, dup=False):
             kvs = None

@@ -169,3 +169,27 @@ def test_img2txt_vqa_and_unsupported_class_envelopes(monkeypatch):
     bad = dict(job, id="v2", parameters={"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"})
     r2 = synchronous_do_work_function(bad, Device("cpu"))
     assert r2.get("fatal_error") is True and "GitForCausalLM" in r2["pipeline_config"]["error"]
+
+
+def test_unet_cfg_shared_prefix_and_temb_table_cpu():
+    """UNet forward with the CFG-shared prefix (cfg_dup) and with precomputed
+    time projections (temb_table rows) equals the plain forward on identical
+    CFG halves (fp32 reference ops)."""
+    from chiaswarm_amd.models import unet as unet_mod
+    from chiaswarm_amd.models.layers import init_random_fast_, prepare_model
+
+    torch.manual_seed(0)
+    m = unet_mod.UNet2DConditionModel(unet_mod.TINY).eval().requires_grad_(False)
+    init_random_fast_(m, seed=1)
+    prepare_model(m)
+    xh = torch.randn(2, 8, 8, 4)
+    x = torch.cat([xh, xh])
+    ctx = torch.randn(4, 77, 32)
+    t = torch.tensor([321.0])
+    with torch.no_grad():
+        ref = m(x, t, encoder_hidden_states=ctx)
+        y = m(x, t, encoder_hidden_states=ctx, cfg_dup=True)
+        tab = m.temb_table(torch.tensor([999.0, 321.0, 5.0]))
+        y2 = m(x, t, encoder_hidden_states=ctx, temb_proj=tab[1:2].expand(4, -1).contiguous())
+    assert torch.allclose(y, ref, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(y2, ref, rtol=1e-4, atol=1e-5)
