@@ -98,6 +98,8 @@ sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
+sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
+    c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)
 sig("csk_dup2", c_void_p, c_void_p, c_int64, c_void_p)
 sig("csk_row_bcast", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
 sig("csk_set_ln_in_kernel", c_int)
@@ -436,9 +438,32 @@ def attention(q, k, v, scale, causal=False, kv_len=None):
     st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
     if kv_len is not None and (kv_len.dtype != torch.int32 or not kv_len.is_cuda):
         raise TypeError("attention: kv_len must be an int32 device tensor")
+    split = attn_kv_split(B, H, Sq, Skv, D) if (not causal and kv_len is None and ATTN_VARIANT == 0) else 1
+    if split > 1:
+        rows = B * H * Sq
+        part_o = torch.empty((split, rows, 64), dtype=torch.float32, device=q.device)
+        part_ml = torch.empty((split, rows, 2), dtype=torch.float32, device=q.device)
+        _lib.call("csk_attention_split", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), split,
+                  _p(part_o), _p(part_ml), _s())
+        return o
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
               ATTN_VARIANT, _p(kv_len), _s())
     return o
+
+
+ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "0"))  # split the keys below this many workgroups (0: off)
+
+
+def attn_kv_split(B, H, Sq, Skv, D) -> int:
+    """Key splits for the d = 64 self-attention when its 128-query workgroups
+    cannot fill the chip (batch-1 jobs): up to 4, each keeping >= 4 key blocks."""
+    if D != 64 or Skv <= 128 or ATTN_SPLIT_WG <= 0:
+        return 1
+    wg = B * H * -(-Sq // 128)
+    split = 1
+    while wg * split < ATTN_SPLIT_WG and split < 4 and -(-Skv // 64) >= 8 * split:
+        split *= 2
+    return split
 
 
 def silu(x):

@@ -41,6 +41,12 @@ struct AttnArgs {
   int causal;
   const int* kv_len;  // optional device-side key count (<= Skv): lets a fixed-shape
                       // KV-cache decode step be captured once in a hipGraph
+  // split-KV (attn32_kernel): kv_split workgroups share a query block, each
+  // over 1/kv_split of the key blocks, and write unnormalised fp32 partials
+  // part_o [split][B*H][Sq][64] and (max, sum) part_ml [split][B*H][Sq][2]
+  int kv_split;
+  float* part_o;
+  float* part_ml;
 };
 
 // DV: the head dim rounded up to 16 (SD1.5's 40 / 80 / 160 live in 64 / 128 / 256
@@ -613,7 +619,9 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   const int Skv = a.kv_len ? min(a.Skv, *a.kv_len) : a.Skv;
   const int nqb = (a.Sq + QROWS - 1) / QROWS;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = wg / nqb, qb = wg % nqb;
+  const int nsp = a.kv_split > 1 ? a.kv_split : 1;
+  const int ks = wg % nsp;  // key split of this workgroup (the splits of a query block share an XCD)
+  const int bh = (wg / nsp) / nqb, qb = (wg / nsp) % nqb;
   const int b = bh / a.H, h = bh % a.H;
   const int q0 = qb * QROWS + wid * QB * 32;
   const bf16_t* qp = a.q + b * a.sqb + h * a.sqh;
@@ -652,7 +660,10 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     const int qlast = min(a.Sq, (qb + 1) * QROWS) - 1 + (Skv - a.Sq);
     kv_end = min(Skv, qlast + 1);
   }
-  const int nkb = (kv_end + KB - 1) / KB;
+  const int nkb_all = (kv_end + KB - 1) / KB;
+  const int per = (nkb_all + nsp - 1) / nsp;
+  const int kb0 = ks * per;  // this workgroup's first key block; kb below counts from it
+  const int nkb = max(0, min(nkb_all, kb0 + per) - kb0);
 
   uint4 rk[LPT], rv[LPT];
   auto load_kv = [&](int kb) {
@@ -662,7 +673,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
-      const int key = min(kb * KB + row, Skv - 1), d = c * 8;  // clamped rows are masked later
+      const int key = min((kb0 + kb) * KB + row, Skv - 1), d = c * 8;  // clamped rows are masked later
       CSK_DCHECK(key >= 0, 24, key, Skv);
       uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (d < a.D) {
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     if (kb + 2 < nkb) load_kv(kb + 2);
     if (kb + 1 < nkb) qk((kb + 1) % NBUF, sn, mun);  // matrix cores busy while the softmax below runs
 
-    const int kbase = kb * KB;
+    const int kbase = (kb0 + kb) * KB;
     const bool masked = a.causal || (kbase + KB > kv_end);
     v8s pf[2][2][QB];  // [key tile][PV k-step][query tile]
 #pragma unroll
@@ -820,6 +831,27 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     if (kb + 1 < nkb) block(kb + 1, s_b, mu_b, s_a, mu_a);
   }
 
+  if (nsp > 1) {  // unnormalised partials; attn_split_combine_kernel merges the splits
+    const size_t rows = (size_t)a.B * a.H * a.Sq;
+#pragma unroll
+    for (int qt = 0; qt < QB; ++qt) {
+      float l = lrow[qt];
+      l += __shfl_xor(l, 32, 64);
+      const int qi = q0 + qt * 32 + r;
+      if (qi >= a.Sq) continue;
+      const size_t row = (size_t)ks * rows + (size_t)bh * a.Sq + qi;
+      if (hh == 0) *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(mrow[qt], l);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          *reinterpret_cast<float4*>(a.part_o + row * 64 + d) =
+              make_float4(oacc[dt][qt][4 * g], oacc[dt][qt][4 * g + 1], oacc[dt][qt][4 * g + 2], oacc[dt][qt][4 * g + 3]);
+        }
+    }
+    return;
+  }
   bf16_t* op = a.o + b * a.sob + h * a.soh;
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
@@ -840,6 +872,37 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         *reinterpret_cast<uint2*>(op + qi * a.sos + d) = w;
       }
   }
+}
+
+// Split-KV combine: O = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s with
+// M = max_s m_s, one thread per (b, h, query, 8 head-dim columns)
+__global__ void attn_split_combine_kernel(const AttnArgs a) {
+  const size_t rows = (size_t)a.B * a.H * a.Sq;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= rows * 8) return;
+  const size_t row = i / 8;
+  const int d = (int)(i % 8) * 8;
+  const int nsp = a.kv_split;
+  float mmax = -1e30f;
+  for (int s = 0; s < nsp; ++s) mmax = fmaxf(mmax, a.part_ml[((size_t)s * rows + row) * 2]);
+  float l = 0.f, o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = 0.f;
+  for (int s = 0; s < nsp; ++s) {
+    const float2 ml = *reinterpret_cast<const float2*>(a.part_ml + ((size_t)s * rows + row) * 2);
+    const float w = __builtin_amdgcn_exp2f(ml.x - mmax);
+    l = __builtin_fmaf(w, ml.y, l);
+    const float4 lo = *reinterpret_cast<const float4*>(a.part_o + ((size_t)s * rows + row) * 64 + d);
+    const float4 hi = *reinterpret_cast<const float4*>(a.part_o + ((size_t)s * rows + row) * 64 + d + 4);
+    o[0] += w * lo.x; o[1] += w * lo.y; o[2] += w * lo.z; o[3] += w * lo.w;
+    o[4] += w * hi.x; o[5] += w * hi.y; o[6] += w * hi.z; o[7] += w * hi.w;
+  }
+  const float inv = l > 0.f ? 1.0f / l : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] *= inv;
+  const int bh = (int)(row / a.Sq), qi = (int)(row % a.Sq);
+  const int b = bh / a.H, h = bh % a.H;
+  if (d < a.D) *reinterpret_cast<uint4*>(a.o + b * a.sob + h * a.soh + (size_t)qi * a.sos + d) = pack8(o);
 }
 
 // Short-KV attention (Skv <= 128, D <= 64, no mask: the UNet's cross-attention
@@ -1043,6 +1106,8 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   a.scale_log2 = scale * 1.4426950408889634f;
   a.causal = causal;
   a.kv_len = (const int*)kv_len;
+  a.kv_split = 1;
+  a.part_o = a.part_ml = nullptr;
   const long long wg4 = (long long)B * H * ((Sq + 255) / 256);
   (void)wg4;  // QT=4 (64 rows/wave) measured slower on MI355X (1 wave/SIMD at 364 regs)
   if (D <= 64) {
@@ -1135,3 +1200,31 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
 }
 
 CSK_DEBUG_EXPORT(attention)
+
+// Split-KV self-attention for grids that cannot fill the chip (batch-1 jobs:
+// CFG batch 2, the CFG-shared prefix at batch 1): kv_split workgroups per
+// 128-query block, fp32 partials in the caller's workspace (graph-capturable),
+// then one combine pass.  D == 64, no mask, no device-side key count.
+// part_o: kv_split * B*H*Sq * 64 floats, part_ml: kv_split * B*H*Sq * 2 floats.
+CSK_API int csk_attention_split(void* o, const void* q, const void* k, const void* v, const long long* strides,
+                                int B, int H, int Sq, int Skv, int D, float scale, int kv_split, void* part_o,
+                                void* part_ml, hipStream_t stream) {
+  if (D != 64 || kv_split < 2 || kv_split > 16 || !part_o || !part_ml) return (int)hipErrorInvalidValue;
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
+  a.sqb = strides[0]; a.sqs = strides[1]; a.sqh = strides[2];
+  a.skb = strides[3]; a.sks = strides[4]; a.skh = strides[5];
+  a.svb = strides[6]; a.svs = strides[7]; a.svh = strides[8];
+  a.sob = strides[9]; a.sos = strides[10]; a.soh = strides[11];
+  a.B = B; a.H = H; a.Sq = Sq; a.Skv = Skv; a.D = D;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.causal = 0;
+  a.kv_len = nullptr;
+  a.kv_split = kv_split;
+  a.part_o = (float*)part_o;
+  a.part_ml = (float*)part_ml;
+  attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128) * kv_split), 256, 0, stream>>>(a);
+  const size_t n = (size_t)B * H * Sq * 8;
+  attn_split_combine_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
