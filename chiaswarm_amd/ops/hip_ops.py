@@ -451,17 +451,20 @@ def attention(q, k, v, scale, causal=False, kv_len=None):
     return o
 
 
-ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "0"))  # split the keys below this many workgroups (0: off)
+ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "512"))  # split the keys below this many workgroups (0: off)
 
 
 def attn_kv_split(B, H, Sq, Skv, D) -> int:
     """Key splits for the d = 64 self-attention when its 128-query workgroups
-    cannot fill the chip (batch-1 jobs): up to 4, each keeping >= 4 key blocks."""
+    cannot fill the chip (batch-1 jobs): up to 4."""
     if D != 64 or Skv <= 128 or ATTN_SPLIT_WG <= 0:
         return 1
     wg = B * H * -(-Sq // 128)
     split = 1
-    while wg * split < ATTN_SPLIT_WG and split < 4 and -(-Skv // 64) >= 8 * split:
+    # each split keeps >= 16 key blocks: at S = 1024 (16 blocks) the combine and
+    # the shorter pipelines cost more than the extra workgroups gain (30.6 vs
+    # 22.5 us, profiles/attn_split_r4t.txt); S = 4096 at batch 1-2: 58 vs 75 us
+    while wg * split < ATTN_SPLIT_WG and split < 4 and -(-Skv // 64) >= 32 * split:
         split *= 2
     return split
 
