@@ -440,14 +440,27 @@ def attention(q, k, v, scale, causal=False, kv_len=None):
         raise TypeError("attention: kv_len must be an int32 device tensor")
     split = attn_kv_split(B, H, Sq, Skv, D) if (not causal and kv_len is None and ATTN_VARIANT == 0) else 1
     if split > 1:
-        rows = B * H * Sq
-        part_o = torch.empty((split, rows, 64), dtype=torch.float32, device=q.device)
-        part_ml = torch.empty((split, rows, 2), dtype=torch.float32, device=q.device)
-        _lib.call("csk_attention_split", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), split,
-                  _p(part_o), _p(part_ml), _s())
-        return o
+        return attention_split(q, k, v, scale, split, o)
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
               ATTN_VARIANT, _p(kv_len), _s())
+    return o
+
+
+def attention_split(q, k, v, scale, split, o=None):
+    """d = 64 non-causal attention with the keys split over ``split`` workgroups
+    per query block (fp32 partials in a torch workspace, then a combine pass)."""
+    B, Sq, H, D = q.shape
+    Skv = k.shape[1]
+    if D != 64 or not 2 <= split <= 16:
+        raise ValueError("attention_split: head dim 64, 2..16 splits")
+    if o is None:
+        o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+    st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
+    rows = B * H * Sq
+    part_o = torch.empty((split, rows, 64), dtype=torch.float32, device=q.device)
+    part_ml = torch.empty((split, rows, 2), dtype=torch.float32, device=q.device)
+    _lib.call("csk_attention_split", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), split,
+              _p(part_o), _p(part_ml), _s())
     return o
 
 
