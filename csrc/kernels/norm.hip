@@ -452,6 +452,100 @@ __global__ __launch_bounds__(256) void gn_finalize_part_wg_kernel(const float* _
   }
 }
 
+// Channel-blocked apply that merges its OWN groups' epilogue partials: grid
+// (C / CB, chunks, B) with CB = lcm(8, C/G) channels (<= 4 whole groups) per
+// workgroup.  The finalize launch between the producer and the apply
+// disappears: every workgroup merges only the nseg*CB partials of its <= 4
+// groups (one wave per group, one memory round trip) instead of all C channels
+// (which made the full-row MODE-2 prologue cost more than a finalize launch at
+// 64x64x320).  The channel block is the fastest grid dimension, so the
+// workgroups sharing a pixel row's cache lines are dispatched together.
+static int g_gn_cb_wg = 512;  // target workgroups of the channel-blocked apply; 0 = off
+CSK_API int csk_set_gn_cb(int wg) {
+  g_gn_cb_wg = wg;
+  return 0;
+}
+
+__global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                 const float* __restrict__ part,
+                                                                 const float* __restrict__ part2,
+                                                                 const bf16_t* __restrict__ gamma,
+                                                                 const bf16_t* __restrict__ beta, int P, int C, int G,
+                                                                 int CB, int chunk, int silu, int affine_bstride,
+                                                                 int nseg, int seg_rows, float eps,
+                                                                 const bf16_t* __restrict__ x2, int C1) {
+  __shared__ float gst[2 * 4];
+  if (!x2) C1 = C;
+  const int cb = blockIdx.x, ck = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+  gamma += (size_t)b * affine_bstride;
+  beta += (size_t)b * affine_bstride;
+  const int Cg = C / G, ng = CB / Cg, gbase = cb * ng;
+  const int w = tid >> 6;
+  if (w < ng) {  // whole waves: wave w merges group gbase + w
+    const int g = gbase + w;
+    const float fn = (float)seg_rows;
+    float mean, rstd;
+    group_moments_wave(
+        [&](int e, float& n, float& m, float& q) {
+          const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
+          const float2 mq = load_part(part, part2, sg, c, C, C1);
+          n = fn; m = mq.x; q = mq.y;
+        },
+        nseg * Cg, tid & 63, mean, rstd, eps);
+    if ((tid & 63) == 0) {
+      gst[2 * w] = mean;
+      gst[2 * w + 1] = rstd;
+    }
+  }
+  __syncthreads();
+  const int NVC = CB >> 3, R = GN_THREADS / NVC;
+  const int cv = tid % NVC, r = tid / NVC;
+  if (r >= R) return;
+  const int c0 = cb * CB + cv * 8;
+  float gf[8], bfv[8], sa[8], sb[8];
+  if (((((size_t)(gamma + c0)) | ((size_t)(beta + c0))) & 15) == 0) {
+    unpack8(*reinterpret_cast<const uint4*>(gamma + c0), gf);
+    unpack8(*reinterpret_cast<const uint4*>(beta + c0), bfv);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gf[j] = bf2f(gamma[c0 + j]);
+      bfv[j] = bf2f(beta[c0 + j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int lg = (c0 + j) / Cg - gbase;
+    const float a = gf[j] * gst[2 * lg + 1];
+    sa[j] = a;
+    sb[j] = bfv[j] - gst[2 * lg] * a;
+  }
+  const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
+  const bool second = c0 >= C1;  // this column vector lives in x2
+  const int xst = second ? C - C1 : C1;
+  const bf16_t* xsrc = (second ? x2 : x) + (size_t)b * P * xst + (second ? c0 - C1 : c0);
+  bf16_t* ydst = y + (size_t)b * P * C + c0;
+  for (int p = p0 + r; p < p1; p += GN_UNROLL * R) {
+    uint4 q[GN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < GN_UNROLL; ++u) q[u] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p + u * R, p1 - 1) * xst);
+#pragma unroll
+    for (int u = 0; u < GN_UNROLL; ++u) {
+      const int pp = p + u * R;
+      if (pp < p1) {
+        float f[8];
+        unpack8(q[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = f[j] * sa[j] + sb[j];
+          f[j] = silu == 1 ? silu_f(t) : (silu == 2 ? gelu_f(t) : t);
+        }
+        *reinterpret_cast<uint4*>(ydst + (size_t)pp * C) = pack8(f);
+      }
+    }
+  }
+}
+
 // stat: B*G*2 floats of workspace
 // x2 / C1: optional second input (channel concat [x | x2], x has C1 channels)
 // part2: optional partials of x2's channels (then `part` holds only x's), so a
@@ -465,6 +559,22 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
   if (part2 && !x2) return (int)hipErrorInvalidValue;
   float* st = (float*)stat;
   const int nseg = P / seg_rows;
+  if (g_gn_cb_wg > 0) {
+    const int Cg = C / G;
+    int CB = 8;
+    while (CB % Cg) CB += 8;  // lcm(8, Cg)
+    if (CB / Cg <= 4 && CB <= 1024 && C % CB == 0 && nseg * Cg <= 1024) {
+      // >= 4 rows per thread (the unroll), ~g_gn_cb_wg workgroups in all
+      const int nblk = C / CB, R = GN_THREADS / (CB / 8);
+      int ch = max(4 * R, (int)(((long)P * B * nblk + g_gn_cb_wg - 1) / g_gn_cb_wg));
+      const int nch = (P + ch - 1) / ch;
+      ch = (P + nch - 1) / nch;
+      gn_apply_cb_kernel<<<dim3(nblk, nch, B), GN_THREADS, 0, stream>>>(
+          (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const float*)part2, (const bf16_t*)gamma,
+          (const bf16_t*)beta, P, C, G, CB, ch, silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1);
+      CSK_CHECK_LAUNCH();
+    }
+  }
   // every apply workgroup re-reads ALL of its sample's partials in a prologue
   // merge; past ~1K entries that L2 traffic (1024 workgroups x nseg*C*8 bytes)
   // costs more than a finalize launch (measured: 24 vs ~12 us at 64x64x320 B8)

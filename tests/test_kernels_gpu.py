@@ -346,6 +346,45 @@ def test_fused_group_norm_stats(gpu, tile):
     assert rel_err(yc.cpu(), refc) < 1e-2
 
 
+@pytest.mark.parametrize("cbwg", [512, 64, 0])
+@pytest.mark.parametrize("H,Cin,C", [(64, 64, 320), (32, 64, 640), (16, 128, 960), (8, 128, 2560)])
+def test_group_norm_channel_blocked_apply(gpu, cbwg, H, Cin, C):
+    """norm.hip gn_apply_cb_kernel: each workgroup merges its own <= 4 groups'
+    epilogue partials (no finalize launch); == the fp32 reference GN, for the
+    UNet's group widths (10, 20, 30, 80 channels), plain and concat inputs."""
+    from chiaswarm_amd.ops import _lib
+
+    x = rnd(2, H, H, Cin, dev=gpu)
+    wp = ops.pack_conv_weight(rnd(C, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+    g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
+    try:
+        _lib.call("csk_set_gn_cb", cbwg)
+        y = hip_ops.conv2d(x, wp, None, 1, 1, None, False, None, gn_stats=True)
+        assert getattr(y, "_csk_gn", None) is not None
+        out = hip_ops.group_norm(y, g, b, 32, 1e-5, True)
+        ref = ops._ref_group_norm(y.float().cpu(), g.float().cpu(), b.float().cpu(), 32, 1e-5, True)
+        assert rel_err(out.cpu(), ref) < 1e-2
+        # per-sample affine rows (the ResNet time-embedding path uses [B, C])
+        g2, b2 = rnd(2, C, dev=gpu), rnd(2, C, dev=gpu)
+        out2 = hip_ops.group_norm(y, g2, b2, 32, 1e-5, False)
+        for i in range(2):
+            r = ops._ref_group_norm(y[i:i + 1].float().cpu(), g2[i].float().cpu(), b2[i].float().cpu(), 32, 1e-5,
+                                    False)
+            assert rel_err(out2[i:i + 1].cpu(), r) < 1e-2
+        # concat [y | y'] with both producers' partials read in place
+        h = C // 2 if C != 960 else 640
+        wa = ops.pack_conv_weight(rnd(h, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+        wb = ops.pack_conv_weight(rnd(C - h, Cin, 3, 3, dev=gpu, scale=(9 * Cin) ** -0.5))
+        a = hip_ops.conv2d(x, wa, None, 1, 1, None, False, None, gn_stats=True)
+        bb = hip_ops.conv2d(x * 0.5 + 1.0, wb, None, 1, 1, None, False, None, gn_stats=True)
+        yc = hip_ops.group_norm_cat(a, bb, g, b, 32, 1e-5, True)
+        refc = ops._ref_group_norm(torch.cat([a, bb], -1).float().cpu(), g.float().cpu(), b.float().cpu(), 32, 1e-5,
+                                   True)
+        assert rel_err(yc.cpu(), refc) < 1e-2
+    finally:
+        _lib.call("csk_set_gn_cb", 512)
+
+
 @pytest.mark.parametrize("H,C", [(256, 128), (256, 256)])
 def test_fused_group_norm_stats_large_vae_maps(gpu, H, C):
     """VAE-sized maps: thousands of epilogue partials per group take the

@@ -31,6 +31,8 @@ def apply_arm(arm):
     elif arm.startswith("gn"):
         v = arm[2:]
         _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("gcb"):  # channel-blocked GN apply merging its own partials: target workgroups (0 = off)
+        _lib.call("csk_set_gn_cb", int(arm[3:]))
     elif arm.startswith("gfw"):  # GN finalize: a workgroup per group above this many partials
         _lib.call("csk_set_gn_finalize_wg", int(arm[3:]))
     elif arm.startswith("kvr"):  # short-KV kernel rows per workgroup (0 = auto), variant 3
