@@ -149,7 +149,7 @@ class ControlNetModel(Prepared):
         temb = self.time_embedding(timestep_embedding(t, self.cfg.block_out_channels[0]).to(dtype))
         temb_s = ops.silu(temb)
         kv_iter = iter(cross_kv) if cross_kv is not None else None
-        h = self.conv_in(sample.to(dtype), residual=cond_emb)
+        h = self.conv_in(sample.to(dtype), residual=cond_emb, gn_stats=True)
         skips = [h]
         for blk in self.down_blocks:
             for j, r in enumerate(blk.resnets):

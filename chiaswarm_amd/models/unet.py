@@ -308,10 +308,10 @@ class UNet2DConditionModel(Prepared):
         dup2 = ops.dup2  # [B/2, ...] -> [B, ...] (both CFG halves)
 
         if half:
-            h = self.conv_in(x[:half])
+            h = self.conv_in(x[:half], gn_stats=True)  # the first ResNet's norm1 statistics
             skips = [dup2(h)]
         else:
-            h = self.conv_in(x)
+            h = self.conv_in(x, gn_stats=True)
             skips = [h]
         for blk in self.down_blocks:
             for j, r in enumerate(blk.resnets):

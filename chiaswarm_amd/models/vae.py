@@ -94,7 +94,7 @@ class Decoder(nn.Module):
         self.conv_out = Conv2d(ch[0], cfg.out_channels, 3, padding=1)
 
     def forward(self, z):
-        h = self.conv_in(z)
+        h = self.conv_in(z, gn_stats=True)  # the mid-block norm1 statistics
         h = self.mid_block(h)
         for blk in self.up_blocks:
             h = blk(h)

@@ -516,7 +516,11 @@ def dup2(x):
     if use_hip(x):
         from . import hip_ops
 
-        return hip_ops.dup2(x)
+        y = hip_ops.dup2(x)
+        st = getattr(x, "_csk_gn", None)
+        if st is not None:  # epilogue GN partials are batch-major [B*P/seg][C][2]: duplicate them too
+            y._csk_gn = (torch.cat([st[0], st[0]]), st[1])
+        return y
     return torch.cat([x, x], 0)
 
 
