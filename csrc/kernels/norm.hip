@@ -461,8 +461,13 @@ __global__ __launch_bounds__(256) void gn_finalize_part_wg_kernel(const float* _
 // 64x64x320).  The channel block is the fastest grid dimension, so the
 // workgroups sharing a pixel row's cache lines are dispatched together.
 static int g_gn_cb_wg = 512;  // target workgroups of the channel-blocked apply; 0 = off
+static int g_gn_cb_mult = 1;  // channel block = this many lcm(8, C/G) units (<= 16 groups)
 CSK_API int csk_set_gn_cb(int wg) {
   g_gn_cb_wg = wg;
+  return 0;
+}
+CSK_API int csk_set_gn_cb_mult(int m) {
+  g_gn_cb_mult = m;
   return 0;
 }
 
@@ -474,14 +479,13 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* _
                                                                  int CB, int chunk, int silu, int affine_bstride,
                                                                  int nseg, int seg_rows, float eps,
                                                                  const bf16_t* __restrict__ x2, int C1) {
-  __shared__ float gst[2 * 4];
+  __shared__ float gst[2 * 16];
   if (!x2) C1 = C;
   const int cb = blockIdx.x, ck = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
   gamma += (size_t)b * affine_bstride;
   beta += (size_t)b * affine_bstride;
   const int Cg = C / G, ng = CB / Cg, gbase = cb * ng;
-  const int w = tid >> 6;
-  if (w < ng) {  // whole waves: wave w merges group gbase + w
+  for (int w = tid >> 6; w < ng; w += GN_THREADS / 64) {  // whole waves: wave w merges group gbase + w
     const int g = gbase + w;
     const float fn = (float)seg_rows;
     float mean, rstd;
@@ -563,7 +567,12 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
     const int Cg = C / G;
     int CB = 8;
     while (CB % Cg) CB += 8;  // lcm(8, Cg)
-    if (CB / Cg <= 4 && CB <= 1024 && C % CB == 0 && nseg * Cg <= 1024) {
+    for (int m = g_gn_cb_mult; m > 1; --m)  // wider blocks (fewer, longer row segments) when they divide C
+      if (C % (CB * m) == 0 && CB * m / Cg <= 16 && CB * m <= 1024) {
+        CB *= m;
+        break;
+      }
+    if (CB / Cg <= 16 && CB <= 1024 && C % CB == 0 && nseg * Cg <= 1024) {
       // >= 4 rows per thread (the unroll), ~g_gn_cb_wg workgroups in all
       const int nblk = C / CB, R = GN_THREADS / (CB / 8);
       int ch = max(4 * R, (int)(((long)P * B * nblk + g_gn_cb_wg - 1) / g_gn_cb_wg));

@@ -346,9 +346,9 @@ def test_fused_group_norm_stats(gpu, tile):
     assert rel_err(yc.cpu(), refc) < 1e-2
 
 
-@pytest.mark.parametrize("cbwg", [512, 64, 0])
+@pytest.mark.parametrize("cbwg,mult", [(512, 1), (64, 1), (0, 1), (512, 2), (512, 4)])
 @pytest.mark.parametrize("H,Cin,C", [(64, 64, 320), (32, 64, 640), (16, 128, 960), (8, 128, 2560)])
-def test_group_norm_channel_blocked_apply(gpu, cbwg, H, Cin, C):
+def test_group_norm_channel_blocked_apply(gpu, cbwg, mult, H, Cin, C):
     """norm.hip gn_apply_cb_kernel: each workgroup merges its own <= 4 groups'
     epilogue partials (no finalize launch); == the fp32 reference GN, for the
     UNet's group widths (10, 20, 30, 80 channels), plain and concat inputs."""
@@ -359,6 +359,7 @@ def test_group_norm_channel_blocked_apply(gpu, cbwg, H, Cin, C):
     g, b = rnd(C, dev=gpu), rnd(C, dev=gpu)
     try:
         _lib.call("csk_set_gn_cb", cbwg)
+        _lib.call("csk_set_gn_cb_mult", mult)
         y = hip_ops.conv2d(x, wp, None, 1, 1, None, False, None, gn_stats=True)
         assert getattr(y, "_csk_gn", None) is not None
         out = hip_ops.group_norm(y, g, b, 32, 1e-5, True)
@@ -383,6 +384,7 @@ def test_group_norm_channel_blocked_apply(gpu, cbwg, H, Cin, C):
         assert rel_err(yc.cpu(), refc) < 1e-2
     finally:
         _lib.call("csk_set_gn_cb", 512)
+        _lib.call("csk_set_gn_cb_mult", 1)
 
 
 @pytest.mark.parametrize("H,C", [(256, 128), (256, 256)])

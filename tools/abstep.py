@@ -31,6 +31,8 @@ def apply_arm(arm):
     elif arm.startswith("gn"):
         v = arm[2:]
         _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("gcm"):  # channel-blocked GN apply: block width in lcm(8, C/G) units
+        _lib.call("csk_set_gn_cb_mult", int(arm[3:]))
     elif arm.startswith("gcb"):  # channel-blocked GN apply merging its own partials: target workgroups (0 = off)
         _lib.call("csk_set_gn_cb", int(arm[3:]))
     elif arm.startswith("gfw"):  # GN finalize: a workgroup per group above this many partials
@@ -73,7 +75,8 @@ def main():
     kv = p.unet.encode_context(ctx)
     graphs = {}
     for arm in a.arms.split(","):
-        apply_arm(arm)
+        for sub in arm.split("+"):  # combined knobs, e.g. gcm2+gcb1024 (settings persist into later arms)
+            apply_arm(sub)
         graphs[arm] = _UNetGraph(p.unet, x, kv, None, cfg_dup=arm != "dup0")
     res = {arm: [] for arm in graphs}
     for _ in range(a.rounds):
