@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256) void gn_finalize_part_wg_kernel(const float* _
 // 64x64x320).  The channel block is the fastest grid dimension, so the
 // workgroups sharing a pixel row's cache lines are dispatched together.
 static int g_gn_cb_wg = 512;  // target workgroups of the channel-blocked apply; 0 = off
-static int g_gn_cb_mult = 1;  // channel block = this many lcm(8, C/G) units (<= 16 groups)
+static int g_gn_cb_mult = 2;  // channel block = this many lcm(8, C/G) units (<= 16 groups); 2: -0.03 ms/step vs 1 (profiles/unet_step_ab_gn_cb_mult_r5f.txt, _r5g)
 CSK_API int csk_set_gn_cb(int wg) {
   g_gn_cb_wg = wg;
   return 0;

@@ -384,7 +384,7 @@ def test_group_norm_channel_blocked_apply(gpu, cbwg, mult, H, Cin, C):
         assert rel_err(yc.cpu(), refc) < 1e-2
     finally:
         _lib.call("csk_set_gn_cb", 512)
-        _lib.call("csk_set_gn_cb_mult", 1)
+        _lib.call("csk_set_gn_cb_mult", 2)  # library default
 
 
 @pytest.mark.parametrize("H,C", [(256, 128), (256, 256)])
