@@ -933,20 +933,6 @@ __global__ __launch_bounds__(256) void attn_shortkv_kernel(const AttnArgs a) {
   const bf16_t* vp = a.v + b * a.svb + h * a.svh;
   const float sl2 = a.scale_log2;
 
-  // K / V -> LDS (rows >= Skv and columns >= D zero: their P and V^T entries vanish)
-  for (int id = tid; id < KMAX * CPR; id += 256) {
-    const int row = id / CPR, c = id % CPR, d = c * 8;
-    uint4 vk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (row < Skv && d < a.D) {
-      vk = *reinterpret_cast<const uint4*>(kp + row * a.sks + d);
-      vv = *reinterpret_cast<const uint4*>(vp + row * a.svs + d);
-    }
-    CSK_DCHECK(kv_off<CPR>(row, c) + 8 <= TILE, 23, row, TILE);
-    *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = vk;
-    *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = vv;
-  }
-  __syncthreads();
-
   // Q rows of tile t (lane: query q0 + fr, d chunk ds * 32 + 8 * fg), loaded one
   // tile ahead so the next tile's global loads overlap this tile's MFMAs
   auto load_q = [&](int t, uint4 (&v)[2]) {
@@ -959,7 +945,29 @@ __global__ __launch_bounds__(256) void attn_shortkv_kernel(const AttnArgs a) {
     }
   };
   uint4 qnext[2];
-  load_q(wid, qnext);
+  load_q(wid, qnext);  // issued before the K / V staging so the two global latencies overlap
+
+  // K / V -> LDS (rows >= Skv and columns >= D zero: their P and V^T entries
+  // vanish); all 8 loads of a thread issued before its first LDS store
+  constexpr int KVI = KMAX * CPR / 256;
+  uint4 vk[KVI], vv[KVI];
+#pragma unroll
+  for (int i = 0; i < KVI; ++i) {
+    const int id = tid + 256 * i, row = id / CPR, d = (id % CPR) * 8;
+    vk[i] = vv[i] = make_uint4(0, 0, 0, 0);
+    if (row < Skv && d < a.D) {
+      vk[i] = *reinterpret_cast<const uint4*>(kp + row * a.sks + d);
+      vv[i] = *reinterpret_cast<const uint4*>(vp + row * a.svs + d);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KVI; ++i) {
+    const int id = tid + 256 * i, row = id / CPR, c = id % CPR;
+    CSK_DCHECK(kv_off<CPR>(row, c) + 8 <= TILE, 23, row, TILE);
+    *reinterpret_cast<uint4*>(ks + kv_off<CPR>(row, c)) = vk[i];
+    *reinterpret_cast<uint4*>(vs + kv_off<CPR>(row, c)) = vv[i];
+  }
+  __syncthreads();
   for (int t = wid; t < ROWS / 16; t += 4) {
     const int q0 = qb * ROWS + t * 16;
     if (q0 >= a.Sq) break;
