@@ -106,6 +106,7 @@ sig("csk_set_ln_in_kernel", c_int)
 sig("csk_set_gn_finalize_wg", c_int)
 sig("csk_set_gn_cb", c_int)
 sig("csk_set_gn_cb_mult", c_int)
+sig("csk_set_gn_cb_small", c_int)
 sig("csk_set_gn_fine", c_int)
 sig("csk_timestep_embedding", c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
 

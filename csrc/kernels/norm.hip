@@ -470,6 +470,13 @@ CSK_API int csk_set_gn_cb_mult(int m) {
   g_gn_cb_mult = m;
   return 0;
 }
+// grids below a quarter of the workgroup target (batch-1 jobs) switch to
+// single-unit blocks and one row per thread minimum, for more workgroups
+static int g_gn_cb_small = 1;
+CSK_API int csk_set_gn_cb_small(int v) {
+  g_gn_cb_small = v;
+  return 0;
+}
 
 __global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                                  const float* __restrict__ part,
@@ -565,19 +572,29 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
   const int nseg = P / seg_rows;
   if (g_gn_cb_wg > 0) {
     const int Cg = C / G;
-    int CB = 8;
-    while (CB % Cg) CB += 8;  // lcm(8, Cg)
+    int CB0 = 8;
+    while (CB0 % Cg) CB0 += 8;  // lcm(8, Cg)
+    int CB = CB0;
     for (int m = g_gn_cb_mult; m > 1; --m)  // wider blocks (fewer, longer row segments) when they divide C
-      if (C % (CB * m) == 0 && CB * m / Cg <= 16 && CB * m <= 1024) {
-        CB *= m;
+      if (C % (CB0 * m) == 0 && CB0 * m / Cg <= 16 && CB0 * m <= 1024) {
+        CB = CB0 * m;
         break;
       }
-    if (CB / Cg <= 16 && CB <= 1024 && C % CB == 0 && nseg * Cg <= 1024) {
-      // >= 4 rows per thread (the unroll), ~g_gn_cb_wg workgroups in all
-      const int nblk = C / CB, R = GN_THREADS / (CB / 8);
-      int ch = max(4 * R, (int)(((long)P * B * nblk + g_gn_cb_wg - 1) / g_gn_cb_wg));
-      const int nch = (P + ch - 1) / ch;
-      ch = (P + nch - 1) / nch;
+    if (CB0 / Cg <= 16 && CB0 <= 1024 && C % CB0 == 0 && nseg * Cg <= 1024) {
+      // ~g_gn_cb_wg workgroups in all, >= minr rows per thread (4: the unroll)
+      int nblk = 0, ch = 0, nch = 0;
+      auto plan = [&](int cbw, int minr) {
+        nblk = C / cbw;
+        const int R = GN_THREADS / (cbw / 8);
+        ch = max(minr * R, (int)(((long)P * B * nblk + g_gn_cb_wg - 1) / g_gn_cb_wg));
+        nch = (P + ch - 1) / ch;
+        ch = (P + nch - 1) / nch;
+        return (long)nblk * nch * B;
+      };
+      if (plan(CB, 4) * 4 < g_gn_cb_wg && g_gn_cb_small) {
+        CB = CB0;
+        plan(CB, 1);
+      }
       gn_apply_cb_kernel<<<dim3(nblk, nch, B), GN_THREADS, 0, stream>>>(
           (const bf16_t*)x, (bf16_t*)y, (const float*)part, (const float*)part2, (const bf16_t*)gamma,
           (const bf16_t*)beta, P, C, G, CB, ch, silu, affine_bstride, nseg, seg_rows, eps, (const bf16_t*)x2, C1);

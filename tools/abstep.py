@@ -31,6 +31,8 @@ def apply_arm(arm):
     elif arm.startswith("gn"):
         v = arm[2:]
         _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("gcs"):  # channel-blocked GN apply: small-grid fallback on (1) / off (0)
+        _lib.call("csk_set_gn_cb_small", int(arm[3:]))
     elif arm.startswith("gcm"):  # channel-blocked GN apply: block width in lcm(8, C/G) units
         _lib.call("csk_set_gn_cb_mult", int(arm[3:]))
     elif arm.startswith("gcb"):  # channel-blocked GN apply merging its own partials: target workgroups (0 = off)
@@ -62,6 +64,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--arms", default="base")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG: 2 x images); 2 = batch-1 jobs")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
@@ -69,9 +72,9 @@ def main():
     ops._lib.load()
     dev = torch.device("cuda", 0)
     p = StableDiffusion("sd21", device=dev, seed=0)
-    x = torch.randn(4, 64, 64, 4, device=dev).bfloat16()
+    x = torch.randn(a.batch // 2, 64, 64, 4, device=dev).bfloat16()
     x = torch.cat([x, x])  # identical CFG halves, as in the product loop
-    ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
+    ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
     graphs = {}
     for arm in a.arms.split(","):
