@@ -13,6 +13,11 @@ from chiaswarm_amd.ops import hip_ops
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG: 2 x images)")
+    a = ap.parse_args()
     dev = "cuda"
     with torch.device(dev):
         m = unet.UNet2DConditionModel(unet.SD21).to(torch.bfloat16).eval().requires_grad_(False)
@@ -33,9 +38,9 @@ def main():
         return orig_cat(a, b, *r, **k)
 
     hip_ops.group_norm, hip_ops.group_norm_cat = gn, cat
-    xh = torch.randn(4, 64, 64, 4, device=dev).bfloat16()
+    xh = torch.randn(a.batch // 2, 64, 64, 4, device=dev).bfloat16()
     x = torch.cat([xh, xh])
-    ctx = torch.randn(8, 77, 1024, device=dev).bfloat16()
+    ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
     with torch.no_grad():
         kv = m.encode_context(ctx)
         m(x, torch.tensor([500.0], device=dev), cross_kv=kv, cfg_dup=True)

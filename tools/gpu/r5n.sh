@@ -1,0 +1,11 @@
+#!/bin/bash
+# In-step tuning of the CFG-batch-2 16x16 conv shapes (all tiles, split 16 now a candidate), then A/B at batch 2.
+mkdir -p gpurun_out /tmp/tn_r5n
+timeout -k 10 560 python -u tools/steptune.py --batch 2 --all-tiles --keys "c:2:16:16:" --budget 300 --out gpurun_out/tune_b2_16x16_r5n.json > gpurun_out/steptune_b2_16x16_r5n.log 2>&1 || { tail -20 gpurun_out/steptune_b2_16x16_r5n.log; exit 1; }
+tail -8 gpurun_out/steptune_b2_16x16_r5n.log
+cp gpurun_out/tune_b2_16x16_r5n.json /tmp/tn_r5n/csk_tune.json
+for arm in ship new ship new; do
+  if [ $arm = new ]; then export SDAAS_ROOT=/tmp/tn_r5n; else unset SDAAS_ROOT; fi
+  timeout -k 10 150 python tools/abstep.py --batch 2 --arms base --rounds 3 > gpurun_out/ab_${arm}_r5n.log 2>&1 || exit 1
+  echo "$arm $(grep median gpurun_out/ab_${arm}_r5n.log)"
+done
