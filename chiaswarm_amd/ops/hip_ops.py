@@ -467,7 +467,7 @@ def attention_split(q, k, v, scale, split, o=None):
     return o
 
 
-ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "512"))  # split the keys below this many workgroups (0: off)
+ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "1024"))  # split the keys below this many workgroups (0: off); 1024 vs 512: -0.045 ms/step at CFG batch 2 (profiles/unet_step_ab_attn_split_wg_b2_r5p.txt)
 
 
 def attn_kv_split(B, H, Sq, Skv, D) -> int:

@@ -31,6 +31,8 @@ def apply_arm(arm):
     elif arm.startswith("gn"):
         v = arm[2:]
         _lib.call("csk_set_gn_prologue_max", (1 << 30) if v == "max" else int(v))
+    elif arm.startswith("asw"):  # split-KV attention: workgroup count below which the key range is split
+        hip_ops.ATTN_SPLIT_WG = int(arm[3:])
     elif arm.startswith("gcs"):  # channel-blocked GN apply: small-grid fallback on (1) / off (0)
         _lib.call("csk_set_gn_cb_small", int(arm[3:]))
     elif arm.startswith("gcm"):  # channel-blocked GN apply: block width in lcm(8, C/G) units
