@@ -6,6 +6,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
+``--gpus N`` without torchrun env vars spawns N rank processes itself (the
+parent never touches the GPU; ranks rendezvous on 127.0.0.1, RCCL on GPUs,
+gloo with ``--device cpu``), so ``python bench.py --gpus 8`` and the torchrun
+form above measure the same N-rank run; each rank asserts WORLD_SIZE == --gpus.
+
 One "step" = one complete txt2img job per GPU: prompt encoding (OpenCLIP-H,
 CFG batch), 50 DPM-Solver++(2M) Karras denoising steps of the full SD2.1 UNet
 (865.9M params) on the CFG batch of 8 latents 64x64, VAE decode 512x512, uint8
@@ -57,8 +62,46 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """``--gpus N`` > 1 without a torchrun environment: start N rank processes
+    of this script (before this process touches the GPU), forward rank 0's
+    JSON line and return the worst exit code.  A rank that fails takes the
+    others down (process group), so the run ends instead of hanging."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, abs(p.wait()))
+            if rc:
+                for q in procs:
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
     # result encoders are separate processes, started before this process touches the GPU
     from chiaswarm_amd.output.encoder import EncoderPool
 
@@ -68,7 +111,9 @@ def main():
     from chiaswarm_amd.pipelines.sd import StableDiffusion
     from chiaswarm_amd.schedulers import get_scheduler
 
-    rank, local_rank, world = comm.init_distributed()
+    rank, local_rank, world = comm.init_distributed(backend="gloo" if args.device == "cpu" else None)
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU required")
     on_gpu = torch.cuda.is_available() and args.device != "cpu"
     device = torch.device("cuda", local_rank) if on_gpu else torch.device("cpu")
     if on_gpu:
@@ -106,12 +151,14 @@ def main():
     comm.barrier()
     if on_gpu:
         torch.cuda.synchronize()
-    lat = []
+    lat = []  # per job: start -> pixels on the host (the GPU part)
+    done = {}  # per job: start -> result envelope encoded (what the hive waits for)
     timings = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         ts = time.perf_counter()
         f, tm, _ = job(args.warmup + i)
+        f.add_done_callback(lambda _f, i=i, ts=ts: done.__setitem__(i, time.perf_counter() - ts))
         futs.append(f)
         if on_gpu:
             torch.cuda.synchronize()
@@ -125,7 +172,10 @@ def main():
     if on_gpu:
         torch.cuda.synchronize()
     elapsed = comm.max_over_ranks(time.perf_counter() - t0)
-    p50 = comm.max_over_ranks(statistics.median(lat))
+    p50_gpu = comm.max_over_ranks(statistics.median(lat))
+    while len(done) < len(futs):  # done-callbacks run on the pool's reader thread
+        time.sleep(0.001)
+    p50 = comm.max_over_ranks(statistics.median(done.values()))
 
     images = args.batch * args.steps * world
     ips = images / elapsed
@@ -158,10 +208,14 @@ def main():
                 "hip_graphs": (not args.no_graphs) and args.impl == "hip",
             },
             "p50_job_latency_ms": round(1000 * p50, 1),
+            "p50_job_latency_note": "job start -> result envelope (JPEG/base64/sha256) done",
+            "p50_gpu_latency_ms": round(1000 * p50_gpu, 1),
+            "world_size": world,
+            "dist_backend": torch.distributed.get_backend() if comm.is_dist() else None,
             "phase_ms_median": phase,
             "model_load_s": round(load_s, 2),
             "load_bytes_read_per_rank": load_bytes,
-            "load_path": "safetensors dir -> sharded byte-range reads + RCCL all_gather" if world > 1 else
+            "load_path": f"safetensors dir -> sharded byte-range reads + {'RCCL' if on_gpu else 'gloo'} all_gather" if world > 1 else
                          "safetensors dir -> local read",
         }
         print(json.dumps(rec), flush=True)

@@ -1,6 +1,6 @@
 """Multi-process distribution paths on CPU (gloo, world_size 2 and 4): sharded
 all_gather of module weights is bitwise identical to the source, broadcast,
-split-job tensor all-gather, and the bench's data-parallel job split."""
+split-job tensor all-gather (the bench's rank spawning: tests/test_bench_cpu.py)."""
 import os
 import socket
 
