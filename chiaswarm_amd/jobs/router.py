@@ -24,8 +24,12 @@ PIPELINE_TYPES = {
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
     "StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline", "AudioLDMPipeline",
     "TextToVideoSDPipeline", "VideoToVideoSDPipeline", "IFPipeline", "IFSuperResolutionPipeline",
-    "KandinskyPipeline", "UnCLIPPipeline", "AltDiffusionPipeline",
 }
+# real diffusers classes with no implementation here: a fatal error naming the
+# class (never silently run as plain SD)
+UNIMPLEMENTED_PIPELINES = {"KandinskyPipeline", "KandinskyImg2ImgPipeline", "KandinskyInpaintPipeline",
+                           "KandinskyV22Pipeline", "UnCLIPPipeline", "UnCLIPImageVariationPipeline",
+                           "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline"}
 
 
 class PipelineType(str):
@@ -33,6 +37,8 @@ class PipelineType(str):
 
 
 def get_pipeline_type(name: str) -> PipelineType:
+    if name in UNIMPLEMENTED_PIPELINES:
+        raise ValueError(f"pipeline class {name} is not implemented by this worker")
     if name not in PIPELINE_TYPES:
         raise AttributeError(f"module 'diffusers' has no attribute '{name}'")
     return PipelineType(name)

@@ -76,6 +76,39 @@ def _read_dir(d: str) -> dict:
     return out
 
 
+def read_pth(path: str) -> dict:
+    """A PyTorch ``.pth`` / ``.pt`` checkpoint read with the weights-only
+    unpickler (tensors and plain containers only: nothing in the file is
+    executed).  Real-ESRGAN / BasicSR checkpoints wrap the state dict as
+    ``{"params_ema": ...}`` (or ``"params"``); that wrapper is unwrapped."""
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(obj, dict):
+        for key in ("params_ema", "params", "state_dict", "model"):
+            if isinstance(obj.get(key), dict):
+                obj = obj[key]
+                break
+    if not isinstance(obj, dict) or not all(torch.is_tensor(v) for v in obj.values()):
+        raise CheckpointMismatch(f"{path}: not a state dict of tensors")
+    return obj
+
+
+def read_weights(path: str) -> dict:
+    """State dict of a directory (``*.safetensors``, else a single ``*.pth`` /
+    ``*.pt``) or of one file of either format."""
+    if os.path.isdir(path):
+        if glob.glob(os.path.join(path, "*.safetensors")):
+            return _read_dir(path)
+        pth = sorted(glob.glob(os.path.join(path, "*.pth")) + glob.glob(os.path.join(path, "*.pt")))
+        if len(pth) != 1:
+            raise CheckpointMismatch(f"{path}: expected *.safetensors or exactly one *.pth, found {pth}")
+        return read_pth(pth[0])
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+
+        return load_file(path, device="cpu")
+    return read_pth(path)
+
+
 def load_into(module: torch.nn.Module, sd: dict, renames: dict | None = None, prefix_strip: str = "",
               strict: bool = True, allow_unexpected: bool = False, name: str = "") -> LoadReport:
     """Copy ``sd`` into ``module``'s parameters/buffers (cast to their dtype).

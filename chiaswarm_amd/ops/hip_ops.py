@@ -204,8 +204,6 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
         # (and the buffer sized for them below) follow the tile that actually runs
         if tile in (25, 26, 31, 32, 33, 34):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
             tile = 11
-        elif ln is not None and 21 <= tile <= 24:  # persistent tiles: no per-tile LN statistics
-            tile = {21: 11, 23: 18}.get(tile, 19)
         if ln is None and code == 3:
             row_stats = False
     seg = _gn_seg(tile, split, gn_rows, M, code, N) if gn_rows and out.is_contiguous() else 0

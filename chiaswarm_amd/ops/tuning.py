@@ -27,8 +27,6 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # LDS-DMA multi-stage variants (gemm_glds.hip)
          11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (128, 128), 16: (128, 32), 17: (128, 64),
          18: (64, 64), 19: (128, 64), 20: (64, 128),
-         # persistent continuous-ring LDS-DMA variants (K % 64 == 0, no split-K)
-         21: (128, 128), 22: (128, 64), 23: (64, 64), 24: (128, 64),
          # one 256x160 workgroup per CU (3-stage, 156 KB LDS): least L2->LDS traffic per output
          25: (256, 160), 26: (128, 160),
          # 4-stage rings (3 K-steps in flight) for latency-bound low-M / long-K shapes
@@ -101,12 +99,11 @@ def candidates(M, N, K):
             continue
         if tile in (2, 6, 12, 17, 19, 22, 24, 29) and N > 1280:
             continue
-        persistent = 21 <= tile <= 24
-        if (persistent or tile >= 31) and K % 64:
+        if tile >= 31 and K % 64:
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)
-            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split or persistent):
+            if split > 1 and (ntiles >= 512 or K // 64 < 4 * split):
                 continue
             if split == 16 and ntiles > 64:
                 continue

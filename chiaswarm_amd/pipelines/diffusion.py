@@ -23,8 +23,52 @@ from ..schedulers import get_scheduler
 from .sd import StableDiffusion, resolve_family
 from ..utils import stable_seed
 
-_DROP = ("supports_xformers", "cross_attention_kwargs", "eta", "callback", "callback_steps", "output_type",
-         "return_dict", "prompt_embeds", "negative_prompt_embeds", "guidance_rescale", "clip_skip")
+# accepted and ignored: memory / progress / return-format knobs of the diffusers
+# call that have no meaning here (the reference's own xformers flag included)
+_DROP = ("supports_xformers", "cross_attention_kwargs", "callback", "callback_steps", "output_type",
+         "return_dict")
+
+# the diffusers classes the SD-family callback runs as StableDiffusion
+SD_CLASSES = {
+    "DiffusionPipeline", "StableDiffusionPipeline", "StableDiffusionImg2ImgPipeline",
+    "StableDiffusionInpaintPipeline", "StableDiffusionInpaintPipelineLegacy", "StableDiffusionControlNetPipeline",
+    "StableDiffusionControlNetImg2ImgPipeline", "StableDiffusionInstructPix2PixPipeline",
+    "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
+}
+UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
+
+
+def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
+    """The pipeline class a generic ``DiffusionPipeline`` load would build
+    (diffusers reads model_index.json's ``_class_name``); name heuristics for
+    the two upscalers when no local checkpoint is present."""
+    import json
+
+    w = find_weights(model_name, revision)
+    if w and os.path.exists(os.path.join(w, "model_index.json")):
+        with open(os.path.join(w, "model_index.json")) as f:
+            return json.load(f).get("_class_name")
+    n = model_name.lower()
+    if "x4-upscaler" in n:
+        return "StableDiffusionUpscalePipeline"
+    if "latent-upscaler" in n:
+        return "StableDiffusionLatentUpscalePipeline"
+    return None
+
+
+def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "main") -> str:
+    """The class this job runs as: the hive-named class, or — for the generic
+    ``DiffusionPipeline`` — the checkpoint's own (reference:
+    swarm/diffusion/diffusion_func.py:41-46 builds ``pipeline_type.from_pretrained``).
+    A class with no implementation here is a fatal ``ValueError`` naming it."""
+    cls = str(pipeline_type or "DiffusionPipeline")
+    if cls == "DiffusionPipeline":
+        ck = checkpoint_class(model_name, revision)
+        if ck in UPSCALE_CLASSES or (ck is not None and ck not in SD_CLASSES):
+            cls = ck
+    if cls in SD_CLASSES or cls in UPSCALE_CLASSES:
+        return cls
+    raise ValueError(f"pipeline class {cls} is not implemented by the Stable Diffusion callback of this worker")
 
 
 def load_sd(model_name: str, device_identifier: str, revision: str = "main", controlnet_name: str | None = None,
@@ -73,6 +117,19 @@ def _apply_textual_inversion(pipe, ti, model_name):
 
 
 def diffusion_callback(device_identifier, model_name, **kwargs):
+    split = kwargs.pop("_split", None)  # {"role": "leader", "peers": [rank, ...]} | {"role": "helper", "leader": r}
+    state = {"transferred": False}
+    try:
+        return _diffusion(device_identifier, model_name, split, state, **kwargs)
+    except BaseException:
+        # ANY failure of a split part (load, adapters, scheduler, arguments, the
+        # pipeline) before its transfer started: release the peers blocked on it
+        if not state["transferred"]:
+            _split_failed(split)
+        raise
+
+
+def _diffusion(device_identifier, model_name, split, state, **kwargs):
     t0 = time.perf_counter()
     scheduler_type = kwargs.pop("scheduler_type", "DPMSolverMultistepScheduler")
     pipeline_type = kwargs.pop("pipeline_type", "DiffusionPipeline")
@@ -98,7 +155,11 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     # all images from one generator stream (swarm/gpu/device.py:35-41).
     image_range = kwargs.pop("_image_range", None)
     return_images = bool(kwargs.pop("_return_images", False))
-    split = kwargs.pop("_split", None)  # {"role": "leader", "peers": [rank, ...]} | {"role": "helper", "leader": r}
+    pcls = pipeline_class_for(pipeline_type, model_name, revision)
+    if pcls in UPSCALE_CLASSES:
+        if split is not None or image_range is not None:
+            raise ValueError(f"{pcls} jobs are not split across GPUs")
+        return _upscale_job(pcls, device_identifier, model_name, scheduler_type, output_processor, **kwargs)
     gen = kwargs.get("generator")
     n_img = int(kwargs.get("num_images_per_prompt", 1) or 1)
     if (isinstance(gen, torch.Generator) and kwargs.get("image") is None
@@ -113,26 +174,14 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     pipe = load_sd(model_name, device_identifier, revision, controlnet_name, controlnet_revision)
     if textual_inversion is not None:
         _apply_textual_inversion(pipe, textual_inversion, model_name)
-    if lora is not None:
-        try:
-            _apply_lora(pipe, lora, cross_attention_scale)
-        except Exception:
-            if textual_inversion is not None:
-                from ..models.lora import unload_textual_inversion
-
-                unload_textual_inversion(pipe)
-            raise
-
-    # the named sampler built from the checkpoint's scheduler config (diffusers from_config)
-    sched = get_scheduler(scheduler_type, **pipe.family.scheduler_kwargs())
-    load_s = time.perf_counter() - t0
-    helper = split is not None and split.get("role") == "helper"
     try:
-        try:
-            p = pipe(scheduler=sched, **dict(kwargs, output_type="uint8_device" if helper else "pil"))
-        except BaseException:
-            _split_failed(split)
-            raise
+        if lora is not None:
+            _apply_lora(pipe, lora, cross_attention_scale)
+        # the named sampler built from the checkpoint's scheduler config (diffusers from_config)
+        sched = get_scheduler(scheduler_type, **pipe.family.scheduler_kwargs())
+        load_s = time.perf_counter() - t0
+        helper = split is not None and split.get("role") == "helper"
+        p = pipe(scheduler=sched, **dict(kwargs, output_type="uint8_device" if helper else "pil"))
     finally:
         from ..models.lora import unload_lora, unload_textual_inversion
 
@@ -143,7 +192,7 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
 
     config = dict(pipe.config)
     config["scheduler"] = ["chiaswarm_amd", sched.name]
-    config["_pipeline_type"] = str(pipeline_type)
+    config["_pipeline_type"] = pcls
     if any(bool(x) for x in (p.nsfw_content_detected or [])):
         config["nsfw"] = True
 
@@ -151,9 +200,11 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
     if helper:  # a split part: uint8 images straight to the leader's GPU over the process group
         from ..parallel import comm
 
+        state["transferred"] = True  # a failure from here on must not send a second header
         comm.send_images(images, int(split["leader"]), any(bool(x) for x in (p.nsfw_content_detected or [])))
         return {}, {"_split_ack": int(images.shape[0])}
     if split is not None and split.get("role") == "leader":
+        state["transferred"] = True  # _gather_split_images drains every helper itself
         images, nsfw_peers = _gather_split_images(images, split)
         if nsfw_peers:
             config["nsfw"] = True
@@ -176,6 +227,57 @@ def diffusion_callback(device_identifier, model_name, **kwargs):
         t["load"] = load_s
         config["timings"] = {k: round(v, 4) for k, v in t.items()}
     return results, config
+
+
+_X4_ARGS = {"prompt", "negative_prompt", "num_inference_steps", "guidance_scale", "noise_level",
+            "num_images_per_prompt", "generator", "image", "eta"}
+_X2_ARGS = {"prompt", "negative_prompt", "num_inference_steps", "guidance_scale", "num_images_per_prompt",
+            "generator", "image"}
+
+
+def _upscale_job(pcls, device_identifier, model_name, scheduler_type, output_processor, **kwargs):
+    """The diffusers upscale pipelines as hive jobs: ``StableDiffusionUpscalePipeline``
+    (x4: low-res RGB concatenated to the latents, ``noise_level`` class
+    conditioning; diffusers defaults 75 steps / guidance 9 / noise_level 20)
+    and ``StableDiffusionLatentUpscalePipeline`` (x2 K-UNet, Euler).  The
+    start image is required; unknown call kwargs raise ``TypeError`` like the
+    diffusers call would."""
+    from .upscale import load_latent_upscaler, load_x4_upscaler
+
+    allowed = _X4_ARGS if pcls == "StableDiffusionUpscalePipeline" else _X2_ARGS
+    bad = sorted(k for k in kwargs if k not in allowed)
+    if bad:
+        raise TypeError(f"{pcls}.__call__() got unexpected keyword arguments {bad}")
+    image = kwargs.get("image")
+    if image is None:
+        raise ValueError(f"{pcls} needs an input image (start_image_uri)")
+    n = max(1, int(kwargs.get("num_images_per_prompt", 1) or 1))
+    images = [image] * n
+    prompt = [kwargs.get("prompt", "")] * n
+    neg = kwargs.get("negative_prompt")
+    neg = [neg or ""] * n if not isinstance(neg, list) else neg
+    g = kwargs.get("generator")
+    t0 = time.perf_counter()
+    if pcls == "StableDiffusionUpscalePipeline":
+        up = load_x4_upscaler(device_identifier, model_name)
+        sched = get_scheduler(scheduler_type, **up.scheduler_kwargs())
+        if kwargs.get("eta") and sched.accepts_eta:
+            sched.eta = float(kwargs["eta"])
+        out = up(prompt, images, num_inference_steps=int(kwargs.get("num_inference_steps", 75)),
+                 guidance_scale=float(kwargs.get("guidance_scale", 9.0)),
+                 noise_level=int(kwargs.get("noise_level", 20)), negative_prompt=neg, generator=g, scheduler=sched)
+        sched_name = sched.name
+    else:
+        up = load_latent_upscaler(device_identifier, model_name)
+        out = up(prompt, images, num_inference_steps=int(kwargs.get("num_inference_steps", 75)),
+                 guidance_scale=float(kwargs.get("guidance_scale", 9.0)), generator=g, negative_prompt=neg)
+        sched_name = "EulerDiscreteScheduler"
+    output_processor.add_outputs(out)
+    config = {"model_name": model_name, "_pipeline_type": pcls, "scheduler": ["chiaswarm_amd", sched_name],
+              "weights": getattr(up, "weights_source", "random-init")}
+    if os.environ.get("SDAAS_TIMINGS"):
+        config["timings"] = {"total": round(time.perf_counter() - t0, 4)}
+    return output_processor.get_results(), config
 
 
 def _split_failed(split):
@@ -256,7 +358,7 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
         op.add_outputs(p.images[i:i + n])
         cfg = dict(pipe.config)
         cfg["scheduler"] = ["chiaswarm_amd", sched.name]
-        cfg["_pipeline_type"] = str(kw.get("pipeline_type", "DiffusionPipeline"))
+        cfg["_pipeline_type"] = pipeline_class_for(kw.get("pipeline_type", "DiffusionPipeline"), model_name)
         if any(bool(x) for x in (p.nsfw_content_detected or [])[i:i + n]):
             cfg["nsfw"] = True
         if os.environ.get("SDAAS_TIMINGS"):

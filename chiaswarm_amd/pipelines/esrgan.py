@@ -21,18 +21,54 @@ from ..output.processor import OutputProcessor
 from ..runtime.model_cache import cache, find_weights
 
 
+# the original ESRGAN repo's RRDB_ESRGAN_x4.pth names -> BasicSR / Real-ESRGAN names
+_OLD_ESRGAN_RENAMES = {"RRDB_trunk.": "body.", ".RDB1.": ".rdb1.", ".RDB2.": ".rdb2.", ".RDB3.": ".rdb3.",
+                       "trunk_conv.": "conv_body.", "upconv1.": "conv_up1.", "upconv2.": "conv_up2.",
+                       "HRconv.": "conv_hr."}
+
+
+def esrgan_state_dict(path: str) -> dict:
+    """Real-ESRGAN x4 weights from a directory or file: ``*.safetensors`` or
+    the published ``.pth`` (``params_ema`` wrapper, weights-only unpickler),
+    BasicSR key names or the original ESRGAN repo's."""
+    from ..models.weights import read_weights
+
+    sd = read_weights(path)
+    if any(k.startswith("RRDB_trunk.") for k in sd):
+        out = {}
+        for k, v in sd.items():
+            for a, b in _OLD_ESRGAN_RENAMES.items():
+                k = k.replace(a, b)
+            out[k] = v
+        sd = out
+    return sd
+
+
 def load_esrgan(model_name: str, device: str):
     def make():
+        import os
+        import re
+
         tiny = model_name.lower().startswith("tiny")
         dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+        w = find_weights(model_name) or (model_name if os.path.isfile(model_name) else None)
+        sd = esrgan_state_dict(w) if w else None
+        kw = dict(TINY_RRDB) if tiny else {}
+        if sd is not None:  # geometry from the checkpoint: block count, width, growth
+            kw["nb"] = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"body\.(\d+)\.", k)] if m)
+            kw["nf"] = int(sd["conv_first.weight"].shape[0])
+            kw["gc"] = int(sd["body.0.rdb1.conv1.weight"].shape[0])
+            kw["in_ch"] = int(sd["conv_first.weight"].shape[1])
+            if kw["in_ch"] != 3:
+                raise ValueError(f"{model_name}: {kw['in_ch']}-channel input (pixel-unshuffled x2/x1 "
+                                 "Real-ESRGAN) is not supported; x4 RRDBNet only")
         with torch.device(device):
-            net = RRDBNet(**(TINY_RRDB if tiny else {})).to(dt).eval().requires_grad_(False)
+            net = RRDBNet(**kw).to(dt).eval().requires_grad_(False)
         init_random_fast_(net, seed=77, std_scale=0.5)
-        w = find_weights(model_name)
-        if w:
-            from ..models.weights import _read_dir, load_into
+        if sd is not None:
+            from ..models.weights import load_into
 
-            load_into(net, _read_dir(w))
+            load_into(net, sd, name=model_name)
         prepare_model(net)
         return net
 

@@ -424,7 +424,10 @@ class StableDiffusion:
     def __call__(self, prompt="", negative_prompt=None, num_inference_steps=30, guidance_scale=7.5,
                  num_images_per_prompt=1, height=None, width=None, generator=None, image=None,
                  mask_image=None, strength=0.8, image_guidance_scale=None, scheduler=None,
-                 controlnet_conditioning_scale=1.0, output_type="pil", latents=None, **unused):
+                 controlnet_conditioning_scale=1.0, output_type="pil", latents=None, eta=0.0, **unexpected):
+        if unexpected:  # the diffusers call raises on unknown kwargs too (a retryable job error)
+            raise TypeError(f"{self.family.pipeline_class}.__call__() got unexpected keyword arguments "
+                            f"{sorted(unexpected)}")
         t0 = time.perf_counter()
         timings = {}
         prompts = prompt if isinstance(prompt, list) else [prompt]
@@ -438,6 +441,8 @@ class StableDiffusion:
         cfg = guidance_scale > 1.0 or is_pix2pix
         sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **self.family.scheduler_kwargs())
         sched.prediction_type = self.family.prediction_type
+        if eta and sched.accepts_eta:  # diffusers forwards eta only to samplers whose step takes it (DDIM)
+            sched.eta = float(eta)
 
         if image is not None and not isinstance(image, list):
             image = [image]

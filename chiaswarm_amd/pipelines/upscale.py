@@ -187,10 +187,28 @@ class X4Upscaler(_Base):
         # low_res_scheduler: DDPM linear betas 1e-4 .. 2e-2
         betas = np.linspace(1e-4, 0.02, 1000, dtype=np.float64)
         self.low_res_acp = np.cumprod(1.0 - betas)
+        # the denoising scheduler's training schedule: the checkpoint's
+        # scheduler/scheduler_config.json, else the published x4 config
+        # (DDIM, scaled_linear 1e-4 .. 2e-2, v-prediction, leading + offset 1)
+        self._sched_cfg = {"beta_start": 0.0001, "beta_end": 0.02, "beta_schedule": "scaled_linear",
+                           "prediction_type": "v_prediction", "steps_offset": 1}
+        if weights_dir:
+            import json
+            import os
+
+            from ..models.hf_config import scheduler_kwargs
+
+            f = os.path.join(weights_dir, "scheduler", "scheduler_config.json")
+            if os.path.exists(f):
+                with open(f) as fh:
+                    self._sched_cfg.update(scheduler_kwargs(json.load(fh)))
+
+    def scheduler_kwargs(self) -> dict:
+        return dict(self._sched_cfg)
 
     @torch.no_grad()
     def __call__(self, prompt, image, num_inference_steps=75, guidance_scale=9.0, noise_level=20,
-                 negative_prompt=None, generator=None):
+                 negative_prompt=None, generator=None, scheduler=None):
         """image: PIL list or NHWC [-1, 1] tensor [B, h, w, 3] -> 4x PIL images."""
         img = _to_nhwc(image if isinstance(image, (list, torch.Tensor)) else [image], self.device)
         b, h, w, _ = img.shape
@@ -202,7 +220,8 @@ class X4Upscaler(_Base):
         nz = torch.randn(img.shape, generator=generator, device=self.device, dtype=torch.float32)
         cond = img * acp ** 0.5 + nz * (1 - acp) ** 0.5
         labels = torch.full((b,), int(noise_level), device=self.device, dtype=torch.long)
-        sched = get_scheduler("DDIMScheduler", prediction_type="v_prediction", use_karras_sigmas=False)
+        sched = scheduler or get_scheduler("DDIMScheduler", use_karras_sigmas=False, **self.scheduler_kwargs())
+        sched.prediction_type = self._sched_cfg.get("prediction_type", "v_prediction")
         sched.set_timesteps(num_inference_steps)
         noise = torch.randn((b, 4, h, w), generator=generator, device=self.device, dtype=torch.float32)
         x = noise.permute(0, 2, 3, 1).contiguous() * sched.init_noise_sigma

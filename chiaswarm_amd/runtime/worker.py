@@ -486,10 +486,23 @@ class Supervisor:
         restarts0 = [e.restarts for e in exs]
         tasks = [asyncio.ensure_future(e.run(sj)) for e, sj in zip(exs, subs)]
         pending = set(tasks)
+        failed_at = None  # when a part first returned an error result
+        grace = float(os.environ.get("SDAAS_SPLIT_GRACE_S", "30"))
         while pending:
-            done, pending = await asyncio.wait(pending, return_when=asyncio.FIRST_COMPLETED)
-            if any(e.restarts != r0 for e, r0 in zip(exs, restarts0)):
-                for e, t in zip(exs, tasks):  # a part crashed: its peers may wait on it forever
+            done, pending = await asyncio.wait(pending, timeout=grace if failed_at is not None else None,
+                                               return_when=asyncio.FIRST_COMPLETED)
+            for t in done:
+                i = tasks.index(t)
+                cfg = t.result().get("pipeline_config") or {}
+                if "error" in cfg or (i > 0 and "_split_ack" not in cfg):
+                    failed_at = failed_at if failed_at is not None else time.monotonic()
+            crashed = any(e.restarts != r0 for e, r0 in zip(exs, restarts0))
+            # a crashed part never sends; a part that failed released its peers
+            # (pipelines.diffusion._split_failed), so survivors still pending
+            # after the grace period are wedged on the transfer: restart them
+            # rather than leave queued sends a later split could match
+            if crashed or (failed_at is not None and pending and time.monotonic() - failed_at >= grace):
+                for e, t in zip(exs, tasks):
                     if not t.done():
                         e.kill()
         results = [t.result() for t in tasks]

@@ -73,7 +73,11 @@ class Scheduler:
     order = 1
     space = "vp"
     default_spacing = "linspace"
-    karras_full_range = False  # DPM-Solver: Karras over the whole training sigma range  # "vp": sample lives in x_t = a x0 + s eps; "k": x = x0 + sigma eps
+    karras_full_range = False  # DPM-Solver: Karras over the whole training sigma range
+    # config keys only some diffusers classes take (from_config drops them for the others):
+    accepts_eta = False  # DDIMScheduler.step(eta=...)
+    accepts_clip_sample = False  # DDIM / DDPM
+    accepts_thresholding = False  # DDIM / DDPM / DPM-Solver family / DEIS / UniPC
 
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
                  beta_schedule="scaled_linear", prediction_type="epsilon", use_karras_sigmas=True,
@@ -85,11 +89,11 @@ class Scheduler:
         if timestep_spacing not in ("linspace", "leading", "trailing"):
             raise ValueError(f"timestep_spacing={timestep_spacing!r} is not supported")
         self.timestep_spacing = timestep_spacing
-        self.clip_sample = bool(clip_sample)
+        self.clip_sample = bool(clip_sample) and self.accepts_clip_sample
         self.clip_sample_range = float(clip_sample_range)
         # Imagen dynamic thresholding of the x0 prediction (DeepFloyd IF:
         # ratio 0.95, max 1.5) -- non-linear in x0, so those steps skip the fused kernel
-        self.thresholding = thresholding
+        self.thresholding = bool(thresholding) and self.accepts_thresholding
         self.dyn_ratio = dynamic_thresholding_ratio
         self.sample_max = sample_max_value
         self.betas = _betas(num_train_timesteps, beta_start, beta_end, beta_schedule)
@@ -270,12 +274,19 @@ class DPMSolverMultistepScheduler(Scheduler):
     order = 2
     karras_full_range = True
 
-    def __init__(self, solver_order=2, lower_order_final=True, **kw):
+    accepts_thresholding = True
+
+    def __init__(self, solver_order=2, lower_order_final=True, algorithm_type="dpmsolver++", **kw):
         super().__init__(**kw)
+        if algorithm_type not in ("dpmsolver++", "sde-dpmsolver++"):
+            raise ValueError(f"{self.name}: algorithm_type={algorithm_type!r} is not supported")
         self.solver_order = solver_order
         self.lower_order_final = lower_order_final
+        self.algorithm_type = algorithm_type
 
     def coeffs(self, i):
+        if self.algorithm_type == "sde-dpmsolver++":
+            return self._sde_coeffs(i)
         s_s, s_t = float(self.sigmas[i]), float(self.sigmas[i + 1])
         p, q = self.x0_coeffs(i)
         a_t = 1.0 / math.sqrt(s_t * s_t + 1)
@@ -296,13 +307,10 @@ class DPMSolverMultistepScheduler(Scheduler):
         C = a_t * em1 * (0.5 / r0)
         return StepCoeffs(p, q, A, B, C, 0.0, 1.0)
 
-
-class DPMSolverSDEScheduler(DPMSolverMultistepScheduler):
-    """DPM-Solver++(2M) SDE variant (stochastic), same linear form + noise."""
-
-    name = "DPMSolverSDEScheduler"
-
-    def coeffs(self, i):
+    def _sde_coeffs(self, i):
+        """DPM-Solver++(2M) SDE (diffusers ``algorithm_type="sde-dpmsolver++"``):
+        the same midpoint form with e^{-h}-damped x and fresh noise of
+        std sigma_t sqrt(1 - e^{-2h}) every step but the last."""
         s_s, s_t = float(self.sigmas[i]), float(self.sigmas[i + 1])
         p, q = self.x0_coeffs(i)
         if s_t == 0.0:
@@ -313,7 +321,7 @@ class DPMSolverSDEScheduler(DPMSolverMultistepScheduler):
         A = sv_t / sv_s * math.exp(-h)
         em = -math.expm1(-2.0 * h)  # 1 - e^{-2h}
         D = sv_t * math.sqrt(max(em, 0.0))
-        if i == 0 or (i == self.n - 1 and self.n < 15):
+        if i == 0 or self.solver_order == 1 or (self.lower_order_final and i == self.n - 1 and self.n < 15):
             return StepCoeffs(p, q, A, a_t * em, 0.0, D)
         h0 = math.log(float(self.sigmas[i - 1]) / s_s)
         r0 = h0 / h
@@ -347,11 +355,19 @@ class EulerAncestralDiscreteScheduler(Scheduler):
 
 
 class DDIMScheduler(Scheduler):
-    """DDIM (eta = 0), "leading" timestep spacing with steps_offset."""
+    """DDIM, "leading" timestep spacing with steps_offset.  ``eta`` (the
+    pipeline call's kwarg, forwarded to ``DDIMScheduler.step`` by diffusers)
+    interpolates between deterministic DDIM (0) and DDPM-like ancestral
+    sampling (1): std_t = eta sqrt((1 - a_prev)/(1 - a_t) (1 - a_t/a_prev)) of fresh
+    noise, the eps direction shrunk to sqrt(1 - a_prev - std_t^2)."""
 
     name = "DDIMScheduler"
+    accepts_eta = True
+    accepts_clip_sample = True
+    accepts_thresholding = True
 
     default_spacing = "leading"
+    eta = 0.0
 
     def _ladder(self, n):
         ts = self._spaced_timesteps(n)
@@ -368,15 +384,21 @@ class DDIMScheduler(Scheduler):
         p, q = self.x0_coeffs(i)
         a, an = 1 / math.sqrt(s * s + 1), 1 / math.sqrt(sn * sn + 1)
         sv, svn = s * a, sn * an
-        A = svn / sv
-        B = an - svn * a / sv
-        return StepCoeffs(p, q, A, B)
+        std = 0.0
+        if self.eta:
+            abar, abar_p = a * a, an * an
+            std = float(self.eta) * math.sqrt(max((1 - abar_p) / (1 - abar) * (1 - abar / abar_p), 0.0))
+        c = math.sqrt(max(svn * svn - std * std, 0.0))  # eps-direction weight
+        A = c / sv
+        B = an - c * a / sv
+        return StepCoeffs(p, q, A, B, 0.0, std)
 
 
 class DDPMScheduler(DDIMScheduler):
     """Ancestral DDPM posterior sampling on the leading-spacing ladder."""
 
     name = "DDPMScheduler"
+    accepts_eta = False
 
     def coeffs(self, i):
         s, sn = float(self.sigmas[i]), float(self.sigmas[i + 1])
@@ -470,6 +492,9 @@ class PNDMScheduler(DDIMScheduler):
     x_prev = sqrt(a_prev/a_t) x - (a_prev - a_t) e / (a_t sqrt(1-a_prev) + sqrt(a_t (1-a_t) a_prev))."""
 
     name = "PNDMScheduler"
+    accepts_eta = False
+    accepts_clip_sample = False
+    accepts_thresholding = False
 
     def set_timesteps(self, n):
         super().set_timesteps(n)  # DDIM ladder: leading spacing + steps_offset, final level acp[0]

@@ -431,7 +431,6 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
-  if (a.ln_part && tile >= 21 && tile <= 24) tile = (tile == 21) ? 11 : (tile == 23 ? 18 : 19);  // persistent: no per-tile LN stats (hip_ops.gemm mirrors)
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;

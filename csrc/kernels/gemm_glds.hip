@@ -265,212 +265,6 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
   gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true>(args, acc, smem, m0, n0, split, lnrow, lnlane, lnl);
 }
 
-// ---------------------------------------------------------------------------
-// Persistent variant: each workgroup walks tiles t = blockIdx.x, +gridDim.x, ...
-// with ONE continuous LDS-DMA ring over all its K-steps, so the next tile's
-// first stages are already in flight while the current tile finishes its
-// MFMAs and epilogue (the non-persistent kernel drains and refills the ring
-// per tile: at K = 320 — the UNet's 64x64-level projections — that fill is
-// most of the tile's time).  FAST staging only, no split-K; the epilogue uses
-// its own LDS region and raw barriers so it never drains the ring.
-// ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int S, bool CONV>
-__global__ __launch_bounds__(256, 1) void gemm_glds_persist_kernel(const GemmArgs args) {
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int MT = WTM / 16, NT = WTN / 16;
-  constexpr int IA = BM / 32, IB = BN / 32;
-  constexpr int LPG = IA + IB;
-  constexpr int STAGE = (BM + BN) * BK;
-  constexpr int SMEM_MAIN = S * STAGE;
-  constexpr int SMEM_EPI = epi_smem_elems<BM, BN>();
-  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM_MAIN + SMEM_EPI];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int M = args.M, N = args.N, K = args.K;
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  const int ntiles = tiles_m * tiles_n;
-  const int nk = K / BK;
-  // this workgroup's tiles: blockIdx.x + i * gridDim.x (XCD-aware remap of the linear id)
-  const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int total = my_tiles * nk;
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;
-  const bf16_t* zero = args.zero;
-  const int Hin = args.up2x ? 2 * args.H : args.H;
-  const int Win = args.up2x ? 2 * args.Wd : args.Wd;
-
-  auto tile_of = [&](int i, int& m0, int& n0) {
-    const int t = xcd_remap(blockIdx.x + i * gridDim.x, ntiles);
-    m0 = (t / tiles_n) * BM;
-    n0 = (t % tiles_n) * BN;
-  };
-
-  // ---- issue-side state (advances tile by tile, K-step by K-step) ----
-  int is_tile = 0, is_k = 0;
-  const bf16_t* fa[IA];
-  const bf16_t* fb[IB];
-  int a_ihb[IA], a_iwb[IA];
-  size_t a_bbase[IA];
-  bool a_ok[IA];
-  int f_ky = 0, f_kx = 0, f_c = 0;
-  auto set_rows = [&]() {
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int ih = a_ihb[i] + f_ky * args.dil, iw = a_iwb[i] + f_kx * args.dil;
-      const bool v = a_ok[i] && ih >= 0 && ih < Hin && iw >= 0 && iw < Win;
-      const int sh = args.up2x ? (ih >> 1) : ih, sw = args.up2x ? (iw >> 1) : iw;
-      fa[i] = v ? args.A + (a_bbase[i] + (size_t)sh * args.Wd + sw) * args.lda + lchunk * 8 : zero + lchunk * 8;
-    }
-  };
-  auto begin_tile = [&](int i) {
-    int m0, n0;
-    tile_of(i, m0, n0);
-#pragma unroll
-    for (int r = 0; r < IA; ++r) {
-      const int m = m0 + (wid * IA + r) * 8 + lrow;
-      a_ok[r] = m < M;
-      const int mm = a_ok[r] ? m : 0;
-      if constexpr (CONV) {
-        const int hw = args.Ho * args.Wo;
-        const int b = mm / hw, rr = mm - b * hw;
-        const int oh = rr / args.Wo, ow = rr - oh * args.Wo;
-        a_ihb[r] = oh * args.stride - args.pt;
-        a_iwb[r] = ow * args.stride - args.pl;
-        a_bbase[r] = (size_t)b * args.H * args.Wd;
-      } else {
-        fa[r] = a_ok[r] ? args.A + (size_t)mm * args.lda + lchunk * 8 : zero + lchunk * 8;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < IB; ++r) {
-      const int n = n0 + (wid * IB + r) * 8 + lrow;
-      fb[r] = n < N ? args.W + (size_t)n * args.ldb + lchunk * 8 : zero + lchunk * 8;
-    }
-    if constexpr (CONV) {
-      f_c = 0;
-      f_ky = 0;
-      f_kx = 0;
-      set_rows();
-    }
-  };
-  auto issue = [&](int buf) {
-    bf16_t* as = smem + buf * STAGE;
-    bf16_t* bs = as + BM * BK;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const bf16_t* src = CONV ? fa[i] + f_c : fa[i];
-      dma16<SITE_PERSIST_A>(args, src, as + (wid * IA + i) * 8 * BK, smem, SMEM_MAIN);
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      dma16<SITE_PERSIST_B>(args, fb[i], bs + (wid * IB + i) * 8 * BK, smem, SMEM_MAIN);
-      fb[i] += BK;
-    }
-    if constexpr (CONV) {
-      f_c += BK;
-      if (f_c == args.Cin) {
-        f_c = 0;
-        if (++f_kx == args.kw) { f_kx = 0; ++f_ky; }
-        set_rows();
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < IA; ++i) fa[i] += BK;
-    }
-    if (++is_k == nk) {
-      is_k = 0;
-      if (++is_tile < my_tiles) begin_tile(is_tile);
-    }
-  };
-
-  v4f acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  if (my_tiles > 0) begin_tile(0);
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < total) issue(s);
-
-  const int fr = lane & 15, fq = lane >> 4;
-  int c_tile = 0, c_k = 0;
-  for (int g = 0; g < total; ++g) {
-    const int younger = min(S - 2, total - 1 - g);
-    if constexpr (S >= 4) {
-      if (younger >= 2) vmcnt_wait<2 * LPG>();
-      else if (younger == 1) vmcnt_wait<LPG>();
-      else vmcnt_wait<0>();
-    } else if constexpr (S == 3) {
-      if (younger >= 1) vmcnt_wait<LPG>();
-      else vmcnt_wait<0>();
-    } else {
-      vmcnt_wait<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (g + S - 1 < total) issue((g + S - 1) % S);
-    const bf16_t* as = smem + (g % S) * STAGE;
-    const bf16_t* bs = as + BM * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v8s af[MT], bfr[NT];
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-        af[i] = *reinterpret_cast<const v8s*>(as + swz(wm * WTM + i * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-        bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (++c_k == nk) {
-      int m0, n0;
-      tile_of(c_tile, m0, n0);
-      gemm_epilogue<BM, BN, WM, WN, true, 1, 256, true>(args, acc, smem + SMEM_MAIN, m0, n0, 0);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-      c_k = 0;
-      ++c_tile;
-    }
-  }
-}
-
-static int g_num_cus = 0;
-
-static int num_cus() {
-  if (!g_num_cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      g_num_cus = 256;
-  }
-  return g_num_cus;
-}
-
-template <int BM, int BN, int WM, int WN, int S>
-static int launch_persist(const GemmArgs& a0, bool conv, hipStream_t s) {
-  GemmArgs a = a0;
-  a.gn_seg = gn_seg_for<BM, BN, WM>();
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  constexpr int LDS = (S * (BM + BN) * BK + epi_smem_elems<BM, BN>()) * 2;
-  const int per_cu = LDS <= 80 * 1024 ? 2 : 1;
-  int grid = num_cus() * per_cu;
-  if (grid > tiles) grid = tiles;
-  if (conv)
-    gemm_glds_persist_kernel<BM, BN, WM, WN, S, true><<<grid, 256, 0, s>>>(a);
-  else
-    gemm_glds_persist_kernel<BM, BN, WM, WN, S, false><<<grid, 256, 0, s>>>(a);
-  return (int)hipGetLastError();
-}
-
 template <int BM, int BN, int WM, int WN, int S>
 static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   GemmArgs a = a0;
@@ -509,20 +303,10 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   a.zero = g_zero;
   // GEGLU pairs 16-column (hidden, gate) tiles inside one wave's columns: every
   // tile below has a per-wave width (BN / WN) that is a multiple of 32
-  if (tile >= 21 && tile <= 24) {  // persistent continuous-ring variants: FAST staging, no split-K
-    const bool fast = (conv ? (a.Cin % BK == 0) : true) && a.K % BK == 0 &&
-                      (size_t)(a.K + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
-                      (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
-    if (!fast || ksplit > 1) tile = 11;  // fall back to the tiled kernel
-  }
   // 256x160: 80 columns per wave (odd 16-column tile count: no GEGLU pairing),
   // 20 vectors per output row (no power-of-two row-statistics butterfly)
   if ((tile == 25 || tile == 26) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 11;
   switch (tile) {
-    case 21: return launch_persist<128, 128, 2, 2, 2>(a, conv, s);
-    case 22: return launch_persist<128, 64, 4, 1, 3>(a, conv, s);
-    case 23: return launch_persist<64, 64, 2, 2, 3>(a, conv, s);
-    case 24: return launch_persist<128, 64, 2, 2, 4>(a, conv, s);
     case 11: return launch_glds<128, 128, 2, 2, 2>(a, ksplit, conv, s);
     case 12: return launch_glds<128, 64, 4, 1, 3>(a, ksplit, conv, s);
     case 13: return launch_glds<64, 128, 2, 2, 3>(a, ksplit, conv, s);

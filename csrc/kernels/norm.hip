@@ -296,8 +296,10 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
   if (L.r >= L.R) return;
   // per-channel scale / shift of this thread's (up to two) 8-channel columns:
   // gamma / beta as one 16-byte load each, the (mean, rstd) of the <= 2 groups
-  // an 8-channel vector touches when Cg >= 4 (24 scalar loads per thread before
-  // the first pixel otherwise)
+  // an 8-channel vector touches when Cg == 4 or Cg >= 6 (24 scalar loads per
+  // thread before the first pixel otherwise).  Cg = 5 is excluded: an aligned
+  // 8-channel vector can span THREE 5-channel groups (channels 8..15 = groups
+  // 1, 2, 3), so it takes the per-channel path.
   float sa[2][8], sb[2][8];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -315,8 +317,9 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
       }
     }
     const int g0 = c0 / Cg;
+    const bool two = Cg == 4 || Cg >= 6;  // <= 2 groups per aligned 8-channel vector
     float2 s0, s1;
-    if (Cg >= 4) {
+    if (two) {
       const int g1 = min(g0 + 1, G - 1);
       if constexpr (MODE == 0) {
         s0 = *reinterpret_cast<const float2*>(stat + (b * G + g0) * 2);
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const bf16_t* __re
       const int c = c0 + j;
       const int g = c / Cg;
       float2 st;
-      if (Cg >= 4) {
+      if (two) {
         st = g == g0 ? s0 : s1;
       } else if constexpr (MODE == 0) {
         st = *reinterpret_cast<const float2*>(stat + (b * G + g) * 2);

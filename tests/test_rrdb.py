@@ -62,3 +62,51 @@ def test_rrdb_gpu_hip_vs_reference(gpu):
     ref = ref_forward(net, x)
     err = ((y.float() - ref).norm() / ref.norm()).item()
     assert err < 3e-2
+
+
+def test_pth_checkpoint_weights_only(tmp_path):
+    """Published Real-ESRGAN weights are ``.pth`` files wrapping the state dict
+    in ``params_ema``: read with the weights-only unpickler, geometry (block
+    count, width, growth) taken from the keys; the original ESRGAN repo's key
+    names map onto the same modules; a pickle that is not plain tensors is refused."""
+    import pickle
+
+    from chiaswarm_amd.models.weights import CheckpointMismatch, read_pth
+    from chiaswarm_amd.pipelines.esrgan import _OLD_ESRGAN_RENAMES, load_esrgan
+
+    src = RRDBNet(**TINY_RRDB).eval()
+    init_random_(src, seed=5)
+    sd = {k: v.clone() for k, v in src.state_dict().items()}
+    f = tmp_path / "RealESRGAN_x4plus_tiny.pth"
+    torch.save({"params_ema": sd, "params": {k: torch.zeros_like(v) for k, v in sd.items()}}, f)
+    net = load_esrgan(str(f), "cpu")
+    assert len(net.body) == TINY_RRDB["nb"] and net.nf == TINY_RRDB["nf"] and net.gc == TINY_RRDB["gc"]
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    # original ESRGAN naming
+    inv = {b: a for a, b in _OLD_ESRGAN_RENAMES.items()}
+    old = {}
+    for k, v in sd.items():
+        for b, a in inv.items():
+            k = k.replace(b, a)
+        old[k] = v
+    assert any(k.startswith("RRDB_trunk.") for k in old)
+    g = tmp_path / "old" / "RRDB_ESRGAN_x4.pth"
+    g.parent.mkdir()
+    torch.save(old, g)
+    net2 = load_esrgan(str(g), "cpu")
+    for k, v in net2.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+
+    class Evil:
+        def __reduce__(self):
+            return (print, ("executed",))
+
+    h = tmp_path / "evil.pth"
+    with open(h, "wb") as fh:
+        pickle.dump({"params_ema": Evil()}, fh)
+    with pytest.raises(Exception):
+        read_pth(str(h))
+    torch.save({"params_ema": {"a": 1}}, tmp_path / "notensors.pth")
+    with pytest.raises(CheckpointMismatch):
+        read_pth(str(tmp_path / "notensors.pth"))

@@ -248,3 +248,95 @@ def test_dynamic_thresholding_matches_imagen_rule():
     assert y.abs().max() <= 1.0 + 1e-6
     off = get_scheduler("DDPMScheduler", use_karras_sigmas=False)
     assert off.threshold_x0(x0) is x0
+
+
+def _diffusers_ddim_step(acp, t, t_prev, x, eps, eta, noise):
+    """diffusers DDIMScheduler.step (epsilon prediction, no clipping) written
+    from its formulas: x0, std = eta sqrt(var(t, t_prev)), eps direction."""
+    a_t = acp[t]
+    a_p = acp[t_prev] if t_prev >= 0 else acp[0]
+    x0 = (x - math.sqrt(1 - a_t) * eps) / math.sqrt(a_t)
+    var = (1 - a_p) / (1 - a_t) * (1 - a_t / a_p)
+    std = eta * math.sqrt(var)
+    return math.sqrt(a_p) * x0 + math.sqrt(1 - a_p - std * std) * eps + std * noise
+
+
+@pytest.mark.parametrize("eta", [0.0, 0.3, 1.0])
+def test_ddim_eta_matches_diffusers_formula(eta):
+    s = get_scheduler("DDIMScheduler", use_karras_sigmas=False)
+    s.eta = eta
+    n = 10
+    s.set_timesteps(n)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(64, generator=g, dtype=torch.float64)
+    ts = [int(t) for t in s.timesteps]
+    for i in range(n):
+        eps = torch.randn(64, generator=g, dtype=torch.float64)
+        c = s.coeffs(i)
+        noise = torch.randn(64, generator=g, dtype=torch.float64)
+        ours = c.A * x + c.B * (c.p * x + c.q * eps) + c.D * noise
+        ref = _diffusers_ddim_step(s.alphas_cumprod, ts[i], ts[i] - 1000 // n, x, eps, eta, noise)
+        assert torch.allclose(ours, ref, atol=1e-9), (i, (ours - ref).abs().max())
+        assert (c.D == 0.0) == (eta == 0.0)
+        x = ref
+
+
+def test_eta_is_ddim_only_and_reaches_the_sampler():
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    assert get_scheduler("DDIMScheduler").accepts_eta
+    for n in ("DDPMScheduler", "PNDMScheduler", "DPMSolverMultistepScheduler", "EulerDiscreteScheduler"):
+        assert not get_scheduler(n).accepts_eta, n
+    pipe = StableDiffusion("tiny", "cpu", seed=1)
+    kw = dict(prompt="x", num_inference_steps=3, height=64, width=64)
+    a = pipe(generator=torch.Generator().manual_seed(0), scheduler=get_scheduler("DDIMScheduler"), **kw).latents
+    b = pipe(generator=torch.Generator().manual_seed(0), scheduler=get_scheduler("DDIMScheduler"), eta=0.0,
+             **kw).latents
+    c = pipe(generator=torch.Generator().manual_seed(0), scheduler=get_scheduler("DDIMScheduler"), eta=1.0,
+             **kw).latents
+    assert torch.equal(a, b) and not torch.allclose(a, c)
+    # samplers whose step takes no eta ignore it (diffusers prepare_extra_step_kwargs)
+    d = pipe(generator=torch.Generator().manual_seed(0), scheduler=get_scheduler("EulerDiscreteScheduler"), **kw)
+    e = pipe(generator=torch.Generator().manual_seed(0), scheduler=get_scheduler("EulerDiscreteScheduler"), eta=1.0,
+             **kw)
+    assert torch.equal(d.latents, e.latents)
+
+
+def test_unknown_pipeline_kwarg_raises():
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    pipe = StableDiffusion("tiny", "cpu", seed=1)
+    with pytest.raises(TypeError, match="not_a_diffusers_arg"):
+        pipe(prompt="x", num_inference_steps=1, height=64, width=64, not_a_diffusers_arg=3)
+
+
+def test_dpmpp_2m_sde_via_algorithm_type():
+    """diffusers' 2M SDE is DPMSolverMultistepScheduler(algorithm_type="sde-dpmsolver++"):
+    fresh noise every step but the last, the deterministic limit of its
+    first-order update is the data-prediction exponential integrator."""
+    s = get_scheduler("DPMSolverMultistepScheduler", algorithm_type="sde-dpmsolver++")
+    s.set_timesteps(20)
+    rows = s.loop_table()[1]
+    assert all(r[5] > 0 for r in rows[:-1]) and rows[-1][5] == 0.0
+    c = s.coeffs(0)
+    s_s, s_t = float(s.sigmas[0]), float(s.sigmas[1])
+    h = math.log(s_s / s_t)
+    a_t = 1 / math.sqrt(s_t ** 2 + 1)
+    assert abs(c.B - a_t * (1 - math.exp(-2 * h))) < 1e-12
+    assert abs(c.D - s_t * a_t * math.sqrt(1 - math.exp(-2 * h))) < 1e-12
+    with pytest.raises(ValueError):
+        get_scheduler("DPMSolverMultistepScheduler", algorithm_type="dpmsolver")
+    # the k-diffusion DPM++ SDE keeps its own name
+    assert type(get_scheduler("DPMSolverSDEScheduler")).__mro__[1].__name__ == "_TwoStageK"
+
+
+def test_clip_sample_only_where_diffusers_takes_it():
+    for n in ("DDIMScheduler", "DDPMScheduler"):
+        assert get_scheduler(n, clip_sample=True).clip_sample, n
+    for n in ("DPMSolverMultistepScheduler", "EulerDiscreteScheduler", "PNDMScheduler", "HeunDiscreteScheduler"):
+        s = get_scheduler(n, clip_sample=True)
+        assert not s.clip_sample, n
+        s.set_timesteps(5)
+        assert s.fused_coeffs() is not None or s.coeffs(0) is None  # never demoted by the key
+    assert not get_scheduler("EulerDiscreteScheduler", thresholding=True).thresholding
+    assert get_scheduler("DPMSolverMultistepScheduler", thresholding=True).thresholding

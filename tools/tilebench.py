@@ -23,10 +23,6 @@ GEMMS = ["32768,320,320", "32768,960,320", "32768,2560,320:geglu", "32768,320,12
          "8192,5120,640:geglu", "8192,640,2560", "2048,1280,1280", "2048,10240,1280:geglu", "2048,1280,5120"]
 
 
-def tiles_persistent(a):
-    return any(21 <= int(t) <= 24 for t in a.tiles.split(","))
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="11,26,31,32")
@@ -93,8 +89,6 @@ def main():
             r = torch.randn(M, no, device=dev).to(torch.bfloat16)
             variants = [(False, False)] + ([(True, False)] if a.probe else []) + ([(False, True)] if a.res else [])
             for probe, res in variants:
-                if probe and tiles_persistent(a):
-                    continue  # the persistent kernels have no probe exit (act 99 would run the epilogue)
                 def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe, res=res, r=r):
                     ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
                     _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, _p(r) if res else None, M, N, K, K, K, no,
