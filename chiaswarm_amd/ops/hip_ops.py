@@ -465,13 +465,25 @@ def attention_split(q, k, v, scale, split, o=None):
     return o
 
 
+ATTN32 = True  # mirrors the library's csk_set_attn32 (set_attn32): the split-KV path runs attn32_kernel only
+
+
+def set_attn32(on: bool):
+    """Turn the 32x32x16 self-attention kernel on / off (A/B and fallback
+    switch) in the library AND here: with it off, the key-split path (which
+    always runs attn32_kernel) is skipped too."""
+    global ATTN32
+    ATTN32 = bool(on)
+    _lib.call("csk_set_attn32", int(ATTN32))
+
+
 ATTN_SPLIT_WG = int(os.environ.get("CSK_ATTN_SPLIT_WG", "1024"))  # split the keys below this many workgroups (0: off); 1024 vs 512: -0.045 ms/step at CFG batch 2 (profiles/unet_step_ab_attn_split_wg_b2_r5p.txt)
 
 
 def attn_kv_split(B, H, Sq, Skv, D) -> int:
     """Key splits for the d = 64 self-attention when its 128-query workgroups
     cannot fill the chip (batch-1 jobs): up to 4."""
-    if D != 64 or Skv <= 128 or ATTN_SPLIT_WG <= 0:
+    if D != 64 or Skv <= 128 or ATTN_SPLIT_WG <= 0 or not ATTN32:
         return 1
     wg = B * H * -(-Sq // 128)
     split = 1

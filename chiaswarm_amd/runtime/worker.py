@@ -333,6 +333,7 @@ class Supervisor:
         self.store = next((s for s in _STORES if any(getattr(e, "env", {}).get("SDAAS_STORE_PORT") == str(s.port)
                                                        for e in self.executors)), None)
         self._last_regroup = 0.0
+        self._regroup_task = None  # a background regroup (never awaited by the poll loop)
         self.regroups = 0
         n = max(1, len(self.executors))
         # batching: each device may hold up to max_batch queued jobs (max_batch <= 1:
@@ -391,10 +392,16 @@ class Supervisor:
         return ok
 
     async def _maybe_regroup(self):
+        """Start a regroup in the background when the group is degraded and the
+        node idle: the hive poll loop never waits on it (a wedged child would
+        otherwise stall polling for the whole per-executor control timeout)."""
+        if self._regroup_task is not None and not self._regroup_task.done():
+            return
         if (self.store is not None and not self.group_ok() and self.busy == 0 and self.work_queue.empty()
                 and all(hasattr(e, "regroup") for e in self.executors) and len(self.executors) > 1
                 and time.monotonic() - self._last_regroup > float(os.environ.get("SDAAS_REGROUP_S", "60"))):
-            await self.regroup()
+            self._regroup_task = asyncio.ensure_future(
+                self.regroup(timeout_s=float(os.environ.get("SDAAS_REGROUP_TIMEOUT_S", "60"))))
 
     # ------------------------------------------------------------------ split jobs
     async def _claim_helpers(self, job, ex) -> list:
@@ -533,12 +540,13 @@ class Supervisor:
         killed = False
         while pending:
             done, pending = await asyncio.wait(pending, return_when=asyncio.FIRST_COMPLETED)
-            if collective and not killed and any(t.exception() is not None for t in done):
+            if collective and not killed and any(t.cancelled() or t.exception() is not None for t in done):
                 killed = True
                 for ex, t in zip(exs, tasks):  # peers of a dead rank are stuck in the all_gather
                     if not t.done():
                         ex.kill()
-        failed = [t.exception() for t in tasks if t.exception() is not None]
+        failed = [asyncio.CancelledError("preload cancelled") if t.cancelled() else t.exception() for t in tasks
+                  if t.cancelled() or t.exception() is not None]
         if failed:
             raise RuntimeError(f"preload failed on {len(failed)} device(s): {failed[0]}")
         return [t.result() for t in tasks]
