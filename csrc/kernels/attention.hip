@@ -597,7 +597,9 @@ __device__ __forceinline__ int kv_off32(int row, int chunk) {
 // at the end.  Q pre-scaled, the QK^T chain starts from -max (PRE), lazy
 // rescale (T13, threshold 2^8), same 3-buffer register-staged K/V ring and
 // one-barrier-per-block software pipeline (QK^T of block kb+1 issued before
-// the softmax of block kb) as attn_fwd_pipe_kernel.
+// the softmax of block kb) as attn_fwd_pipe_kernel.  Two VALU loads moved
+// onto the (under-used) matrix cores: the row sum is an all-ones O^T tile of
+// the PV chain, and the -mu offset one MFMA from an inline-zero accumulator.
 // QB: 32-query tiles per wave (QB = 2, 256 rows per workgroup at one wave per
 // SIMD, was 1.6x slower and spills; only QB = 1 is instantiated).
 // PROBE (profiling builds, wrong results by design; variants 31/32/34/38):
@@ -645,15 +647,29 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
       qf[qt][ds] = __builtin_bit_cast(v8s, pack8(f));
     }
   v16f oacc[2][QB];  // O^T d-tile dt: query r, d = dt*32 + (i & 3) + 8 (i >> 2) + 4 hh
+  // row sums ride on the PV MFMAs: an all-ones A operand makes every row of this
+  // O^T tile the query's sum of P over the keys (replaces 32 VALU adds per block)
+  v16f osum[QB];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][qt][i] = 0.f;
-  float mrow[QB], lrow[QB];  // running max (log2 units); this lane's partial row sum
+  float mrow[QB];  // running max (log2 units)
 #pragma unroll
-  for (int qt = 0; qt < QB; ++qt) { mrow[qt] = -1e30f; lrow[qt] = 0.f; }
+  for (int qt = 0; qt < QB; ++qt) {
+    mrow[qt] = -1e30f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) osum[qt][i] = 0.f;
+  }
+  constexpr short BF_ONE = 0x3F80;
+  const v8s ones8 = {BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE};
+  // -mu enters the QK^T chain as one extra MFMA from a zero accumulator (no
+  // per-block 32-register init): A = [1, 1, 0..] in k-slots 0-1 of every key
+  // row, B = [-mu_hi, -mu_lo, 0..] (bf16 hi/lo split, exact in the fp32 sum)
+  const v8s kmu = hh == 0 ? v8s{BF_ONE, BF_ONE, 0, 0, 0, 0, 0, 0} : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  const v16f zero16 = {0.f};
 
   int kv_end = Skv;
   if (a.causal) {
@@ -698,14 +714,20 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   // scores of one 64-key block: s[kt][qt] = S^T of keys kt*32.. (issued with offset -mu)
   auto qk = [&](int buf, v16f (&s)[2][QB], float (&mu)[QB]) {
     const bf16_t* ks = smem + buf * 2 * TILE;
+    v8s qmu[QB];
 #pragma unroll
-    for (int qt = 0; qt < QB; ++qt) mu[qt] = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
+    for (int qt = 0; qt < QB; ++qt) {
+      const float m = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
+      const bf16_t hi = f2bf(m);
+      const bf16_t lo = f2bf(m - bf2f(hi));
+      mu[qt] = bf2f(hi) + bf2f(lo);  // the value the MFMA subtracts, exactly
+      qmu[qt] = hh == 0 ? v8s{(short)(hi ^ 0x8000), (short)(lo ^ 0x8000), 0, 0, 0, 0, 0, 0}
+                        : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int qt = 0; qt < QB; ++qt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
+      for (int qt = 0; qt < QB; ++qt) s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kmu, qmu[qt], zero16, 0, 0, 0);
 #pragma unroll
       for (int ds = 0; ds < ((PROBE & 8) ? 0 : 4); ++ds) {
         const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off32(kt * 32 + r, 2 * ds + hh));
@@ -758,7 +780,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         const float mnew = fmaxf(mrow[qt], mb);
         const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
         mrow[qt] = mnew;
-        lrow[qt] *= alpha;
+        osum[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) oacc[dt][qt] *= alpha;
       }
@@ -775,16 +797,6 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
           for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
       }
-      // 4 independent single-instruction add chains (no v_pk_add_f32 beside MFMAs)
-      float l4[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        l4[c] = vadd(sc[0][qt][c], sc[0][qt][c + 4]);
-        l4[c] = vadd(l4[c], vadd(sc[0][qt][c + 8], sc[0][qt][c + 12]));
-        l4[c] = vadd(l4[c], vadd(sc[1][qt][c], sc[1][qt][c + 4]));
-        l4[c] = vadd(l4[c], vadd(sc[1][qt][c + 8], sc[1][qt][c + 12]));
-      }
-      lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -819,6 +831,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
               asm volatile("" ::"v"(vf), "v"(pf[kt][st][qt]));
             } else {
               oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
+              if (dt == 1)  // the row-sum tile of this k-step
+                osum[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones8, pf[kt][st][qt], osum[qt], 0, 0, 0);
             }
           }
         }
@@ -835,8 +849,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     const size_t rows = (size_t)a.B * a.H * a.Sq;
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt) {
-      float l = lrow[qt];
-      l += __shfl_xor(l, 32, 64);
+      const float l = osum[qt][0];
       const int qi = q0 + qt * 32 + r;
       if (qi >= a.Sq) continue;
       const size_t row = (size_t)ks * rows + (size_t)bh * a.Sq + qi;
@@ -855,8 +868,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   bf16_t* op = a.o + b * a.sob + h * a.soh;
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
-    float l = lrow[qt];
-    l += __shfl_xor(l, 32, 64);
+    const float l = osum[qt][0];
     const float inv = l > 0.f ? 1.0f / l : 0.f;
     const int qi = q0 + qt * 32 + r;
     if (qi >= a.Sq) continue;
