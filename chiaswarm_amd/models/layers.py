@@ -278,12 +278,19 @@ class BasicTransformerBlock(nn.Module):
         qkv = ops.layer_norm_gemm(x, self.norm1, a1.w_qkv, a1.b_qkv,
                                   self._fold("qkv", a1.w_qkv, a1.b_qkv, self.norm1) if fus else None)
         x = a1.attend_qkv(qkv, residual=x, row_stats=hip)
-        fus = ops.ln_fusable(x)
-        q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
-                                self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None)
-        if dup:
-            q, x = ops.dup2(q), ops.dup2(x)
-        x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
+        if hip and not dup and kv is not None and x.dim() == 3 and ops.xattn_fusable(x, kv, x.shape[1]):
+            # LN2 + Q projection + attention over the context + out-projection +
+            # residual in ONE kernel (csrc/kernels/xattn.hip)
+            w2, colsum, b2 = self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2)
+            x = ops.xattn_block(x, w2, colsum, b2, kv, a2.to_out[0].weight, a2.to_out[0].bias, self.norm2.eps,
+                                a2.scale, x.shape[1], row_stats=hip)
+        else:
+            fus = ops.ln_fusable(x)
+            q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
+                                    self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None)
+            if dup:
+                q, x = ops.dup2(q), ops.dup2(x)
+            x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
         g = ff.net[0]
         g.ensure()
         fus = ops.ln_fusable(x)
@@ -348,10 +355,36 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0) if cin != cout else None
         self.out_channels = cout
 
+    def _halo_ok(self, x, x2=None) -> bool:
+        return (ops.use_hip(x) and self.norm1.weight.dim() == 1 and self.conv1.kernel_size == (3, 3)
+                and self.conv1.stride == (1, 1) and self.conv1.padding == (1, 1) and ops.conv_halo_ok(x, self.conv1, x2))
+
+    def _forward_halo(self, x, x2, temb_proj, sc_fn):
+        """norm1 -> conv1 -> norm2 -> conv2 with both GroupNorm(+SiLU)s applied
+        inside the halo convs' LDS tiles (csrc/kernels/conv_halo.hip): the two
+        GroupNorm apply passes (a full read + write of the activation each) are
+        gone; the producers' epilogue statistics are finalized per (sample,
+        group) by a tiny kernel.  Returns None when the statistics are missing."""
+        n1, n2 = self.norm1, self.norm2
+        st1 = ops.gn_finalize(x, n1.num_groups, n1.eps, x2)
+        if st1 is None:
+            return None
+        sc = sc_fn()
+        h = ops.conv_halo(x, self.conv1, bias2d=temb_proj, gn=(st1, n1.weight, n1.bias, n1.num_groups, True), x2=x2)
+        st2 = ops.gn_finalize(h, n2.num_groups, n2.eps) if ops.conv_halo_ok(h, self.conv2) else None
+        if st2 is None:
+            return self.conv2(self.norm2(h, silu=True), residual=sc, gn_stats=True)
+        return ops.conv_halo(h, self.conv2, residual=sc, gn=(st2, n2.weight, n2.bias, n2.num_groups, True))
+
     def forward(self, x, temb_proj=None):
         """``temb_proj``: this block's [B, Cout] time projection (already
         computed by the model's batched time-embedding GEMM).  A 1x1 shortcut
         runs on a side stream, overlapping norm1 / conv1 / norm2."""
+        if self._halo_ok(x):
+            y = self._forward_halo(x, None, temb_proj,
+                                   lambda: self.conv_shortcut(x) if self.conv_shortcut is not None else x)
+            if y is not None:
+                return y
         sc = x
         with ops.side_branch(x) as br:
             if self.conv_shortcut is not None:
@@ -369,6 +402,18 @@ class ResnetBlock2D(nn.Module):
         (the concat cost a full read + write of both tensors per up-block
         ResNet)."""
         sc_conv = self.conv_shortcut
+        if (sc_conv is not None and sc_conv.kernel_size == (1, 1) and a.shape[-1] % 64 == 0 and a.is_contiguous()
+                and b.is_contiguous() and self._halo_ok(a, b)):
+            w = sc_conv.weight.view(sc_conv.out_channels, sc_conv.in_channels)
+            ca = a.shape[-1]
+
+            def shortcut():
+                s1 = ops.gemm(a, w[:, :ca])
+                return ops.gemm(b, w[:, ca:], sc_conv.bias, residual=s1)
+
+            y = self._forward_halo(a, b, temb_proj, shortcut)
+            if y is not None:
+                return y
         hn = None
         if ops.use_hip(a) and sc_conv is not None and sc_conv.kernel_size == (1, 1) and self.norm1.weight.dim() == 1:
             hn = ops.group_norm_cat(a, b, self.norm1.weight, self.norm1.bias, self.norm1.num_groups,

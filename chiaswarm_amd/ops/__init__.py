@@ -204,6 +204,73 @@ def layer_norm_gemm(x, norm, w, bias, folded, act=None, residual=None, row_stats
                 row_stats=row_stats)
 
 
+def conv_halo_ok(x: torch.Tensor, conv, x2=None) -> bool:
+    """The halo 3x3 conv kernel (csrc/kernels/conv_halo.hip) takes ``conv`` on
+    ``x`` (or on the channel concat [x | x2]) on the HIP path."""
+    if not use_hip(x) or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1):
+        return False
+    from . import hip_ops
+
+    return hip_ops.conv_halo_ok(x, conv._wp(), x2)
+
+
+def gn_finalize(x, groups, eps, x2=None):
+    """(mean, rstd) [B, G, 2] of x (or of [x | x2]) from the producers' fused
+    epilogue statistics, or None (HIP path)."""
+    from . import hip_ops
+
+    return hip_ops.gn_finalize(x, groups, eps, x2)
+
+
+def conv_halo(x, conv, bias2d=None, residual=None, gn=None, x2=None, gn_stats=True):
+    """conv(act(GroupNorm(x))) through the halo kernel (``gn = (stat, gamma,
+    beta, groups, silu)``); ``conv`` is the Conv2d module (its packed weight and
+    bias)."""
+    from . import hip_ops
+
+    return hip_ops.conv_halo(x, conv._wp(), conv.bias, bias2d=bias2d, residual=residual, gn=gn, x2=x2,
+                             gn_stats=gn_stats)
+
+
+def xattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
+    """The fused cross-attention sub-block kernel takes this block (HIP path)."""
+    if not use_hip(x):
+        return False
+    from . import hip_ops
+
+    return hip_ops.xattn_ok(x, kv, rows_per_b)
+
+
+def xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats=True):
+    """x + CrossAttention(LayerNorm(x)) with the LayerNorm folded into ``wq`` /
+    ``colsum`` / ``bq`` (fold_layer_norm) and ``kv`` the per-request K/V
+    [B, Skv, 2, H, D]; one HIP kernel, or the reference composition."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats=row_stats)
+    return _ref_xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale)
+
+
+def _ref_xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale):
+    """fp32 reference: LN(x) @ Wq^T from the folded form (== the unfolded LN +
+    projection), softmax attention over kv, out-projection, residual."""
+    xf = x.float()
+    mean = xf.mean(-1, keepdim=True)
+    rstd = torch.rsqrt(xf.var(-1, unbiased=False, keepdim=True) + eps)
+    q = rstd * (xf @ wq.float().t() - mean * colsum.float()) + bq.float()
+    b, s, c = x.shape
+    heads, d = kv.shape[3], kv.shape[4]
+    k, v = kv[:b, :, 0].float(), kv[:b, :, 1].float()  # [B, Skv, H, D]
+    qh = q.view(b, s, heads, d).transpose(1, 2)
+    att = torch.softmax((qh @ k.permute(0, 2, 3, 1)) * scale, -1)
+    o = (att @ v.transpose(1, 2)).transpose(1, 2).reshape(b, s, c)
+    y = o @ wo.float().t() + xf
+    if bo is not None:
+        y = y + bo.float()
+    return y.to(x.dtype)
+
+
 def cat_channels(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """torch.cat on the channel (last) dim that keeps fused GroupNorm
     statistics: they are per (row tile, channel), so the concatenated tensor's

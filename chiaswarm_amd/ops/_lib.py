@@ -31,7 +31,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 DEBUG = os.environ.get("CSK_DEBUG", "") not in ("", "0")
 LIB_PATH = os.environ.get("CSK_LIB_PATH") or os.path.join(LIB_DIR, "libcsk_debug.so" if DEBUG else "libcsk.so")
 # translation units that export csk_debug_read_<tu> / csk_debug_clear_<tu> in debug builds
-DEBUG_TUS = ("gemm", "gemm_glds", "gemm8p", "attention", "attention_wide")
+DEBUG_TUS = ("gemm", "gemm_glds", "gemm8p", "attention", "attention_wide", "xattn", "conv_halo")
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -171,6 +171,18 @@ def call(name: str, *args):
     err = fn(*args)
     if err != 0:
         raise RuntimeError(f"HIP kernel launcher {name} failed with hipError {err}")
+
+
+def call_int(name: str, *args) -> int:
+    """A library query that returns a value (not a hipError_t), e.g. a support check."""
+    fn = _BOUND.get(name)
+    if fn is None:
+        lib = load()
+        fn = getattr(lib, name)
+        fn.argtypes = _SIGS[name]
+        fn.restype = c_int
+        _BOUND[name] = fn
+    return int(fn(*args))
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

@@ -98,6 +98,8 @@ sig("csk_set_sw_odd", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
+sig("csk_xattn_block", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)
 sig("csk_dup2", c_void_p, c_void_p, c_int64, c_void_p)
@@ -611,4 +613,139 @@ def canny(img, low, high):
     a4, a1 = -(-(H * W * 4) // 256) * 256, -(-(H * W) // 256) * 256
     ws = torch.empty(256 + a4 + 2 * a1, dtype=torch.uint8, device=img.device)  # torch: 256 B-aligned
     _lib.call("csk_canny", _p(out), _p(img), H, W, C, float(low), float(high), _p(ws), _s())
+    return out
+
+
+XATTN_FUSED = os.environ.get("CSK_XATTN", "1") == "1"  # fused cross-attention sub-block (csrc/kernels/xattn.hip)
+XATTN_CHANNELS = (320,)
+
+
+def xattn_ok(x, kv, rows_per_b) -> bool:
+    """Shapes the fused cross-attention sub-block kernel takes: C = 320 (5 heads
+    of 64), <= 80 context tokens, whole 128-row tiles of one sample."""
+    C = x.shape[-1]
+    return (XATTN_FUSED and C in XATTN_CHANNELS and kv is not None and kv.dim() == 5 and kv.shape[2] == 2
+            and kv.shape[3] * kv.shape[4] == C and kv.shape[4] == 64 and 1 <= kv.shape[1] <= 80
+            and rows_per_b % 128 == 0 and x.numel() // C % rows_per_b == 0
+            and kv.shape[0] >= x.numel() // C // rows_per_b)
+
+
+def xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats=True):
+    """y = x + softmax((LN(x) Wq^T) scale K^T) V Wo^T + bo in ONE kernel
+    (LayerNorm folded into ``wq`` / ``colsum`` / ``bq``: ops.fold_layer_norm).
+    x: [B, S, C] bf16; kv: [Bc, Skv, 2, H, 64] (Attention.context_kv).  With
+    ``row_stats`` the output carries ``_csk_rows`` = (part, 1, C) for the next
+    fused LayerNorm."""
+    for t, n in ((x, "x"), (wq, "wq"), (bq, "bq"), (kv, "kv"), (wo, "wo")):
+        _bf16(t, "xattn_block." + n)
+    if bo is not None:
+        _bf16(bo, "xattn_block.bo")
+    C = x.shape[-1]
+    M = x.numel() // C
+    x2 = x.reshape(M, C)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    kv = kv.contiguous()
+    if colsum.dtype != torch.float32 or colsum.numel() != C:
+        raise ValueError("xattn_block: colsum must be fp32 [C]")
+    y = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+    rp = torch.empty(M * 2, dtype=torch.float32, device=x.device) if row_stats else None
+    _lib.call("csk_xattn_block", _p(y), _p(x2), _p(wq.contiguous()), _p(colsum.contiguous()), _p(bq.contiguous()),
+              _p(kv), _p(wo.contiguous()), _p(None if bo is None else bo.contiguous()), _p(rp), M, C, int(rows_per_b),
+              int(kv.shape[0]), int(kv.shape[1]), float(eps), float(scale), _s())
+    out = y.view(x.shape)
+    if rp is not None:
+        out._csk_rows = (rp, 1, C)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Halo-tiled 3x3 conv with the input GroupNorm(+SiLU) applied in its LDS halo
+# (csrc/kernels/conv_halo.hip): the ResNet norm -> conv pairs without the
+# GroupNorm apply pass.
+sig("csk_gn_finalize", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p)
+sig("csk_conv_halo_supported", c_int, c_int, c_int, c_int, c_int)
+sig("csk_conv_halo_gn_seg", c_int)
+sig("csk_conv_halo", c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+    c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+    c_int, c_void_p)
+CONV_HALO = os.environ.get("CSK_CONV_HALO", "1") == "1"
+HALO_STATS = [0, 0]  # [fused GroupNorm + conv calls, conv calls] (tests)
+
+
+def gn_finalize(x, groups, eps, x2=None):
+    """(mean, rstd) per (sample, group) [B, G, 2] fp32 of x (or of the channel
+    concat [x | x2]) from the producers' fused epilogue statistics
+    (``_csk_gn``); None if they are missing or incompatible."""
+    sa = getattr(x, "_csk_gn", None)
+    if sa is None:
+        return None
+    B, C1 = x.shape[0], x.shape[-1]
+    P = x.numel() // (B * C1)
+    part2, C = None, C1
+    seg = sa[1]
+    if x2 is not None:
+        sb = getattr(x2, "_csk_gn", None)
+        if sb is None or sb[1] != seg or x2.shape[:-1] != x.shape[:-1]:
+            return None
+        part2, C = sb[0], C1 + x2.shape[-1]
+    if C % groups or P % seg:
+        return None
+    stat = torch.empty((B, groups, 2), dtype=torch.float32, device=x.device)
+    _lib.call("csk_gn_finalize", _p(stat), _p(sa[0]), _p(part2), C1, seg, B, P, C, groups, float(eps), _s())
+    return stat
+
+
+def conv_halo_ok(x, wp, x2=None) -> bool:
+    if not CONV_HALO or x.dim() != 4:
+        return False
+    B, H, W, Ca = x.shape
+    Cin = Ca + (x2.shape[-1] if x2 is not None else 0)
+    return (wp.dim() == 4 and wp.shape[1:] == (3, 3, Cin) and (x2 is None or Ca % 64 == 0)
+            and _lib.call_int("csk_conv_halo_supported", B, H, W, Cin, wp.shape[0]) > 0)
+
+
+def conv_halo(x, wp, bias=None, bias2d=None, residual=None, gn=None, x2=None, act=None, out_scale=1.0,
+              gn_stats=True):
+    """3x3 / stride 1 / pad 1 NHWC conv of ``x`` (or of the concat [x | x2]),
+    optionally of GroupNorm(+SiLU)(input): ``gn = (stat, gamma, beta, groups,
+    silu)`` with ``stat`` from ``gn_finalize``.  ``gn_stats``: the output
+    carries ``_csk_gn`` statistics for the next GroupNorm."""
+    _bf16(x, "conv_halo.x")
+    _bf16(wp, "conv_halo.w")
+    x = x.contiguous()
+    B, H, W, Ca = x.shape
+    lda2 = 0
+    if x2 is not None:
+        _bf16(x2, "conv_halo.x2")
+        x2 = x2.contiguous()
+        lda2 = x2.shape[-1]
+    Cin = Ca + lda2
+    Cout = wp.shape[0]
+    out = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
+    b2s = 0
+    if bias2d is not None:
+        _bf16(bias2d, "conv_halo.bias2d")
+        if bias2d.stride(1) != 1 or bias2d.data_ptr() % 16 or bias2d.stride(0) % 8:
+            bias2d = bias2d.contiguous()
+        b2s = bias2d.stride(0) if B > 1 else Cout
+    if residual is not None:
+        _bf16(residual, "conv_halo.residual")
+        residual = residual.contiguous()
+    seg = _lib.call_int("csk_conv_halo_gn_seg", W) if gn_stats else 0
+    part = _gn_part(B * H * W, Cout, seg, x.device) if seg and (H * W) % seg == 0 else None
+    stat = gamma = beta = None
+    groups, silu = 1, 0
+    if gn is not None:
+        stat, gamma, beta, groups, silu = gn
+        _bf16(gamma, "conv_halo.gamma")
+        _bf16(beta, "conv_halo.beta")
+    HALO_STATS[1] += 1
+    HALO_STATS[0] += gn is not None
+    _lib.call("csk_conv_halo", _p(out), _p(x), Ca, _p(x2), lda2, Ca, _p(wp.contiguous()), _p(bias), _p(bias2d), b2s,
+              _p(residual), B, H, W, Cin, Cout, ACT[act], float(out_scale), _p(part), _p(stat),
+              _p(None if gamma is None else gamma.contiguous()), _p(None if beta is None else beta.contiguous()),
+              int(groups), int(bool(silu)), _s())
+    if part is not None:
+        out._csk_gn = (part, seg)
     return out

@@ -597,15 +597,16 @@ __device__ __forceinline__ int kv_off32(int row, int chunk) {
 // at the end.  Q pre-scaled, the QK^T chain starts from -max (PRE), lazy
 // rescale (T13, threshold 2^8), same 3-buffer register-staged K/V ring and
 // one-barrier-per-block software pipeline (QK^T of block kb+1 issued before
-// the softmax of block kb) as attn_fwd_pipe_kernel.  Two VALU loads moved
-// onto the (under-used) matrix cores: the row sum is an all-ones O^T tile of
-// the PV chain, and the -mu offset one MFMA from an inline-zero accumulator.
+// the softmax of block kb) as attn_fwd_pipe_kernel.
 // QB: 32-query tiles per wave (QB = 2, 256 rows per workgroup at one wave per
 // SIMD, was 1.6x slower and spills; only QB = 1 is instantiated).
 // PROBE (profiling builds, wrong results by design; variants 31/32/34/38):
 // 1 = no exp, 2 = no K/V global loads past the first two blocks, 4 = no PV
 // MFMAs, 8 = no QK^T MFMAs
-template <int QB, int PROBE = 0>
+// TRICKS (A/B, csk_set_attn32(1 + TRICKS)): 1 = the -mu offset as one MFMA from
+// a zero accumulator instead of 32 register moves per block; 2 = the row sum
+// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block
+template <int QB, int PROBE = 0, int TRICKS = 0>
 __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
   constexpr int DP = 64, CPR = DP / 8, KB = 64;
   constexpr int QROWS = QB * 32 * 4;
@@ -656,10 +657,11 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     for (int qt = 0; qt < QB; ++qt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][qt][i] = 0.f;
-  float mrow[QB];  // running max (log2 units)
+  float mrow[QB], lrow[QB];  // running max (log2 units); this lane's partial row sum (TRICKS & 2: osum)
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
     mrow[qt] = -1e30f;
+    lrow[qt] = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) osum[qt][i] = 0.f;
   }
@@ -718,16 +720,27 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt) {
       const float m = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
-      const bf16_t hi = f2bf(m);
-      const bf16_t lo = f2bf(m - bf2f(hi));
-      mu[qt] = bf2f(hi) + bf2f(lo);  // the value the MFMA subtracts, exactly
-      qmu[qt] = hh == 0 ? v8s{(short)(hi ^ 0x8000), (short)(lo ^ 0x8000), 0, 0, 0, 0, 0, 0}
-                        : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr ((TRICKS & 1) != 0) {
+        const bf16_t hi = f2bf(m);
+        const bf16_t lo = f2bf(m - bf2f(hi));
+        mu[qt] = bf2f(hi) + bf2f(lo);  // the value the MFMA subtracts, exactly
+        qmu[qt] = hh == 0 ? v8s{(short)(hi ^ 0x8000), (short)(lo ^ 0x8000), 0, 0, 0, 0, 0, 0}
+                          : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      } else {
+        mu[qt] = m;
+      }
     }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int qt = 0; qt < QB; ++qt) s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kmu, qmu[qt], zero16, 0, 0, 0);
+      for (int qt = 0; qt < QB; ++qt) {
+        if constexpr ((TRICKS & 1) != 0) {
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kmu, qmu[qt], zero16, 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
+        }
+      }
 #pragma unroll
       for (int ds = 0; ds < ((PROBE & 8) ? 0 : 4); ++ds) {
         const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off32(kt * 32 + r, 2 * ds + hh));
@@ -780,7 +793,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         const float mnew = fmaxf(mrow[qt], mb);
         const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
         mrow[qt] = mnew;
-        osum[qt] *= alpha;
+        lrow[qt] *= alpha;
+        if constexpr ((TRICKS & 2) != 0) osum[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) oacc[dt][qt] *= alpha;
       }
@@ -796,6 +810,18 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
+      }
+      if constexpr ((TRICKS & 2) == 0) {
+        // 4 independent single-instruction add chains (no v_pk_add_f32 beside MFMAs)
+        float l4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          l4[c] = vadd(sc[0][qt][c], sc[0][qt][c + 4]);
+          l4[c] = vadd(l4[c], vadd(sc[0][qt][c + 8], sc[0][qt][c + 12]));
+          l4[c] = vadd(l4[c], vadd(sc[1][qt][c], sc[1][qt][c + 4]));
+          l4[c] = vadd(l4[c], vadd(sc[1][qt][c + 8], sc[1][qt][c + 12]));
+        }
+        lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
       }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -831,7 +857,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
               asm volatile("" ::"v"(vf), "v"(pf[kt][st][qt]));
             } else {
               oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
-              if (dt == 1)  // the row-sum tile of this k-step
+              if ((TRICKS & 2) != 0 && dt == 1)  // the row-sum tile of this k-step
                 osum[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones8, pf[kt][st][qt], osum[qt], 0, 0, 0);
             }
           }
@@ -849,7 +875,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     const size_t rows = (size_t)a.B * a.H * a.Sq;
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt) {
-      const float l = osum[qt][0];
+      float l = osum[qt][0];
+      if constexpr ((TRICKS & 2) == 0) l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
       const int qi = q0 + qt * 32 + r;
       if (qi >= a.Sq) continue;
       const size_t row = (size_t)ks * rows + (size_t)bh * a.Sq + qi;
@@ -868,7 +895,8 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   bf16_t* op = a.o + b * a.sob + h * a.soh;
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
-    const float l = osum[qt][0];
+    float l = osum[qt][0];
+    if constexpr ((TRICKS & 2) == 0) l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
     const float inv = l > 0.f ? 1.0f / l : 0.f;
     const int qi = q0 + qt * 32 + r;
     if (qi >= a.Sq) continue;
@@ -1144,7 +1172,13 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
       return (int)hipGetLastError();
     }
     if (variant == 20) {  // 32x32x16 MFMA kernel, 128 query rows per workgroup
-      attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128)), 256, 0, stream>>>(a);
+      const dim3 g32(B * H * ((Sq + 127) / 128));
+      switch (g_attn32) {
+        case 2: attn32_kernel<1, 0, 1><<<g32, 256, 0, stream>>>(a); break;
+        case 3: attn32_kernel<1, 0, 2><<<g32, 256, 0, stream>>>(a); break;
+        case 4: attn32_kernel<1, 0, 3><<<g32, 256, 0, stream>>>(a); break;
+        default: attn32_kernel<1><<<g32, 256, 0, stream>>>(a); break;
+      }
       return (int)hipGetLastError();
     }
     if (variant >= 2 || (variant == 0 && Skv > 128)) {

@@ -23,11 +23,13 @@ def main():
     ap.add_argument("--shape", default="8,4096,4096,5,64")
     ap.add_argument("--short-kv", type=int, default=-1, help="Skv <= 128 kernel: 1 plain, 2 pipelined, 3 K/V-resident")
     ap.add_argument("--kv-rows", type=int, default=0, help="K/V-resident kernel rows per workgroup (0 auto)")
+    ap.add_argument("--attn32", type=int, default=1, help="csk_set_attn32 value (0 off, 1 default, 2-4 TRICKS A/B)")
     a = ap.parse_args()
     _lib.load()
     if a.short_kv >= 0:
         _lib.call("csk_set_short_kv_variant", a.short_kv)
     _lib.call("csk_set_short_kv_rows", a.kv_rows)
+    _lib.call("csk_set_attn32", a.attn32)
     B, Sq, Skv, H, D = map(int, a.shape.split(","))
     q, k, v = (torch.randn(B, s, H, D, device="cuda").bfloat16() for s in (Sq, Skv, Skv))
     hip_ops.ATTN_VARIANT = a.variant
@@ -41,7 +43,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"variant {a.variant} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: {ms * 1000:.1f} us  "
+    print(f"attn32 {a.attn32} variant {a.variant} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: {ms * 1000:.1f} us  "
           f"{4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")
 
 
