@@ -669,7 +669,14 @@ sig("csk_conv_halo_gn_seg", c_int)
 sig("csk_conv_halo", c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
     c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
     c_int, c_void_p)
-CONV_HALO = os.environ.get("CSK_CONV_HALO", "1") == "1"
+# Off by default: measured slower than the tuned implicit-GEMM conv + GroupNorm
+# apply on every UNet shape (profiles/halobench_r6f.txt: 64x64 320->320 at CFG
+# batch 8: halo 132 us / halo+GN 187 us vs conv 77.5 us + apply 20 us) — one
+# workgroup per CU with four waves has no second workgroup to hide the
+# per-step barrier and LDS latency, and the in-LDS GroupNorm transform
+# (2.1x halo x 2 column tiles of the elements, SiLU's two transcendentals)
+# is not overlapped with the matrix cores.  CSK_CONV_HALO=1 enables it.
+CONV_HALO = os.environ.get("CSK_CONV_HALO", "0") == "1"
 HALO_STATS = [0, 0]  # [fused GroupNorm + conv calls, conv calls] (tests)
 
 

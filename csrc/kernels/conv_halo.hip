@@ -22,8 +22,10 @@
 // Pipeline (one workgroup per CU, 4 waves, wave tile BM/2 x BN/2 on
 // v_mfma_f32_16x16x32_bf16, B·A order so the row-layout epilogue of
 // gemm_common.h applies): the A halo is double-buffered (chunk c + 1 lands
-// during chunk c's nine taps), the weights run through a 2-stage LDS-DMA ring
-// over the (chunk, tap) steps with one raw barrier per step.  The input may be
+// during chunk c's nine taps), the weights run through a 4-stage LDS-DMA ring
+// over the (chunk, tap) steps (three steps in flight: one workgroup per CU has
+// no second workgroup to cover a load wait) with one raw barrier per step and
+// exact counted vmcnt waits.  The input may be
 // the channel concat [a | a2] of two tensors read in place (UNet skip
 // connections), split at a multiple of 64 channels.
 #include "gemm_common.h"
@@ -39,9 +41,13 @@ struct HaloArgs {
   const bf16_t* a2_end;   // CSK_DEBUG bounds
 };
 
+// s_waitcnt vmcnt(N) as the builtin (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
+// expcnt / lgkmcnt at their no-wait maxima): unlike inline asm the compiler's
+// wait insertion sees it and knows which LDS-DMAs it retired
 template <int N>
 __device__ __forceinline__ void halo_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 __device__ __forceinline__ void halo_dma(const bf16_t* src, bf16_t* dst) {
@@ -61,9 +67,10 @@ struct HaloGeom {
   static constexpr int B_ELEMS = BN * 64;
   static constexpr int PIECES_A = HPP / 8 / 4;        // DMA pieces per wave per chunk
   static constexpr int PIECES_B = BN / 8 / 4;
-  static constexpr int MAIN = 2 * A_ELEMS + 2 * B_ELEMS;
+  static constexpr int NB = 4;                        // weight ring stages (NB - 1 steps in flight)
+  static constexpr int CMAX = IW == 64 ? 960 : (IW == 32 ? 1920 : 2560);  // largest Cin (UNet up blocks)
   static constexpr int EPI = epi_smem_elems<BM, BN, epi_passes<BM, BN, 2>()>();
-  static constexpr int SMEM = MAIN > EPI ? MAIN : EPI;
+  static_assert(EPI <= 2 * A_ELEMS, "the epilogue stages through the halo buffers");
   static_assert(BM % IW == 0 && BN % 32 == 0, "tile");
 };
 
@@ -72,8 +79,17 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
   using Gm = HaloGeom<BM, BN, IW>;
   constexpr int WM = 2, WN = 2, WTM = BM / WM, WTN = BN / WN, MT = WTM / 16, NT = WTN / 16;
   constexpr int EP = epi_passes<BM, BN, WM>();
-  __shared__ __attribute__((aligned(16))) bf16_t smem[Gm::SMEM];
-  __shared__ float s_aff[2][2][64];  // [chunk parity][scale | shift][channel]
+  constexpr int NB = Gm::NB;
+  static_assert(NB == 4, "wait counts below assume two younger weight steps");
+  // separate LDS objects for the halo buffers and the weight ring: the
+  // compiler's wait insertion then tells a weight DMA in flight from the
+  // transform's halo writes (one array made it drain every DMA there)
+  __shared__ __attribute__((aligned(16))) bf16_t s_ah[2 * Gm::A_ELEMS];
+  __shared__ __attribute__((aligned(16))) bf16_t s_bw[NB * Gm::B_ELEMS];
+  // GroupNorm operands staged once in the prologue (no global loads inside the
+  // main loop: any would make the compiler drain the DMAs in flight before it)
+  __shared__ float s_stat[2 * 64];                                      // (mean, rstd) per group, G <= 64
+  __shared__ __attribute__((aligned(16))) bf16_t s_gb[2 * Gm::CMAX];    // gamma | beta
   const GemmArgs& a = ha.g;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -104,7 +120,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
     const int ld = second ? ha.lda2 : a.lda;
     const int ch = second ? 64 * c - ha.Ca : 64 * c;
     const int lr = fresh(lrow);
-    bf16_t* dst = smem + (c & 1) * Gm::A_ELEMS;
+    bf16_t* dst = s_ah + (c & 1) * Gm::A_ELEMS;
 #pragma unroll
     for (int i = 0; i < Gm::PIECES_A; ++i) {
       const int p = wid * Gm::PIECES_A + i;
@@ -125,7 +141,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
     const int c = s / 9, tap = s - 9 * c;
     const int koff = tap * Cin + 64 * c;
     const int lr = fresh(lrow);
-    bf16_t* dst = smem + 2 * Gm::A_ELEMS + (s & 1) * Gm::B_ELEMS;
+    bf16_t* dst = s_bw + (s % Gm::NB) * Gm::B_ELEMS;
 #pragma unroll
     for (int i = 0; i < Gm::PIECES_B; ++i) {
       const int n = n0 + (wid * Gm::PIECES_B + i) * 8 + lr;
@@ -134,34 +150,27 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
       halo_dma(src, dst + 512 * (wid * Gm::PIECES_B + i));
     }
   };
-  // ---- GroupNorm affine of chunk c's 64 channels (scale, shift) -> s_aff[c & 1] ----
-  auto fill_aff = [&](int c) {
-    if (tid < 64) {
-      const int ch = 64 * c + tid;
-      const int cg = Cin / ha.G;
-      const float2 st = *reinterpret_cast<const float2*>(ha.gn_stat + ((size_t)b * ha.G + ch / cg) * 2);
-      const float sc = bf2f(ha.gamma[ch]) * st.y;
-      s_aff[c & 1][0][tid] = sc;
-      s_aff[c & 1][1][tid] = bf2f(ha.beta[ch]) - st.x * sc;
-    }
-  };
   // ---- normalise (+ SiLU) the landed halo of chunk c in place ----
   auto transform = [&](int c) {
-    bf16_t* as = smem + (c & 1) * Gm::A_ELEMS;
-    const float* sc = s_aff[c & 1][0];
-    const float* sh = s_aff[c & 1][1];
+    bf16_t* as = s_ah + (c & 1) * Gm::A_ELEMS;
+    const int cg = Cin / ha.G;
     for (int e = tid; e < Gm::HP * 8; e += 256) {
       const int hp = e >> 3, phys = e & 7;
       const int hr = hp / Gm::HW, hc = hp - hr * Gm::HW;
       const int y = y0 - 1 + hr, x = hc - 1;
       if (y < 0 || y >= H || x < 0 || x >= IW) continue;  // padding stays zero
-      const int lc = phys ^ (hp & 7);
+      const int ch0 = 64 * c + 8 * (phys ^ (hp & 7));
+      float gm[8], bt[8];
+      unpack8(*reinterpret_cast<const uint4*>(s_gb + ch0), gm);
+      unpack8(*reinterpret_cast<const uint4*>(s_gb + Gm::CMAX + ch0), bt);
       uint4* q = reinterpret_cast<uint4*>(as + hp * 64 + phys * 8);
       float f[8];
       unpack8(*q, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float v = __builtin_fmaf(f[j], sc[lc * 8 + j], sh[lc * 8 + j]);
+        const int g = (ch0 + j) / cg;
+        const float sc = gm[j] * s_stat[2 * g + 1];
+        const float v = __builtin_fmaf(f[j] - s_stat[2 * g], sc, bt[j]);
         f[j] = ha.silu ? silu_f(v) : v;
       }
       *q = pack8(f);
@@ -182,53 +191,70 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk 0's halo, step 0's weights, chunk 0's affine
+  // prologue: chunk 0's halo, the first NB - 1 steps' weights, chunk 0's affine
   issue_a(0);
-  issue_b(0);
-  if (gn) fill_aff(0);
-
-  for (int c = 0; c < nch; ++c) {
-    const bf16_t* as = smem + (c & 1) * Gm::A_ELEMS;
-    // A(c) and B(9c) landed: both were issued before anything still in flight
-    halo_vmcnt<0>();
-    __syncthreads();
-    if (gn) {
-      transform(c);
-      if (c + 1 < nch) fill_aff(c + 1);
-      __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s)
+    if (s < steps) issue_b(s);
+  if (gn) {
+    for (int i = tid; i < 2 * ha.G; i += 256) s_stat[i] = ha.gn_stat[(size_t)b * ha.G * 2 + i];
+    for (int i = tid; i < Cin; i += 256) {
+      s_gb[i] = ha.gamma[i];
+      s_gb[Gm::CMAX + i] = ha.beta[i];
     }
-    for (int tap = 0; tap < 9; ++tap) {
-      const int s = 9 * c + tap;
-      if (tap > 0) {
-        // B(s) landed.  Loads retire in order: at tap 1 the next chunk's halo
-        // (issued after B(s)) may stay in flight; from tap 2 on it has landed
-        // too — two taps of MFMAs to hide it
-        if (tap == 1 && c + 1 < nch) halo_vmcnt<Gm::PIECES_A>();
-        else halo_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
+  }
+
+  for (int s = 0; s < steps; ++s) {
+    const int c = s / 9, tap = s - 9 * c;
+    // B(s) (and at a chunk's first tap its halo A(c)) landed.  Loads retire in
+    // issue order, so the count of younger ones is exact: B(s+1), B(s+2) and,
+    // for the three steps after a chunk start, A(c+1) (issued after B(9c+3))
+    const int y2 = min(NB - 2, steps - 1 - s);
+    const bool ya = tap >= 1 && tap <= NB - 1 && c + 1 < nch;
+    if (tap == 0) {
+      // a chunk's first step: at least 8 more steps follow, so exactly
+      // B(s+1), B(s+2) are younger; this branch's own wait tells the compiler
+      // the halo DMA retired before the transform touches that buffer
+      halo_vmcnt<2 * Gm::PIECES_B>();
+      __builtin_amdgcn_s_barrier();
+      if (gn) {
+        transform(c);
+        __syncthreads();
       }
-      if (s + 1 < steps) issue_b(s + 1);  // into the stage step s - 1 used
-      // the next chunk's halo (its buffer's last readers, chunk c - 1's taps,
-      // finished before this chunk's first barrier)
-      if (tap == 0 && c + 1 < nch) issue_a(c + 1);
-      const bf16_t* bs = smem + 2 * Gm::A_ELEMS + (s & 1) * Gm::B_ELEMS;
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      const int toff = ky * Gm::HW + kx;
+    } else {
+      if (ya) {
+        if (y2 == 2) halo_vmcnt<2 * Gm::PIECES_B + Gm::PIECES_A>();
+        else if (y2 == 1) halo_vmcnt<Gm::PIECES_B + Gm::PIECES_A>();
+        else halo_vmcnt<Gm::PIECES_A>();
+      } else {
+        if (y2 == 2) halo_vmcnt<2 * Gm::PIECES_B>();
+        else if (y2 == 1) halo_vmcnt<Gm::PIECES_B>();
+        else halo_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    // B(s + NB - 1) into the stage step s - 1 used; at a chunk start the next
+    // chunk's halo into the buffer chunk c - 1 used (both free past the barrier)
+    if (s + NB - 1 < steps) issue_b(s + NB - 1);
+    if (tap == 0 && c + 1 < nch) issue_a(c + 1);
+    const bf16_t* as = s_ah + (c & 1) * Gm::A_ELEMS;
+    const bf16_t* bs = s_bw + (s % NB) * Gm::B_ELEMS;
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const int toff = ky * Gm::HW + kx;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        v8s af[MT], bfr[NT];
+    for (int ks = 0; ks < 2; ++ks) {
+      v8s af[MT], bfr[NT];
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-          af[i] = *reinterpret_cast<const v8s*>(as + halo_off(hbase[i] + toff, ks * 4 + fq));
+      for (int i = 0; i < MT; ++i)
+        af[i] = *reinterpret_cast<const v8s*>(as + halo_off(hbase[i] + toff, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          bfr[j] = *reinterpret_cast<const v8s*>(bs + swz(wn * WTN + j * 16 + fr, ks * 4 + fq));
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();
@@ -236,7 +262,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo_kernel(const HaloArgs ha) {
   float2 lnlane[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) lnlane[i] = make_float2(0.f, 1.f);
-  gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true>(a, acc, smem, m0, n0, 0, lnrow, lnlane, false);
+  gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true>(a, acc, s_ah, m0, n0, 0, lnrow, lnlane, false);
 }
 
 CSK_DEBUG_EXPORT(conv_halo)
@@ -255,9 +281,11 @@ static int launch_halo(HaloArgs ha, hipStream_t s) {
 // tile at W = 64 spills: 160 accumulators + 8 A fragments per lane).
 static int halo_bm(int W) { return (W == 64 || W == 32 || W == 16) ? 128 : 0; }
 
+static int halo_cmax(int W) { return W == 64 ? 960 : (W == 32 ? 1920 : 2560); }
+
 CSK_API int csk_conv_halo_supported(int B, int H, int W, int Cin, int Cout) {
   const int bm = halo_bm(W);
-  return bm && Cin % 64 == 0 && Cout % 160 == 0 && (H * W) % bm == 0 && B > 0 ? bm : 0;
+  return bm && Cin % 64 == 0 && Cin <= halo_cmax(W) && Cout % 160 == 0 && (H * W) % bm == 0 && B > 0 ? bm : 0;
 }
 
 // y = conv3x3(act(GN(x)))  [+ bias + bias2d, act, * out_scale, + residual], NHWC.
@@ -270,7 +298,8 @@ CSK_API int csk_conv_halo(void* y, const void* x, int lda, const void* x2, int l
                           int Cin, int Cout, int act, float out_scale, void* gn_part, const void* gn_stat,
                           const void* gamma, const void* beta, int G, int silu, hipStream_t stream) {
   const int bm = csk_conv_halo_supported(B, H, W, Cin, Cout);
-  if (!bm || !csk_zero_ptr() || (x2 && (Ca % 64 || Ca >= Cin)) || (gn_stat && (!gamma || !beta || Cin % G)))
+  if (!bm || !csk_zero_ptr() || (x2 && (Ca % 64 || Ca >= Cin)) ||
+      (gn_stat && (!gamma || !beta || Cin % G || G > 64 || Cin > halo_cmax(W))))
     return (int)hipErrorInvalidValue;
   HaloArgs ha{};
   GemmArgs& a = ha.g;

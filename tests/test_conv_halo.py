@@ -15,6 +15,15 @@ from chiaswarm_amd import ops
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _halo_on(monkeypatch):
+    """The path is off by default (measured slower, ops/hip_ops.py CONV_HALO):
+    the numerics tests switch it on."""
+    from chiaswarm_amd.ops import hip_ops
+
+    monkeypatch.setattr(hip_ops, "CONV_HALO", True)
+
+
 def rel(a, b):
     a, b = a.float(), b.float()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
