@@ -756,3 +756,4 @@ def conv_halo(x, wp, bias=None, bias2d=None, residual=None, gn=None, x2=None, ac
     if part is not None:
         out._csk_gn = (part, seg)
     return out
+sig("csk_set_xattn_probe", c_int)

@@ -92,7 +92,10 @@ __device__ __forceinline__ v8s xa_pack8(const v4f& lo, const v4f& hi, float s) {
   return __builtin_bit_cast(v8s, u);
 }
 
-template <int C>
+// PROBE (profiling builds, wrong results by design; csk_set_xattn_probe): 1 = no
+// Q-projection MFMAs, 2 = no attention (S / softmax / PV), 4 = no out-projection
+// MFMAs, 8 = no per-head DMA (operands of head 0 reused)
+template <int C, int PROBE = 0>
 __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) {
   constexpr int H = C / 64, NCS = C / 32, NNT = C / 16, CPR = C / 8;
   constexpr int WQ = 64 * C, WO = C * 64, KVI = XA_KVR * 64;
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     const bool more = h + 1 < H;
     // K / V of the next head into the other buffer (its last reader, the
     // attention of head h - 1, finished before barrier B2 of that head)
-    if (more) {
+    if (more && (PROBE & 8) == 0) {
       if (cur) dma_kv(h + 1, s_kv0);
       else dma_kv(h + 1, s_kv1);
     }
@@ -247,14 +250,16 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          qa[rt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cs & 1][dt], xf[rt][cs], qa[rt][dt], 0, 0, 0);
+        for (int dt = 0; dt < 4; ++dt) {
+          if constexpr ((PROBE & 1) != 0) asm volatile("" ::"v"(wf[cs & 1][dt]), "v"(xf[rt][cs]));
+          else qa[rt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cs & 1][dt], xf[rt][cs], qa[rt][dt], 0, 0, 0);
+        }
       asm volatile("" ::: "memory");
     }
     // B1: every wave is done with Wq_h -> the next head's rows may land there
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (more) dma_wq(h + 1);
+    if (more && (PROBE & 8) == 0) dma_wq(h + 1);
 
     // q = (rstd (acc - mean colsum) + bq) * scale * log2(e), as S^T B fragments
     v8s qf[2][2];
@@ -335,10 +340,14 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
       of[rt][1] = xa_pack8(o[2], o[3], inv);
     }
     };
-    if (cur) attend(s_kv1);
-    else attend(s_kv0);
+    if constexpr ((PROBE & 2) != 0) {
+      of[0][0] = qf[0][0]; of[0][1] = qf[0][1]; of[1][0] = qf[1][0]; of[1][1] = qf[1][1];
+    } else {
+      if (cur) attend(s_kv1);
+      else attend(s_kv0);
+    }
     // B2: Wo_h has landed (newer in flight: K/V_{h+1}, Wq_{h+1})
-    if (more) xa_vmcnt<NKV + NWQ>();
+    if (more && (PROBE & 8) == 0) xa_vmcnt<NKV + NWQ>();
     else xa_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
 
@@ -355,15 +364,17 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds)
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-          out[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wof[nt & 1][ds], of[rt][ds], out[rt][nt], 0, 0, 0);
+        for (int rt = 0; rt < 2; ++rt) {
+          if constexpr ((PROBE & 4) != 0) asm volatile("" ::"v"(wof[nt & 1][ds]), "v"(of[rt][ds]));
+          else out[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wof[nt & 1][ds], of[rt][ds], out[rt][nt], 0, 0, 0);
+        }
       asm volatile("" ::: "memory");
     }
     // B3: everyone is done with Wo_h and K/V_h; Wq_{h+1} and K/V_{h+1} landed
     xa_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (more) dma_wo(h + 1);
+    if (more && (PROBE & 8) == 0) dma_wo(h + 1);
   }
 
   // ---------------- epilogue: + bias + residual, row statistics ----------------
@@ -418,6 +429,12 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 
 CSK_DEBUG_EXPORT(xattn)
 
+static int g_xattn_probe = 0;
+CSK_API int csk_set_xattn_probe(int p) {
+  g_xattn_probe = p;
+  return 0;
+}
+
 const bf16_t* csk_zero_ptr();
 
 // x, wq, wo: [M][C] / [C][C] bf16; colsum fp32 [C]; bq / bo bf16 [C];
@@ -449,7 +466,16 @@ CSK_API int csk_xattn_block(void* y, const void* x, const void* wq, const void* 
   a.scale_log2 = scale * 1.4426950408889634f;
   const dim3 grid((M + XA_BM - 1) / XA_BM);
   switch (C) {
-    case 320: xattn_block_kernel<320><<<grid, 256, 0, stream>>>(a); break;
+    case 320:
+      switch (g_xattn_probe) {
+        case 1: xattn_block_kernel<320, 1><<<grid, 256, 0, stream>>>(a); break;
+        case 2: xattn_block_kernel<320, 2><<<grid, 256, 0, stream>>>(a); break;
+        case 4: xattn_block_kernel<320, 4><<<grid, 256, 0, stream>>>(a); break;
+        case 8: xattn_block_kernel<320, 8><<<grid, 256, 0, stream>>>(a); break;
+        case 15: xattn_block_kernel<320, 15><<<grid, 256, 0, stream>>>(a); break;
+        default: xattn_block_kernel<320><<<grid, 256, 0, stream>>>(a); break;
+      }
+      break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
