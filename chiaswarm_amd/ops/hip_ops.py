@@ -618,6 +618,9 @@ def canny(img, low, high):
 
 XATTN_FUSED = os.environ.get("CSK_XATTN", "1") == "1"  # fused cross-attention sub-block (csrc/kernels/xattn.hip)
 XATTN_CHANNELS = (320,)
+# workgroup shape of the fused kernel: 4 waves x 32 rows or 8 waves x 16 rows (csk_set_xattn_waves)
+XATTN_WAVES = int(os.environ.get("CSK_XATTN_WAVES", "8"))  # 8: 40 vs 50 us, profiles/xattnbench_waves_r6h.txt
+_xattn_waves_applied = [None]
 
 
 def xattn_ok(x, kv, rows_per_b) -> bool:
@@ -650,6 +653,9 @@ def xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats
         raise ValueError("xattn_block: colsum must be fp32 [C]")
     y = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
     rp = torch.empty(M * 2, dtype=torch.float32, device=x.device) if row_stats else None
+    if _xattn_waves_applied[0] != XATTN_WAVES:
+        _lib.call("csk_set_xattn_waves", int(XATTN_WAVES))
+        _xattn_waves_applied[0] = XATTN_WAVES
     _lib.call("csk_xattn_block", _p(y), _p(x2), _p(wq.contiguous()), _p(colsum.contiguous()), _p(bq.contiguous()),
               _p(kv), _p(wo.contiguous()), _p(None if bo is None else bo.contiguous()), _p(rp), M, C, int(rows_per_b),
               int(kv.shape[0]), int(kv.shape[1]), float(eps), float(scale), _s())
@@ -756,4 +762,7 @@ def conv_halo(x, wp, bias=None, bias2d=None, residual=None, gn=None, x2=None, ac
     if part is not None:
         out._csk_gn = (part, seg)
     return out
+
+
 sig("csk_set_xattn_probe", c_int)
+sig("csk_set_xattn_waves", c_int)

@@ -11,8 +11,9 @@
 // the next LayerNorm's consumer GEMM (ln_nparts = 1).
 //
 // Shape: C = 64 H (head dim 64), Skv <= 80 context tokens (77 CLIP tokens).
-// Workgroup = 4 waves = 128 rows of one sample; every wave owns 32 rows (two
-// 16-row tiles) end to end, so no intermediate crosses a lane or a wave:
+// Workgroup = 128 rows of one sample: 4 waves x 32 rows (two 16-row tiles) or
+// 8 waves x 16 rows (csk_set_xattn_waves); every wave owns its rows end to end,
+// so no intermediate crosses a lane or a wave:
 //   * x rows live in registers as MFMA B fragments (lane: row fr, channels
 //     32 cs + 8 g ..+7); the LayerNorm statistics are reduced from them;
 //   * Q^T = Wq' x^T (A = Wq' rows from LDS) puts row fr and head-dims
@@ -95,13 +96,14 @@ __device__ __forceinline__ v8s xa_pack8(const v4f& lo, const v4f& hi, float s) {
 // PROBE (profiling builds, wrong results by design; csk_set_xattn_probe): 1 = no
 // Q-projection MFMAs, 2 = no attention (S / softmax / PV), 4 = no out-projection
 // MFMAs, 8 = no per-head DMA (operands of head 0 reused)
-template <int C, int PROBE = 0>
-__global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) {
+template <int C, int NW, int RT, int PROBE = 0>
+__global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs a) {
   constexpr int H = C / 64, NCS = C / 32, NNT = C / 16, CPR = C / 8;
   constexpr int WQ = 64 * C, WO = C * 64, KVI = XA_KVR * 64;
   constexpr int WQ_PIECES = WQ / 512, WO_PIECES = WO / 512, KV_PIECES = 2 * KVI / 512;
-  static_assert(WQ_PIECES % 4 == 0 && WO_PIECES % 4 == 0 && KV_PIECES % 4 == 0, "pieces per wave");
-  constexpr int NWQ = WQ_PIECES / 4, NWO = WO_PIECES / 4, NKV = KV_PIECES / 4;
+  static_assert(WQ_PIECES % NW == 0 && WO_PIECES % NW == 0 && KV_PIECES % NW == 0, "pieces per wave");
+  static_assert(NW * RT * 16 == XA_BM, "workgroup rows");
+  constexpr int NWQ = WQ_PIECES / NW, NWO = WO_PIECES / NW, NKV = KV_PIECES / NW;
   // separate LDS objects: the compiler's wait insertion can then tell an
   // LDS-DMA into one buffer from reads of another (one array made it drain
   // every DMA in flight before the first LDS read after an issue)
@@ -117,13 +119,13 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * XA_BM;
   const int b = m0 / a.rows_per_b;
   const int Skv = a.Skv;
-  const int row_w = m0 + wid * 32;  // this wave's first row
+  const int row_w = m0 + wid * (RT * 16);  // this wave's first row
 
   // ---- LDS-DMA issue helpers (every wave issues the same counts) ----
   auto dma_wq = [&](int h) {
 #pragma unroll
     for (int i = 0; i < NWQ; ++i) {
-      const int p = wid + 4 * i;
+      const int p = wid + NW * i;
       const int f = 64 * p + lane, row = f / CPR, slot = f % CPR;
       CSK_DCHECK(h * 64 + row < C, 71, row, C);
       xa_dma_off(a.wq, (unsigned)((h * 64 + row) * C + 8 * (slot ^ (row & 7))), s_wq + 512 * p);
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
   auto dma_wo = [&](int h) {
 #pragma unroll
     for (int i = 0; i < NWO; ++i) {
-      const int p = wid + 4 * i;
+      const int p = wid + NW * i;
       const int row = 8 * p + (lane >> 3), slot = lane & 7;
       CSK_DCHECK(row < C, 72, row, C);
       xa_dma_off(a.wo, (unsigned)(row * C + h * 64 + 8 * (slot ^ (row & 7))), s_wo + 512 * p);
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
   auto dma_kv = [&](int h, bf16_t* dst) {
 #pragma unroll
     for (int i = 0; i < NKV; ++i) {
-      const int p = wid + 4 * i;  // pieces 0..11: K rows, 12..23: V rows
+      const int p = wid + NW * i;  // pieces 0..11: K rows, 12..23: V rows
       const int which = p >= KV_PIECES / 2;
       const int row = 8 * (p - which * (KV_PIECES / 2)) + (lane >> 3), slot = lane & 7;
       // rows past Skv repeat the last key: finite values whose scores are
@@ -154,16 +156,16 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
   };
 
   // ---- prologue: head 0 operands in flight while the x rows load ----
-  for (int i = tid; i < C; i += 256) {
+  for (int i = tid; i < C; i += NW * 64) {
     s_cb[i] = a.colsum[i];
     s_cb[C + i] = bf2f(a.bq[i]);
   }
   dma_wq(0);
   dma_wo(0);
   dma_kv(0, s_kv0);
-  v8s xf[2][NCS];
+  v8s xf[RT][NCS];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+  for (int rt = 0; rt < RT; ++rt) {
     const int m = row_w + rt * 16 + fr;
 #pragma unroll
     for (int cs = 0; cs < NCS; ++cs) {
@@ -176,9 +178,9 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     }
   }
   // LayerNorm statistics of the two rows this lane holds (four lane groups x NCS x 8)
-  float mean[2], rstd[2];
+  float mean[RT], rstd[RT];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+  for (int rt = 0; rt < RT; ++rt) {
     float s = 0.f;
 #pragma unroll
     for (int cs = 0; cs < NCS; ++cs) {
@@ -206,9 +208,9 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     rstd[rt] = rsqrtf(q * (1.0f / C) + a.eps);
   }
 
-  v4f out[2][NNT];
+  v4f out[RT][NNT];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int nt = 0; nt < NNT; ++nt) out[rt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
 
@@ -228,9 +230,9 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     }
 
     // ---------------- Q projection (LayerNorm folded) ----------------
-    v4f qa[2][4];
+    v4f qa[RT][4];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) qa[rt][dt] = v4f{0.f, 0.f, 0.f, 0.f};
     // one k-step of Wq' fragments in flight ahead of the MFMAs (the fences keep
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     for (int cs = 0; cs < NCS; ++cs) {
       if (cs + 1 < NCS) ld_wq(cs + 1, wf[(cs + 1) & 1]);
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           if constexpr ((PROBE & 1) != 0) asm volatile("" ::"v"(wf[cs & 1][dt]), "v"(xf[rt][cs]));
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     if (more && (PROBE & 8) == 0) dma_wq(h + 1);
 
     // q = (rstd (acc - mean colsum) + bq) * scale * log2(e), as S^T B fragments
-    v8s qf[2][2];
+    v8s qf[RT][2];
     {
       v4f cw[4], bw[4];
 #pragma unroll
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
         bw[dt] = *reinterpret_cast<const v4f*>(s_cb + C + d);
       }
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
         v4f qv[4];
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -285,11 +287,11 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     }
 
     // ---------------- attention over the Skv context tokens ----------------
-    v8s of[2][2];
+    v8s of[RT][2];
     auto attend = [&](const bf16_t* ks) {
     const bf16_t* vs = ks + KVI;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
       v4f s[5];
 #pragma unroll
       for (int kt = 0; kt < 5; ++kt) {
@@ -341,7 +343,10 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
     }
     };
     if constexpr ((PROBE & 2) != 0) {
-      of[0][0] = qf[0][0]; of[0][1] = qf[0][1]; of[1][0] = qf[1][0]; of[1][1] = qf[1][1];
+      for (int rt = 0; rt < RT; ++rt) {
+        of[rt][0] = qf[rt][0];
+        of[rt][1] = qf[rt][1];
+      }
     } else {
       if (cur) attend(s_kv1);
       else attend(s_kv0);
@@ -364,7 +369,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds)
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           if constexpr ((PROBE & 4) != 0) asm volatile("" ::"v"(wof[nt & 1][ds]), "v"(of[rt][ds]));
           else out[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wof[nt & 1][ds], of[rt][ds], out[rt][nt], 0, 0, 0);
         }
@@ -379,7 +384,7 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 
   // ---------------- epilogue: + bias + residual, row statistics ----------------
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+  for (int rt = 0; rt < RT; ++rt) {
     const int m = row_w + rt * 16 + fr;
     const bool ok = m < a.M;
     float s = 0.f;
@@ -430,9 +435,28 @@ __global__ __launch_bounds__(256, 1) void xattn_block_kernel(const XattnArgs a) 
 CSK_DEBUG_EXPORT(xattn)
 
 static int g_xattn_probe = 0;
+static int g_xattn_waves = 8;  // profiles/xattnbench_waves_r6h.txt: 40.1 vs 49.8 us (4 waves)
 CSK_API int csk_set_xattn_probe(int p) {
   g_xattn_probe = p;
   return 0;
+}
+// 8 waves x 16 rows (default) or 4 waves x 32 rows per 128-row workgroup
+CSK_API int csk_set_xattn_waves(int w) {
+  if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
+  g_xattn_waves = w;
+  return 0;
+}
+
+template <int C, int NW, int RT>
+static void xattn_launch(const XattnArgs& a, dim3 grid, hipStream_t stream) {
+  switch (g_xattn_probe) {
+    case 1: xattn_block_kernel<C, NW, RT, 1><<<grid, NW * 64, 0, stream>>>(a); break;
+    case 2: xattn_block_kernel<C, NW, RT, 2><<<grid, NW * 64, 0, stream>>>(a); break;
+    case 4: xattn_block_kernel<C, NW, RT, 4><<<grid, NW * 64, 0, stream>>>(a); break;
+    case 8: xattn_block_kernel<C, NW, RT, 8><<<grid, NW * 64, 0, stream>>>(a); break;
+    case 15: xattn_block_kernel<C, NW, RT, 15><<<grid, NW * 64, 0, stream>>>(a); break;
+    default: xattn_block_kernel<C, NW, RT><<<grid, NW * 64, 0, stream>>>(a); break;
+  }
 }
 
 const bf16_t* csk_zero_ptr();
@@ -467,14 +491,8 @@ CSK_API int csk_xattn_block(void* y, const void* x, const void* wq, const void* 
   const dim3 grid((M + XA_BM - 1) / XA_BM);
   switch (C) {
     case 320:
-      switch (g_xattn_probe) {
-        case 1: xattn_block_kernel<320, 1><<<grid, 256, 0, stream>>>(a); break;
-        case 2: xattn_block_kernel<320, 2><<<grid, 256, 0, stream>>>(a); break;
-        case 4: xattn_block_kernel<320, 4><<<grid, 256, 0, stream>>>(a); break;
-        case 8: xattn_block_kernel<320, 8><<<grid, 256, 0, stream>>>(a); break;
-        case 15: xattn_block_kernel<320, 15><<<grid, 256, 0, stream>>>(a); break;
-        default: xattn_block_kernel<320><<<grid, 256, 0, stream>>>(a); break;
-      }
+      if (g_xattn_waves == 8) xattn_launch<320, 8, 1>(a, grid, stream);
+      else xattn_launch<320, 4, 2>(a, grid, stream);
       break;
     default: return (int)hipErrorInvalidValue;
   }

@@ -57,15 +57,24 @@ def rel(a, b):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("B,S,Skv", [(2, 256, 77), (8, 4096, 77), (1, 128, 1), (3, 384, 80), (2, 512, 40)])
-def test_xattn_block_kernel_vs_fp32(gpu, B, S, Skv):
-    from chiaswarm_amd.ops import hip_ops
+def test_xattn_block_kernel_vs_fp32(gpu, B, S, Skv, waves):
+    from chiaswarm_amd.ops import _lib, hip_ops
 
     blk, x, kv = _setup(gpu, torch.bfloat16, B=B, S=S, Skv=Skv)
     a2 = blk.attn2
     w2, colsum, b2 = ops.fold_layer_norm(a2.to_q.weight, a2.to_q.bias, blk.norm2.weight, blk.norm2.bias)
     assert hip_ops.xattn_ok(x, kv, S)
-    y = hip_ops.xattn_block(x, w2, colsum, b2, kv, a2.to_out[0].weight, a2.to_out[0].bias, blk.norm2.eps, a2.scale, S)
+    _lib.call("csk_set_xattn_waves", waves)
+    hip_ops._xattn_waves_applied[0] = waves
+    try:
+        y = hip_ops.xattn_block(x, w2, colsum, b2, kv, a2.to_out[0].weight, a2.to_out[0].bias, blk.norm2.eps,
+                                a2.scale, S)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("csk_set_xattn_waves", hip_ops.XATTN_WAVES)
+        hip_ops._xattn_waves_applied[0] = hip_ops.XATTN_WAVES
     ref = _unfused(x.cpu().float(), blk.cpu().float(), kv.cpu().float())
     blk.to(gpu)
     # the residual dominates y: bound the attention branch on its own too

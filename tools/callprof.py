@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Exact per-call kernel time of one SD2.1 UNet step (CFG batch 8, 64x64):
+"""Exact per-call kernel time of one SD2.1 UNet step (CFG batch 8, 64x64; or\n``--model sdxl --batch 2``: the SDXL 1024-px CFG-batch-2 step):
 every libcsk call is followed by a 1-element int32 fill, so in a rocprofv3
 kernel trace the separator kernels split the dispatch stream into calls; the
 calls' shapes are recorded on the host in the same order.  No host syncs, so
@@ -19,7 +19,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def record(path, batch, iters, dup=True):
+def record(path, batch, iters, dup=True, model="sd21"):
     import torch
 
     from chiaswarm_amd.models import unet as unet_mod
@@ -29,19 +29,26 @@ def record(path, batch, iters, dup=True):
 
     _lib.load()
     dev = torch.device("cuda", 0)
+    sdxl = model == "sdxl"
+    cfg, lat, cdim = (unet_mod.SDXL, 128, 2048) if sdxl else (unet_mod.SD21, 64, 1024)
     with torch.device(dev):
-        m = unet_mod.UNet2DConditionModel(unet_mod.SD21).to(torch.bfloat16).eval().requires_grad_(False)
+        m = unet_mod.UNet2DConditionModel(cfg).to(torch.bfloat16).eval().requires_grad_(False)
     init_random_fast_(m, seed=0)
     prepare_model(m)
-    x = torch.randn(batch // 2 if dup else batch, 64, 64, 4, device=dev).to(torch.bfloat16)
+    dup = dup and not sdxl  # SDXL's halves differ in the pooled text embedding (no shared prefix)
+    x = torch.randn(batch // 2 if dup else batch, lat, lat, 4, device=dev).to(torch.bfloat16)
     if dup:  # identical CFG halves and the shared prefix, as in the product loop
         x = torch.cat([x, x])
-    ctx = torch.randn(batch, 77, 1024, device=dev).to(torch.bfloat16)
+    ctx = torch.randn(batch, 77, cdim, device=dev).to(torch.bfloat16)
     kv = m.encode_context(ctx)
     t = torch.tensor([500.0], device=dev)
+    kw = {"cfg_dup": dup}
+    if sdxl:
+        kw["added_cond"] = {"text_embeds": torch.randn(batch, 1280, device=dev).to(torch.bfloat16),
+                            "time_ids": torch.tensor([[1024.0, 1024, 0, 0, 1024, 1024]] * batch, device=dev)}
     with torch.no_grad():
         for _ in range(2):
-            m(x, t, cross_kv=kv, cfg_dup=dup)
+            m(x, t, cross_kv=kv, **kw)
     torch.cuda.synchronize()
     sep = torch.zeros(1, dtype=torch.int32, device=dev)
     orig = _lib.call
@@ -56,7 +63,7 @@ def record(path, batch, iters, dup=True):
     _lib.call = wrapped
     with torch.no_grad():
         for _ in range(iters):
-            m(x, t, cross_kv=kv, cfg_dup=dup)
+            m(x, t, cross_kv=kv, **kw)
     torch.cuda.synchronize()
     _lib.call = orig
     with open(path, "w") as f:
@@ -123,10 +130,11 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-cfg-dup", action="store_true")
+    ap.add_argument("--model", default="sd21", choices=("sd21", "sdxl"), help="sdxl: 128x128 latents (1024 px)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if a.record:
-        record(a.record, a.batch, a.iters, not a.no_cfg_dup)
+        record(a.record, a.batch, a.iters, not a.no_cfg_dup, a.model)
     if a.db:
         dbs = glob.glob(a.db) or [a.db]
         analyse(dbs[0], a.calls, a.json)

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--only-tiles", default="", help="comma list: try only these tiles (e.g. a new kernel)")
     ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG doubles the images: 8 = 4 images, 2 = 1)")
     ap.add_argument("--latent", type=int, default=64, help="latent side (64 = 512 px)")
+    ap.add_argument("--model", default="sd21", choices=("sd21", "sdxl"),
+                    help="sdxl: tune the SDXL step (use --batch 2 --latent 128 for 1024 px batch-1 jobs)")
     ap.add_argument("--no-cfg-dup", action="store_true",
                     help="tune the unshared step (default: the product's CFG-shared prefix, identical halves)")
     a = ap.parse_args()
@@ -55,11 +57,17 @@ def main():
 
     _lib.load()
     dev = torch.device("cuda", 0)
-    p = StableDiffusion("sd21", device=dev, seed=0)
+    sdxl = a.model == "sdxl"
+    p = StableDiffusion(a.model, device=dev, seed=0)
     x = torch.randn(a.batch // 2, a.latent, a.latent, 4, device=dev).bfloat16()
     x = torch.cat([x, x])  # CFG halves are identical copies in the product loop
-    ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
+    ctx = torch.randn(a.batch, 77, 2048 if sdxl else 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
+    added = None
+    if sdxl:  # pooled text embedding + size conditioning; the halves differ, so no shared prefix
+        added = {"text_embeds": torch.randn(a.batch, 1280, device=dev).bfloat16(),
+                 "time_ids": torch.tensor([[8.0 * a.latent, 8 * a.latent, 0, 0, 8 * a.latent, 8 * a.latent]] * a.batch,
+                                          device=dev)}
 
     used = {}
     orig_choose = tuning.choose
@@ -74,7 +82,7 @@ def main():
     present0 = set(table)  # keys present before the first capture
 
     def capture():
-        return _UNetGraph(p.unet, x, kv, None, warmup=1, cfg_dup=not a.no_cfg_dup)
+        return _UNetGraph(p.unet, x, kv, added, warmup=1, cfg_dup=not a.no_cfg_dup and not sdxl)
 
     def timed(g, rounds=3):
         for _ in range(2):

@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """The fused cross-attention sub-block (xattn.hip) on the SD2.1 64x64-level
 shape, with its profiling probes (csk_set_xattn_probe: 1 no Q-projection MFMAs,
-2 no attention, 4 no out-projection MFMAs, 8 no per-head DMA, 15 all), against
+2 no attention, 4 no out-projection MFMAs, 8 no per-head DMA, 15 all) for the
+4-wave and 8-wave workgroups (csk_set_xattn_waves), against
 the unfused chain (LN-fused Q GEMM + attn_shortkv + out-projection GEMM):
 
     python tools/xattnbench.py [--batch 8] [--iters 30]
@@ -51,11 +52,20 @@ def main():
     w2, colsum, b2 = blk._fold("q", a2.to_q.weight, a2.to_q.bias, blk.norm2)
     wo, bo = a2.to_out[0].weight, a2.to_out[0].bias
     fl = 2.0 * a.batch * S * C * C * 2 + 4.0 * a.batch * S * 77 * C
-    for probe in (0, 1, 2, 4, 8, 15):
-        _lib.call("csk_set_xattn_probe", probe)
-        t = timeit(lambda: hip_ops.xattn_block(x, w2, colsum, b2, kv, wo, bo, 1e-5, a2.scale, S), a.iters)
-        print(f"xattn probe {probe:2d}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s", flush=True)
-    _lib.call("csk_set_xattn_probe", 0)
+    ref = None
+    for waves in (4, 8):
+        hip_ops.XATTN_WAVES = waves  # applied by the next xattn_block call
+        for probe in (0, 1, 2, 4, 8, 15):
+            _lib.call("csk_set_xattn_probe", probe)
+            t = timeit(lambda: hip_ops.xattn_block(x, w2, colsum, b2, kv, wo, bo, 1e-5, a2.scale, S), a.iters)
+            print(f"xattn {waves} waves probe {probe:2d}: {t:7.1f} us  {fl / t / 1e6:6.1f} TF/s", flush=True)
+        _lib.call("csk_set_xattn_probe", 0)
+        y = hip_ops.xattn_block(x, w2, colsum, b2, kv, wo, bo, 1e-5, a2.scale, S).float()
+        if ref is None:
+            ref = y
+        else:
+            print(f"  {waves} waves vs 4 waves: max abs diff {(y - ref).abs().max().item():.3e}", flush=True)
+    hip_ops.XATTN_WAVES = 4
     xr = ops.row_stats_wanted(x)
     x1 = ops.gemm(x, blk.attn1.to_out[0].weight, None, row_stats=xr)  # a producer carrying row statistics
 
