@@ -95,6 +95,7 @@ sig("csk_set_gn_prologue_max", c_int)
 sig("csk_debug_selftest", c_int, c_void_p)  # CSK_DEBUG builds: one deliberate record (tests)
 sig("csk_set_gn_lds", c_int)
 sig("csk_set_sw_odd", c_int)
+sig("csk_set_epi_band", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
@@ -206,6 +207,8 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
         # (and the buffer sized for them below) follow the tile that actually runs
         if tile in (25, 26, 31, 32, 33, 34):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
             tile = 11
+        elif tile in (35, 36):  # 64x160 -> 64x128 (gemm_glds.hip csk_gemm_glds_launch)
+            tile = 13
         if ln is None and code == 3:
             row_stats = False
     seg = _gn_seg(tile, split, gn_rows, M, code, N) if gn_rows and out.is_contiguous() else 0

@@ -418,6 +418,11 @@ CSK_API int csk_set_sw_odd(int v) {
   g_sw_odd = v;
   return 0;
 }
+int g_epi_band = 1;  // tools/abstep.py arms band0 / band1: LDS-staged epilogue band path off / on
+CSK_API int csk_set_epi_band(int v) {
+  g_epi_band = v;
+  return 0;
+}
 CSK_API int csk_set_gn_lds(int v) {
   g_gn_lds = v;
   return 0;
@@ -428,6 +433,7 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
   a.gn_lds = g_gn_lds;
   a.sw_odd = g_sw_odd;
+  a.epi_band = g_epi_band;
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
@@ -550,7 +556,7 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = tile >= 11 && tile <= 29 && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
+  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 35 || tile == 36) && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
     if (!rows) return (int)hipErrorInvalidValue;

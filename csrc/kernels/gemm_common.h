@@ -89,6 +89,7 @@ struct GemmArgs {
   int gn_seg;  // rows per gn_part segment (divides BM; 0 -> BM)
   int gn_lds;  // 1: GroupNorm statistics through the LDS epilogue even where the direct one can (A/B knob)
   int sw_odd;  // 1: row-layout tiles with an odd fragment count (160 wide) use the direct epilogue (A/B knob)
+  int epi_band;  // 1: LDS-staged epilogue stores through the compile-time band path (A/B knob, default 1)
   // fused LayerNorm of the INPUT rows (SURVEY K11 folded into K9/K10): the
   // weight was pre-multiplied by gamma (W' = W diag(gamma)), the bias holds
   // b + W beta, and the epilogue applies
@@ -323,6 +324,11 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int LDC_S = BN + 4;
+  // the 128x160 and 256-row tiles' main loops already hold 256 VGPRs: the
+  // epilogue operand prefetch and the band store path below spilled there
+  // (scratch 32-112 B per lane, tiles 26 / 33 / 31 slower: profiles/lib_ab_epilogue_prefetch_r6l.txt),
+  // so those tiles keep the loads at their use and the generic store loop
+  constexpr bool ROOMY = !((BM == 128 && BN == 160) || BM >= 256);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR address math
   const int wm = wid / WN, wn = wid % WN;
@@ -460,6 +466,13 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
         // wave's WTM rows -> LDS [WM][BN][2] -> (mean, M2) per gn_seg-row segment
         float* gred = reinterpret_cast<float*>(smem);
         if (gnp) epi_barrier<RAW>();  // main-loop LDS reads are done
+        // The epilogue operands of a fragment pair (bias, LN colsum, the residual
+        // rows of every row block, the per-sample bias row) are issued together
+        // before the pair's first store: C may alias them, so the compiler will
+        // not move a load over a store, and loaded at their use every residual
+        // row cost one exposed memory latency (global_load; s_waitcnt vmcnt(0);
+        // global_store, per row block).  Now one latency per pair.
+        const bool b2u = args.bias2d && (args.rows_per_b % BM) == 0 && (m0 % args.rows_per_b) + BM <= args.rows_per_b;
 #pragma unroll
         for (int f = 0; f + 1 < NT; f += 2) {
           // the 8 columns this lane stores for fragment pair f (same for every row block)
@@ -467,6 +480,16 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
           float bb[8], cs[8], gs[8], gq[8];
 #pragma unroll
           for (int r = 0; r < 8; ++r) bb[r] = cs[r] = gs[r] = gq[r] = 0.f;
+          uint4 rpre[MT];
+          uint4 b2pre = make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int m = m0 + wm * WTM + i * 16 + fr;
+            rpre[i] = make_uint4(0, 0, 0, 0);
+            if (ROOMY && args.res && col < outN && m < M)
+              rpre[i] = *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + col);
+          }
+          if (b2u && col < outN) b2pre = *reinterpret_cast<const uint4*>(args.bias2d + (size_t)(m0 / args.rows_per_b) * args.ldb2 + col);
           if (col < outN) {
             if (args.bias) add8(bb, args.bias + col, true, 8);
             if (lnf) {
@@ -484,13 +507,29 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
             if (m >= M || col >= outN) continue;
 #pragma unroll
             for (int r = 0; r < 8; ++r) o[r] = lnr[i] * (o[r] - lnm[i] * cs[r]) + bb[r];
-            if (args.bias2d) add8(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col, true, 8);
+            if (b2u) {
+              float g[8];
+              unpack8(b2pre, g);
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] += g[r];
+            } else if (args.bias2d) {
+              add8(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col, true, 8);
+            }
             act8(act, o);
             if (osc != 1.0f) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) o[r] *= osc;
             }
-            if (args.res) add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
+            if (args.res) {
+              if constexpr (ROOMY) {
+                float g[8];
+                unpack8(rpre[i], g);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] += g[r];
+              } else {
+                add8(o, args.res + (size_t)m * args.ldr + col, true, 8);
+              }
+            }
             if (rst) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) {
@@ -546,8 +585,18 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
               cs[0] = c0.x; cs[1] = c0.y; cs[2] = c0.z; cs[3] = c0.w;
             }
           }
-          auto add4 = [](float (&o)[4], const bf16_t* p) {
-            const uint2 u = *reinterpret_cast<const uint2*>(p);
+          uint2 r4[MT], b4[MT];  // residual / per-sample bias rows, issued before the stores (see above)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int m = m0 + wm * WTM + i * 16 + fr;
+            r4[i] = b4[i] = make_uint2(0, 0);
+            if (ROOMY && m < M && col < outN) {
+              if (args.res) r4[i] = *reinterpret_cast<const uint2*>(args.res + (size_t)m * args.ldr + col);
+              if (args.bias2d)
+                b4[i] = *reinterpret_cast<const uint2*>(args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col);
+            }
+          }
+          auto add4u = [](float (&o)[4], uint2 u) {
             o[0] += __uint_as_float(u.x << 16); o[1] += __uint_as_float(u.x & 0xffff0000u);
             o[2] += __uint_as_float(u.y << 16); o[3] += __uint_as_float(u.y & 0xffff0000u);
           };
@@ -558,14 +607,21 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
             float o[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = lnr[i] * (acc[i][f][r] - lnm[i] * cs[r]) + bb[r];
-            if (args.bias2d) add4(o, args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col);
+            if (args.bias2d) {
+              if constexpr (!ROOMY)
+                b4[i] = *reinterpret_cast<const uint2*>(args.bias2d + (size_t)(m / args.rows_per_b) * args.ldb2 + col);
+              add4u(o, b4[i]);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = apply_act(act, o[r]);
             if (osc != 1.0f) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) o[r] *= osc;
             }
-            if (args.res) add4(o, args.res + (size_t)m * args.ldr + col);
+            if (args.res) {
+              if constexpr (!ROOMY) r4[i] = *reinterpret_cast<const uint2*>(args.res + (size_t)m * args.ldr + col);
+              add4u(o, r4[i]);
+            }
             if (rst) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -755,34 +811,45 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
         }
   }
   epi_barrier<RAW>();
-  // Fast store path — the common short-K GEMM case (no GN / row statistics /
-  // fused LN / GEGLU / per-sample bias; full, 16-byte-aligned 8-column vectors).
-  // Each thread keeps ONE column vector for the whole band (VPR divides 256), so
-  // its bias is loaded once and the row loop is pointer increments; the generic
-  // loop below re-derives row and column (a runtime division), the bias and the
-  // addresses for every 8 outputs, and at K = 320 the epilogue is most of a
-  // tile's instruction stream (the SIMDs were issue-saturated, PMC r1i).
-  constexpr int VPR = BN / 8;
-  if constexpr (NTHR % VPR == 0 && PR % (NTHR / VPR) == 0) {
-    const bool fast = !args.gn_part && !args.row_part && !ln && act != ACT_GEGLU && !args.bias2d &&
-                      (N % 8) == 0 && (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
-                      (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
-                      (!args.res || ((args.ldr % 8) == 0 && ((((size_t)args.res) & 15) == 0)));
-    if (fast) {
-      constexpr int RPI = NTHR / VPR;  // band rows per iteration
+  // Band store path with compile-time geometry: VPR = BN / 8 column vectors per
+  // row, NTHR / VPR rows per iteration (the threads past that idle when VPR does
+  // not divide NTHR: the 160-wide tiles), so no runtime division per 8 outputs;
+  // each thread keeps ONE column vector, its bias (+ a band-uniform per-sample
+  // bias row) loaded once, and the residual rows of all its iterations are
+  // issued before the first store (C may alias them, so loaded at the use every
+  // row waited one memory latency).  Covers the GroupNorm statistics (final
+  // values back into LDS for the column pass below) and the fused-LN consumer
+  // (applied while staging).  At K = 320 the epilogue is most of a tile's
+  // instruction stream (the SIMDs were issue-saturated, PMC r1i).
+  bool banded = false;
+  {
+    constexpr int VPR = BN / 8, RPI = NTHR / VPR, NIT = (PR + RPI - 1) / RPI;
+    const int mb0 = m0 + pr0, mb1 = min(mb0 + PR, M) - 1;
+    const bool b2 = args.bias2d != nullptr;
+    banded = ROOMY && args.epi_band && !args.row_part && act != ACT_GEGLU && act != ACT_PROBE_NO_STORE && (N % 8) == 0 &&
+             (args.ldc % 8) == 0 && ((((size_t)args.C) & 15) == 0) &&
+             (!args.bias || ((((size_t)args.bias) & 15) == 0)) &&
+             (!args.res || ((args.ldr % 8) == 0 && ((((size_t)args.res) & 15) == 0))) &&
+             (!b2 || ((args.ldb2 % 8) == 0 && ((((size_t)args.bias2d) & 15) == 0) &&
+                      mb0 / args.rows_per_b == mb1 / args.rows_per_b));
+    if (banded) {
       const int cv = tid % VPR, r0 = tid / VPR;
       const int n = n0 + cv * 8;
-      if (n < N) {
+      if (r0 < RPI && n < N) {
         float bb[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) bb[j] = 0.f;
-        if (args.bias) add8(bb, args.bias + n, true, 8);
         const float osc = args.out_scale;
-        int m = m0 + pr0 + r0;
-        bf16_t* cp = args.C + (size_t)m * args.ldc + n;
-        const bf16_t* rp = args.res ? args.res + (size_t)m * args.ldr + n : nullptr;
-        const size_t cstep = (size_t)RPI * args.ldc, rstep = (size_t)RPI * args.ldr;
-        for (int row = r0; row < PR && m < M; row += RPI, m += RPI) {
+        auto ld_res = [&](int k) {
+          const int row = r0 + k * RPI, m = mb0 + row;
+          uint4 u = make_uint4(0, 0, 0, 0);
+          // uniform base + 32-bit element offset (saddr + voffset: no 64-bit
+          // per-thread pointers kept live, which spilled the 256-VGPR tiles)
+          if (args.res && row < PR && m < M) u = *reinterpret_cast<const uint4*>(args.res + (unsigned)(m * args.ldr + n));
+          return u;
+        };
+        auto store_row = [&](int k, uint4 rres) {
+          const int row = r0 + k * RPI, m = mb0 + row;
           const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8);
           const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC_S + cv * 8 + 4);
           float f[8] = {lo.x + bb[0], lo.y + bb[1], lo.z + bb[2], lo.w + bb[3],
@@ -792,18 +859,31 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] *= osc;
           }
-          if (rp) {
+          if (args.res) {
             float rf[8];
-            unpack8(*reinterpret_cast<const uint4*>(rp), rf);
+            unpack8(rres, rf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] += rf[j];
-            rp += rstep;
           }
-          *reinterpret_cast<uint4*>(cp) = pack8(f);
-          cp += cstep;
+          *reinterpret_cast<uint4*>(args.C + (unsigned)(m * args.ldc + n)) = pack8(f);
+          if (args.gn_part) {
+            float* crow = cs + row * LDC_S + cv * 8;
+            *reinterpret_cast<float4*>(crow) = make_float4(f[0], f[1], f[2], f[3]);
+            *reinterpret_cast<float4*>(crow + 4) = make_float4(f[4], f[5], f[6], f[7]);
+          }
+        };
+        uint4 rv[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) rv[k] = ld_res(k);
+        if (args.bias) add8(bb, args.bias + n, true, 8);
+        if (b2) add8(bb, args.bias2d + (size_t)(mb0 / args.rows_per_b) * args.ldb2 + n, true, 8);
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          if (r0 + k * RPI >= PR || mb0 + r0 + k * RPI >= M) break;
+          store_row(k, rv[k]);
         }
       }
-      continue;  // next band: nothing else to do without GN / row statistics
+      if (!args.gn_part) continue;  // next band: nothing else to do without GN statistics
     }
   }
   const int outN = act == ACT_GEGLU ? N / 2 : N;
@@ -812,7 +892,7 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
   const int vpr = BNo / 8;
   // PR * vpr is a multiple of NTHR for every tile, so each wave runs the same
   // number of iterations and the row-statistics shuffles below see all lanes
-  for (int v = tid; v < PR * vpr; v += NTHR) {
+  for (int v = banded ? PR * vpr : tid; v < PR * vpr; v += NTHR) {
     const int row = v / vpr, cv = v - row * vpr;  // row within the band
     const int m = m0 + pr0 + row, n = on0 + cv * 8;
     const bool live = m < M && n < outN;

@@ -31,10 +31,11 @@ __device__ __forceinline__ void vmcnt_wait() {
 }
 
 // waves per SIMD the register budget must allow: the 128x160 tile runs two
-// workgroups per CU (its 74 KB ring), so <= 256 registers per lane
+// workgroups per CU (its 74 KB ring), so <= 256 registers per lane; 64x160 too
+// (unconstrained it took 271 and one workgroup per CU)
 template <int BM, int BN>
 constexpr int glds_min_waves() {
-  return (BM == 128 && BN == 160) ? 2 : 1;
+  return (BN == 160 && BM <= 128) ? 2 : 1;
 }
 
 template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST>
@@ -306,6 +307,7 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   // 256x160: 80 columns per wave (odd 16-column tile count: no GEGLU pairing),
   // 20 vectors per output row (no power-of-two row-statistics butterfly)
   if ((tile == 25 || tile == 26) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 11;
+  if ((tile == 35 || tile == 36) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 13;
   switch (tile) {
     case 11: return launch_glds<128, 128, 2, 2, 2>(a, ksplit, conv, s);
     case 12: return launch_glds<128, 64, 4, 1, 3>(a, ksplit, conv, s);
@@ -332,6 +334,12 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     case 27: return launch_glds<128, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 28: return launch_glds<64, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 29: return launch_glds<128, 64, 2, 2, 4>(a, ksplit, conv, s);
+    // 64x160: exactly 256 tiles at M = 2048, N = 1280 (SDXL's 32x32-level
+    // projections, SD2.1's 16x16 level), 9 % fewer L2->LDS bytes per output than
+    // 64x128 (whose 320 tiles leave a quarter of the CUs a second tile) — these
+    // mid-size GEMMs are bound by the LDS-DMA fill (profiles/tilebench_midsize_r6k.txt)
+    case 35: return launch_glds<64, 160, 2, 2, 3>(a, ksplit, conv, s);
+    case 36: return launch_glds<64, 160, 2, 2, 2>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
