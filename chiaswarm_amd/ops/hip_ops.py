@@ -207,7 +207,7 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
         # (and the buffer sized for them below) follow the tile that actually runs
         if tile in (25, 26, 31, 32, 33, 34):  # 160-column and 8-wave tiles: no LN / row statistics -> tile 11
             tile = 11
-        elif tile in (35, 36):  # 64x160 -> 64x128 (gemm_glds.hip csk_gemm_glds_launch)
+        elif tile == 36:  # 64x160 -> 64x128 (gemm_glds.hip csk_gemm_glds_launch)
             tile = 13
         if ln is None and code == 3:
             row_stats = False

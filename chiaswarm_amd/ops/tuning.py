@@ -35,13 +35,12 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          31: (256, 256), 32: (256, 128),
          # 8-wave 256x160 3-stage ring (gemm8p.hip gemm8r_kernel): 0.0102 B/FLOP, 256 tiles at the 64x64 level
          33: (256, 160), 34: (256, 128),
-         # 64x160 (3- / 2-stage): 256 tiles at M = 2048, N = 1280 (the SDXL 32x32 level's
-         # 197 projection GEMMs) with 9 % fewer L2->LDS bytes than 64x128's 320 tiles
-         35: (64, 160), 36: (64, 160)}
+         # 64x160 2-stage (fewest L2->LDS bytes per output of the 64-row tiles)
+         36: (64, 160)}
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
 # cannot exceed that band (hip_ops._gn_seg mirrors gemm_common.h gn_seg_for)
-EPI_WM = {25: 2, 26: 2, 31: 2, 32: 2, 33: 4, 34: 4, 35: 2, 36: 2}
+EPI_WM = {25: 2, 26: 2, 31: 2, 32: 2, 33: 4, 34: 4, 36: 2}
 
 
 def _user_path():

@@ -556,7 +556,7 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 35 || tile == 36) && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
+  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36) && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
     if (!rows) return (int)hipErrorInvalidValue;

@@ -307,7 +307,7 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
   // 256x160: 80 columns per wave (odd 16-column tile count: no GEGLU pairing),
   // 20 vectors per output row (no power-of-two row-statistics butterfly)
   if ((tile == 25 || tile == 26) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 11;
-  if ((tile == 35 || tile == 36) && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 13;
+  if (tile == 36 && (a.act == ACT_GEGLU || a.ln_part || a.row_part)) tile = 13;
   switch (tile) {
     case 11: return launch_glds<128, 128, 2, 2, 2>(a, ksplit, conv, s);
     case 12: return launch_glds<128, 64, 4, 1, 3>(a, ksplit, conv, s);
@@ -334,11 +334,10 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     case 27: return launch_glds<128, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 28: return launch_glds<64, 128, 2, 2, 4>(a, ksplit, conv, s);
     case 29: return launch_glds<128, 64, 2, 2, 4>(a, ksplit, conv, s);
-    // 64x160: exactly 256 tiles at M = 2048, N = 1280 (SDXL's 32x32-level
-    // projections, SD2.1's 16x16 level), 9 % fewer L2->LDS bytes per output than
-    // 64x128 (whose 320 tiles leave a quarter of the CUs a second tile) — these
-    // mid-size GEMMs are bound by the LDS-DMA fill (profiles/tilebench_midsize_r6k.txt)
-    case 35: return launch_glds<64, 160, 2, 2, 3>(a, ksplit, conv, s);
+    // 64x160, 2-stage, two workgroups per CU: fewest L2->LDS bytes per output
+    // among the 64-row tiles; wins M8192 N640 K2560 in isolation (36.5 vs 39.9 us).
+    // Its 3-stage sibling (one workgroup per CU: exactly 256 tiles at M2048 N1280)
+    // was slower than 64x64 there (19.7 vs 14.8 us, profiles/tilebench_64x160_r6m.txt)
     case 36: return launch_glds<64, 160, 2, 2, 2>(a, ksplit, conv, s);
     default: return (int)hipErrorInvalidValue;
   }

@@ -495,15 +495,38 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* _
   gamma += (size_t)b * affine_bstride;
   beta += (size_t)b * affine_bstride;
   const int Cg = C / G, ng = CB / Cg, gbase = cb * ng;
+  const int NVC = CB >> 3, R = GN_THREADS / NVC;
+  const int cv = tid % NVC, r = tid / NVC;
+  const bool rows = r < R;
+  const int c0 = cb * CB + cv * 8;
+  const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
+  const bool second = c0 >= C1;  // this column vector lives in x2
+  const int xst = second ? C - C1 : C1;
+  const bf16_t* xsrc = (second ? x2 : x) + (size_t)b * P * xst + (second ? c0 - C1 : c0);
+  bf16_t* ydst = y + (size_t)b * P * C + c0;
+  // The first unrolled batch of x rows and the affine parameters do not depend
+  // on the statistics: issued before the partials merge so the two memory round
+  // trips overlap (at batch-1 grids that batch is a thread's whole chunk).
+  uint4 q[GN_UNROLL];
+  uint4 gq = make_uint4(0, 0, 0, 0), bq = make_uint4(0, 0, 0, 0);
+  const bool avec = ((((size_t)(gamma + c0)) | ((size_t)(beta + c0))) & 15) == 0;
+  if (rows) {
+#pragma unroll
+    for (int u = 0; u < GN_UNROLL; ++u) q[u] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p0 + r + u * R, p1 - 1) * xst);
+    if (avec) {
+      gq = *reinterpret_cast<const uint4*>(gamma + c0);
+      bq = *reinterpret_cast<const uint4*>(beta + c0);
+    }
+  }
   for (int w = tid >> 6; w < ng; w += GN_THREADS / 64) {  // whole waves: wave w merges group gbase + w
     const int g = gbase + w;
     const float fn = (float)seg_rows;
     float mean, rstd;
     group_moments_wave(
-        [&](int e, float& n, float& m, float& q) {
+        [&](int e, float& n, float& m, float& qq) {
           const int sg = b * nseg + e / Cg, c = g * Cg + e % Cg;
           const float2 mq = load_part(part, part2, sg, c, C, C1);
-          n = fn; m = mq.x; q = mq.y;
+          n = fn; m = mq.x; qq = mq.y;
         },
         nseg * Cg, tid & 63, mean, rstd, eps);
     if ((tid & 63) == 0) {
@@ -512,14 +535,11 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* _
     }
   }
   __syncthreads();
-  const int NVC = CB >> 3, R = GN_THREADS / NVC;
-  const int cv = tid % NVC, r = tid / NVC;
-  if (r >= R) return;
-  const int c0 = cb * CB + cv * 8;
+  if (!rows) return;
   float gf[8], bfv[8], sa[8], sb[8];
-  if (((((size_t)(gamma + c0)) | ((size_t)(beta + c0))) & 15) == 0) {
-    unpack8(*reinterpret_cast<const uint4*>(gamma + c0), gf);
-    unpack8(*reinterpret_cast<const uint4*>(beta + c0), bfv);
+  if (avec) {
+    unpack8(gq, gf);
+    unpack8(bq, bfv);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -534,15 +554,11 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_cb_kernel(const bf16_t* _
     sa[j] = a;
     sb[j] = bfv[j] - gst[2 * lg] * a;
   }
-  const int p0 = ck * chunk, p1 = min(P, p0 + chunk);
-  const bool second = c0 >= C1;  // this column vector lives in x2
-  const int xst = second ? C - C1 : C1;
-  const bf16_t* xsrc = (second ? x2 : x) + (size_t)b * P * xst + (second ? c0 - C1 : c0);
-  bf16_t* ydst = y + (size_t)b * P * C + c0;
   for (int p = p0 + r; p < p1; p += GN_UNROLL * R) {
-    uint4 q[GN_UNROLL];
+    if (p != p0 + r) {
 #pragma unroll
-    for (int u = 0; u < GN_UNROLL; ++u) q[u] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p + u * R, p1 - 1) * xst);
+      for (int u = 0; u < GN_UNROLL; ++u) q[u] = *reinterpret_cast<const uint4*>(xsrc + (size_t)min(p + u * R, p1 - 1) * xst);
+    }
 #pragma unroll
     for (int u = 0; u < GN_UNROLL; ++u) {
       const int pp = p + u * R;

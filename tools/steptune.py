@@ -32,7 +32,7 @@ import torch  # noqa: E402
 from chiaswarm_amd import ops  # noqa: E402
 from chiaswarm_amd.ops import _lib, tuning  # noqa: E402
 
-SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 33, 15, 27, 28, 29, 35, 36)
+SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 33, 15, 27, 28, 29, 36)
 
 
 def main():
