@@ -383,6 +383,24 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
   }
 
   // ---------------- epilogue: + bias + residual, row statistics ----------------
+  // Every residual / bias fragment is loaded before the first store: y may alias
+  // x as far as the compiler knows, so loads left at their use each waited one
+  // memory latency behind the previous store (20 per row tile).
+  uint2 xres[RT][NNT], bres[NNT];
+#pragma unroll
+  for (int nt = 0; nt < NNT; ++nt) {
+    bres[nt] = make_uint2(0, 0);
+    if (a.bo) bres[nt] = *reinterpret_cast<const uint2*>(a.bo + 16 * nt + 4 * g);
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int m = row_w + rt * 16 + fr;
+#pragma unroll
+    for (int nt = 0; nt < NNT; ++nt) {
+      xres[rt][nt] = make_uint2(0, 0);
+      if (m < a.M) xres[rt][nt] = *reinterpret_cast<const uint2*>(a.x + (size_t)m * C + 16 * nt + 4 * g);
+    }
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int m = row_w + rt * 16 + fr;
@@ -391,10 +409,8 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
 #pragma unroll
     for (int nt = 0; nt < NNT; ++nt) {
       const int n = 16 * nt + 4 * g;
-      uint2 u = make_uint2(0, 0);
-      if (ok) u = *reinterpret_cast<const uint2*>(a.x + (size_t)m * C + n);
-      uint2 ub = make_uint2(0, 0);
-      if (a.bo) ub = *reinterpret_cast<const uint2*>(a.bo + n);
+      const uint2 u = xres[rt][nt];
+      const uint2 ub = bres[nt];
       float rv[4] = {bf2f((bf16_t)(u.x & 0xffff)), bf2f((bf16_t)(u.x >> 16)), bf2f((bf16_t)(u.y & 0xffff)),
                      bf2f((bf16_t)(u.y >> 16))};
       const float bov[4] = {bf2f((bf16_t)(ub.x & 0xffff)), bf2f((bf16_t)(ub.x >> 16)), bf2f((bf16_t)(ub.y & 0xffff)),

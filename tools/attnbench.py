@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--short-kv", type=int, default=-1, help="Skv <= 128 kernel: 1 plain, 2 pipelined, 3 K/V-resident")
     ap.add_argument("--kv-rows", type=int, default=0, help="K/V-resident kernel rows per workgroup (0 auto)")
     ap.add_argument("--attn32", type=int, default=1, help="csk_set_attn32 value (0 off, 1 default, 2-4 TRICKS A/B)")
+    ap.add_argument("--split", type=int, default=0, help="force this many key splits (attention_split); 0: the op's rule")
     a = ap.parse_args()
     _lib.load()
     if a.short_kv >= 0:
@@ -33,17 +34,23 @@ def main():
     B, Sq, Skv, H, D = map(int, a.shape.split(","))
     q, k, v = (torch.randn(B, s, H, D, device="cuda").bfloat16() for s in (Sq, Skv, Skv))
     hip_ops.ATTN_VARIANT = a.variant
+    def run():
+        if a.split > 1:
+            return hip_ops.attention_split(q, k, v, D ** -0.5, a.split)
+        return hip_ops.attention(q, k, v, D ** -0.5)
+
     for _ in range(3):
-        hip_ops.attention(q, k, v, D ** -0.5)
+        run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.iters):
-        hip_ops.attention(q, k, v, D ** -0.5)
+        run()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"attn32 {a.attn32} variant {a.variant} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: {ms * 1000:.1f} us  "
+    print(f"attn32 {a.attn32} variant {a.variant} split {a.split} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: "
+          f"{ms * 1000:.1f} us  "
           f"{4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")
 
 
