@@ -434,6 +434,12 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.gn_lds = g_gn_lds;
   a.sw_odd = g_sw_odd;
   a.epi_band = g_epi_band;
+  // profiling probes (act 97-99) exist only in the LDS-DMA tiles (gemm_glds.hip);
+  // any other kernel would run them as a plain full-width epilogue — into a
+  // caller's GEGLU-sized (N/2) output that is an out-of-bounds write
+  if ((a.act == ACT_PROBE_NO_EPILOGUE || a.act == ACT_PROBE_NO_STORE || a.act == ACT_PROBE_NO_A) &&
+      !((tile >= 11 && tile <= 29) || tile == 36))
+    return (int)hipErrorInvalidValue;
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;

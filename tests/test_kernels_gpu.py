@@ -750,3 +750,21 @@ def test_attention_split_kv(gpu, B, S, H, split):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
     if hip_ops.attn_kv_split(B, H, S, S, 64) > 1:  # the default path takes the split itself
         assert rel_err(hip_ops.attention(q, k, v, 0.125).cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
+
+
+@pytest.mark.parametrize("tile", [1, 4, 31, 32, 33, 34])
+def test_profiling_probe_act_rejected_outside_lds_dma_tiles(gpu, tile):
+    """act 97-99 (tilebench probes) exist only in the LDS-DMA tiles; any other
+    kernel would run them as a plain full-width epilogue (an out-of-bounds write
+    into a GEGLU-sized output), so the library refuses them before launching."""
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.ops.hip_ops import _p, _s
+
+    M, N, K = 256, 256, 128
+    a, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu)
+    y = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=gpu)
+    with pytest.raises(RuntimeError):
+        _lib.call("csk_gemm", _p(y), _p(a), _p(w), None, None, None, M, N, K, K, K, N // 2, N // 2, 1, 99, 1.0, None,
+                  tile, 1, None, _s())
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(y)) == 0

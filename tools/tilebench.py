@@ -84,15 +84,20 @@ def main():
             w = (torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
             no = N // 2 if geglu else N
             y = torch.empty(M, no, dtype=torch.bfloat16, device=dev)
+            yfull = torch.empty(M, N, dtype=torch.bfloat16, device=dev)  # probe runs: act 99 is not GEGLU
             fl = 2.0 * M * N * K
 
             r = torch.randn(M, no, device=dev).to(torch.bfloat16)
             variants = [(False, False)] + ([(True, False)] if a.probe else []) + ([(False, True)] if a.res else [])
             for probe, res in variants:
-                def run(tile, split, x=x, w=w, y=y, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe, res=res, r=r):
+                def run(tile, split, x=x, w=w, y=y, yfull=yfull, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe, res=res,
+                        r=r):
                     ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
-                    _lib.call("csk_gemm", _p(y), _p(x), _p(w), None, None, _p(r) if res else None, M, N, K, K, K, no,
-                              no, 1, 99 if probe else (3 if geglu else 0), 1.0, None, tile, split, _p(ws), _s())
+                    # a probe is not a GEGLU epilogue: full-width output buffer and row stride
+                    out, ldo = (yfull, N) if probe else (y, no)
+                    _lib.call("csk_gemm", _p(out), _p(x), _p(w), None, None, _p(r) if (res and not probe) else None, M,
+                              N, K, K, K, ldo, ldo, 1, 99 if probe else (3 if geglu else 0), 1.0, None, tile, split,
+                              _p(ws), _s())
                 jobs.append((f"gemm {spec}" + (" noepi" if probe else "") + (" res" if res else ""), fl, run))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for name, fl, run in jobs:
