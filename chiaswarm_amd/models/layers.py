@@ -284,6 +284,15 @@ class BasicTransformerBlock(nn.Module):
             w2, colsum, b2 = self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2)
             x = ops.xattn_block(x, w2, colsum, b2, kv, a2.to_out[0].weight, a2.to_out[0].bias, self.norm2.eps,
                                 a2.scale, x.shape[1], row_stats=hip)
+        elif hip and not dup and kv is not None and x.dim() == 3 and ops.qattn_fusable(x, kv, x.shape[1]):
+            # LN2 + Q projection with the attention in its epilogue (the query
+            # tensor and the short-KV attention launch disappear), then the
+            # out-projection + residual
+            fus = ops.ln_fusable(x)
+            o = ops.layer_norm_gemm_attn(x, self.norm2, a2.to_q.weight, a2.to_q.bias,
+                                         self._fold("q", a2.to_q.weight, a2.to_q.bias, self.norm2) if fus else None,
+                                         kv, a2.scale, x.shape[1])
+            x = a2.to_out[0](o, residual=x, row_stats=hip)
         else:
             fus = ops.ln_fusable(x)
             q = ops.layer_norm_gemm(x, self.norm2, a2.to_q.weight, a2.to_q.bias,

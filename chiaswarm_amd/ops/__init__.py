@@ -232,6 +232,48 @@ def conv_halo(x, conv, bias2d=None, residual=None, gn=None, x2=None, gn_stats=Tr
                              gn_stats=gn_stats)
 
 
+def qattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
+    """The query projection of this cross-attention can carry the attention in
+    its epilogue (HIP path; head dim 64, <= 80 context tokens)."""
+    if not use_hip(x):
+        return False
+    from . import hip_ops
+
+    return hip_ops.qattn_ok(x, kv, rows_per_b)
+
+
+def layer_norm_gemm_attn(x, norm, w, bias, folded, kv, scale, rows_per_b):
+    """softmax((LayerNorm(x) @ w^T + bias) K^T * scale) V over the per-request
+    ``kv`` [B, Skv, 2, H, D] (the attention output before the out-projection),
+    the attention running in the query projection's epilogue on the HIP path."""
+    lead = x.shape[:-1]
+    if use_hip(x):
+        from . import hip_ops
+
+        if ln_fusable(x):
+            w2, colsum, b2 = folded
+            o = hip_ops.gemm_attn(x.reshape(-1, x.shape[-1]), w2, b2, kv, scale, rows_per_b,
+                                  ln=(x._csk_rows, colsum, float(norm.eps)))
+        else:
+            xn = layer_norm(x, norm.weight, norm.bias, norm.eps)
+            o = hip_ops.gemm_attn(xn.reshape(-1, x.shape[-1]), w, bias, kv, scale, rows_per_b)
+        return o.view(*lead, o.shape[-1])
+    return _ref_gemm_attn(layer_norm(x, norm.weight, norm.bias, norm.eps), w, bias, kv, scale)
+
+
+def _ref_gemm_attn(xn, w, bias, kv, scale):
+    """fp32 reference: q = xn @ w^T + bias, softmax(q K^T * scale) V per head."""
+    b, s, c = xn.shape
+    q = xn.float() @ w.float().t()
+    if bias is not None:
+        q = q + bias.float()
+    heads, d = kv.shape[3], kv.shape[4]
+    k, v = kv[:b, :, 0].float(), kv[:b, :, 1].float()
+    qh = q.view(b, s, heads, d).transpose(1, 2)
+    att = torch.softmax((qh @ k.permute(0, 2, 3, 1)) * scale, -1)
+    return (att @ v.transpose(1, 2)).transpose(1, 2).reshape(b, s, c).to(xn.dtype)
+
+
 def xattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
     """The fused cross-attention sub-block kernel takes this block (HIP path)."""
     if not use_hip(x):

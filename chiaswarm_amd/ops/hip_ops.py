@@ -236,6 +236,68 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
     return out
 
 
+# Cross-attention query projection with the attention in the GEMM epilogue
+# (gemm_common.h gemm_attn_epilogue): O = softmax(q K^T * scale) V straight from
+# the Q-projection accumulators, one head per 128x64 tile.
+sig("csk_gemm_ln_attn", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_void_p)
+QATTN = os.environ.get("CSK_QATTN", "1") == "1"
+# below this many 128x64 tiles the one-head-per-tile grid under-fills the chip
+# and the unfused query GEMM + short-KV attention win (CFG batch 2 of SD2.1:
+# 80 / 160 tiles, +0.01 ms/step; batch 8: 320 / 640 tiles, -0.09 ms/step,
+# profiles/unet_step_ab_qattn_r6s.txt)
+QATTN_MIN_TILES = int(os.environ.get("CSK_QATTN_MIN_TILES", "256"))
+QATTN_STATS = [0]  # calls (tests assert the fused path ran)
+
+
+def qattn_ok(x, kv, rows_per_b) -> bool:
+    """Shapes the attention-epilogue GEMM takes: head dim 64 (heads = C / 64),
+    <= 80 context tokens, 128-row tiles inside one sample."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    return (QATTN and kv is not None and kv.dim() == 5 and kv.shape[2] == 2 and kv.shape[4] == 64
+            and kv.shape[3] * 64 == C and 1 <= kv.shape[1] <= 80 and C % 64 == 0 and rows_per_b % 128 == 0
+            and M % rows_per_b == 0 and kv.shape[0] >= M // rows_per_b
+            and (M // 128) * (C // 64) >= QATTN_MIN_TILES)
+
+
+def gemm_attn(a2, w, bias, kv, scale, rows_per_b, ln=None):
+    """Attention output O [M, C] of the cross-attention whose query projection
+    is ``a2 @ w^T + bias`` (``ln = (rows, colsum, eps)``: LayerNorm folded as in
+    ``gemm``), over the per-request ``kv`` [Bc, Skv, 2, H, 64]."""
+    _bf16(a2, "gemm_attn.a")
+    _bf16(w, "gemm_attn.w")
+    _bf16(kv, "gemm_attn.kv")
+    M, K = a2.shape
+    N = w.shape[0]
+    if w.shape[1] != K or K % 8:
+        raise ValueError(f"gemm_attn: K mismatch {a2.shape} x {w.shape}")
+    if a2.stride(1) != 1 or a2.stride(0) % 8 != 0 or (a2.data_ptr() % 16):
+        a2 = a2.contiguous()
+    w = w.contiguous()
+    kv = kv.contiguous()
+    if bias is not None:
+        _bf16(bias, "gemm_attn.bias")
+        bias = bias.contiguous()
+    # the table's 128x64 row-layout tile for this shape (3-stage 12 or 2-stage 19)
+    hit = tuning.table().get(f"g:{M}:{N}:{K}:0")
+    tile = 12 if hit is not None and int(hit[0]) == 12 else 19
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
+    lp = lc = rowbuf = None
+    nparts = pcols = 0
+    eps = 0.0
+    if ln is not None:
+        (lp, nparts, pcols), lc, eps = ln
+        if nparts * pcols < K or lp.numel() < nparts * M * 2:
+            raise ValueError("gemm_attn: fused LayerNorm statistics do not match the input")
+        rowbuf = torch.empty(M * 2, dtype=torch.float32, device=a2.device)
+    QATTN_STATS[0] += 1
+    _lib.call("csk_gemm_ln_attn", _p(out), _p(a2), _p(w), _p(bias), M, N, K, a2.stride(0), w.stride(0), N,
+              int(rows_per_b), _p(lp), _p(lc), nparts, pcols, float(eps), _p(rowbuf), _p(kv), int(kv.shape[0]),
+              int(kv.shape[1]), float(scale), tile, _s())
+    return out
+
+
 def _pix_stride(t):
     """Pixel stride of an NHWC tensor / channel-slice view (None if not NHWC-strided)."""
     B, H, W, C = t.shape

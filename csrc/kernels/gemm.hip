@@ -573,6 +573,46 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   return dispatch<false>(a, tile, ksplit, stream);
 }
 
+// Cross-attention query projection with the attention in its epilogue:
+// O = softmax(((LN(A) W^T + bias) * scale) K^T) V per head (heads = N / 64,
+// head dim 64), K / V from kv [Bc][Skv][2][N/64][64] (Attention.context_kv),
+// sample m / rows_per_b.  Tiles 12 / 19 only (128 x 64, one head per tile, one
+// sample per tile: rows_per_b % 128 == 0); no residual / activation / split-K.
+CSK_API int csk_gemm_ln_attn(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, int lda,
+                             int ldb, int ldc, int rows_per_b, const void* ln_part, const void* ln_colsum,
+                             int ln_nparts, int ln_pcols, float ln_eps, void* ln_rowbuf, const void* kv, int Bc,
+                             int Skv, float scale, int tile, hipStream_t stream) {
+  if ((tile != 12 && tile != 19) || N % 64 != 0 || Skv < 1 || Skv > 80 || rows_per_b <= 0 || rows_per_b % 128 != 0 ||
+      M % rows_per_b != 0 || M / rows_per_b > Bc || ldc % 4 != 0 || !kv)
+    return (int)hipErrorInvalidValue;
+  if (K % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0) return (int)hipErrorInvalidValue;
+  if (ln_part && (!ln_colsum || ln_nparts <= 0 || ln_pcols <= 0 || (long long)ln_nparts * ln_pcols < K))
+    return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldc;
+  a.rows_per_b = rows_per_b; a.act = ACT_NONE; a.out_scale = 1.0f;
+  a.ldb2 = N;
+  a.ln_part = (const float*)ln_part; a.ln_colsum = (const float*)ln_colsum;
+  a.ln_nparts = ln_nparts; a.ln_pcols = ln_pcols; a.ln_eps = ln_eps;
+  a.a_end = a.A + (size_t)(M > 0 ? M - 1 : 0) * lda + K;
+  a.w_end = a.W + (size_t)(N > 0 ? N - 1 : 0) * ldb + K;
+  a.attn_kv = (const bf16_t*)kv;
+  a.attn_kv_end = a.attn_kv + (size_t)Bc * Skv * 2 * N;
+  a.attn_skv = Skv;
+  a.attn_sl2 = scale * 1.4426950408889634f;
+  if (M == 0) return 0;
+  if (ln_part && !g_ln_in_kernel) {
+    float* rows = (float*)ln_rowbuf;
+    if (!rows) return (int)hipErrorInvalidValue;
+    ln_rowstats_kernel<<<(M + 255) / 256, 256, 0, stream>>>((const float*)ln_part, rows, M, K, ln_nparts, ln_pcols,
+                                                           ln_eps);
+    a.ln_row = rows;
+  }
+  return dispatch<false>(a, tile, 1, stream);
+}
+
 CSK_API int csk_gemm(void* C, const void* A, const void* W, const void* bias, const void* bias2d, const void* res,
                      int M, int N, int K, int lda, int ldb, int ldc, int ldr, int rows_per_b, int act, float out_scale,
                      void* gn_part, int tile, int ksplit, void* ws, hipStream_t stream) {

@@ -2,6 +2,7 @@
 // register-staged pipeline; gemm_glds.hip: LDS-DMA multi-stage pipeline).
 #pragma once
 #include "common.h"
+#include "attn_tile.h"
 
 enum {
   ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GEGLU = 3, ACT_QGELU = 4,
@@ -109,6 +110,14 @@ struct GemmArgs {
   // one past the last element an LDS-DMA may read from A / W (CSK_DEBUG checks)
   const bf16_t* a_end;
   const bf16_t* w_end;
+  // attention epilogue (csk_gemm_ln_attn, 128x64 row-layout tiles): the tile's
+  // 64 output columns are ONE head's queries; they attend over that head's
+  // per-request K / V (attn_kv [Bc][attn_skv][2][N/64][64], sample m / rows_per_b)
+  // and the tile stores the attention output instead of the projection
+  const bf16_t* attn_kv;
+  const bf16_t* attn_kv_end;
+  int attn_skv;
+  float attn_sl2;  // softmax scale * log2(e)
 };
 
 #define ZERO_BYTES (128 * 1024)  // the LDS-DMA zero page (gemm_glds.hip: csk_init)
@@ -307,6 +316,106 @@ __device__ __forceinline__ int sw_pair(v4f& x, v4f& y, int f, int fq, float (&o)
   return (fq & 1) ? f * 16 + (fq - 1) * 4 : (f + 1) * 16 + fq * 4;
 }
 
+// Attention epilogue of the cross-attention query projection (SURVEY K8 + K9;
+// reference call site swarm/diffusion/diffusion_func.py:96): the 128x64 tile's
+// accumulators are the queries of one head for 128 rows of one sample, in row
+// layout — lane (row fr, head-dims 16 j + 4 g + r) — which is exactly the
+// B-fragment layout of S^T = K Q^T (attn_tile.h), so each wave attends its own
+// 32 rows over the head's K / V staged once per workgroup in LDS and stores
+// O = softmax(q K^T) V: the [M, C] query tensor never reaches memory and the
+// separate short-KV attention launch disappears.
+template <int BM, int WM, int NTHR, bool RAW>
+__device__ __forceinline__ void gemm_attn_epilogue(const GemmArgs& args, v4f (&acc)[BM / WM / 16][4], bf16_t* smem,
+                                                   int m0, int n0, const float2 (&ln_lane)[BM / WM / 16],
+                                                   bool ln_in) {
+  constexpr int WTM = BM / WM, MT = WTM / 16, KVR = 96, KVI = KVR * 64;
+  constexpr int CH = 2 * KVR * 8, CPT = (CH + NTHR - 1) / NTHR;  // 16-byte chunks of the two images
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wm = __builtin_amdgcn_readfirstlane(tid >> 6);  // WN == 1: the wave's row band
+  const int fr = lane & 15, g = lane >> 4;
+  const int M = args.M, H = args.N / 64, Skv = args.attn_skv;
+  const int h = n0 / 64, b = m0 / args.rows_per_b;
+  // K / V rows of (b, h), issued before the barrier that frees the main loop's LDS
+  uint4 kvv[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int q = tid + i * NTHR;
+    kvv[i] = make_uint4(0, 0, 0, 0);
+    if (q < CH) {
+      const int which = q / (KVR * 8), rem = q - which * (KVR * 8), row = rem >> 3, c = rem & 7;
+      const int rr = min(row, Skv - 1);  // rows past Skv repeat the last key: finite, masked below
+      const bf16_t* src = args.attn_kv + ((size_t)(b * Skv + rr) * 2 + which) * (H * 64) + h * 64 + c * 8;
+      CSK_DCHECK(src + 8 <= args.attn_kv_end, 60, rr, Skv);
+      kvv[i] = *reinterpret_cast<const uint4*>(src);
+    }
+  }
+  // queries: the fused LayerNorm correction and bias, scaled by scale * log2(e)
+  const bool lnf = args.ln_part != nullptr;
+  v8s qf[MT][2];
+  {
+    float4 cs[4], bq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + 16 * j + 4 * g;
+      cs[j] = lnf ? *reinterpret_cast<const float4*>(args.ln_colsum + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bq[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (args.bias) {
+        const uint2 u = *reinterpret_cast<const uint2*>(args.bias + col);
+        bq[j] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float mu = 0.f, rs = 1.f;
+      if (lnf && ln_in) {
+        mu = ln_lane[i].x;
+        rs = ln_lane[i].y;
+      } else if (lnf) {
+        const float2 st = *reinterpret_cast<const float2*>(args.ln_row + (size_t)min(m0 + wm * WTM + i * 16 + fr, M - 1) * 2);
+        mu = st.x;
+        rs = st.y;
+      }
+      v4f qv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c4[4] = {cs[j].x, cs[j].y, cs[j].z, cs[j].w};
+        const float b4[4] = {bq[j].x, bq[j].y, bq[j].z, bq[j].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qv[j][r] = __builtin_fmaf(rs, acc[i][j][r] - mu * c4[r], b4[r]);
+      }
+      qf[i][0] = at_pack8(qv[0], qv[1], args.attn_sl2);
+      qf[i][1] = at_pack8(qv[2], qv[3], args.attn_sl2);
+    }
+  }
+  bf16_t* ks = smem;
+  bf16_t* vs = smem + KVI;
+  epi_barrier<RAW>();  // the main loop's LDS reads are done
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int q = tid + i * NTHR;
+    if (q < CH) {
+      const int which = q / (KVR * 8), rem = q - which * (KVR * 8), row = rem >> 3, c = rem & 7;
+      *reinterpret_cast<uint4*>((which ? vs : ks) + at_off64(row, c)) = kvv[i];
+    }
+  }
+  epi_barrier<RAW>();
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    v4f o[4];
+    float inv;
+    at_attend_rowtile(ks, vs, qf[i], Skv, o, inv);
+    const int m = m0 + wm * WTM + i * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const uint2 w = make_uint2(pack2(o[dt][0] * inv, o[dt][1] * inv), pack2(o[dt][2] * inv, o[dt][3] * inv));
+        *reinterpret_cast<uint2*>(args.C + (size_t)m * args.ldc + n0 + 16 * dt + 4 * g) = w;
+      }
+    }
+  }
+}
+
 // SW: the accumulators are row-layout (the MFMA ran as B * A, C^T in registers):
 // lane = output row i*16 + fr, registers = 4 consecutive output columns
 // j*16 + fq*4 + r.  Lets the common short-K epilogue (bias / per-sample bias /
@@ -317,7 +426,8 @@ __device__ __forceinline__ int sw_pair(v4f& x, v4f& y, int f, int fq, float (&o)
 // kernel prologue (ln_merge_tile); a reference to a fixed-size array so the
 // values stay in registers (a pointer that may be null made hipcc keep the
 // array in scratch)
-template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false>
+template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false,
+          bool ATTN = false>
 __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],
                                                  bf16_t* smem, int m0, int n0, int split, float2 lnrow,
                                                  const float2 (&ln_lane)[BM / WM / 16], bool ln_in) {
@@ -362,6 +472,12 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
         }
       }
     return;
+  }
+  if constexpr (ATTN && SW && BN == 64 && WN == 1) {  // a separate instance: the others keep their registers
+    {
+      gemm_attn_epilogue<BM, WM, NTHR, RAW>(args, acc, smem, m0, n0, ln_lane, ln_in);
+      return;
+    }
   }
   if constexpr (SW) {
     // ---- direct row-vector stores (no fp32 LDS staging) ----

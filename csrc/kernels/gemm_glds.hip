@@ -38,7 +38,7 @@ constexpr int glds_min_waves() {
   return (BN == 160 && BM <= 128) ? 2 : 1;
 }
 
-template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST>
+template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST, bool ATTN = false>
 __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_kernel(const GemmArgs args) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     if (sum == 1234.5f) args.C[threadIdx.x] = f2bf(sum);  // keeps the MFMAs alive
     return;
   }
-  gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true>(args, acc, smem, m0, n0, split, lnrow, lnlane, lnl);
+  gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true, ATTN>(args, acc, smem, m0, n0, split, lnrow, lnlane, lnl);
 }
 
 template <int BM, int BN, int WM, int WN, int S>
@@ -278,6 +278,15 @@ static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s)
                     (size_t)(span + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
                     (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
   dim3 grid(tiles, ksplit);
+  if (a.attn_kv) {  // the query projection with the attention epilogue (csk_gemm_ln_attn)
+    if constexpr (BM == 128 && BN == 64 && WM == 4 && WN == 1) {
+      if (conv || !fast || ksplit != 1) return (int)hipErrorInvalidValue;
+      gemm_glds_kernel<BM, BN, WM, WN, S, false, true, true><<<grid, 256, 0, s>>>(a);
+      return (int)hipGetLastError();
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  }
   if (conv) {
     if (fast) gemm_glds_kernel<BM, BN, WM, WN, S, true, true><<<grid, 256, 0, s>>>(a);
     else gemm_glds_kernel<BM, BN, WM, WN, S, true, false><<<grid, 256, 0, s>>>(a);

@@ -34,9 +34,8 @@
 //            |B2: Wo_h landed|  out-proj h  |B3: Wq_{h+1}, K/V_{h+1} landed|
 // so every transfer has at least one compute phase to land in, and the waits
 // are counted (vmcnt) — the prefetches stay in flight across B1 / B2.
-#include "common.h"
+#include "attn_tile.h"
 
-typedef __attribute__((address_space(3))) v4s lds_v4s;
 typedef __attribute__((address_space(1))) const void* xa_gptr_t;
 typedef __attribute__((address_space(3))) void* xa_lptr_t;
 
@@ -74,24 +73,8 @@ __device__ __forceinline__ void xa_dma_off(const bf16_t* base, unsigned off, bf1
   xa_dma(base + off, dst);
 }
 
-// element offset of 16-byte chunk c of row r in a [rows][64] image (slot c ^ (r & 7))
-__device__ __forceinline__ int xa_off64(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
-
-__device__ __forceinline__ v8s xa_cat(v4s a, v4s b) { return v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
-
-// two 8-byte halves (head-dims d0..d0+3 and d0+16..d0+19) of row r of a [rows][64] image
-__device__ __forceinline__ v8s xa_perm_frag(const bf16_t* img, int r, int d0) {
-  const int c0 = d0 >> 3, h = d0 & 7;
-  const v4s a = *reinterpret_cast<const v4s*>(img + xa_off64(r, c0) + h);
-  const v4s b = *reinterpret_cast<const v4s*>(img + xa_off64(r, c0 + 2) + h);
-  return xa_cat(a, b);
-}
-
-__device__ __forceinline__ v8s xa_pack8(const v4f& lo, const v4f& hi, float s) {
-  const uint4 u = make_uint4(pack2(lo[0] * s, lo[1] * s), pack2(lo[2] * s, lo[3] * s), pack2(hi[0] * s, hi[1] * s),
-                             pack2(hi[2] * s, hi[3] * s));
-  return __builtin_bit_cast(v8s, u);
-}
+__device__ __forceinline__ int xa_off64(int r, int c) { return at_off64(r, c); }
+__device__ __forceinline__ v8s xa_pack8(const v4f& lo, const v4f& hi, float s) { return at_pack8(lo, hi, s); }
 
 // PROBE (profiling builds, wrong results by design; csk_set_xattn_probe): 1 = no
 // Q-projection MFMAs, 2 = no attention (S / softmax / PV), 4 = no out-projection
@@ -218,7 +201,6 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
   __syncthreads();
 
   const float sl2 = a.scale_log2;
-  const int qq = fr >> 2, pp = fr & 3;
   for (int h = 0; h < H; ++h) {
     const int cur = h & 1;
     const bool more = h + 1 < H;
@@ -289,58 +271,14 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
     // ---------------- attention over the Skv context tokens ----------------
     v8s of[RT][2];
     auto attend = [&](const bf16_t* ks) {
-    const bf16_t* vs = ks + KVI;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      v4f s[5];
-#pragma unroll
-      for (int kt = 0; kt < 5; ++kt) {
-        s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ds = 0; ds < 2; ++ds)
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa_perm_frag(ks, 16 * kt + fr, 32 * ds + 4 * g), qf[rt][ds],
-                                                          s[kt], 0, 0, 0);
+      for (int rt = 0; rt < RT; ++rt) {
+        v4f o[4];
+        float inv;
+        at_attend_rowtile(ks, ks + KVI, qf[rt], Skv, o, inv);
+        of[rt][0] = xa_pack8(o[0], o[1], inv);
+        of[rt][1] = xa_pack8(o[2], o[3], inv);
       }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 5; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (16 * kt + 4 * g + r >= Skv) s[kt][r] = -INFINITY;
-          mx = fmaxf(mx, s[kt][r]);
-        }
-      mx = max_rowgroups(mx);
-      float l = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 5; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[kt][r] - mx);
-          s[kt][r] = p;
-          l += p;
-        }
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-      v4f o[4];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k2 = 0; k2 < 3; ++k2) {
-        const v4f z = v4f{0.f, 0.f, 0.f, 0.f};
-        const v8s pf = xa_pack8(s[2 * k2], k2 < 2 ? s[2 * k2 + 1] : z, 1.0f);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int col = dt * 16 + 4 * pp;
-          const int r0 = k2 * 32 + 4 * g + qq, r1 = r0 + 16;
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + xa_off64(r0, col >> 3) + (col & 7)));
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vs + xa_off64(r1, col >> 3) + (col & 7)));
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa_cat(lo, hi), pf, o[dt], 0, 0, 0);
-        }
-      }
-      const float inv = l > 0.f ? 1.0f / l : 0.f;
-      of[rt][0] = xa_pack8(o[0], o[1], inv);
-      of[rt][1] = xa_pack8(o[2], o[3], inv);
-    }
     };
     if constexpr ((PROBE & 2) != 0) {
       for (int rt = 0; rt < RT; ++rt) {
@@ -358,13 +296,13 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
 
     // ---------------- out-projection of this head, accumulated ----------------
     v8s wof[2][2];
-    wof[0][0] = xa_perm_frag(s_wo, fr, 4 * g);
-    wof[0][1] = xa_perm_frag(s_wo, fr, 32 + 4 * g);
+    wof[0][0] = at_perm_frag(s_wo, fr, 4 * g);
+    wof[0][1] = at_perm_frag(s_wo, fr, 32 + 4 * g);
 #pragma unroll
     for (int nt = 0; nt < NNT; ++nt) {
       if (nt + 1 < NNT) {
-        wof[(nt + 1) & 1][0] = xa_perm_frag(s_wo, 16 * (nt + 1) + fr, 4 * g);
-        wof[(nt + 1) & 1][1] = xa_perm_frag(s_wo, 16 * (nt + 1) + fr, 32 + 4 * g);
+        wof[(nt + 1) & 1][0] = at_perm_frag(s_wo, 16 * (nt + 1) + fr, 4 * g);
+        wof[(nt + 1) & 1][1] = at_perm_frag(s_wo, 16 * (nt + 1) + fr, 32 + 4 * g);
       }
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds)
