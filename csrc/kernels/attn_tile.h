@@ -4,7 +4,7 @@
 //
 // Layouts (head dim 64, Skv <= 80 keys, images of 96 rows, rows past Skv
 // repeat a valid key and are masked):
-//   * K / V images: [96][64] bf16, 16-byte chunk c of row r at slot c ^ (r & 7);
+//   * K / V images: [96][64] bf16, 16-byte chunk c of row r at slot c ^ at_key(r);
 //   * the queries arrive as the B fragments of S^T = K Q^T: lane (fr, g) holds
 //     query row fr, head-dims {4g + r, 16 + 4g + r} (k-step 0) and
 //     {32 + 4g + r, 48 + 4g + r} (k-step 1) — exactly the row-layout
@@ -19,8 +19,16 @@
 
 typedef __attribute__((address_space(3))) v4s at_lds_v4s;
 
+// chunk swizzle key of row r: (r & 7) ^ ((r >> 3) & 1).  The 8-byte fragment
+// reads (at_perm_frag) take 16 consecutive rows per 32-lane bank group; with the
+// plain (r & 7) key rows r and r + 8 (128-byte rows: same bank half) hit the same
+// banks, a 2-way conflict on every K / Wo read (PMC: 1.5 conflict cycles per LDS
+// instruction in the fused block, profiles/pmc_unet_step_r6r_1.txt); flipping the
+// low bit for the second 8 rows spreads the 16 rows over all 64 banks
+__device__ __forceinline__ int at_key(int r) { return (r & 7) ^ ((r >> 3) & 1); }
+
 // element offset of 16-byte chunk c of row r in a [rows][64] image
-__device__ __forceinline__ int at_off64(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
+__device__ __forceinline__ int at_off64(int r, int c) { return r * 64 + ((c ^ at_key(r)) << 3); }
 
 __device__ __forceinline__ v8s at_cat(v4s a, v4s b) { return v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
 

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
       const int p = wid + NW * i;
       const int row = 8 * p + (lane >> 3), slot = lane & 7;
       CSK_DCHECK(row < C, 72, row, C);
-      xa_dma_off(a.wo, (unsigned)(row * C + h * 64 + 8 * (slot ^ (row & 7))), s_wo + 512 * p);
+      xa_dma_off(a.wo, (unsigned)(row * C + h * 64 + 8 * (slot ^ at_key(row))), s_wo + 512 * p);
     }
   };
   auto dma_kv = [&](int h, bf16_t* dst) {
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(NW * 64, 1) void xattn_block_kernel(const XattnArgs
       // rows past Skv repeat the last key: finite values whose scores are
       // masked to -inf and whose P is 0 (no per-lane pointer select)
       const int rr = min(row, Skv - 1);
-      const unsigned off = (unsigned)(((b * Skv + rr) * 2 + which) * (H * 64) + h * 64 + 8 * (slot ^ (row & 7)));
+      const unsigned off = (unsigned)(((b * Skv + rr) * 2 + which) * (H * 64) + h * 64 + 8 * (slot ^ at_key(row)));
       CSK_DCHECK(a.kv + off + 8 <= a.kv_end, 73, row, Skv);
       xa_dma_off(a.kv, off, dst + 512 * p);
     }
