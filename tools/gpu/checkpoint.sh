@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4 checkpoint: full GPU suite, smoke, headline bench, secondary configs.
+# Checkpoint: full GPU suite, smoke, headline bench, secondary configs (usage: bash tools/gpu/checkpoint.sh TAG).
 TAG=${1:-x}
 mkdir -p gpurun_out
 O=gpurun_out

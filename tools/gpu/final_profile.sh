@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4 final-tree profiling: kernel tests (incl. the probe-act guard), per-call
+# Final-tree profiling: kernel tests (incl. the probe-act guard), per-call
 # UNet step profile, PMC passes over the UNet step and the VAE decode.
 TAG=${1:-x}
 mkdir -p gpurun_out
