@@ -138,10 +138,57 @@ class AutoencoderKL(Prepared):
         else:  # decoder-only: a full checkpoint's encoder tensors are expected extras
             self.checkpoint_ignore = ("encoder.", "quant_conv.")
 
-    def decode(self, z):
-        """z: NHWC latents (already divided by scaling_factor) -> NHWC [-1, 1] image."""
+    # Output pixels per decode call above which the decoder runs one sample at a
+    # time (slicing) and in overlapping spatial tiles (tiling) — the reference
+    # turns diffusers' enable_vae_slicing / enable_vae_tiling on for low-memory
+    # GPUs (swarm/diffusion/diffusion_func.py:89-92).  With 288 GB of HBM a
+    # whole 4 x 2048^2 decode fits, so only larger outputs take this path.
+    SLICE_PIXELS = 4 * 2048 * 2048
+    TILE_PIXELS = 4096 * 4096
+
+    @property
+    def upscale(self) -> int:
+        return 2 ** (len(self.cfg.block_out_channels) - 1)
+
+    def _decode_full(self, z):
         z = z.to(self.post_quant_conv.weight.dtype)
         return self.decoder(self.post_quant_conv(z))
+
+    def decode(self, z):
+        """z: NHWC latents (already divided by scaling_factor) -> NHWC [-1, 1] image."""
+        B, h, w = z.shape[0], z.shape[1], z.shape[2]
+        px = h * w * self.upscale * self.upscale
+        if px > self.TILE_PIXELS:
+            return torch.cat([self.tiled_decode(z[i:i + 1]) for i in range(B)])
+        if B > 1 and B * px > self.SLICE_PIXELS:
+            return torch.cat([self._decode_full(z[i:i + 1]) for i in range(B)])
+        return self._decode_full(z)
+
+    def tiled_decode(self, z, tile: int = 64, overlap: float = 0.25):
+        """Decode in ``tile``-latent tiles overlapping by ``overlap``: each tile
+        is linearly cross-faded into its upper and left neighbours over the
+        overlap and cropped to the stride (diffusers' tiled VAE decode
+        semantics, NHWC).  Bounded memory for arbitrarily large outputs."""
+        f = self.upscale
+        stride = max(1, int(tile * (1 - overlap)))
+        blend = int(tile * f * overlap)
+        keep = tile * f - blend
+        H, W = z.shape[1], z.shape[2]
+        rows = [[self._decode_full(z[:, i:i + tile, j:j + tile]) for j in range(0, W, stride)]
+                for i in range(0, H, stride)]
+        out_rows = []
+        for i, row in enumerate(rows):
+            res = []
+            for j, t in enumerate(row):
+                # in place, as diffusers: a tile's neighbours below / to the right
+                # blend against its already cross-faded pixels
+                if i > 0:
+                    _blend_(rows[i - 1][j], t, blend, dim=1)
+                if j > 0:
+                    _blend_(row[j - 1], t, blend, dim=2)
+                res.append(t[:, :keep, :keep])
+            out_rows.append(torch.cat(res, dim=2))
+        return torch.cat(out_rows, dim=1)[:, :H * f, :W * f]
 
     def encode(self, x, generator=None, sample=True):
         """x: NHWC [-1, 1] image -> NHWC latents (NOT yet scaled)."""
@@ -154,3 +201,20 @@ class AutoencoderKL(Prepared):
         std = torch.exp(0.5 * logvar)
         noise = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=torch.float32)
         return mean + std * noise
+
+
+def _blend_(a, b, extent, dim):
+    """In place: the first ``extent`` rows (dim 1) / columns (dim 2) of b
+    cross-faded from the trailing ``extent`` of its neighbour ``a`` (weight
+    y / extent on b)."""
+    e = min(a.shape[dim], b.shape[dim], extent)
+    if e <= 0:
+        return b
+    w = torch.arange(e, device=b.device, dtype=torch.float32) / e
+    shape = [1, 1, 1, 1]
+    shape[dim] = e
+    w = w.view(shape)
+    tail = a.narrow(dim, a.shape[dim] - e, e).float()
+    head = b.narrow(dim, 0, e).float()
+    b.narrow(dim, 0, e).copy_((tail * (1 - w) + head * w).to(b.dtype))
+    return b
