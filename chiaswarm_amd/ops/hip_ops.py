@@ -279,9 +279,10 @@ def gemm_attn(a2, w, bias, kv, scale, rows_per_b, ln=None):
     if bias is not None:
         _bf16(bias, "gemm_attn.bias")
         bias = bias.contiguous()
-    # the table's 128x64 row-layout tile for this shape (3-stage 12 or 2-stage 19)
-    hit = tuning.table().get(f"g:{M}:{N}:{K}:0")
-    tile = 12 if hit is not None and int(hit[0]) == 12 else 19
+    # 128x64 row-layout tile: 3-stage (12) for the long-K C = 1280 projections,
+    # 2-stage (19) otherwise (18.3 vs 19.1 us at K = 1280, 21.7 vs 18.9 at K = 640;
+    # profiles/qattnbench_r7a.txt)
+    tile = 12 if K >= 1280 else 19
     out = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
     lp = lc = rowbuf = None
     nparts = pcols = 0
