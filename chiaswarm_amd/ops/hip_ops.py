@@ -261,7 +261,7 @@ def qattn_ok(x, kv, rows_per_b) -> bool:
             and (M // 128) * (C // 64) >= QATTN_MIN_TILES)
 
 
-def gemm_attn(a2, w, bias, kv, scale, rows_per_b, ln=None):
+def gemm_attn(a2, w, bias, kv, scale, rows_per_b, ln=None, tile=None):
     """Attention output O [M, C] of the cross-attention whose query projection
     is ``a2 @ w^T + bias`` (``ln = (rows, colsum, eps)``: LayerNorm folded as in
     ``gemm``), over the per-request ``kv`` [Bc, Skv, 2, H, 64]."""
@@ -282,7 +282,10 @@ def gemm_attn(a2, w, bias, kv, scale, rows_per_b, ln=None):
     # 128x64 row-layout tile: 3-stage (12) for the long-K C = 1280 projections,
     # 2-stage (19) otherwise (18.3 vs 19.1 us at K = 1280, 21.7 vs 18.9 at K = 640;
     # profiles/qattnbench_r7a.txt)
-    tile = 12 if K >= 1280 else 19
+    if tile is None:
+        tile = 12 if K >= 1280 else 19
+    elif tile not in (12, 19):
+        raise ValueError("gemm_attn: tile 12 or 19")
     out = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
     lp = lc = rowbuf = None
     nparts = pcols = 0

@@ -87,7 +87,7 @@ def test_composed_reference_matches_unfused_cpu():
 def test_gemm_attn_kernel_vs_fp32(gpu, any_grid, B, S, C, Skv, tile):
     """Unfolded (plain query projection of LayerNorm'd rows) and folded
     (LayerNorm from the producer's row statistics inside the GEMM)."""
-    from chiaswarm_amd.ops import hip_ops, tuning
+    from chiaswarm_amd.ops import hip_ops
 
     blk, x, kv = _setup(gpu, torch.bfloat16, B=B, S=S, C=C, Skv=Skv)
     a2 = blk.attn2
@@ -96,27 +96,17 @@ def test_gemm_attn_kernel_vs_fp32(gpu, any_grid, B, S, C, Skv, tile):
 
     twin = copy.deepcopy(blk).cpu().float()  # Module.float() is in place: keep blk bf16 on the GPU
     ref = _ref_o(x.cpu().float(), twin, kv.cpu().float())
-    M, K = B * S, C
-    key = f"g:{M}:{C}:{K}:0"
-    t = tuning.table()
-    old = t.get(key)
-    t[key] = [tile, 1, 0.0]
-    try:
-        xn = ops.layer_norm(x, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
-        o = hip_ops.gemm_attn(xn.reshape(M, C), a2.to_q.weight, a2.to_q.bias, kv, a2.scale, S)
-        assert rel(o.view(B, S, C).cpu(), ref) < 2e-2
-        # LayerNorm folded: x produced by a GEMM that emits row statistics
-        x1 = ops.gemm(x, blk.attn1.to_out[0].weight, None, row_stats=True)
-        w2, colsum, b2 = ops.fold_layer_norm(a2.to_q.weight, a2.to_q.bias, blk.norm2.weight, blk.norm2.bias)
-        o2 = hip_ops.gemm_attn(x1.reshape(M, C), w2, b2, kv, a2.scale, S, ln=(x1._csk_rows, colsum,
-                                                                               float(blk.norm2.eps)))
-        ref2 = _ref_o(x1.cpu().float(), twin, kv.cpu().float())
-        assert rel(o2.view(B, S, C).cpu(), ref2) < 2e-2
-    finally:
-        if old is None:
-            t.pop(key, None)
-        else:
-            t[key] = old
+    M = B * S
+    xn = ops.layer_norm(x, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
+    o = hip_ops.gemm_attn(xn.reshape(M, C), a2.to_q.weight, a2.to_q.bias, kv, a2.scale, S, tile=tile)
+    assert rel(o.view(B, S, C).cpu(), ref) < 2e-2
+    # LayerNorm folded: x produced by a GEMM that emits row statistics
+    x1 = ops.gemm(x, blk.attn1.to_out[0].weight, None, row_stats=True)
+    w2, colsum, b2 = ops.fold_layer_norm(a2.to_q.weight, a2.to_q.bias, blk.norm2.weight, blk.norm2.bias)
+    o2 = hip_ops.gemm_attn(x1.reshape(M, C), w2, b2, kv, a2.scale, S,
+                           ln=(x1._csk_rows, colsum, float(blk.norm2.eps)), tile=tile)
+    ref2 = _ref_o(x1.cpu().float(), twin, kv.cpu().float())
+    assert rel(o2.view(B, S, C).cpu(), ref2) < 2e-2
 
 
 @pytest.mark.gpu

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from chiaswarm_amd import ops  # noqa: E402
-from chiaswarm_amd.ops import _lib, hip_ops, tuning  # noqa: E402
+from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
 
 SHAPES = [(8, 1024, 640), (8, 256, 1280), (2, 1024, 1280), (2, 4096, 640)]
 
@@ -42,24 +42,16 @@ def timed(fn, reps=20):
 def main():
     _lib.load()
     dev = torch.device("cuda", 0)
-    t = tuning.table()
     for B, S, C in SHAPES:
         M = B * S
         x = torch.randn(M, C, device=dev).bfloat16()
         w = (torch.randn(C, C, device=dev) * C ** -0.5).bfloat16()
         bias = torch.randn(C, device=dev).bfloat16()
         kv = torch.randn(B, 77, 2, C // 64, 64, device=dev).bfloat16()
-        key = f"g:{M}:{C}:{C}:0"
-        old = t.get(key)
         line = f"B{B} S{S} C{C}:"
         for tile in (19, 12):
-            t[key] = [tile, 1, 0.0]
-            us = timed(lambda: hip_ops.gemm_attn(x, w, bias, kv, 0.125, S))
+            us = timed(lambda: hip_ops.gemm_attn(x, w, bias, kv, 0.125, S, tile=tile))
             line += f"  qattn tile {tile} {us:6.1f} us"
-        if old is None:
-            t.pop(key, None)
-        else:
-            t[key] = old
         q3 = x.view(B, S, C)
 
         def unfused():
