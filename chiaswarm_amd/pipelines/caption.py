@@ -14,10 +14,14 @@ the implementation:
 * ``BlipForQuestionAnswering``: visual question answering — the prompt is the
   question (the reference's "conditional image captioning and VQA" branch,
   :21-23);
+* ``GitForCausalLM`` (+ ``GitProcessor`` / ``AutoProcessor``): GIT captioning
+  (``models/git.py``), conditional on the prompt when one is given ([CLS] +
+  prompt tokens, the GIT conditional-captioning / VQA form);
 
 any other class is refused with a ``ValueError`` that names it (a fatal job
 error: retrying cannot help).  Model geometry comes from the checkpoint's
-``config.json`` (a transformers ``BlipConfig``), name heuristics only without one.
+``config.json`` (a transformers ``BlipConfig`` / ``GitConfig``), name heuristics
+only without one.
 """
 from __future__ import annotations
 
@@ -29,18 +33,20 @@ from ..models.wordpiece import WordPiece
 from ..output.processor import make_text_result
 from ..runtime.model_cache import cache, find_weights
 
-MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa"}
-PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", None}
+MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git"}
+PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", "GitProcessor", "CLIPImageProcessor", None}
 
 
 def resolve_task(params: dict | None, model_name: str) -> str:
-    """'caption' | 'vqa' from the hive's class names; ValueError for anything else."""
+    """'caption' | 'vqa' | 'git' from the hive's class names; ValueError for anything else."""
     params = params or {}
     mt, pt = params.get("model_type"), params.get("processor_type")
     if pt not in PROCESSOR_TYPES:
-        raise ValueError(f"img2txt: processor_type {pt!r} is not supported (supported: BlipProcessor, AutoProcessor)")
+        raise ValueError(f"img2txt: processor_type {pt!r} is not supported "
+                         "(supported: BlipProcessor, GitProcessor, AutoProcessor)")
     if mt is None:
-        return "vqa" if "vqa" in model_name.lower() else "caption"
+        n = model_name.lower()
+        return "vqa" if "vqa" in n else ("git" if "/git-" in n or n.startswith("git-") else "caption")
     if mt not in MODEL_TYPES:
         raise ValueError(f"img2txt: model_type {mt!r} is not supported "
                          f"(supported: {', '.join(sorted(MODEL_TYPES))})")
@@ -57,7 +63,45 @@ def _config(model_name: str, w: str | None) -> BlipConfig:
     return TINY_BLIP if n.startswith("tiny") else (BLIP_LARGE if "large" in n else BLIP_BASE)
 
 
+def _git_config(model_name: str, w: str | None):
+    from ..models.git import GIT_BASE, GIT_LARGE, TINY_GIT, GitConfig
+    from ..models.hf_config import component_config
+
+    raw = component_config(w, "") if w else None
+    if raw is not None and "vision_config" in raw:
+        return GitConfig.from_hf(raw)
+    n = model_name.lower()
+    return TINY_GIT if n.startswith("tiny") else (GIT_LARGE if "large" in n else GIT_BASE)
+
+
+def load_git(model_name: str, device: str):
+    def make():
+        from ..models.git import GitCaptioner, convert_hf_git
+
+        w = find_weights(model_name)
+        cfg = _git_config(model_name, w)
+        dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+        with torch.device(device):
+            m = GitCaptioner(cfg).to(dt).eval().requires_grad_(False)
+        init_random_fast_(m, seed=11)
+        m.weights_source = "random-init"
+        if w:
+            from ..models.weights import _read_dir, load_into
+
+            sd = _read_dir(w)
+            if sd:
+                m.load_report = load_into(m, convert_hf_git(sd), name=model_name)
+                m.weights_source = w
+        prepare_model(m)
+        return m, WordPiece(w, cfg.vocab)
+
+    return cache().get(("git", model_name, device), make)
+
+
 def load_captioner(model_name: str, device: str, task: str = "caption"):
+    if task == "git":
+        return load_git(model_name, device)
+
     def make():
         w = find_weights(model_name)
         cfg = _config(model_name, w)
@@ -86,7 +130,7 @@ def caption_callback(device_identifier, model_name, **kwargs):
     config, results = {}, {}
     task = resolve_task(kwargs.pop("parameters", None), model_name)  # unsupported classes: fatal ValueError
     try:
-        print("Image captioning..." if task == "caption" else "Visual question answering...")
+        print("Visual question answering..." if task == "vqa" else "Image captioning...")
         model, tok = load_captioner(model_name, device_identifier, task)
         image = kwargs["image"]
         prompt = kwargs.get("prompt") or ""

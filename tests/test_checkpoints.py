@@ -210,8 +210,10 @@ def test_img2txt_class_names(tmp_path):
     assert resolve_task({"processor_type": "BlipProcessor", "model_type": "BlipForQuestionAnswering"},
                         "Salesforce/blip-vqa-base") == "vqa"
     assert resolve_task(None, "Salesforce/blip-vqa-base") == "vqa"
-    with pytest.raises(ValueError, match="GitForCausalLM"):
-        resolve_task({"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"}, "microsoft/git-base")
+    assert resolve_task({"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"}, "microsoft/git-base") \
+        == "git"
+    with pytest.raises(ValueError, match="Blip2ForConditionalGeneration"):
+        resolve_task({"processor_type": "AutoProcessor", "model_type": "Blip2ForConditionalGeneration"}, "x")
     with pytest.raises(ValueError, match="ViltProcessor"):
         resolve_task({"processor_type": "ViltProcessor", "model_type": "BlipForQuestionAnswering"}, "x")
 

@@ -166,9 +166,14 @@ def test_img2txt_vqa_and_unsupported_class_envelopes(monkeypatch):
     assert "fatal_error" not in r and "error" not in r["pipeline_config"], r["pipeline_config"]
     blob = json.loads(base64.b64decode(r["artifacts"]["primary"]["blob"]))
     assert blob["caption"] == r["pipeline_config"]["caption"]
-    bad = dict(job, id="v2", parameters={"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"})
-    r2 = synchronous_do_work_function(bad, Device("cpu"))
-    assert r2.get("fatal_error") is True and "GitForCausalLM" in r2["pipeline_config"]["error"]
+    git = dict(job, id="v2", model_name="tiny/git", prompt="",
+               parameters={"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"})
+    r2 = synchronous_do_work_function(git, Device("cpu"))
+    assert "fatal_error" not in r2 and "error" not in r2["pipeline_config"], r2["pipeline_config"]
+    bad = dict(job, id="v3", parameters={"processor_type": "AutoProcessor",
+                                         "model_type": "Blip2ForConditionalGeneration"})
+    r3 = synchronous_do_work_function(bad, Device("cpu"))
+    assert r3.get("fatal_error") is True and "Blip2ForConditionalGeneration" in r3["pipeline_config"]["error"]
 
 
 def test_unet_cfg_shared_prefix_and_temb_table_cpu():
