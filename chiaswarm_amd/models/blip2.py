@@ -1,0 +1,243 @@
+"""BLIP-2 image captioning / prompted VQA with an OPT language model
+(transformers ``Blip2ForConditionalGeneration`` + ``Blip2Processor``, the
+``Salesforce/blip2-opt-*`` checkpoints).  Reference: the hive names the
+processor / model classes at swarm/captioning/caption_image.py:11-29 and the
+reference instantiates whatever transformers class it is given.
+
+Three stages, all on the shared kernels (fused-QKV GEMMs, flash attention,
+LayerNorm, GEMM epilogues):
+
+* vision: ViT (post-LN on every token; EVA ViT-g/14 geometry by default,
+  q/v biases with a zero k bias);
+* Q-Former: 32 learned query tokens through a BERT-style post-LN stack that
+  cross-attends to the image tokens every ``cross_attention_frequency``
+  layers (query FFN only: captioning feeds no text to the Q-Former);
+* OPT decoder (pre-LN, ReLU MLP, learned positions with offset 2, LM head tied
+  to the token embeddings) over ``[projected queries; </s>; prompt]``.
+
+Greedy decode with transformers' default ``max_length=20`` counted on the text
+part (``</s>`` + prompt + generated; the query embeddings are not tokens),
+stopping at ``</s>``.  Every step re-runs the (<= ~60-row) sequence: at that
+size each GEMM streams its weights once either way, so a KV cache would save
+no HBM traffic.  FlanT5-based BLIP-2 checkpoints are refused by name.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+import torch
+import torch.nn as nn
+from PIL import Image
+
+from .layers import LayerNorm, Linear
+from .transformer import PostLNBlock, PreLNBlock, ViT
+
+MEAN = np.array([0.48145466, 0.4578275, 0.40821073], np.float32)
+STD = np.array([0.26862954, 0.26130258, 0.27577711], np.float32)
+
+
+@dataclasses.dataclass
+class Blip2Config:
+    image_size: int = 224
+    patch: int = 14
+    vision_dim: int = 1408
+    vision_depth: int = 39
+    vision_heads: int = 16
+    vision_mlp: int = 6144
+    vision_eps: float = 1e-6
+    q_dim: int = 768
+    q_depth: int = 12
+    q_heads: int = 12
+    q_mlp: int = 3072
+    q_eps: float = 1e-12
+    cross_freq: int = 2
+    num_query: int = 32
+    lm_dim: int = 2560
+    lm_depth: int = 32
+    lm_heads: int = 32
+    lm_ffn: int = 10240
+    lm_eps: float = 1e-5
+    vocab: int = 50272
+    max_pos: int = 2048
+    bos_id: int = 2
+    eos_id: int = 2
+    pad_id: int = 1
+
+    @classmethod
+    def from_hf(cls, cfg: dict) -> "Blip2Config":
+        """A transformers ``Blip2Config`` config.json (vision / qformer / text
+        sub-configs; the text model must be OPT)."""
+        v, q, t = cfg.get("vision_config") or {}, cfg.get("qformer_config") or {}, cfg.get("text_config") or {}
+        lm = t.get("model_type", "opt")
+        if lm != "opt":
+            raise ValueError(f"img2txt: BLIP-2 with a {lm!r} language model is not supported (OPT only)")
+        if t.get("word_embed_proj_dim", t.get("hidden_size", 2560)) != t.get("hidden_size", 2560):
+            raise ValueError("img2txt: OPT with word_embed_proj_dim != hidden_size is not supported")
+        return cls(image_size=v.get("image_size", 224), patch=v.get("patch_size", 14),
+                   vision_dim=v.get("hidden_size", 1408), vision_depth=v.get("num_hidden_layers", 39),
+                   vision_heads=v.get("num_attention_heads", 16), vision_mlp=v.get("intermediate_size", 6144),
+                   vision_eps=v.get("layer_norm_eps", 1e-6), q_dim=q.get("hidden_size", 768),
+                   q_depth=q.get("num_hidden_layers", 12), q_heads=q.get("num_attention_heads", 12),
+                   q_mlp=q.get("intermediate_size", 3072), q_eps=q.get("layer_norm_eps", 1e-12),
+                   cross_freq=q.get("cross_attention_frequency", 2), num_query=cfg.get("num_query_tokens", 32),
+                   lm_dim=t.get("hidden_size", 2560), lm_depth=t.get("num_hidden_layers", 32),
+                   lm_heads=t.get("num_attention_heads", 32), lm_ffn=t.get("ffn_dim", 10240),
+                   vocab=t.get("vocab_size", 50272), max_pos=t.get("max_position_embeddings", 2048),
+                   bos_id=t.get("bos_token_id", 2), eos_id=t.get("eos_token_id", 2), pad_id=t.get("pad_token_id", 1))
+
+
+BLIP2_OPT_2_7B = Blip2Config()
+BLIP2_OPT_6_7B = Blip2Config(lm_dim=4096, lm_ffn=16384)
+TINY_BLIP2 = Blip2Config(image_size=28, patch=14, vision_dim=32, vision_depth=2, vision_heads=2, vision_mlp=64,
+                         q_dim=32, q_depth=2, q_heads=2, q_mlp=64, num_query=4, lm_dim=32, lm_depth=2, lm_heads=2,
+                         lm_ffn=64, vocab=100, max_pos=64)
+
+_Q = {"attention.attention.query": "attn.q", "attention.attention.key": "attn.k",
+      "attention.attention.value": "attn.v", "attention.output.dense": "attn.o", "attention.output.LayerNorm": "ln1",
+      "crossattention.attention.query": "cross.q", "crossattention.attention.key": "cross.k",
+      "crossattention.attention.value": "cross.v", "crossattention.output.dense": "cross.o",
+      "crossattention.output.LayerNorm": "ln_x", "intermediate_query.dense": "fc1", "output_query.dense": "fc2",
+      "output_query.LayerNorm": "ln2"}
+_V = {"self_attn.projection": "attn.o", "layer_norm1": "ln1", "layer_norm2": "ln2", "mlp.fc1": "fc1",
+      "mlp.fc2": "fc2"}
+_LM = {"self_attn.q_proj": "attn.q", "self_attn.k_proj": "attn.k", "self_attn.v_proj": "attn.v",
+       "self_attn.out_proj": "attn.o", "self_attn_layer_norm": "ln1", "final_layer_norm": "ln2", "fc1": "fc1",
+       "fc2": "fc2"}
+
+
+def _sub(rest: str, table: dict) -> str | None:
+    for a, b in table.items():
+        if rest.startswith(a + "."):
+            return b + rest[len(a):]
+    return None
+
+
+def convert_hf_blip2(sd: dict) -> dict:
+    """transformers ``Blip2ForConditionalGeneration`` (OPT) state dict -> this
+    module's keys.  Vision attention biases come either as the fused
+    ``qkv.bias`` or as the original checkpoints' ``q_bias`` / ``v_bias`` (k bias
+    zero); the Q-Former's text FFN (``intermediate.`` / ``output.``, unused
+    without Q-Former text input) is dropped; the LM head is tied."""
+    out: dict = {}
+    for k, v in sd.items():
+        if k.endswith("position_ids") or k == "language_model.lm_head.weight":
+            continue
+        if k == "query_tokens":
+            out[k] = v.reshape(v.shape[-2], v.shape[-1])
+        elif k.startswith("vision_model.embeddings."):
+            r = k.removeprefix("vision_model.embeddings.")
+            if r == "class_embedding":
+                v = v.reshape(-1)
+            elif r == "position_embedding":
+                v = v.reshape(v.shape[-2], v.shape[-1])
+            out["vision_model." + r] = v
+        elif k.startswith("vision_model.post_layernorm."):
+            out["vision_model.post_ln." + k.rsplit(".", 1)[1]] = v
+        elif k.startswith("vision_model.encoder.layers."):
+            n, rest = k.removeprefix("vision_model.encoder.layers.").split(".", 1)
+            pre = f"vision_model.layers.{n}.attn."
+            if rest == "self_attn.qkv.weight" or rest == "self_attn.qkv.bias":
+                for name, part in zip("qkv", v.chunk(3, 0)):
+                    out[pre + f"{name}." + rest.rsplit(".", 1)[1]] = part.contiguous()
+            elif rest == "self_attn.q_bias":
+                out[pre + "q.bias"] = v
+                out.setdefault(pre + "k.bias", torch.zeros_like(v))
+            elif rest == "self_attn.v_bias":
+                out[pre + "v.bias"] = v
+            else:
+                s = _sub(rest, _V)
+                out[f"vision_model.layers.{n}.{s}" if s else k] = v
+        elif k.startswith("qformer.layernorm."):
+            out["qformer_ln." + k.rsplit(".", 1)[1]] = v
+        elif k.startswith("qformer.encoder.layer."):
+            n, rest = k.removeprefix("qformer.encoder.layer.").split(".", 1)
+            if rest.startswith(("intermediate.", "output.")):
+                continue
+            s = _sub(rest, _Q)
+            out[f"qformer.{n}.{s}" if s else k] = v
+        elif k.startswith("language_projection."):
+            out[k] = v
+        elif k.startswith("language_model.model.decoder."):
+            r = k.removeprefix("language_model.model.decoder.")
+            if r.startswith("layers."):
+                n, rest = r.removeprefix("layers.").split(".", 1)
+                s = _sub(rest, _LM)
+                out[f"lm.{n}.{s}" if s else k] = v
+            elif r.startswith("final_layer_norm."):
+                out["lm_ln." + r.rsplit(".", 1)[1]] = v
+            elif r == "embed_tokens.weight":
+                out["embed_tokens.weight"] = v
+            elif r == "embed_positions.weight":
+                out["embed_positions.weight"] = v
+            else:
+                out[k] = v
+        else:
+            out[k] = v  # unknown keys surface as a CheckpointMismatch in load_into
+    return out
+
+
+class Blip2Captioner(nn.Module):
+    def __init__(self, cfg: Blip2Config = BLIP2_OPT_2_7B):
+        super().__init__()
+        self.cfg = cfg
+        self.vision_model = ViT(cfg.image_size, cfg.patch, cfg.vision_dim, cfg.vision_depth, cfg.vision_heads,
+                                cfg.vision_mlp, eps=cfg.vision_eps)
+        self.query_tokens = nn.Parameter(torch.zeros(cfg.num_query, cfg.q_dim))
+        self.qformer_ln = LayerNorm(cfg.q_dim, eps=cfg.q_eps)
+        self.qformer = nn.ModuleList([
+            PostLNBlock(cfg.q_dim, cfg.q_heads, cfg.q_mlp, cross_dim=cfg.vision_dim if i % cfg.cross_freq == 0 else None,
+                        eps=cfg.q_eps) for i in range(cfg.q_depth)])
+        self.language_projection = Linear(cfg.q_dim, cfg.lm_dim)
+        self.embed_tokens = nn.Embedding(cfg.vocab, cfg.lm_dim)
+        self.embed_positions = nn.Embedding(cfg.max_pos + 2, cfg.lm_dim)
+        self.lm = nn.ModuleList([PreLNBlock(cfg.lm_dim, cfg.lm_heads, cfg.lm_ffn, act="relu", eps=cfg.lm_eps)
+                                 for _ in range(cfg.lm_depth)])
+        self.lm_ln = LayerNorm(cfg.lm_dim, eps=cfg.lm_eps)
+
+    def preprocess(self, image: Image.Image) -> torch.Tensor:
+        """BlipImageProcessor: bicubic resize to image_size², CLIP mean / std; NHWC."""
+        s = self.cfg.image_size
+        a = np.asarray(image.convert("RGB").resize((s, s), Image.Resampling.BICUBIC), np.float32) / 255.0
+        return torch.from_numpy((a - MEAN) / STD)[None]
+
+    @torch.no_grad()
+    def image_prefix(self, pixels: torch.Tensor) -> torch.Tensor:
+        """Projected Q-Former query outputs [1, num_query, lm_dim]: the language
+        model's input embeddings ahead of the text."""
+        dt = self.embed_tokens.weight.dtype
+        img = self.vision_model(pixels.to(dt))
+        q = self.qformer_ln(self.query_tokens[None].to(dt))
+        for blk in self.qformer:
+            q = blk(q, ctx=img)
+        return self.language_projection(q)
+
+    @torch.no_grad()
+    def text_logits(self, prefix: torch.Tensor, ids: list[int]) -> torch.Tensor:
+        """Next-token logits [vocab] for [prefix embeddings; embed(ids)]."""
+        dev = self.embed_tokens.weight.device
+        t = torch.tensor([ids], device=dev)
+        x = torch.cat([prefix, self.embed_tokens(t)], 1)
+        x = x + self.embed_positions.weight[2: 2 + x.shape[1]][None]
+        for blk in self.lm:
+            x = blk(x, causal=True)
+        h = self.lm_ln(x[:, -1:])
+        return (h.float() @ self.embed_tokens.weight.float().t())[0, -1]
+
+    @torch.no_grad()
+    def generate(self, image: Image.Image, prefix_ids: list[int], max_new_tokens: int | None = None,
+                 max_length: int = 20) -> list[int]:
+        """Greedy decode from ``</s> + prefix`` after the image queries; returns
+        prefix + generated ids (without the leading ``</s>``)."""
+        if max_new_tokens is None:
+            max_new_tokens = max(0, max_length - 1 - len(prefix_ids))
+        prefix = self.image_prefix(self.preprocess(image).to(self.embed_tokens.weight.device))
+        ids = [self.cfg.bos_id] + list(prefix_ids)
+        out = []
+        for _ in range(max_new_tokens):
+            nxt = int(self.text_logits(prefix, ids).argmax())
+            if nxt == self.cfg.eos_id:
+                break
+            ids.append(nxt)
+            out.append(nxt)
+        return list(prefix_ids) + out

@@ -1,4 +1,4 @@
-"""CLIP byte-level BPE tokenizer (own implementation).
+r"""CLIP byte-level BPE tokenizer (own implementation).
 
 Loads a HF ``tokenizer/`` directory (``vocab.json`` + ``merges.txt`` and, when
 present, ``tokenizer_config.json`` / ``special_tokens_map.json`` for the
@@ -258,6 +258,18 @@ class ByteBPETokenizer(CLIPTokenizer):
                 h = int.from_bytes(hashlib.blake2b(tok.encode(), digest_size=8).digest(), "little")
                 ids.append(h % (self.vocab_size - 4) + 4)
         return ids
+
+    def decode(self, ids: list[int]) -> str:
+        """Text of ``ids`` with bos / eos / pad dropped (``skip_special_tokens``)."""
+        skip = {self._bos, self._eos, self._pad_id}
+        ids = [i for i in ids if i not in skip]
+        if self.encoder is None:
+            return " ".join(f"w{i}" for i in ids)
+        if not hasattr(self, "_decoder"):
+            self._decoder = {v: k for k, v in self.encoder.items()}
+            self._byte_decoder = {c: b for b, c in self.byte_encoder.items()}
+        text = "".join(self._decoder.get(i, "") for i in ids)
+        return bytes(self._byte_decoder[c] for c in text if c in self._byte_decoder).decode("utf-8", "replace")
 
     def __call__(self, texts: list[str] | str, pad: bool = False) -> list[list[int]]:  # type: ignore[override]
         """Unpadded id lists ([bos] ids [eos]); attention needs no padding mask."""

@@ -17,10 +17,13 @@ the implementation:
 * ``GitForCausalLM`` (+ ``GitProcessor`` / ``AutoProcessor``): GIT captioning
   (``models/git.py``), conditional on the prompt when one is given ([CLS] +
   prompt tokens, the GIT conditional-captioning / VQA form);
+* ``Blip2ForConditionalGeneration`` (+ ``Blip2Processor`` / ``AutoProcessor``):
+  BLIP-2 with an OPT language model (``models/blip2.py``); the prompt, when
+  given, is the text the LM continues ("Question: ... Answer:" for VQA);
 
 any other class is refused with a ``ValueError`` that names it (a fatal job
 error: retrying cannot help).  Model geometry comes from the checkpoint's
-``config.json`` (a transformers ``BlipConfig`` / ``GitConfig``), name heuristics
+``config.json`` (a transformers ``BlipConfig`` / ``GitConfig`` / ``Blip2Config``), name heuristics
 only without one.
 """
 from __future__ import annotations
@@ -33,19 +36,23 @@ from ..models.wordpiece import WordPiece
 from ..output.processor import make_text_result
 from ..runtime.model_cache import cache, find_weights
 
-MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git"}
-PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", "GitProcessor", "CLIPImageProcessor", None}
+MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git",
+               "Blip2ForConditionalGeneration": "blip2"}
+PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", "GitProcessor", "CLIPImageProcessor",
+                   "Blip2Processor", None}
 
 
 def resolve_task(params: dict | None, model_name: str) -> str:
-    """'caption' | 'vqa' | 'git' from the hive's class names; ValueError for anything else."""
+    """'caption' | 'vqa' | 'git' | 'blip2' from the hive's class names; ValueError for anything else."""
     params = params or {}
     mt, pt = params.get("model_type"), params.get("processor_type")
     if pt not in PROCESSOR_TYPES:
         raise ValueError(f"img2txt: processor_type {pt!r} is not supported "
-                         "(supported: BlipProcessor, GitProcessor, AutoProcessor)")
+                         "(supported: BlipProcessor, GitProcessor, Blip2Processor, AutoProcessor)")
     if mt is None:
         n = model_name.lower()
+        if "blip2" in n:
+            return "blip2"
         return "vqa" if "vqa" in n else ("git" if "/git-" in n or n.startswith("git-") else "caption")
     if mt not in MODEL_TYPES:
         raise ValueError(f"img2txt: model_type {mt!r} is not supported "
@@ -98,9 +105,46 @@ def load_git(model_name: str, device: str):
     return cache().get(("git", model_name, device), make)
 
 
+def load_blip2(model_name: str, device: str):
+    def make():
+        from ..models.blip2 import BLIP2_OPT_2_7B, BLIP2_OPT_6_7B, TINY_BLIP2, Blip2Captioner, Blip2Config, \
+            convert_hf_blip2
+        from ..models.hf_config import component_config
+        from ..models.tokenizer import ByteBPETokenizer
+
+        w = find_weights(model_name)
+        raw = component_config(w, "") if w else None
+        if raw is not None and "qformer_config" in raw:
+            cfg = Blip2Config.from_hf(raw)
+        else:
+            n = model_name.lower()
+            if "t5" in n:
+                raise ValueError(f"img2txt: BLIP-2 with a T5 language model is not supported ({model_name})")
+            cfg = TINY_BLIP2 if n.startswith("tiny") else (BLIP2_OPT_6_7B if "6.7b" in n else BLIP2_OPT_2_7B)
+        dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+        with torch.device(device):
+            m = Blip2Captioner(cfg).to(dt).eval().requires_grad_(False)
+        init_random_fast_(m, seed=11)
+        m.weights_source = "random-init"
+        if w:
+            from ..models.weights import _read_dir, load_into
+
+            sd = _read_dir(w)
+            if sd:
+                m.load_report = load_into(m, convert_hf_blip2(sd), name=model_name)
+                m.weights_source = w
+        prepare_model(m)
+        return m, ByteBPETokenizer(w, max_length=512, vocab_size=cfg.vocab, bos=cfg.bos_id, eos=cfg.eos_id,
+                                   pad=cfg.pad_id)
+
+    return cache().get(("blip2", model_name, device), make)
+
+
 def load_captioner(model_name: str, device: str, task: str = "caption"):
     if task == "git":
         return load_git(model_name, device)
+    if task == "blip2":
+        return load_blip2(model_name, device)
 
     def make():
         w = find_weights(model_name)
@@ -144,7 +188,7 @@ def caption_callback(device_identifier, model_name, **kwargs):
             mnt = kwargs.get("max_new_tokens")
             ids = model.generate(image, prefix, max_new_tokens=None if mnt is None else int(mnt),
                                  max_length=int(kwargs.get("max_length", 20)))
-            caption = tok.decode(ids)
+            caption = tok.decode(ids).strip()
         results["primary"] = make_text_result(caption)
         config["caption"] = caption
         return results, config

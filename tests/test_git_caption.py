@@ -70,7 +70,7 @@ def test_caption_dispatch_accepts_git():
         == "git"
     assert resolve_task({"model_type": "GitForCausalLM", "processor_type": "AutoProcessor"}, "x") == "git"
     with pytest.raises(ValueError):
-        resolve_task({"model_type": "Blip2ForConditionalGeneration"}, "Salesforce/blip2-opt-2.7b")
+        resolve_task({"model_type": "InstructBlipForConditionalGeneration"}, "Salesforce/instructblip-vicuna-7b")
 
 
 def test_caption_callback_git_end_to_end():
