@@ -244,6 +244,47 @@ static int launch(const GemmArgs& a0, int ksplit, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// f[q][0..7] += partials of splits [s0, s0 + U) at rows w[q] (split stride
+// `total` floats): all U * R * 2 loads issued before the first add
+template <int U, int R>
+__device__ __forceinline__ void add_splits(float (&f)[R][8], const float* const (&w)[R], size_t total, int s0) {
+  float4 lo[U][R], hi[U][R];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const float* p = w[q] + (size_t)(s0 + u) * total;
+      lo[u][q] = *reinterpret_cast<const float4*>(p);
+      hi[u][q] = *reinterpret_cast<const float4*>(p + 4);
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      f[q][0] += lo[u][q].x; f[q][1] += lo[u][q].y; f[q][2] += lo[u][q].z; f[q][3] += lo[u][q].w;
+      f[q][4] += hi[u][q].x; f[q][5] += hi[u][q].y; f[q][6] += hi[u][q].z; f[q][7] += hi[u][q].w;
+    }
+  // keep the loads together: under register pressure (the GN reduce) the
+  // scheduler otherwise interleaves each load pair with its adds and waits
+  __builtin_amdgcn_sched_group_barrier(0x020, 2 * U * R, 0);  // VMEM reads
+  __builtin_amdgcn_sched_group_barrier(0x002, 8 * U * R, 0);  // VALU adds
+}
+
+// sum of all ksplit partials, SU (1 / 4 / 8) splits per memory round trip
+template <int SU, int R>
+__device__ __forceinline__ void sum_splits(float (&f)[R][8], const float* const (&w)[R], size_t total, int ksplit) {
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[q][j] = 0.f;
+  int s = 0;
+  if constexpr (SU >= 8)
+    for (; s + 8 <= ksplit; s += 8) add_splits<8, R>(f, w, total, s);
+  if constexpr (SU >= 4)
+    for (; s + 4 <= ksplit; s += 4) add_splits<4, R>(f, w, total, s);
+  for (; s < ksplit; ++s) add_splits<1, R>(f, w, total, s);
+}
+
 // split-K reduce: out = epilogue(sum_s ws[s]) (bias, bias2d, act, residual)
 __global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
   const int M = a.M, N = a.N;
@@ -263,20 +304,18 @@ __global__ void splitk_reduce_kernel(const GemmArgs a, int ksplit) {
 
 // 8 columns per thread: 2x float4 per split, 16-byte bias / residual / output
 // accesses (the scalar kernel above issues one 4-byte load per split per value)
+template <int SU>
 __global__ void splitk_reduce8_kernel(const GemmArgs a, int ksplit) {
   const int M = a.M, N = a.N, NV = N / 8;
   const size_t total = (size_t)M * N, nvec = (size_t)M * NV;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / NV), n = (int)(i - (size_t)m * NV) * 8;
-    const float* w = a.ws + (size_t)m * N + n;
-    float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
-    for (int sidx = 1; sidx < ksplit; ++sidx) {
-      const float4 l2 = *reinterpret_cast<const float4*>(w + sidx * total);
-      const float4 h2 = *reinterpret_cast<const float4*>(w + sidx * total + 4);
-      lo.x += l2.x; lo.y += l2.y; lo.z += l2.z; lo.w += l2.w;
-      hi.x += h2.x; hi.y += h2.y; hi.z += h2.z; hi.w += h2.w;
-    }
-    float f[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const float* const w[1] = {a.ws + (size_t)m * N + n};
+    float ff[1][8];
+    sum_splits<SU, 1>(ff, w, total, ksplit);
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = ff[0][j];
     if (a.bias) add8(f, a.bias + n, true, 8);
     if (a.bias2d) add8(f, a.bias2d + (size_t)(m / a.rows_per_b) * a.ldb2 + n, true, 8);
     act8(a.act, f);
@@ -298,7 +337,9 @@ __global__ void splitk_reduce8_kernel(const GemmArgs a, int ksplit) {
 // (Welford); the RPI row groups are merged in LDS (Chan).  The first version
 // walked its rows one dependent load at a time and cost the step 0.36 ms
 // (tools/abstep.py skgn0 / skgn1); the rows' loads now go out together.
-template <int VC>
+// SU: splits whose partials are loaded together (one memory round trip per SU
+// splits; the plain loop waited on every split's loads before issuing the next)
+template <int VC, int SU>
 __global__ __launch_bounds__(256) void splitk_reduce8_gn_kernel(const GemmArgs a, int ksplit) {
   constexpr int RPI = 256 / VC, RPT = SPLITK_GN_SEG / RPI;  // row groups, rows per thread
   static_assert(SPLITK_GN_SEG % RPI == 0, "segment rows split evenly over the row groups");
@@ -315,22 +356,10 @@ __global__ __launch_bounds__(256) void splitk_reduce8_gn_kernel(const GemmArgs a
     // all of this thread's rows' partial sums first (independent loads in flight
     // together), then the epilogue and the Welford update row by row
     float f[RPT][8];
+    const float* w[RPT];
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const float* w = a.ws + (size_t)(blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI) * N + n;
-      const float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
-      f[q][0] = lo.x; f[q][1] = lo.y; f[q][2] = lo.z; f[q][3] = lo.w;
-      f[q][4] = hi.x; f[q][5] = hi.y; f[q][6] = hi.z; f[q][7] = hi.w;
-    }
-    for (int sidx = 1; sidx < ksplit; ++sidx) {
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) {
-        const float* w = a.ws + sidx * total + (size_t)(blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI) * N + n;
-        const float4 lo = *reinterpret_cast<const float4*>(w), hi = *reinterpret_cast<const float4*>(w + 4);
-        f[q][0] += lo.x; f[q][1] += lo.y; f[q][2] += lo.z; f[q][3] += lo.w;
-        f[q][4] += hi.x; f[q][5] += hi.y; f[q][6] += hi.z; f[q][7] += hi.w;
-      }
-    }
+    for (int q = 0; q < RPT; ++q) w[q] = a.ws + (size_t)(blockIdx.x * SPLITK_GN_SEG + r0 + q * RPI) * N + n;
+    sum_splits<SU, RPT>(f, w, total, ksplit);
     float bb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) bb[j] = 0.f;
@@ -389,6 +418,14 @@ __global__ __launch_bounds__(256) void splitk_reduce8_gn_kernel(const GemmArgs a
     *reinterpret_cast<float2*>(a.gn_part + ((size_t)blockIdx.x * N + nc) * 2) = make_float2(mu, q);
 }
 
+// splits loaded per memory round trip in the split-K reduces (1: the old
+// one-split-at-a-time loop; A/B knob for tools/abstep.py skr1 / skr4 / skr8)
+static int g_skr_unroll = 4;  // 4: -0.022 ms (CFG 8) / -0.023 ms (CFG 2) per step vs 1; 8 no better (profiles/unet_step_ab_skr_r7d.txt)
+CSK_API int csk_set_skr_unroll(int v) {
+  g_skr_unroll = v;
+  return 0;
+}
+
 static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
   const size_t total = (size_t)a.M * a.N;
   const bool vec = a.N % 8 == 0 && a.ldc % 8 == 0 && (!a.res || a.ldr % 8 == 0) && (!a.bias2d || a.ldb2 % 8 == 0) &&
@@ -397,13 +434,18 @@ static int splitk_reduce(const GemmArgs& a, int ksplit, hipStream_t s) {
   if (a.gn_part) {  // host guarantees the vector layout and gn_seg | M (hip_ops._gn_seg)
     constexpr int VC = 8;
     if (!vec || a.gn_seg != SPLITK_GN_SEG || a.M % SPLITK_GN_SEG != 0) return (int)hipErrorInvalidValue;
-    splitk_reduce8_gn_kernel<VC><<<dim3(a.M / SPLITK_GN_SEG, (a.N / 8 + VC - 1) / VC), 256, 0, s>>>(a, ksplit);
+    const dim3 g(a.M / SPLITK_GN_SEG, (a.N / 8 + VC - 1) / VC);
+    if (g_skr_unroll >= 8) splitk_reduce8_gn_kernel<VC, 8><<<g, 256, 0, s>>>(a, ksplit);
+    else if (g_skr_unroll >= 4) splitk_reduce8_gn_kernel<VC, 4><<<g, 256, 0, s>>>(a, ksplit);
+    else splitk_reduce8_gn_kernel<VC, 1><<<g, 256, 0, s>>>(a, ksplit);
     return (int)hipGetLastError();
   }
   if (vec) {
     int grid = (int)((total / 8 + 255) / 256);
     if (grid > 8192) grid = 8192;
-    splitk_reduce8_kernel<<<grid, 256, 0, s>>>(a, ksplit);
+    if (g_skr_unroll >= 8) splitk_reduce8_kernel<8><<<grid, 256, 0, s>>>(a, ksplit);
+    else if (g_skr_unroll >= 4) splitk_reduce8_kernel<4><<<grid, 256, 0, s>>>(a, ksplit);
+    else splitk_reduce8_kernel<1><<<grid, 256, 0, s>>>(a, ksplit);
     return (int)hipGetLastError();
   }
   int grid = (int)((total + 255) / 256);

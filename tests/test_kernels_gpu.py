@@ -34,7 +34,7 @@ def test_gemm(gpu, M, N, K, act):
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 25, 26, 27, 28, 29, 36])
-@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("split", [1, 3, 13])  # 13: 10 / 7 effective splits (8+1+1 / 4+1+1+1 load batches)
 def test_gemm_conv_every_tile_and_splitk(gpu, tile, split):
     from chiaswarm_amd.ops import _lib
     from chiaswarm_amd.ops.hip_ops import _p, _s
@@ -409,7 +409,7 @@ def test_fused_group_norm_stats_large_vae_maps(gpu, H, C):
 
 
 @pytest.mark.parametrize("tile", [1, 11, 14, 26, 31, 32, 33, 34])
-@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("split", [2, 4, 7, 16])  # 7 -> 6, 16 -> 9 effective: 4- and 8-split load batches
 def test_fused_group_norm_stats_split_k(gpu, tile, split):
     """Split-K producers emit GN statistics from the reduce kernel
     (splitk_reduce8_gn_kernel, 64-row segments): fused GN == own-stats GN, and

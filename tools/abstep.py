@@ -52,6 +52,8 @@ def apply_arm(arm):
         hip_ops.ATTN_VARIANT = int(arm[4:])
     elif arm in ("skgn0", "skgn1"):
         hip_ops.SPLITK_GN = arm == "skgn1"
+    elif arm.startswith("skr"):  # split-K reduces: partial splits loaded per memory round trip (1 / 4 / 8)
+        _lib.call("csk_set_skr_unroll", int(arm[3:]))
     elif arm in ("lnoff", "lnon"):
         ops.LN_FUSE = arm == "lnon"
     elif arm in ("lnk0", "lnk1"):  # fused-LN row statistics: merge kernel (0) / in the consumer prologue (1)
