@@ -605,7 +605,8 @@ __device__ __forceinline__ int kv_off32(int row, int chunk) {
 // MFMAs, 8 = no QK^T MFMAs
 // TRICKS (A/B, csk_set_attn32(1 + TRICKS)): 1 = the -mu offset as one MFMA from
 // a zero accumulator instead of 32 register moves per block; 2 = the row sum
-// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block
+// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block;
+// 4 = the row max as a depth-3 tree of max3 instead of a 17-deep chain
 template <int QB, int PROBE = 0, int TRICKS = 0>
 __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
   constexpr int DP = 64, CPR = DP / 8, KB = 64;
@@ -777,13 +778,30 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
           }
       }
       mfma_fence16(sc[0][qt], sc[1][qt]);
-      float mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
+      float mx;
+      if constexpr ((TRICKS & 4) != 0) {
+        // tree: 11 independent max3 over the 32 scores, then 4 + 2 (depth 3
+        // instead of a 17-deep dependent chain)
+        const v16f& x0 = sc[0][qt];
+        const v16f& x1 = sc[1][qt];
+        const float t0 = vmax3(x0[0], x0[1], x0[2]), t1 = vmax3(x0[3], x0[4], x0[5]);
+        const float t2 = vmax3(x0[6], x0[7], x0[8]), t3 = vmax3(x0[9], x0[10], x0[11]);
+        const float t4 = vmax3(x0[12], x0[13], x0[14]), t5 = vmax3(x0[15], x1[0], x1[1]);
+        const float t6 = vmax3(x1[2], x1[3], x1[4]), t7 = vmax3(x1[5], x1[6], x1[7]);
+        const float t8 = vmax3(x1[8], x1[9], x1[10]), t9 = vmax3(x1[11], x1[12], x1[13]);
+        const float t10 = vmax3(x1[14], x1[15], x1[15]);
+        const float u0 = vmax3(t0, t1, t2), u1 = vmax3(t3, t4, t5), u2 = vmax3(t6, t7, t8);
+        const float u3 = vmax3(t9, t10, t10);
+        mx = vmax3(vmax3(u0, u1, u2), u3, u3);
+      } else {
+        mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
 #pragma unroll
-      for (int i = 3; i < 15; i += 2) mx = vmax3(mx, sc[0][qt][i], sc[0][qt][i + 1]);
-      mx = vmax3(mx, sc[0][qt][15], sc[1][qt][0]);
+        for (int i = 3; i < 15; i += 2) mx = vmax3(mx, sc[0][qt][i], sc[0][qt][i + 1]);
+        mx = vmax3(mx, sc[0][qt][15], sc[1][qt][0]);
 #pragma unroll
-      for (int i = 1; i < 15; i += 2) mx = vmax3(mx, sc[1][qt][i], sc[1][qt][i + 1]);
-      mx = vmax3(mx, sc[1][qt][15], sc[1][qt][15]);
+        for (int i = 1; i < 15; i += 2) mx = vmax3(mx, sc[1][qt][i], sc[1][qt][i + 1]);
+        mx = vmax3(mx, sc[1][qt][15], sc[1][qt][15]);
+      }
       {  // the other 32 keys of this query live in lane ^ 32
         const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
         mx = vmax3(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[1]));
@@ -1177,6 +1195,7 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
         case 2: attn32_kernel<1, 0, 1><<<g32, 256, 0, stream>>>(a); break;
         case 3: attn32_kernel<1, 0, 2><<<g32, 256, 0, stream>>>(a); break;
         case 4: attn32_kernel<1, 0, 3><<<g32, 256, 0, stream>>>(a); break;
+        case 5: attn32_kernel<1, 0, 4><<<g32, 256, 0, stream>>>(a); break;
         default: attn32_kernel<1><<<g32, 256, 0, stream>>>(a); break;
       }
       return (int)hipGetLastError();
@@ -1277,7 +1296,9 @@ CSK_API int csk_attention_split(void* o, const void* q, const void* k, const voi
   a.kv_split = kv_split;
   a.part_o = (float*)part_o;
   a.part_ml = (float*)part_ml;
-  attn32_kernel<1><<<dim3(B * H * ((Sq + 127) / 128) * kv_split), 256, 0, stream>>>(a);
+  const dim3 gs(B * H * ((Sq + 127) / 128) * kv_split);
+  if (g_attn32 == 5) attn32_kernel<1, 0, 4><<<gs, 256, 0, stream>>>(a);
+  else attn32_kernel<1><<<gs, 256, 0, stream>>>(a);
   const size_t n = (size_t)B * H * Sq * 8;
   attn_split_combine_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(a);
   return (int)hipGetLastError();

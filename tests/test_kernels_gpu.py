@@ -238,6 +238,31 @@ def test_attention_spike_rescale(gpu, variant):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
+@pytest.mark.parametrize("a32", [2, 3, 4, 5])
+@pytest.mark.parametrize("B,Sq,Skv,H,D,causal,spike", [(2, 1024, 1024, 5, 64, False, False),
+                                                        (1, 300, 517, 3, 64, False, True),
+                                                        (2, 77, 77, 4, 64, True, False)])
+def test_attn32_trick_variants(gpu, a32, B, Sq, Skv, H, D, causal, spike):
+    """The attn32 A/B variants (csk_set_attn32 2-5: -mu as an MFMA, row sum on
+    the PV chain, both, tree-shaped row max) against fp32, incl. a causal mask
+    and rescale spikes."""
+    from chiaswarm_amd.ops import _lib
+
+    q, k, v = (rnd(B, s, H, D, dev=gpu) for s in (Sq, Skv, Skv))
+    if spike:
+        k[0, 100, 0] = q[0, 5, 0] * 8
+        k[0, 260, 1] = q[0, 70, 1] * 14
+    old = hip_ops.ATTN_VARIANT
+    hip_ops.ATTN_VARIANT = 20
+    _lib.call("csk_set_attn32", a32)
+    try:
+        y = hip_ops.attention(q, k, v, 1 / math.sqrt(D), causal)
+    finally:
+        _lib.call("csk_set_attn32", 1)
+        hip_ops.ATTN_VARIANT = old
+    assert rel_err(y.cpu(), _attn_ref(q, k, v, 1 / math.sqrt(D), causal)) < 1.5e-2
+
+
 @pytest.mark.parametrize("variant", [2, 3, 5, 20])
 def test_attention_far_negative_logits(gpu, variant):
     # every score far below 0 (softmax is shift-invariant): the running-max offset
