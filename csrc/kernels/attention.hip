@@ -605,8 +605,7 @@ __device__ __forceinline__ int kv_off32(int row, int chunk) {
 // MFMAs, 8 = no QK^T MFMAs
 // TRICKS (A/B, csk_set_attn32(1 + TRICKS)): 1 = the -mu offset as one MFMA from
 // a zero accumulator instead of 32 register moves per block; 2 = the row sum
-// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block;
-// 4 = the row max as a depth-3 tree of max3 instead of a 17-deep chain
+// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block
 template <int QB, int PROBE = 0, int TRICKS = 0>
 __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
   constexpr int DP = 64, CPR = DP / 8, KB = 64;
@@ -778,10 +777,11 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
           }
       }
       mfma_fence16(sc[0][qt], sc[1][qt]);
+      // row max as a depth-3 tree of max3 (11 independent, then 4 + 2) instead of
+      // a 17-deep dependent chain: -0.018 ms per CFG-8 step, neutral at CFG 2
+      // (profiles/unet_step_ab_attn32_tree_r7g.txt)
       float mx;
-      if constexpr ((TRICKS & 4) != 0) {
-        // tree: 11 independent max3 over the 32 scores, then 4 + 2 (depth 3
-        // instead of a 17-deep dependent chain)
+      {
         const v16f& x0 = sc[0][qt];
         const v16f& x1 = sc[1][qt];
         const float t0 = vmax3(x0[0], x0[1], x0[2]), t1 = vmax3(x0[3], x0[4], x0[5]);
@@ -793,14 +793,6 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         const float u0 = vmax3(t0, t1, t2), u1 = vmax3(t3, t4, t5), u2 = vmax3(t6, t7, t8);
         const float u3 = vmax3(t9, t10, t10);
         mx = vmax3(vmax3(u0, u1, u2), u3, u3);
-      } else {
-        mx = vmax3(sc[0][qt][0], sc[0][qt][1], sc[0][qt][2]);
-#pragma unroll
-        for (int i = 3; i < 15; i += 2) mx = vmax3(mx, sc[0][qt][i], sc[0][qt][i + 1]);
-        mx = vmax3(mx, sc[0][qt][15], sc[1][qt][0]);
-#pragma unroll
-        for (int i = 1; i < 15; i += 2) mx = vmax3(mx, sc[1][qt][i], sc[1][qt][i + 1]);
-        mx = vmax3(mx, sc[1][qt][15], sc[1][qt][15]);
       }
       {  // the other 32 keys of this query live in lane ^ 32
         const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
@@ -1195,7 +1187,6 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
         case 2: attn32_kernel<1, 0, 1><<<g32, 256, 0, stream>>>(a); break;
         case 3: attn32_kernel<1, 0, 2><<<g32, 256, 0, stream>>>(a); break;
         case 4: attn32_kernel<1, 0, 3><<<g32, 256, 0, stream>>>(a); break;
-        case 5: attn32_kernel<1, 0, 4><<<g32, 256, 0, stream>>>(a); break;
         default: attn32_kernel<1><<<g32, 256, 0, stream>>>(a); break;
       }
       return (int)hipGetLastError();
@@ -1297,8 +1288,7 @@ CSK_API int csk_attention_split(void* o, const void* q, const void* k, const voi
   a.part_o = (float*)part_o;
   a.part_ml = (float*)part_ml;
   const dim3 gs(B * H * ((Sq + 127) / 128) * kv_split);
-  if (g_attn32 == 5) attn32_kernel<1, 0, 4><<<gs, 256, 0, stream>>>(a);
-  else attn32_kernel<1><<<gs, 256, 0, stream>>>(a);
+  attn32_kernel<1><<<gs, 256, 0, stream>>>(a);
   const size_t n = (size_t)B * H * Sq * 8;
   attn_split_combine_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(a);
   return (int)hipGetLastError();
