@@ -1,6 +1,6 @@
-"""BLIP-2 image captioning / prompted VQA with an OPT language model
+"""BLIP-2 image captioning / prompted VQA with an OPT or Flan-T5 language model
 (transformers ``Blip2ForConditionalGeneration`` + ``Blip2Processor``, the
-``Salesforce/blip2-opt-*`` checkpoints).  Reference: the hive names the
+``Salesforce/blip2-opt-*`` and ``blip2-flan-t5-*`` checkpoints).  Reference: the hive names the
 processor / model classes at swarm/captioning/caption_image.py:11-29 and the
 reference instantiates whatever transformers class it is given.
 
@@ -12,14 +12,19 @@ LayerNorm, GEMM epilogues):
 * Q-Former: 32 learned query tokens through a BERT-style post-LN stack that
   cross-attends to the image tokens every ``cross_attention_frequency``
   layers (query FFN only: captioning feeds no text to the Q-Former);
-* OPT decoder (pre-LN, ReLU MLP, learned positions with offset 2, LM head tied
-  to the token embeddings) over ``[projected queries; </s>; prompt]``.
+* language model, either
+  - OPT (``blip2-opt-*``): pre-LN decoder, ReLU MLP, learned positions with
+    offset 2, LM head tied to the token embeddings, over
+    ``[projected queries; </s>; prompt]``; or
+  - Flan-T5 (``blip2-flan-t5-*``, ``models/t5.py::T5Seq2Seq``): the encoder
+    reads ``[projected queries; prompt; </s>]``, the decoder generates from the
+    decoder start token (pad, 0) with cross-attention over it.
 
-Greedy decode with transformers' default ``max_length=20`` counted on the text
-part (``</s>`` + prompt + generated; the query embeddings are not tokens),
-stopping at ``</s>``.  Every step re-runs the (<= ~60-row) sequence: at that
-size each GEMM streams its weights once either way, so a KV cache would save
-no HBM traffic.  FlanT5-based BLIP-2 checkpoints are refused by name.
+Greedy decode with transformers' default ``max_length=20`` (OPT: counted on the
+text part, ``</s>`` + prompt + generated; T5: decoder tokens), stopping at the
+eos token.  Every step re-runs the (short) decoder sequence: at that size each
+GEMM streams its weights once either way, so a KV cache would save no HBM
+traffic.  The original-T5 (ReLU FFN) language models are refused.
 """
 from __future__ import annotations
 
@@ -31,6 +36,7 @@ import torch.nn as nn
 from PIL import Image
 
 from .layers import LayerNorm, Linear
+from .t5 import T5Config, T5Seq2Seq
 from .transformer import PostLNBlock, PreLNBlock, ViT
 
 MEAN = np.array([0.48145466, 0.4578275, 0.40821073], np.float32)
@@ -63,32 +69,64 @@ class Blip2Config:
     bos_id: int = 2
     eos_id: int = 2
     pad_id: int = 1
+    lm_type: str = "opt"
+    t5: T5Config | None = None  # lm_type "t5": the Flan-T5 geometry (lm_dim = t5.d_model)
+    t5_dec_layers: int = 0
+    t5_tied: bool = False
 
     @classmethod
     def from_hf(cls, cfg: dict) -> "Blip2Config":
         """A transformers ``Blip2Config`` config.json (vision / qformer / text
-        sub-configs; the text model must be OPT)."""
+        sub-configs; the text model is OPT or (Flan-)T5 v1.1)."""
         v, q, t = cfg.get("vision_config") or {}, cfg.get("qformer_config") or {}, cfg.get("text_config") or {}
         lm = t.get("model_type", "opt")
-        if lm != "opt":
-            raise ValueError(f"img2txt: BLIP-2 with a {lm!r} language model is not supported (OPT only)")
+        if lm not in ("opt", "t5"):
+            raise ValueError(f"img2txt: BLIP-2 with a {lm!r} language model is not supported (OPT, Flan-T5)")
+        if lm == "t5":
+            proj = t.get("feed_forward_proj", "relu")
+            if "gated" not in proj:
+                raise ValueError(f"img2txt: BLIP-2 t5 language model with feed_forward_proj={proj!r} is not supported "
+                                 "(gated-gelu: T5 v1.1 / Flan-T5)")
+            t5 = T5Config(vocab=t.get("vocab_size", 32128), d_model=t.get("d_model", 2048), d_kv=t.get("d_kv", 64),
+                          heads=t.get("num_heads", 32), d_ff=t.get("d_ff", 5120), layers=t.get("num_layers", 24),
+                          buckets=t.get("relative_attention_num_buckets", 32),
+                          max_distance=t.get("relative_attention_max_distance", 128),
+                          eps=t.get("layer_norm_epsilon", 1e-6))
+            base = cls._vision_qformer(cfg, v, q)
+            return dataclasses.replace(base, lm_type="t5", t5=t5, lm_dim=t5.d_model, vocab=t5.vocab,
+                                       t5_dec_layers=t.get("num_decoder_layers") or t5.layers,
+                                       # original T5 scales the decoder output by d_model^-0.5 before
+                                       # the (tied) head; v1.1 / Flan-T5 configs say
+                                       # tie_word_embeddings=false (newer transformers:
+                                       # scale_decoder_outputs)
+                                       t5_tied=bool(t.get("scale_decoder_outputs",
+                                                          t.get("tie_word_embeddings", True) is not False)),
+                                       bos_id=t.get("decoder_start_token_id", 0), eos_id=t.get("eos_token_id", 1),
+                                       pad_id=t.get("pad_token_id", 0))
         if t.get("word_embed_proj_dim", t.get("hidden_size", 2560)) != t.get("hidden_size", 2560):
             raise ValueError("img2txt: OPT with word_embed_proj_dim != hidden_size is not supported")
+        return dataclasses.replace(
+            cls._vision_qformer(cfg, v, q), lm_dim=t.get("hidden_size", 2560), lm_depth=t.get("num_hidden_layers", 32),
+            lm_heads=t.get("num_attention_heads", 32), lm_ffn=t.get("ffn_dim", 10240),
+            vocab=t.get("vocab_size", 50272), max_pos=t.get("max_position_embeddings", 2048),
+            bos_id=t.get("bos_token_id", 2), eos_id=t.get("eos_token_id", 2), pad_id=t.get("pad_token_id", 1))
+
+    @classmethod
+    def _vision_qformer(cls, cfg, v, q) -> "Blip2Config":
         return cls(image_size=v.get("image_size", 224), patch=v.get("patch_size", 14),
                    vision_dim=v.get("hidden_size", 1408), vision_depth=v.get("num_hidden_layers", 39),
                    vision_heads=v.get("num_attention_heads", 16), vision_mlp=v.get("intermediate_size", 6144),
                    vision_eps=v.get("layer_norm_eps", 1e-6), q_dim=q.get("hidden_size", 768),
                    q_depth=q.get("num_hidden_layers", 12), q_heads=q.get("num_attention_heads", 12),
                    q_mlp=q.get("intermediate_size", 3072), q_eps=q.get("layer_norm_eps", 1e-12),
-                   cross_freq=q.get("cross_attention_frequency", 2), num_query=cfg.get("num_query_tokens", 32),
-                   lm_dim=t.get("hidden_size", 2560), lm_depth=t.get("num_hidden_layers", 32),
-                   lm_heads=t.get("num_attention_heads", 32), lm_ffn=t.get("ffn_dim", 10240),
-                   vocab=t.get("vocab_size", 50272), max_pos=t.get("max_position_embeddings", 2048),
-                   bos_id=t.get("bos_token_id", 2), eos_id=t.get("eos_token_id", 2), pad_id=t.get("pad_token_id", 1))
+                   cross_freq=q.get("cross_attention_frequency", 2), num_query=cfg.get("num_query_tokens", 32))
 
 
 BLIP2_OPT_2_7B = Blip2Config()
 BLIP2_OPT_6_7B = Blip2Config(lm_dim=4096, lm_ffn=16384)
+_FLAN_T5_XL = T5Config(d_model=2048, d_kv=64, heads=32, d_ff=5120, layers=24)
+BLIP2_FLAN_T5_XL = Blip2Config(lm_type="t5", t5=_FLAN_T5_XL, lm_dim=2048, vocab=32128, t5_dec_layers=24,
+                               bos_id=0, eos_id=1, pad_id=0)
 TINY_BLIP2 = Blip2Config(image_size=28, patch=14, vision_dim=32, vision_depth=2, vision_heads=2, vision_mlp=64,
                          q_dim=32, q_depth=2, q_heads=2, q_mlp=64, num_query=4, lm_dim=32, lm_depth=2, lm_heads=2,
                          lm_ffn=64, vocab=100, max_pos=64)
@@ -121,8 +159,12 @@ def convert_hf_blip2(sd: dict) -> dict:
     without Q-Former text input) is dropped; the LM head is tied."""
     out: dict = {}
     for k, v in sd.items():
-        if k.endswith("position_ids") or k == "language_model.lm_head.weight":
+        if k.endswith("position_ids"):
             continue
+        if k == "language_model.lm_head.weight":
+            if "language_model.shared.weight" in sd:  # T5: own (or tied-and-saved) head
+                out["t5.lm_head.weight"] = v
+            continue  # OPT: tied to the token embeddings
         if k == "query_tokens":
             out[k] = v.reshape(v.shape[-2], v.shape[-1])
         elif k.startswith("vision_model.embeddings."):
@@ -158,6 +200,11 @@ def convert_hf_blip2(sd: dict) -> dict:
             out[f"qformer.{n}.{s}" if s else k] = v
         elif k.startswith("language_projection."):
             out[k] = v
+        elif k.startswith("language_model.") and not k.startswith("language_model.model.") and \
+                not k.startswith("language_model.lm_head"):
+            r = k.removeprefix("language_model.")
+            if not r.endswith("embed_tokens.weight"):
+                out["t5." + r] = v  # T5ForConditionalGeneration names (models/t5.py::T5Seq2Seq)
         elif k.startswith("language_model.model.decoder."):
             r = k.removeprefix("language_model.model.decoder.")
             if r.startswith("layers."):
@@ -174,6 +221,8 @@ def convert_hf_blip2(sd: dict) -> dict:
                 out[k] = v
         else:
             out[k] = v  # unknown keys surface as a CheckpointMismatch in load_into
+    if "language_model.shared.weight" in sd and "t5.lm_head.weight" not in out:
+        out["t5.lm_head.weight"] = sd["language_model.shared.weight"]  # tied head not saved
     return out
 
 
@@ -189,11 +238,18 @@ class Blip2Captioner(nn.Module):
             PostLNBlock(cfg.q_dim, cfg.q_heads, cfg.q_mlp, cross_dim=cfg.vision_dim if i % cfg.cross_freq == 0 else None,
                         eps=cfg.q_eps) for i in range(cfg.q_depth)])
         self.language_projection = Linear(cfg.q_dim, cfg.lm_dim)
+        if cfg.lm_type == "t5":
+            self.t5 = T5Seq2Seq(cfg.t5, cfg.t5_dec_layers or cfg.t5.layers, tie_embeddings=cfg.t5_tied)
+            return
         self.embed_tokens = nn.Embedding(cfg.vocab, cfg.lm_dim)
         self.embed_positions = nn.Embedding(cfg.max_pos + 2, cfg.lm_dim)
         self.lm = nn.ModuleList([PreLNBlock(cfg.lm_dim, cfg.lm_heads, cfg.lm_ffn, act="relu", eps=cfg.lm_eps)
                                  for _ in range(cfg.lm_depth)])
         self.lm_ln = LayerNorm(cfg.lm_dim, eps=cfg.lm_eps)
+
+    @property
+    def _emb(self) -> nn.Embedding:
+        return self.t5.shared if self.cfg.lm_type == "t5" else self.embed_tokens
 
     def preprocess(self, image: Image.Image) -> torch.Tensor:
         """BlipImageProcessor: bicubic resize to image_size², CLIP mean / std; NHWC."""
@@ -205,7 +261,7 @@ class Blip2Captioner(nn.Module):
     def image_prefix(self, pixels: torch.Tensor) -> torch.Tensor:
         """Projected Q-Former query outputs [1, num_query, lm_dim]: the language
         model's input embeddings ahead of the text."""
-        dt = self.embed_tokens.weight.dtype
+        dt = self._emb.weight.dtype
         img = self.vision_model(pixels.to(dt))
         q = self.qformer_ln(self.query_tokens[None].to(dt))
         for blk in self.qformer:
@@ -229,6 +285,8 @@ class Blip2Captioner(nn.Module):
                  max_length: int = 20) -> list[int]:
         """Greedy decode from ``</s> + prefix`` after the image queries; returns
         prefix + generated ids (without the leading ``</s>``)."""
+        if self.cfg.lm_type == "t5":
+            return self._generate_t5(image, prefix_ids, max_new_tokens, max_length)
         if max_new_tokens is None:
             max_new_tokens = max(0, max_length - 1 - len(prefix_ids))
         prefix = self.image_prefix(self.preprocess(image).to(self.embed_tokens.weight.device))
@@ -241,3 +299,25 @@ class Blip2Captioner(nn.Module):
             ids.append(nxt)
             out.append(nxt)
         return list(prefix_ids) + out
+
+    @torch.no_grad()
+    def t5_encoder_states(self, prefix: torch.Tensor, prompt_ids: list[int]) -> torch.Tensor:
+        """Flan-T5 encoder over [projected queries; prompt; </s>]."""
+        t5 = self.t5
+        ids = torch.tensor([list(prompt_ids) + [self.cfg.eos_id]], device=prefix.device)
+        return t5.encode(torch.cat([prefix, t5.shared(ids).to(prefix.dtype)], 1))
+
+    def _generate_t5(self, image, prompt_ids, max_new_tokens, max_length) -> list[int]:
+        """Greedy decode from the decoder start token; returns the generated ids
+        (the prompt lives in the encoder)."""
+        if max_new_tokens is None:
+            max_new_tokens = max(0, max_length - 1)
+        prefix = self.image_prefix(self.preprocess(image).to(self.t5.shared.weight.device))
+        enc = self.t5_encoder_states(prefix, prompt_ids)
+        ids = [self.cfg.bos_id]
+        for _ in range(max_new_tokens):
+            nxt = int(self.t5.decode_logits(enc, ids).argmax())
+            if nxt == self.cfg.eos_id:
+                break
+            ids.append(nxt)
+        return ids[1:]

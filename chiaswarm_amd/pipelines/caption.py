@@ -18,8 +18,9 @@ the implementation:
   (``models/git.py``), conditional on the prompt when one is given ([CLS] +
   prompt tokens, the GIT conditional-captioning / VQA form);
 * ``Blip2ForConditionalGeneration`` (+ ``Blip2Processor`` / ``AutoProcessor``):
-  BLIP-2 with an OPT language model (``models/blip2.py``); the prompt, when
-  given, is the text the LM continues ("Question: ... Answer:" for VQA);
+  BLIP-2 with an OPT or Flan-T5 language model (``models/blip2.py``); the
+  prompt, when given, is the text the LM continues / answers ("Question: ...
+  Answer:" for VQA);
 
 any other class is refused with a ``ValueError`` that names it (a fatal job
 error: retrying cannot help).  Model geometry comes from the checkpoint's
@@ -107,8 +108,8 @@ def load_git(model_name: str, device: str):
 
 def load_blip2(model_name: str, device: str):
     def make():
-        from ..models.blip2 import BLIP2_OPT_2_7B, BLIP2_OPT_6_7B, TINY_BLIP2, Blip2Captioner, Blip2Config, \
-            convert_hf_blip2
+        from ..models.blip2 import BLIP2_FLAN_T5_XL, BLIP2_OPT_2_7B, BLIP2_OPT_6_7B, TINY_BLIP2, Blip2Captioner, \
+            Blip2Config, convert_hf_blip2
         from ..models.hf_config import component_config
         from ..models.tokenizer import ByteBPETokenizer
 
@@ -118,9 +119,10 @@ def load_blip2(model_name: str, device: str):
             cfg = Blip2Config.from_hf(raw)
         else:
             n = model_name.lower()
-            if "t5" in n:
-                raise ValueError(f"img2txt: BLIP-2 with a T5 language model is not supported ({model_name})")
-            cfg = TINY_BLIP2 if n.startswith("tiny") else (BLIP2_OPT_6_7B if "6.7b" in n else BLIP2_OPT_2_7B)
+            if "t5" in n and "xxl" in n:
+                raise ValueError(f"img2txt: no built-in geometry for {model_name}; its config.json is required")
+            cfg = TINY_BLIP2 if n.startswith("tiny") else (
+                BLIP2_FLAN_T5_XL if "flan-t5" in n else (BLIP2_OPT_6_7B if "6.7b" in n else BLIP2_OPT_2_7B))
         dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
         with torch.device(device):
             m = Blip2Captioner(cfg).to(dt).eval().requires_grad_(False)
@@ -134,6 +136,10 @@ def load_blip2(model_name: str, device: str):
                 m.load_report = load_into(m, convert_hf_blip2(sd), name=model_name)
                 m.weights_source = w
         prepare_model(m)
+        if cfg.lm_type == "t5":
+            from ..models.t5 import T5Tokenizer
+
+            return m, T5Tokenizer(w, max_length=512, vocab=cfg.vocab, lower=False)
         return m, ByteBPETokenizer(w, max_length=512, vocab_size=cfg.vocab, bos=cfg.bos_id, eos=cfg.eos_id,
                                    pad=cfg.pad_id)
 

@@ -93,29 +93,36 @@ def test_blip2_original_qv_bias_form():
     assert m.image_prefix(px).shape == (1, NQ, 32)
 
 
-def test_blip2_t5_refused():
+def test_blip2_other_lm_refused():
     from chiaswarm_amd.models.blip2 import Blip2Config
 
-    with pytest.raises(ValueError, match="t5"):
-        Blip2Config.from_hf({"text_config": {"model_type": "t5"}})
+    with pytest.raises(ValueError, match="llama"):
+        Blip2Config.from_hf({"text_config": {"model_type": "llama"}})
 
 
 @pytest.mark.gpu
-def test_blip2_gpu_matches_fp32(gpu):
+@pytest.mark.parametrize("lm", ["opt", "t5"])
+def test_blip2_gpu_matches_fp32(gpu, lm):
+    """bf16 HIP path against the fp32 CPU model: next-token logits (OPT) /
+    decoder logits over the encoder states (Flan-T5)."""
     import copy
 
     from chiaswarm_amd.models.layers import prepare_model
 
-    hf_cfg, hf = _hf_tiny()
+    hf_cfg, hf = _hf_tiny() if lm == "opt" else _hf_tiny_t5(False)
     m = _ours(hf_cfg, hf.state_dict())
     g = copy.deepcopy(m).to(gpu).to(torch.bfloat16)
     prepare_model(g)
     px = m.preprocess(_image())
-    ids = [2, 17, 42, 5]
-    ref = m.text_logits(m.image_prefix(px), ids)
-    got = g.text_logits(g.image_prefix(px.to(gpu)), ids).cpu()
+    if lm == "opt":
+        ids = [2, 17, 42, 5]
+        ref = m.text_logits(m.image_prefix(px), ids)
+        got = g.text_logits(g.image_prefix(px.to(gpu)), ids).cpu()
+    else:
+        ref = m.t5.decode_logits(m.t5_encoder_states(m.image_prefix(px), [17, 42]), [0, 9, 33])
+        got = g.t5.decode_logits(g.t5_encoder_states(g.image_prefix(px.to(gpu)), [17, 42]), [0, 9, 33]).cpu()
     assert ((got - ref).norm() / ref.norm()).item() < 3e-2
-    assert len(g.generate(_image(), [], max_length=8)) <= 7
+    assert len(g.generate(_image(), [], max_length=8)) <= 8
 
 
 def test_blip2_dispatch_and_callback():
@@ -153,3 +160,90 @@ def test_gpt2_bpe_decode_roundtrip(tmp_path):
     ids = tok.encode(text)
     assert vocab["Ġthe"] in ids
     assert tok.decode([2] + ids) == text
+
+
+def _hf_tiny_t5(tied=False):
+    from transformers import Blip2Config, Blip2ForConditionalGeneration
+
+    vis = dict(hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=2, image_size=28,
+               patch_size=14)
+    qf = dict(hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=2,
+              encoder_hidden_size=32, cross_attention_frequency=2)
+    txt = dict(model_type="t5", vocab_size=100, d_model=32, d_kv=16, num_heads=2, d_ff=64, num_layers=2,
+               num_decoder_layers=3, feed_forward_proj="gated-gelu", tie_word_embeddings=tied,
+               decoder_start_token_id=0, eos_token_id=1, pad_token_id=0)
+    cfg = Blip2Config(vision_config=vis, qformer_config=qf, text_config=txt, num_query_tokens=NQ,
+                      image_token_index=IMG_TOK)
+    torch.manual_seed(1)
+    m = Blip2ForConditionalGeneration(cfg).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "norm" in n.lower() or n.endswith("bias") or "query_tokens" in n:
+                p.add_(torch.randn_like(p) * 0.1)
+            elif p.dim() >= 2 and p.std() < 1e-3:
+                p.normal_(0, 0.05)
+    return cfg, m
+
+
+@pytest.mark.parametrize("tied", [False, True])
+def test_blip2_flan_t5_logits_and_generate_match_transformers(tied):
+    """Flan-T5 language model: the encoder over [queries; prompt; </s>], the
+    decoder from the start token; logits and greedy decode vs transformers."""
+    hf_cfg, hf = _hf_tiny_t5(tied)
+    m = _ours(hf_cfg, hf.state_dict())
+    assert m.cfg.lm_type == "t5" and m.cfg.t5_tied == tied
+    img = _image()
+    px = m.preprocess(img)
+    prompt = [17, 42, 5]
+    enc_ids = torch.tensor([[IMG_TOK] * NQ + prompt + [1]])
+
+    def hf_logits(dec):
+        return hf(pixel_values=px.permute(0, 3, 1, 2), input_ids=enc_ids,
+                  decoder_input_ids=torch.tensor([dec])).logits[0, -1]
+
+    with torch.no_grad():
+        ref = hf_logits([0, 9, 33])
+    enc = m.t5_encoder_states(m.image_prefix(px), prompt)
+    got = m.t5.decode_logits(enc, [0, 9, 33])
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+    dec = [0]
+    with torch.no_grad():
+        while len(dec) < 10:
+            nxt = int(hf_logits(dec).argmax())
+            if nxt == 1:
+                break
+            dec.append(nxt)
+    assert m.generate(img, prompt, max_length=10) == dec[1:]
+
+
+def test_blip2_t5_v10_refused():
+    from chiaswarm_amd.models.blip2 import Blip2Config
+
+    with pytest.raises(ValueError, match="feed_forward_proj"):
+        Blip2Config.from_hf({"text_config": {"model_type": "t5", "feed_forward_proj": "relu"}})
+
+
+def test_blip2_flan_t5_callback(tmp_path, monkeypatch):
+    """img2txt job on a BLIP-2 Flan-T5 checkpoint directory (config.json of the
+    tiny geometry, its weights as safetensors): loads strictly and captions."""
+    import json
+
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.pipelines.caption import caption_callback
+
+    hf_cfg, hf = _hf_tiny_t5(False)
+    root = tmp_path / "tiny" / "blip2-flan-t5"
+    root.mkdir(parents=True)
+    (root / "config.json").write_text(json.dumps(hf_cfg.to_dict()))
+    save_file({k: v.clone().contiguous() for k, v in hf.state_dict().items()}, str(root / "model.safetensors"))
+    monkeypatch.setenv("SDAAS_MODEL_DIR", str(tmp_path))
+    res, cfg = caption_callback("cpu", "tiny/blip2-flan-t5", image=_image(), prompt="",
+                                parameters={"model_type": "Blip2ForConditionalGeneration",
+                                            "processor_type": "Blip2Processor"})
+    assert "error" not in cfg, cfg
+    assert isinstance(cfg["caption"], str)
+    from chiaswarm_amd.pipelines.caption import load_blip2
+
+    m, _ = load_blip2("tiny/blip2-flan-t5", "cpu")
+    assert m.cfg.lm_type == "t5" and m.weights_source == str(root)
