@@ -693,10 +693,20 @@ XATTN_WAVES = int(os.environ.get("CSK_XATTN_WAVES", "8"))  # 8: 40 vs 50 us, pro
 _xattn_waves_applied = [None]
 
 
+# below this many 128-row workgroups the fused kernel (one workgroup per CU)
+# leaves CUs idle and the unfused Q GEMM + short-KV attention + out GEMM chain
+# wins: CFG batch 2 (64 workgroups) 5.632 vs 5.679 ms per step unfused / fused,
+# CFG batch 8 (256) 11.765 vs 11.799 fused / unfused (profiles/unet_step_ab_xattn_gate_r7j.txt)
+XATTN_MIN_WG = int(os.environ.get("CSK_XATTN_MIN_WG", "256"))
+
+
 def xattn_ok(x, kv, rows_per_b) -> bool:
     """Shapes the fused cross-attention sub-block kernel takes: C = 320 (5 heads
-    of 64), <= 80 context tokens, whole 128-row tiles of one sample."""
+    of 64), <= 80 context tokens, whole 128-row tiles of one sample, and a grid
+    of at least XATTN_MIN_WG workgroups."""
     C = x.shape[-1]
+    if x.numel() // max(C, 1) // 128 < XATTN_MIN_WG:
+        return False
     return (XATTN_FUSED and C in XATTN_CHANNELS and kv is not None and kv.dim() == 5 and kv.shape[2] == 2
             and kv.shape[3] * kv.shape[4] == C and kv.shape[4] == 64 and 1 <= kv.shape[1] <= 80
             and rows_per_b % 128 == 0 and x.numel() // C % rows_per_b == 0

@@ -11,6 +11,26 @@ from chiaswarm_amd import ops
 from chiaswarm_amd.models.layers import BasicTransformerBlock, init_random_
 
 
+@pytest.fixture(autouse=True)
+def _any_grid(monkeypatch):
+    """Numerics run the fused kernel on small grids too (the product gates it
+    on >= XATTN_MIN_WG workgroups)."""
+    from chiaswarm_amd.ops import hip_ops
+
+    monkeypatch.setattr(hip_ops, "XATTN_MIN_WG", 0)
+
+
+def test_xattn_grid_gate_cpu(monkeypatch):
+    """The fused block runs for the CFG-batch-8 64x64 level (256 workgroups),
+    the unfused chain for CFG batch 2 (64)."""
+    from chiaswarm_amd.ops import hip_ops
+
+    monkeypatch.setattr(hip_ops, "XATTN_MIN_WG", 256)
+    kv = torch.empty(8, 77, 2, 5, 64, dtype=torch.bfloat16)
+    assert hip_ops.xattn_ok(torch.empty(8, 4096, 320, dtype=torch.bfloat16), kv, 4096)
+    assert not hip_ops.xattn_ok(torch.empty(2, 4096, 320, dtype=torch.bfloat16), kv, 4096)
+
+
 def _unfused(x, blk, kv):
     a2 = blk.attn2
     h = torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), blk.norm2.weight.float(), blk.norm2.bias.float(),

@@ -54,6 +54,10 @@ def apply_arm(arm):
         hip_ops.SPLITK_GN = arm == "skgn1"
     elif arm.startswith("skr"):  # split-K reduces: partial splits loaded per memory round trip (1 / 4 / 8)
         _lib.call("csk_set_skr_unroll", int(arm[3:]))
+    elif arm.startswith("xw"):  # fused cross-attention: minimum grid (workgroups) for the fused kernel
+        hip_ops.XATTN_MIN_WG = int(arm[2:])
+    elif arm in ("xa0", "xa1"):  # C = 320 cross-attention: unfused chain (0) / one fused kernel (1)
+        hip_ops.XATTN_FUSED = arm == "xa1"
     elif arm in ("lnoff", "lnon"):
         ops.LN_FUSE = arm == "lnon"
     elif arm in ("lnk0", "lnk1"):  # fused-LN row statistics: merge kernel (0) / in the consumer prologue (1)
