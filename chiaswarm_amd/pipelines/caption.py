@@ -17,6 +17,9 @@ the implementation:
 * ``GitForCausalLM`` (+ ``GitProcessor`` / ``AutoProcessor``): GIT captioning
   (``models/git.py``), conditional on the prompt when one is given ([CLS] +
   prompt tokens, the GIT conditional-captioning / VQA form);
+* ``VisionEncoderDecoderModel`` (+ ``ViTImageProcessor`` / ``AutoProcessor``):
+  ViT -> GPT-2 captioning (``models/vit_gpt2.py``, e.g.
+  nlpconnect/vit-gpt2-image-captioning);
 * ``Blip2ForConditionalGeneration`` (+ ``Blip2Processor`` / ``AutoProcessor``):
   BLIP-2 with an OPT or Flan-T5 language model (``models/blip2.py``); the
   prompt, when given, is the text the LM continues / answers ("Question: ...
@@ -38,22 +41,24 @@ from ..output.processor import make_text_result
 from ..runtime.model_cache import cache, find_weights
 
 MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git",
-               "Blip2ForConditionalGeneration": "blip2"}
+               "Blip2ForConditionalGeneration": "blip2", "VisionEncoderDecoderModel": "vitgpt2"}
 PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", "GitProcessor", "CLIPImageProcessor",
-                   "Blip2Processor", None}
+                   "Blip2Processor", "ViTImageProcessor", "ViTFeatureExtractor", None}
 
 
 def resolve_task(params: dict | None, model_name: str) -> str:
-    """'caption' | 'vqa' | 'git' | 'blip2' from the hive's class names; ValueError for anything else."""
+    """'caption' | 'vqa' | 'git' | 'blip2' | 'vitgpt2' from the hive's class names; ValueError for anything else."""
     params = params or {}
     mt, pt = params.get("model_type"), params.get("processor_type")
     if pt not in PROCESSOR_TYPES:
         raise ValueError(f"img2txt: processor_type {pt!r} is not supported "
-                         "(supported: BlipProcessor, GitProcessor, Blip2Processor, AutoProcessor)")
+                         "(supported: BlipProcessor, GitProcessor, Blip2Processor, ViTImageProcessor, AutoProcessor)")
     if mt is None:
         n = model_name.lower()
         if "blip2" in n:
             return "blip2"
+        if "vit-gpt2" in n:
+            return "vitgpt2"
         return "vqa" if "vqa" in n else ("git" if "/git-" in n or n.startswith("git-") else "caption")
     if mt not in MODEL_TYPES:
         raise ValueError(f"img2txt: model_type {mt!r} is not supported "
@@ -146,11 +151,44 @@ def load_blip2(model_name: str, device: str):
     return cache().get(("blip2", model_name, device), make)
 
 
+def load_vitgpt2(model_name: str, device: str):
+    def make():
+        from ..models.hf_config import component_config
+        from ..models.tokenizer import ByteBPETokenizer
+        from ..models.vit_gpt2 import TINY_VIT_GPT2, VIT_GPT2, VitGpt2Captioner, VitGpt2Config, convert_hf_vit_gpt2
+
+        w = find_weights(model_name)
+        raw = component_config(w, "") if w else None
+        if raw is not None and "encoder" in raw and "decoder" in raw:
+            cfg = VitGpt2Config.from_hf(raw, component_config(w, "", "preprocessor_config.json"))
+        else:
+            cfg = TINY_VIT_GPT2 if model_name.lower().startswith("tiny") else VIT_GPT2
+        dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+        with torch.device(device):
+            m = VitGpt2Captioner(cfg).to(dt).eval().requires_grad_(False)
+        init_random_fast_(m, seed=11)
+        m.weights_source = "random-init"
+        if w:
+            from ..models.weights import _read_dir, load_into
+
+            sd = _read_dir(w)
+            if sd:
+                m.load_report = load_into(m, convert_hf_vit_gpt2(sd), name=model_name)
+                m.weights_source = w
+        prepare_model(m)
+        return m, ByteBPETokenizer(w, max_length=1024, vocab_size=cfg.vocab, bos=cfg.start_id, eos=cfg.eos_id,
+                                   pad=cfg.pad_id)
+
+    return cache().get(("vitgpt2", model_name, device), make)
+
+
 def load_captioner(model_name: str, device: str, task: str = "caption"):
     if task == "git":
         return load_git(model_name, device)
     if task == "blip2":
         return load_blip2(model_name, device)
+    if task == "vitgpt2":
+        return load_vitgpt2(model_name, device)
 
     def make():
         w = find_weights(model_name)
