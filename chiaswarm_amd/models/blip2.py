@@ -1,4 +1,4 @@
-"""BLIP-2 image captioning / prompted VQA with an OPT or Flan-T5 language model
+"""BLIP-2 / InstructBLIP image captioning / prompted VQA (OPT, Flan-T5 or Vicuna-LLaMA language models)
 (transformers ``Blip2ForConditionalGeneration`` + ``Blip2Processor``, the
 ``Salesforce/blip2-opt-*`` and ``blip2-flan-t5-*`` checkpoints).  Reference: the hive names the
 processor / model classes at swarm/captioning/caption_image.py:11-29 and the
@@ -18,7 +18,12 @@ LayerNorm, GEMM epilogues):
     ``[projected queries; </s>; prompt]``; or
   - Flan-T5 (``blip2-flan-t5-*``, ``models/t5.py::T5Seq2Seq``): the encoder
     reads ``[projected queries; prompt; </s>]``, the decoder generates from the
-    decoder start token (pad, 0) with cross-attention over it.
+    decoder start token (pad, 0) with cross-attention over it;
+  - Vicuna / LLaMA (``instructblip-vicuna-*``, ``models/llama.py``) after
+    ``[projected queries; <s> prompt]``.
+* InstructBLIP (``InstructBlipForConditionalGeneration``): the instruction, in
+  the Q-Former's own WordPiece tokens, joins the 32 queries in the Q-Former's
+  self-attention (the instruction rows take the text FFN).
 
 Greedy decode with transformers' default ``max_length=20`` (OPT: counted on the
 text part, ``</s>`` + prompt + generated; T5: decoder tokens), stopping at the
@@ -36,6 +41,7 @@ import torch.nn as nn
 from PIL import Image
 
 from .layers import LayerNorm, Linear
+from .llama import LlamaConfig, LlamaLM
 from .t5 import T5Config, T5Seq2Seq
 from .transformer import PostLNBlock, PreLNBlock, ViT
 
@@ -73,6 +79,12 @@ class Blip2Config:
     t5: T5Config | None = None  # lm_type "t5": the Flan-T5 geometry (lm_dim = t5.d_model)
     t5_dec_layers: int = 0
     t5_tied: bool = False
+    llama: LlamaConfig | None = None  # lm_type "llama" (InstructBLIP's Vicuna)
+    instruct: bool = False  # InstructBLIP: the Q-Former also reads the instruction text
+    q_vocab: int = 30522
+    q_max_pos: int = 512
+    q_cls_id: int = 101  # the Q-Former tokenizer's [CLS] / [SEP] (bert-base-uncased)
+    q_sep_id: int = 102
 
     @classmethod
     def from_hf(cls, cfg: dict) -> "Blip2Config":
@@ -80,6 +92,13 @@ class Blip2Config:
         sub-configs; the text model is OPT or (Flan-)T5 v1.1)."""
         v, q, t = cfg.get("vision_config") or {}, cfg.get("qformer_config") or {}, cfg.get("text_config") or {}
         lm = t.get("model_type", "opt")
+        instruct = cfg.get("model_type") == "instructblip" or bool(q.get("vocab_size") and "instructblip" in
+                                                                     str(cfg.get("architectures", "")).lower())
+        if lm == "llama" and instruct:
+            base = cls._vision_qformer(cfg, v, q)
+            lc = LlamaConfig.from_hf(t)
+            return dataclasses.replace(base, lm_type="llama", llama=lc, lm_dim=lc.dim, vocab=lc.vocab,
+                                       bos_id=lc.bos_id, eos_id=lc.eos_id, pad_id=t.get("pad_token_id") or 0)
         if lm not in ("opt", "t5"):
             raise ValueError(f"img2txt: BLIP-2 with a {lm!r} language model is not supported (OPT, Flan-T5)")
         if lm == "t5":
@@ -113,7 +132,9 @@ class Blip2Config:
 
     @classmethod
     def _vision_qformer(cls, cfg, v, q) -> "Blip2Config":
-        return cls(image_size=v.get("image_size", 224), patch=v.get("patch_size", 14),
+        instruct = cfg.get("model_type") == "instructblip" or "instructblip" in str(cfg.get("architectures", "")).lower()
+        return cls(instruct=instruct, q_vocab=q.get("vocab_size", 30522), q_max_pos=q.get("max_position_embeddings", 512),
+                   image_size=v.get("image_size", 224), patch=v.get("patch_size", 14),
                    vision_dim=v.get("hidden_size", 1408), vision_depth=v.get("num_hidden_layers", 39),
                    vision_heads=v.get("num_attention_heads", 16), vision_mlp=v.get("intermediate_size", 6144),
                    vision_eps=v.get("layer_norm_eps", 1e-6), q_dim=q.get("hidden_size", 768),
@@ -151,19 +172,24 @@ def _sub(rest: str, table: dict) -> str | None:
     return None
 
 
-def convert_hf_blip2(sd: dict) -> dict:
+def convert_hf_blip2(sd: dict, instruct: bool | None = None) -> dict:
     """transformers ``Blip2ForConditionalGeneration`` (OPT) state dict -> this
     module's keys.  Vision attention biases come either as the fused
     ``qkv.bias`` or as the original checkpoints' ``q_bias`` / ``v_bias`` (k bias
     zero); the Q-Former's text FFN (``intermediate.`` / ``output.``, unused
     without Q-Former text input) is dropped; the LM head is tied."""
     out: dict = {}
+    if instruct is None:  # InstructBLIP: the Q-Former has its own text embeddings
+        instruct = "qformer.embeddings.word_embeddings.weight" in sd
+    llama = "language_model.model.embed_tokens.weight" in sd
     for k, v in sd.items():
         if k.endswith("position_ids"):
             continue
         if k == "language_model.lm_head.weight":
             if "language_model.shared.weight" in sd:  # T5: own (or tied-and-saved) head
                 out["t5.lm_head.weight"] = v
+            elif llama:
+                out["llama.lm_head.weight"] = v
             continue  # OPT: tied to the token embeddings
         if k == "query_tokens":
             out[k] = v.reshape(v.shape[-2], v.shape[-1])
@@ -190,14 +216,25 @@ def convert_hf_blip2(sd: dict) -> dict:
             else:
                 s = _sub(rest, _V)
                 out[f"vision_model.layers.{n}.{s}" if s else k] = v
-        elif k.startswith("qformer.layernorm."):
+        elif k.startswith("qformer.layernorm.") or k.startswith("qformer.embeddings.layernorm."):
             out["qformer_ln." + k.rsplit(".", 1)[1]] = v
+        elif k == "qformer.embeddings.word_embeddings.weight" and instruct:
+            out["q_word.weight"] = v
+        elif k == "qformer.embeddings.position_embeddings.weight" and instruct:
+            out["q_pos.weight"] = v
         elif k.startswith("qformer.encoder.layer."):
             n, rest = k.removeprefix("qformer.encoder.layer.").split(".", 1)
             if rest.startswith(("intermediate.", "output.")):
+                if instruct:  # the instruction tokens' FFN (InstructBLIP)
+                    t = {"intermediate.dense": "fc1", "output.dense": "fc2", "output.LayerNorm": "ln"}
+                    s = _sub(rest, t)
+                    out[f"qtext.{n}.{s}" if s else k] = v
                 continue
             s = _sub(rest, _Q)
             out[f"qformer.{n}.{s}" if s else k] = v
+        elif k.startswith("language_model.model.") and not k.startswith("language_model.model.decoder.") and \
+                "language_model.model.embed_tokens.weight" in sd:  # LLaMA (InstructBLIP Vicuna)
+            out["llama." + k.removeprefix("language_model.")] = v
         elif k.startswith("language_projection."):
             out[k] = v
         elif k.startswith("language_model.") and not k.startswith("language_model.model.") and \
@@ -237,7 +274,14 @@ class Blip2Captioner(nn.Module):
         self.qformer = nn.ModuleList([
             PostLNBlock(cfg.q_dim, cfg.q_heads, cfg.q_mlp, cross_dim=cfg.vision_dim if i % cfg.cross_freq == 0 else None,
                         eps=cfg.q_eps) for i in range(cfg.q_depth)])
+        if cfg.instruct:  # InstructBLIP: instruction tokens enter the Q-Former too
+            self.q_word = nn.Embedding(cfg.q_vocab, cfg.q_dim)
+            self.q_pos = nn.Embedding(cfg.q_max_pos, cfg.q_dim)
+            self.qtext = nn.ModuleList([_TextFFN(cfg) for _ in range(cfg.q_depth)])
         self.language_projection = Linear(cfg.q_dim, cfg.lm_dim)
+        if cfg.lm_type == "llama":
+            self.llama = LlamaLM(cfg.llama)
+            return
         if cfg.lm_type == "t5":
             self.t5 = T5Seq2Seq(cfg.t5, cfg.t5_dec_layers or cfg.t5.layers, tie_embeddings=cfg.t5_tied)
             return
@@ -249,6 +293,8 @@ class Blip2Captioner(nn.Module):
 
     @property
     def _emb(self) -> nn.Embedding:
+        if self.cfg.lm_type == "llama":
+            return self.llama.model.embed_tokens
         return self.t5.shared if self.cfg.lm_type == "t5" else self.embed_tokens
 
     def preprocess(self, image: Image.Image) -> torch.Tensor:
@@ -258,15 +304,34 @@ class Blip2Captioner(nn.Module):
         return torch.from_numpy((a - MEAN) / STD)[None]
 
     @torch.no_grad()
-    def image_prefix(self, pixels: torch.Tensor) -> torch.Tensor:
+    def image_prefix(self, pixels: torch.Tensor, qtext_ids: list[int] | None = None) -> torch.Tensor:
         """Projected Q-Former query outputs [1, num_query, lm_dim]: the language
-        model's input embeddings ahead of the text."""
+        model's input embeddings ahead of the text.  InstructBLIP: the
+        instruction's Q-Former tokens ([CLS] ... [SEP]) follow the queries through
+        the self-attention (cross-attention and the query FFN on the query rows,
+        the text FFN on the instruction rows)."""
         dt = self._emb.weight.dtype
         img = self.vision_model(pixels.to(dt))
-        q = self.qformer_ln(self.query_tokens[None].to(dt))
-        for blk in self.qformer:
-            q = blk(q, ctx=img)
-        return self.language_projection(q)
+        q = self.query_tokens[None].to(dt)
+        if not self.cfg.instruct:
+            q = self.qformer_ln(q)
+            for blk in self.qformer:
+                q = blk(q, ctx=img)
+            return self.language_projection(q)
+        ids = torch.tensor([list(qtext_ids or [])], device=q.device, dtype=torch.long)
+        t = self.q_word(ids).to(dt) + self.q_pos.weight[: ids.shape[1]][None].to(dt)
+        h = self.qformer_ln(torch.cat([q, t], 1))
+        nq = q.shape[1]
+        for blk, tf in zip(self.qformer, self.qtext):
+            h = blk.ln1(blk.attn(h, residual=h))
+            qp, tp = h[:, :nq], h[:, nq:]
+            if blk.cross is not None:
+                qp = blk.ln_x(blk.cross(qp, ctx=img, residual=qp))
+            qp = blk.ln2(blk.fc2(blk.fc1(qp, act="gelu"), residual=qp))
+            if tp.shape[1]:
+                tp = tf.ln(tf.fc2(tf.fc1(tp, act="gelu"), residual=tp))
+            h = torch.cat([qp, tp], 1)
+        return self.language_projection(h[:, :nq])
 
     @torch.no_grad()
     def text_logits(self, prefix: torch.Tensor, ids: list[int]) -> torch.Tensor:
@@ -282,11 +347,13 @@ class Blip2Captioner(nn.Module):
 
     @torch.no_grad()
     def generate(self, image: Image.Image, prefix_ids: list[int], max_new_tokens: int | None = None,
-                 max_length: int = 20) -> list[int]:
+                 max_length: int = 20, qtext_ids: list[int] | None = None) -> list[int]:
         """Greedy decode from ``</s> + prefix`` after the image queries; returns
         prefix + generated ids (without the leading ``</s>``)."""
         if self.cfg.lm_type == "t5":
-            return self._generate_t5(image, prefix_ids, max_new_tokens, max_length)
+            return self._generate_t5(image, prefix_ids, max_new_tokens, max_length, qtext_ids)
+        if self.cfg.lm_type == "llama":
+            return self._generate_llama(image, prefix_ids, max_new_tokens, max_length, qtext_ids)
         if max_new_tokens is None:
             max_new_tokens = max(0, max_length - 1 - len(prefix_ids))
         prefix = self.image_prefix(self.preprocess(image).to(self.embed_tokens.weight.device))
@@ -307,12 +374,12 @@ class Blip2Captioner(nn.Module):
         ids = torch.tensor([list(prompt_ids) + [self.cfg.eos_id]], device=prefix.device)
         return t5.encode(torch.cat([prefix, t5.shared(ids).to(prefix.dtype)], 1))
 
-    def _generate_t5(self, image, prompt_ids, max_new_tokens, max_length) -> list[int]:
+    def _generate_t5(self, image, prompt_ids, max_new_tokens, max_length, qtext_ids=None) -> list[int]:
         """Greedy decode from the decoder start token; returns the generated ids
         (the prompt lives in the encoder)."""
         if max_new_tokens is None:
             max_new_tokens = max(0, max_length - 1)
-        prefix = self.image_prefix(self.preprocess(image).to(self.t5.shared.weight.device))
+        prefix = self.image_prefix(self.preprocess(image).to(self.t5.shared.weight.device), qtext_ids)
         enc = self.t5_encoder_states(prefix, prompt_ids)
         ids = [self.cfg.bos_id]
         for _ in range(max_new_tokens):
@@ -321,3 +388,31 @@ class Blip2Captioner(nn.Module):
                 break
             ids.append(nxt)
         return ids[1:]
+
+    def _generate_llama(self, image, prompt_ids, max_new_tokens, max_length, qtext_ids=None) -> list[int]:
+        """InstructBLIP (Vicuna): greedy decode after [queries; <s> prompt];
+        returns the generated ids."""
+        if max_new_tokens is None:
+            max_new_tokens = max(0, max_length - 1)
+        emb = self.llama.model.embed_tokens
+        prefix = self.image_prefix(self.preprocess(image).to(emb.weight.device), qtext_ids)
+        ids = [self.cfg.bos_id] + list(prompt_ids)
+        out = []
+        for _ in range(max_new_tokens):
+            x = torch.cat([prefix, emb(torch.tensor([ids], device=prefix.device)).to(prefix.dtype)], 1)
+            nxt = int(self.llama.last_logits(x).argmax())
+            if nxt == self.cfg.eos_id:
+                break
+            ids.append(nxt)
+            out.append(nxt)
+        return out
+
+
+class _TextFFN(nn.Module):
+    """InstructBLIP Q-Former FFN of the instruction tokens (post-LN)."""
+
+    def __init__(self, cfg: Blip2Config):
+        super().__init__()
+        self.fc1 = Linear(cfg.q_dim, cfg.q_mlp)
+        self.fc2 = Linear(cfg.q_mlp, cfg.q_dim)
+        self.ln = LayerNorm(cfg.q_dim, eps=cfg.q_eps)

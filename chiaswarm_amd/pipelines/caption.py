@@ -20,8 +20,10 @@ the implementation:
 * ``VisionEncoderDecoderModel`` (+ ``ViTImageProcessor`` / ``AutoProcessor``):
   ViT -> GPT-2 captioning (``models/vit_gpt2.py``, e.g.
   nlpconnect/vit-gpt2-image-captioning);
-* ``Blip2ForConditionalGeneration`` (+ ``Blip2Processor`` / ``AutoProcessor``):
-  BLIP-2 with an OPT or Flan-T5 language model (``models/blip2.py``); the
+* ``Blip2ForConditionalGeneration`` / ``InstructBlipForConditionalGeneration``
+  (+ ``Blip2Processor`` / ``InstructBlipProcessor`` / ``AutoProcessor``):
+  BLIP-2 / InstructBLIP with an OPT, Flan-T5 or Vicuna language model
+  (``models/blip2.py``); the
   prompt, when given, is the text the LM continues / answers ("Question: ...
   Answer:" for VQA);
 
@@ -32,6 +34,8 @@ only without one.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..models.blip import BLIP_BASE, BLIP_LARGE, TINY_BLIP, BlipCaptioner, BlipConfig, BlipVQA
@@ -41,9 +45,10 @@ from ..output.processor import make_text_result
 from ..runtime.model_cache import cache, find_weights
 
 MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git",
-               "Blip2ForConditionalGeneration": "blip2", "VisionEncoderDecoderModel": "vitgpt2"}
+               "Blip2ForConditionalGeneration": "blip2", "InstructBlipForConditionalGeneration": "blip2",
+               "VisionEncoderDecoderModel": "vitgpt2"}
 PROCESSOR_TYPES = {"BlipProcessor", "AutoProcessor", "BlipImageProcessor", "GitProcessor", "CLIPImageProcessor",
-                   "Blip2Processor", "ViTImageProcessor", "ViTFeatureExtractor", None}
+                   "Blip2Processor", "InstructBlipProcessor", "ViTImageProcessor", "ViTFeatureExtractor", None}
 
 
 def resolve_task(params: dict | None, model_name: str) -> str:
@@ -55,7 +60,7 @@ def resolve_task(params: dict | None, model_name: str) -> str:
                          "(supported: BlipProcessor, GitProcessor, Blip2Processor, ViTImageProcessor, AutoProcessor)")
     if mt is None:
         n = model_name.lower()
-        if "blip2" in n:
+        if "blip2" in n or "instructblip" in n:
             return "blip2"
         if "vit-gpt2" in n:
             return "vitgpt2"
@@ -124,6 +129,8 @@ def load_blip2(model_name: str, device: str):
             cfg = Blip2Config.from_hf(raw)
         else:
             n = model_name.lower()
+            if "instructblip" in n and not n.startswith("tiny"):
+                raise ValueError(f"img2txt: {model_name}: InstructBLIP needs its config.json")
             if "t5" in n and "xxl" in n:
                 raise ValueError(f"img2txt: no built-in geometry for {model_name}; its config.json is required")
             cfg = TINY_BLIP2 if n.startswith("tiny") else (
@@ -141,14 +148,43 @@ def load_blip2(model_name: str, device: str):
                 m.load_report = load_into(m, convert_hf_blip2(sd), name=model_name)
                 m.weights_source = w
         prepare_model(m)
+        if cfg.instruct:  # the Q-Former's own BERT tokenizer, [CLS] instruction [SEP]
+            m.qformer_tokenizer = WordPiece(os.path.join(w, "qformer_tokenizer") if w else None, cfg.q_vocab)
         if cfg.lm_type == "t5":
             from ..models.t5 import T5Tokenizer
 
             return m, T5Tokenizer(w, max_length=512, vocab=cfg.vocab, lower=False)
+        if cfg.lm_type == "llama":
+            return m, _SentencePiece(w, "tokenizer.model", cfg.vocab, skip=(cfg.bos_id, cfg.eos_id, cfg.pad_id))
         return m, ByteBPETokenizer(w, max_length=512, vocab_size=cfg.vocab, bos=cfg.bos_id, eos=cfg.eos_id,
                                    pad=cfg.pad_id)
 
     return cache().get(("blip2", model_name, device), make)
+
+
+class _SentencePiece:
+    """SentencePiece model file of a checkpoint (LLaMA ``tokenizer.model``), no
+    special tokens added; hash fallback without one (random-init runs)."""
+
+    def __init__(self, w: str | None, name: str, vocab: int, skip=()):
+        self.sp, self.vocab, self.skip = None, vocab, set(skip)
+        path = os.path.join(w, name) if w else None
+        if path and os.path.exists(path):
+            import sentencepiece
+
+            self.sp = sentencepiece.SentencePieceProcessor(model_file=path)
+
+    def encode(self, text: str) -> list[int]:
+        if self.sp is not None:
+            return list(self.sp.encode(text))
+        import hashlib
+
+        return [int.from_bytes(hashlib.blake2b(t.encode(), digest_size=8).digest(), "little") % (self.vocab - 10) + 3
+                for t in text.split()]
+
+    def decode(self, ids: list[int]) -> str:
+        ids = [int(i) for i in ids if int(i) not in self.skip]
+        return self.sp.decode(ids) if self.sp is not None else " ".join(f"w{i}" for i in ids)
 
 
 def load_vitgpt2(model_name: str, device: str):
@@ -230,8 +266,15 @@ def caption_callback(device_identifier, model_name, **kwargs):
         else:
             prefix = tok.encode(prompt) if prompt else []
             mnt = kwargs.get("max_new_tokens")
+            extra = {}
+            qt = getattr(model, "qformer_tokenizer", None)
+            if qt is not None:  # InstructBLIP: the instruction also enters the Q-Former
+                c = model.cfg  # [CLS] / [SEP] from the Q-Former vocab.txt (bert-base-uncased: 101 / 102)
+                cls_id = qt.vocab.get("[CLS]", min(c.q_cls_id, c.q_vocab - 2))
+                sep_id = qt.vocab.get("[SEP]", min(c.q_sep_id, c.q_vocab - 1))
+                extra["qtext_ids"] = [cls_id] + (qt.encode(prompt) if prompt else []) + [sep_id]
             ids = model.generate(image, prefix, max_new_tokens=None if mnt is None else int(mnt),
-                                 max_length=int(kwargs.get("max_length", 20)))
+                                 max_length=int(kwargs.get("max_length", 20)), **extra)
             caption = tok.decode(ids).strip()
         results["primary"] = make_text_result(caption)
         config["caption"] = caption

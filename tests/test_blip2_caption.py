@@ -101,7 +101,7 @@ def test_blip2_other_lm_refused():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lm", ["opt", "t5"])
+@pytest.mark.parametrize("lm", ["opt", "t5", "instruct-llama"])
 def test_blip2_gpu_matches_fp32(gpu, lm):
     """bf16 HIP path against the fp32 CPU model: next-token logits (OPT) /
     decoder logits over the encoder states (Flan-T5)."""
@@ -109,7 +109,7 @@ def test_blip2_gpu_matches_fp32(gpu, lm):
 
     from chiaswarm_amd.models.layers import prepare_model
 
-    hf_cfg, hf = _hf_tiny() if lm == "opt" else _hf_tiny_t5(False)
+    hf_cfg, hf = _hf_tiny() if lm == "opt" else (_hf_tiny_t5(False) if lm == "t5" else _hf_tiny_instruct("llama"))
     m = _ours(hf_cfg, hf.state_dict())
     g = copy.deepcopy(m).to(gpu).to(torch.bfloat16)
     prepare_model(g)
@@ -118,9 +118,14 @@ def test_blip2_gpu_matches_fp32(gpu, lm):
         ids = [2, 17, 42, 5]
         ref = m.text_logits(m.image_prefix(px), ids)
         got = g.text_logits(g.image_prefix(px.to(gpu)), ids).cpu()
-    else:
+    elif lm == "t5":
         ref = m.t5.decode_logits(m.t5_encoder_states(m.image_prefix(px), [17, 42]), [0, 9, 33])
         got = g.t5.decode_logits(g.t5_encoder_states(g.image_prefix(px.to(gpu)), [17, 42]), [0, 9, 33]).cpu()
+    else:
+        qids, ids = [3, 11, 25, 4], torch.tensor([[1, 17, 42, 5]])
+        ref = m.llama.last_logits(torch.cat([m.image_prefix(px, qids), m.llama.model.embed_tokens(ids)], 1))
+        pre = g.image_prefix(px.to(gpu), qids)
+        got = g.llama.last_logits(torch.cat([pre, g.llama.model.embed_tokens(ids.to(gpu))], 1)).cpu()
     assert ((got - ref).norm() / ref.norm()).item() < 3e-2
     assert len(g.generate(_image(), [], max_length=8)) <= 8
 
@@ -247,3 +252,100 @@ def test_blip2_flan_t5_callback(tmp_path, monkeypatch):
 
     m, _ = load_blip2("tiny/blip2-flan-t5", "cpu")
     assert m.cfg.lm_type == "t5" and m.weights_source == str(root)
+
+
+def _hf_tiny_instruct(lm):
+    from transformers import InstructBlipConfig, InstructBlipForConditionalGeneration
+
+    vis = dict(hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=2, image_size=28,
+               patch_size=14)
+    qf = dict(hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=2,
+              encoder_hidden_size=32, cross_attention_frequency=2, vocab_size=60, max_position_embeddings=32)
+    if lm == "t5":
+        txt = dict(model_type="t5", vocab_size=100, d_model=32, d_kv=16, num_heads=2, d_ff=64, num_layers=2,
+                   num_decoder_layers=2, feed_forward_proj="gated-gelu", tie_word_embeddings=False,
+                   decoder_start_token_id=0, eos_token_id=1, pad_token_id=0)
+    else:
+        txt = dict(model_type="llama", vocab_size=100, hidden_size=32, intermediate_size=64, num_hidden_layers=2,
+                   num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64, bos_token_id=1,
+                   eos_token_id=2, pad_token_id=0)
+    cfg = InstructBlipConfig(vision_config=vis, qformer_config=qf, text_config=txt, num_query_tokens=NQ,
+                             image_token_index=IMG_TOK)
+    torch.manual_seed(3)
+    m = InstructBlipForConditionalGeneration(cfg).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "norm" in n.lower() or n.endswith("bias") or "query_tokens" in n:
+                p.add_(torch.randn_like(p) * 0.1)
+            elif p.dim() >= 2 and p.std() < 1e-3:
+                p.normal_(0, 0.05)
+    return cfg, m
+
+
+@pytest.mark.parametrize("lm", ["t5", "llama"])
+def test_instructblip_logits_and_generate_match_transformers(lm):
+    """InstructBLIP (Flan-T5 / Vicuna-LLaMA language model): the instruction's
+    Q-Former tokens join the queries; logits and greedy decode vs transformers."""
+    cfg, hf = _hf_tiny_instruct(lm)
+    m = _ours(cfg, hf.state_dict())
+    assert m.cfg.instruct and m.cfg.lm_type == lm
+    img = _image()
+    px = m.preprocess(img)
+    qids = [3, 11, 25, 4]  # Q-Former tokens of the instruction ([CLS] ... [SEP])
+    prompt = [17, 42, 5]
+    pv = px.permute(0, 3, 1, 2)
+    if lm == "t5":
+        enc_ids = torch.tensor([[IMG_TOK] * NQ + prompt + [1]])
+
+        def hf_logits(dec):
+            return hf(pixel_values=pv, qformer_input_ids=torch.tensor([qids]), input_ids=enc_ids,
+                      decoder_input_ids=torch.tensor([dec])).logits[0, -1]
+
+        with torch.no_grad():
+            ref = hf_logits([0, 9, 33])
+        got = m.t5.decode_logits(m.t5_encoder_states(m.image_prefix(px, qids), prompt), [0, 9, 33])
+        start, eos = [0], 1
+    else:
+        def hf_logits(dec):
+            ids = torch.tensor([[IMG_TOK] * NQ + [1] + prompt + dec])
+            return hf(pixel_values=pv, qformer_input_ids=torch.tensor([qids]), input_ids=ids).logits[0, -1]
+
+        with torch.no_grad():
+            ref = hf_logits([9, 33])
+        pre = m.image_prefix(px, qids)
+        emb = m.llama.model.embed_tokens
+        got = m.llama.last_logits(torch.cat([pre, emb(torch.tensor([[1] + prompt + [9, 33]]))], 1))
+        start, eos = [], 2
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+    dec = list(start)
+    with torch.no_grad():
+        while len(dec) < 8:
+            nxt = int(hf_logits(dec).argmax())
+            if nxt == eos:
+                break
+            dec.append(nxt)
+    assert m.generate(img, prompt, max_length=8 if lm == "t5" else 9, qtext_ids=qids) == dec[len(start):]
+
+
+def test_instructblip_vicuna_callback(tmp_path, monkeypatch):
+    """img2txt job naming InstructBlipForConditionalGeneration on a Vicuna-LLaMA
+    checkpoint directory (config.json + safetensors): strict load, caption."""
+    import json
+
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.pipelines.caption import caption_callback, load_blip2
+
+    cfg, hf = _hf_tiny_instruct("llama")
+    root = tmp_path / "tiny" / "instructblip-vicuna"
+    root.mkdir(parents=True)
+    (root / "config.json").write_text(json.dumps(cfg.to_dict()))
+    save_file({k: v.clone().contiguous() for k, v in hf.state_dict().items()}, str(root / "model.safetensors"))
+    monkeypatch.setenv("SDAAS_MODEL_DIR", str(tmp_path))
+    m, _ = load_blip2("tiny/instructblip-vicuna", "cpu")
+    assert m.cfg.instruct and m.cfg.lm_type == "llama" and m.weights_source == str(root)
+    res, out = caption_callback("cpu", "tiny/instructblip-vicuna", image=_image(), prompt="what is in the picture?",
+                                parameters={"model_type": "InstructBlipForConditionalGeneration",
+                                            "processor_type": "InstructBlipProcessor"})
+    assert "error" not in out, out
+    assert isinstance(out["caption"], str)

@@ -212,8 +212,8 @@ def test_img2txt_class_names(tmp_path):
     assert resolve_task(None, "Salesforce/blip-vqa-base") == "vqa"
     assert resolve_task({"processor_type": "AutoProcessor", "model_type": "GitForCausalLM"}, "microsoft/git-base") \
         == "git"
-    with pytest.raises(ValueError, match="InstructBlipForConditionalGeneration"):
-        resolve_task({"processor_type": "AutoProcessor", "model_type": "InstructBlipForConditionalGeneration"}, "x")
+    with pytest.raises(ValueError, match="Kosmos2ForConditionalGeneration"):
+        resolve_task({"processor_type": "AutoProcessor", "model_type": "Kosmos2ForConditionalGeneration"}, "x")
     with pytest.raises(ValueError, match="ViltProcessor"):
         resolve_task({"processor_type": "ViltProcessor", "model_type": "BlipForQuestionAnswering"}, "x")
 

@@ -70,7 +70,7 @@ def test_caption_dispatch_accepts_git():
         == "git"
     assert resolve_task({"model_type": "GitForCausalLM", "processor_type": "AutoProcessor"}, "x") == "git"
     with pytest.raises(ValueError):
-        resolve_task({"model_type": "InstructBlipForConditionalGeneration"}, "Salesforce/instructblip-vicuna-7b")
+        resolve_task({"model_type": "Kosmos2ForConditionalGeneration"}, "microsoft/kosmos-2-patch14-224")
 
 
 def test_caption_callback_git_end_to_end():

@@ -171,9 +171,9 @@ def test_img2txt_vqa_and_unsupported_class_envelopes(monkeypatch):
     r2 = synchronous_do_work_function(git, Device("cpu"))
     assert "fatal_error" not in r2 and "error" not in r2["pipeline_config"], r2["pipeline_config"]
     bad = dict(job, id="v3", parameters={"processor_type": "AutoProcessor",
-                                         "model_type": "InstructBlipForConditionalGeneration"})
+                                         "model_type": "Kosmos2ForConditionalGeneration"})
     r3 = synchronous_do_work_function(bad, Device("cpu"))
-    assert r3.get("fatal_error") is True and "InstructBlipForConditionalGeneration" in r3["pipeline_config"]["error"]
+    assert r3.get("fatal_error") is True and "Kosmos2ForConditionalGeneration" in r3["pipeline_config"]["error"]
 
 
 def test_unet_cfg_shared_prefix_and_temb_table_cpu():
