@@ -230,6 +230,17 @@ class UNet2DConditionModel(Prepared):
         return [m.context_kv(ctx) for m in self.cross_attention_modules()]
 
     # ------------------------------------------------------------------
+    def add_emb(self, added_cond, dtype=None):
+        """SDXL ``text_time`` addition embedding (pooled text embeds + the
+        sinusoidal size / crop ids through ``add_embedding``): constant over a
+        request's denoising steps."""
+        dtype = dtype or self.conv_in.weight.dtype
+        text_embeds = added_cond["text_embeds"]
+        tid = timestep_embedding(added_cond["time_ids"].reshape(-1), self.cfg.addition_time_embed_dim)
+        tid = tid.reshape(text_embeds.shape[0], -1)
+        add_in = torch.cat([text_embeds.float(), tid], dim=-1).to(dtype)
+        return self.add_embedding(add_in)
+
     def time_embed(self, timestep, batch, dtype, added_cond=None, class_labels=None):
         t = timestep
         if not torch.is_tensor(t):
@@ -244,12 +255,8 @@ class UNet2DConditionModel(Prepared):
                                      self.cfg.block_out_channels[0]).to(dtype)
         temb = self.time_embedding(emb)
         if self.cfg.addition_embed_type == "text_time":
-            text_embeds = added_cond["text_embeds"]
-            time_ids = added_cond["time_ids"]
-            tid = timestep_embedding(time_ids.reshape(-1), self.cfg.addition_time_embed_dim)
-            tid = tid.reshape(text_embeds.shape[0], -1)
-            add_in = torch.cat([text_embeds.float(), tid], dim=-1).to(dtype)
-            temb = temb + self.add_embedding(add_in)
+            ae = added_cond.get("add_emb")  # precomputed once per request (pipelines.sd._UNetGraph)
+            temb = temb + (ae if ae is not None else self.add_emb(added_cond, dtype))
         if self.cfg.class_embed_type == "timestep" and class_labels is not None:
             cl = timestep_embedding(class_labels.reshape(-1).float(), self.cfg.block_out_channels[0])
             temb = temb + self.class_embedding(cl.to(dtype))

@@ -565,6 +565,7 @@ def _cfg_dup(unet, nrep, image_latents, added) -> bool:
 
 CFG_SHARE_PREFIX = os.environ.get("CSK_CFG_SHARE", "1") != "0"
 TEMB_TABLE = os.environ.get("CSK_TEMB_TABLE", "1") != "0"  # per-request time-projection table in the loop graph
+ADD_EMB_CACHE = os.environ.get("CSK_ADD_EMB_CACHE", "1") != "0"  # SDXL text_time embedding once per request
 LOOP_GRAPHS = True  # device-resident sampler loop (StableDiffusion._denoise_loop); False: per-step host loop
 
 
@@ -605,6 +606,12 @@ class _UNetGraph:
         self.kv = list(cross_kv) if share_kv else [k.clone() for k in cross_kv]
         self._kv_req = None
         self.added = {k: v.clone() for k, v in added.items()} if added else None
+        # SDXL: the text_time addition embedding is constant over a request, so
+        # the graph reads it from a static buffer filled in prepare() (the
+        # add_embedding GEMMs and their sinusoidal inputs leave every step)
+        self._add_req = None
+        if self.added is not None and getattr(unet.cfg, "addition_embed_type", None) == "text_time" and ADD_EMB_CACHE:
+            self.added["add_emb"] = unet.add_emb(self.added)
         # device-resident loop: the ResNet time projections of every step come
         # from a per-request table (UNet2DConditionModel.temb_table) gathered by
         # the step's device index, not recomputed (5 small kernels) every step
@@ -664,6 +671,9 @@ class _UNetGraph:
         if added:
             for k, v in added.items():
                 self.added[k].copy_(v)
+            if "add_emb" in self.added and (req is None or req != self._add_req):
+                self.added["add_emb"].copy_(self.unet.add_emb(self.added))
+                self._add_req = req
 
     def run(self, x_in, t, cross_kv, added, cc=None, req=None):
         self.prepare(x_in, cross_kv, added, cc, req)

@@ -61,6 +61,32 @@ def test_sdxl_unet_text_time_parity_vs_fp32(gpu):
 
 
 @torch.no_grad()
+def test_sdxl_graph_add_emb_cache_matches_eager(gpu):
+    """The step graph reads SDXL's text_time addition embedding from a static
+    buffer filled once per request (pipelines.sd._UNetGraph): same output as the
+    eager UNet computing it inline, and a new request's conditioning is picked
+    up."""
+    from chiaswarm_amd.pipelines.sd import _UNetGraph
+
+    m = _build(unet.UNet2DConditionModel, unet.SDXL, gpu)
+    x = torch.randn(2, 32, 32, 4, device=gpu).bfloat16()
+    kv = m.encode_context(torch.randn(2, 77, 2048, device=gpu).bfloat16())
+
+    def cond(seed):
+        g = torch.Generator(device=gpu).manual_seed(seed)
+        return {"text_embeds": torch.randn(2, 1280, device=gpu, generator=g).bfloat16(),
+                "time_ids": torch.tensor([[1024, 1024, 0, 0, 1024, 1024]] * 2, device=gpu, dtype=torch.float32)}
+
+    a1, a2 = cond(1), cond(2)
+    gph = _UNetGraph(m, x, kv, a1)
+    assert "add_emb" in gph.added
+    for req, added in ((1, a1), (2, a2)):
+        y = gph.run(x, 700.0, kv, added, req=req).clone()
+        ref = m(x, torch.tensor([700.0], device=gpu), cross_kv=kv, added_cond=added)
+        assert rel_err(y, ref) <= 1e-2, req
+
+
+@torch.no_grad()
 @pytest.mark.parametrize("cfg_name", ["CLIP_L", "OPENCLIP_BIGG"])
 def test_sdxl_text_encoders_parity_vs_fp32(gpu, cfg_name):
     cfg = getattr(clip, cfg_name)
