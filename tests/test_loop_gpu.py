@@ -77,3 +77,26 @@ def test_sched_loop_kernel_vs_torch(gpu):
         for r in range(nrep):
             torch.testing.assert_close(x_in[r * B:(r + 1) * B, ..., :4].float(), want.float(), rtol=1e-2, atol=1e-2)
         assert torch.equal(x_in[..., 4:], extra)  # image-latent channels untouched
+
+
+def test_sdxl_loop_matches_host_loop(gpu):
+    """SDXL in the device loop (the text_time addition embedding from the
+    graph's per-request buffer) — same latents as the per-step host loop,
+    across two requests with different prompts."""
+    pipe = StableDiffusion("sdxl", device=gpu, seed=0)
+    for prompt in ("a red fox", "a blue car"):
+        outs = []
+        for loop in (False, True):
+            sd_mod.LOOP_GRAPHS = loop
+            try:
+                g = torch.Generator(device=gpu).manual_seed(5)
+                out = pipe(prompt=prompt, negative_prompt="blur", num_inference_steps=4, guidance_scale=5.0,
+                           num_images_per_prompt=1, height=128, width=128, generator=g,
+                           scheduler=get_scheduler("EulerDiscreteScheduler"), output_type="latent")
+                torch.cuda.synchronize()
+                outs.append(out.latents.float())
+            finally:
+                sd_mod.LOOP_GRAPHS = True
+        a, b = outs
+        assert torch.isfinite(b).all()
+        assert ((a - b).norm() / a.norm()).item() < 1e-3, prompt
