@@ -102,6 +102,10 @@ sig("csk_set_short_kv_rows", c_int)
 sig("csk_set_attn32", c_int)
 sig("csk_xattn_block", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p)
+sig("csk_attention_fa", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
+    c_int, c_float, c_int, c_void_p)
+sig("csk_set_attn_fa", c_int)
+sig("csk_attn_fa_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)
 sig("csk_dup2", c_void_p, c_void_p, c_int64, c_void_p)
@@ -511,7 +515,12 @@ def attention(q, k, v, scale, causal=False, kv_len=None):
     st = (c_int64 * 12)(*q.stride()[:3], *k.stride()[:3], *v.stride()[:3], *o.stride()[:3])
     if kv_len is not None and (kv_len.dtype != torch.int32 or not kv_len.is_cuda):
         raise TypeError("attention: kv_len must be an int32 device tensor")
-    split = attn_kv_split(B, H, Sq, Skv, D) if (not causal and kv_len is None and ATTN_VARIANT == 0) else 1
+    plain = not causal and kv_len is None and ATTN_VARIANT == 0
+    if plain and attn_fa_ok(B, H, Sq, Skv, D):  # persistent stream-K kernel (no split path needed)
+        _lib.call("csk_attention_fa", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), ATTN_FA_WORKERS,
+                  _s())
+        return o
+    split = attn_kv_split(B, H, Sq, Skv, D) if plain else 1
     if split > 1:
         return attention_split(q, k, v, scale, split, o)
     _lib.call("csk_attention", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), int(bool(causal)),
@@ -535,6 +544,32 @@ def attention_split(q, k, v, scale, split, o=None):
     _lib.call("csk_attention_split", _p(o), _p(q), _p(k), _p(v), st, B, H, Sq, Skv, D, float(scale), split,
               _p(part_o), _p(part_ml), _s())
     return o
+
+
+ATTN_FA = os.environ.get("CSK_ATTN_FA", "1") == "1"  # mirrors csk_set_attn_fa (set_attn_fa)
+ATTN_FA_WORKERS = 0  # 0: one persistent workgroup per CU; tests pass fewer to force more stream-K cuts
+
+
+def attn_fa_ok(B, H, Sq, Skv, D) -> bool:
+    """Shapes the persistent stream-K d = 64 attention (csrc/kernels/attn_fa.hip) takes."""
+    return ATTN_FA and _lib.call_int("csk_attn_fa_ok", B, H, Sq, Skv, D, 0, 0) == 1
+
+
+def set_attn_fa(on: bool):
+    global ATTN_FA
+    ATTN_FA = bool(on)
+    _lib.call("csk_set_attn_fa", int(ATTN_FA))
+
+
+def attn_fa_errors() -> int:
+    """Merge-protocol spins that gave up since the library loaded (must stay 0)."""
+    out = ctypes.c_uint(0)
+    fn = _lib.load().csk_attn_fa_errors
+    fn.restype = ctypes.c_int
+    err = fn(ctypes.byref(out))
+    if err:
+        raise RuntimeError(f"csk_attn_fa_errors: hipError {err}")
+    return int(out.value)
 
 
 ATTN32 = True  # mirrors the library's csk_set_attn32 (set_attn32): the split-KV path runs attn32_kernel only

@@ -1146,6 +1146,10 @@ CSK_API int csk_set_attn32(int on) {
 // 3 = pipelined + PRE, 4 = pipelined + ONES, 5 = pipelined + PRE + ONES
 extern "C" int csk_attention_wide(void* o, const void* q, const void* k, const void* v, const long long* strides,
                                   int B, int H, int Sq, int Skv, int D, float scale, hipStream_t stream);
+// attn_fa.hip: persistent stream-K d = 64 kernel (default for the shapes it takes)
+extern "C" int csk_attn_fa_ok(int B, int H, int Sq, int Skv, int D, int causal, int has_kv_len);
+extern "C" int csk_attention_fa(void* o, const void* q, const void* k, const void* v, const long long* strides, int B,
+                                int H, int Sq, int Skv, int D, float scale, int workers, hipStream_t stream);
 
 CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, const long long* strides, int B, int H,
                           int Sq, int Skv, int D, float scale, int causal, int variant, const void* kv_len,
@@ -1154,6 +1158,8 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
   if (D > 256 && D <= 512 && !causal && !kv_len)  // VAE mid-block: single head, d = 512
     return csk_attention_wide(o, q, k, v, strides, B, H, Sq, Skv, D, scale, stream);
   if (D % 8 != 0 || D > 256) return (int)hipErrorInvalidValue;
+  if (variant == 0 && csk_attn_fa_ok(B, H, Sq, Skv, D, causal, kv_len != nullptr))
+    return csk_attention_fa(o, q, k, v, strides, B, H, Sq, Skv, D, scale, 0, stream);
   AttnArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
   a.sqb = strides[0]; a.sqs = strides[1]; a.sqh = strides[2];

@@ -300,11 +300,15 @@ static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s)
 const bf16_t* csk_zero_ptr() { return g_zero; }
 int csk_zero_bytes() { return ZERO_BYTES; }
 
+extern "C" int csk_attn_fa_init();  // attn_fa.hip: the stream-K attention's merge workspace
+
 CSK_API int csk_init() {
   if (g_zero) return 0;
   hipError_t e = hipMalloc(&g_zero, ZERO_BYTES);
   if (e != hipSuccess) return (int)e;
-  return (int)hipMemset(g_zero, 0, ZERO_BYTES);
+  e = hipMemset(g_zero, 0, ZERO_BYTES);
+  if (e != hipSuccess) return (int)e;
+  return csk_attn_fa_init();
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hipStream_t s) {

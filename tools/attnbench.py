@@ -25,12 +25,19 @@ def main():
     ap.add_argument("--kv-rows", type=int, default=0, help="K/V-resident kernel rows per workgroup (0 auto)")
     ap.add_argument("--attn32", type=int, default=1, help="csk_set_attn32 value (0 off, 1 default, 2-4 TRICKS A/B)")
     ap.add_argument("--split", type=int, default=0, help="force this many key splits (attention_split); 0: the op's rule")
+    ap.add_argument("--fa", type=int, default=1, help="persistent stream-K d=64 kernel (attn_fa.hip) on / off")
+    ap.add_argument("--workers", type=int, default=0, help="attn_fa workers (0: one per CU)")
+    ap.add_argument("--probe", type=int, default=0, help="attn_fa profiling probe (wrong results): 1 exp 2 waits 4 PV 8 QK 16 barrier")
     a = ap.parse_args()
     _lib.load()
     if a.short_kv >= 0:
         _lib.call("csk_set_short_kv_variant", a.short_kv)
     _lib.call("csk_set_short_kv_rows", a.kv_rows)
     _lib.call("csk_set_attn32", a.attn32)
+    hip_ops.set_attn_fa(bool(a.fa))
+    hip_ops.ATTN_FA_WORKERS = a.workers
+    _lib.load().csk_set_attn_fa_probe(a.probe)
+    _lib.load().csk_set_attn_fa_min_skv(128)
     B, Sq, Skv, H, D = map(int, a.shape.split(","))
     q, k, v = (torch.randn(B, s, H, D, device="cuda").bfloat16() for s in (Sq, Skv, Skv))
     hip_ops.ATTN_VARIANT = a.variant
@@ -49,7 +56,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"attn32 {a.attn32} variant {a.variant} split {a.split} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: "
+    print(f"fa {a.fa} probe {a.probe} w {a.workers} attn32 {a.attn32} variant {a.variant} split {a.split} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: "
           f"{ms * 1000:.1f} us  "
           f"{4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")
 
