@@ -7,7 +7,9 @@ model catalogue (``GET /api/models`` -> ``models.json``) and provisions every
 (swarm/initialize.py:62-94, ``from_pretrained`` with revision / variant): a
 ``huggingface_hub.snapshot_download`` into the HF cache, restricted to what this
 framework reads — safetensors weights (the requested ``variant`` when given),
-JSON configs and tokenizer files; never pickled ``.bin``/``.ckpt`` files.
+JSON configs and tokenizer files; a repo without any safetensors is fetched
+again for its ``.bin`` weights (read later with the weights-only loader,
+never unpickled), never ``.ckpt`` / ``.pth`` single-file checkpoints.
 ``--offline`` (or no network) only locates local copies (``$SDAAS_MODEL_DIR``
 or the HF cache).  The packed bf16 weight cache (``runtime/packed_cache.py``)
 is written on each model's first load, not here.
@@ -66,12 +68,31 @@ def allow_patterns(variant: str | None) -> list:
     return ["*.json", "*.txt", "*.model", f"*.{variant}.safetensors"]
 
 
+BIN_ALLOW = ["*.json", "*.txt", "*.model", "*.bin"]
+
+
+def _has_safetensors(path) -> bool:
+    import glob
+    import os
+
+    return bool(path) and bool(glob.glob(os.path.join(str(path), "**", "*.safetensors"), recursive=True))
+
+
 def fetch(name: str, revision: str = "main", variant: str | None = None, token=None, downloader=None) -> str:
-    """Download (or re-validate) one model into the HF cache; returns its path."""
+    """Download (or re-validate) one model into the HF cache; returns its path.
+    Safetensors first; a repo that ships only pickled ``pytorch_model.bin`` /
+    ``diffusion_pytorch_model.bin`` weights (what the reference's
+    ``from_pretrained`` reads, swarm/initialize.py:84-89) is fetched again with
+    ``*.bin`` allowed."""
     if downloader is None:
         from huggingface_hub import snapshot_download as downloader
-    return downloader(name, revision=revision, allow_patterns=allow_patterns(variant), ignore_patterns=IGNORE,
-                      token=token if isinstance(token, str) and token else None)
+    tok = token if isinstance(token, str) and token else None
+    path = downloader(name, revision=revision, allow_patterns=allow_patterns(variant), ignore_patterns=IGNORE,
+                      token=tok)
+    if not _has_safetensors(path):
+        path = downloader(name, revision=revision, allow_patterns=BIN_ALLOW,
+                          ignore_patterns=[p for p in IGNORE if p != "*.bin"], token=tok)
+    return path
 
 
 def prepare_models(settings, offline=False, downloader=None) -> list:

@@ -568,10 +568,11 @@ class Bark:
 
 
 def load_bark(model_name: str, device: str) -> Bark:
-    from ..runtime.model_cache import cache, find_weights
+    from ..runtime.model_cache import cache
+    from ..runtime.provision import ensure_weights
 
     name = model_name.lower()
     size = "tiny" if name.startswith("tiny") else ("small" if "small" in name else "large")
     return cache().get(("bark", model_name, device),
-                       lambda: Bark(device, size=size, weights_dir=find_weights(model_name),
+                       lambda: Bark(device, size=size, weights_dir=ensure_weights(model_name),
                                     seed=stable_seed(model_name)))

@@ -26,11 +26,11 @@ import torch
 
 
 def _resolve(path_or_name: str) -> str:
-    from ..runtime.model_cache import find_weights
+    from ..runtime.provision import ensure_weights
 
     if os.path.isfile(path_or_name):
         return path_or_name
-    d = path_or_name if os.path.isdir(path_or_name) else find_weights(path_or_name)
+    d = path_or_name if os.path.isdir(path_or_name) else ensure_weights(path_or_name)
     if d and os.path.isdir(d):
         for f in sorted(os.listdir(d)):
             if f.endswith(".safetensors"):

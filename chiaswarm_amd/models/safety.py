@@ -109,12 +109,34 @@ _HF_RENAMES = {"vision_model.embeddings.patch_embedding.": "vision_model.patch_e
                ".layer_norm1.": ".ln1.", ".layer_norm2.": ".ln2.", ".mlp.fc1.": ".fc1.", ".mlp.fc2.": ".fc2."}
 
 
+def config_from_dir(weights_dir) -> SafetyConfig | None:
+    """The checker's geometry from its ``config.json`` (a transformers
+    ``CLIPConfig``: ``vision_config`` + ``projection_dim``; fields it omits take
+    the ViT-L/14 defaults), or None without one."""
+    import json
+    import os
+
+    path = os.path.join(weights_dir, "config.json") if weights_dir else None
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        raw = json.load(f)
+    v = raw.get("vision_config") or raw.get("vision_config_dict") or {}
+    d = CLIP_L14
+    return SafetyConfig(image_size=int(v.get("image_size", d.image_size)), patch=int(v.get("patch_size", d.patch)),
+                        dim=int(v.get("hidden_size", d.dim)), depth=int(v.get("num_hidden_layers", d.depth)),
+                        heads=int(v.get("num_attention_heads", d.heads)),
+                        mlp=int(v.get("intermediate_size", d.mlp)),
+                        proj=int(raw.get("projection_dim", v.get("projection_dim", d.proj))))
+
+
 def load_safety_checker(device, weights_dir=None, tiny=False) -> SafetyChecker:
     from .layers import init_random_fast_, prepare_model
 
     dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
+    cfg = TINY_SAFETY if tiny else (config_from_dir(weights_dir) or CLIP_L14)
     with torch.device(device):
-        m = SafetyChecker(TINY_SAFETY if tiny else CLIP_L14).to(dt).eval().requires_grad_(False)
+        m = SafetyChecker(cfg).to(dt).eval().requires_grad_(False)
     keep = {k: v.clone() for k, v in m.state_dict().items() if "embeds" in k}
     init_random_fast_(m, seed=99)
     m.load_state_dict({**m.state_dict(), **keep})  # random tower, never-flag thresholds

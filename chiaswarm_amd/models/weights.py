@@ -1,4 +1,5 @@
-"""Checkpoint loading (safetensors only — never pickles).
+"""Checkpoint loading (safetensors; pickled ``.bin`` / ``.pth`` files only
+through ``torch.load(weights_only=True)``, which executes nothing from the file).
 
 Reads a diffusers-layout model directory (``unet/``, ``vae/``, ``text_encoder/``
 [, ``text_encoder_2/``] each holding ``*.safetensors``) into our modules, whose
@@ -62,11 +63,33 @@ class LoadReport:
         return "; ".join(parts)
 
 
+# pickled files of a transformers / diffusers repo that hold no model weights
+_NON_WEIGHT_BINS = ("training_args.bin", "optimizer.bin", "scheduler.bin", "rng_state.bin", "scaler.bin")
+
+
+def weight_files(d: str) -> tuple:
+    """(kind, files) of a component directory: its ``*.safetensors``, else the
+    ``*.bin`` weight files (``pytorch_model.bin`` / ``diffusion_pytorch_model.bin``,
+    sharded or not) that ``from_pretrained`` would read; ("", []) if none."""
+    st = sorted(glob.glob(os.path.join(d, "*.safetensors")))
+    if st:
+        return "safetensors", st
+    bins = sorted(f for f in glob.glob(os.path.join(d, "*.bin")) if os.path.basename(f) not in _NON_WEIGHT_BINS)
+    return ("bin", bins) if bins else ("", [])
+
+
 def _read_dir(d: str) -> dict:
     from safetensors.torch import load_file
 
     out = {}
-    files = sorted(glob.glob(os.path.join(d, "*.safetensors")))
+    kind, files = weight_files(d)
+    if kind == "bin":
+        fp16 = [f for f in files if ".fp16." in os.path.basename(f)]
+        if fp16 and len(fp16) < len(files):
+            files = [f for f in files if f not in fp16]
+        for f in files:
+            out.update(read_pth(f))
+        return out
     # diffusers ships fp32 and fp16 variants side by side: take one of each model file
     fp16 = [f for f in files if ".fp16." in os.path.basename(f)]
     if fp16 and len(fp16) < len(files):
@@ -96,7 +119,7 @@ def read_weights(path: str) -> dict:
     """State dict of a directory (``*.safetensors``, else a single ``*.pth`` /
     ``*.pt``) or of one file of either format."""
     if os.path.isdir(path):
-        if glob.glob(os.path.join(path, "*.safetensors")):
+        if weight_files(path)[1] and not glob.glob(os.path.join(path, "*.pth")):
             return _read_dir(path)
         pth = sorted(glob.glob(os.path.join(path, "*.pth")) + glob.glob(os.path.join(path, "*.pt")))
         if len(pth) != 1:
@@ -152,7 +175,7 @@ def read_checkpoint(d: str, like: torch.nn.Module | None = None) -> dict:
     (parallel/sharded.py); otherwise a plain local read."""
     from ..parallel import comm
 
-    if comm.collective_load_active():
+    if comm.collective_load_active() and weight_files(d)[0] == "safetensors":
         from ..parallel.sharded import safetensors_files, sharded_state_dict
 
         p = next(like.parameters(), None) if like is not None else None
@@ -165,9 +188,10 @@ def read_checkpoint(d: str, like: torch.nn.Module | None = None) -> dict:
 
 
 def load_component(module, weights_dir: str, sub: str, renames=None, **kw) -> LoadReport | None:
-    """Strict load of ``weights_dir/sub/*.safetensors`` (None if that dir is absent)."""
+    """Strict load of ``weights_dir/sub`` (safetensors or weights-only ``.bin``;
+    None if that dir is absent)."""
     d = os.path.join(weights_dir, sub) if sub else weights_dir
-    if not os.path.isdir(d) or not glob.glob(os.path.join(d, "*.safetensors")):
+    if not os.path.isdir(d) or not weight_files(d)[1]:
         return None
     return load_into(module, read_checkpoint(d, module), renames, name=sub or os.path.basename(d), **kw)
 
@@ -191,14 +215,14 @@ def load_sd_weights(pipe, weights_dir: str) -> bool:
     parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)]
     for i, te in enumerate(pipe.text_encoders):
         parts.append(("text_encoder" if i == 0 else f"text_encoder_{i + 1}", te, None))
-    present = [sub for sub, _, _ in parts if glob.glob(os.path.join(weights_dir, sub, "*.safetensors"))]
+    present = [sub for sub, _, _ in parts if weight_files(os.path.join(weights_dir, sub))[1]]
     if not present:
         return False
     absent = [sub for sub, _, _ in parts if sub not in present]
     if absent:
         # a real UNet beside a random-init VAE / text encoder would produce
         # plausible-looking garbage while reporting the checkpoint as loaded
-        raise CheckpointMismatch(f"{weights_dir}: no safetensors weights for {absent} (present: {present}); "
+        raise CheckpointMismatch(f"{weights_dir}: no weights for {absent} (present: {present}); "
                                  "refusing a partial load")
     reports = {}
     for sub, mod, ren in parts:

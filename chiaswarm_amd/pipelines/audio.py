@@ -29,7 +29,8 @@ from ..models.vae import AUDIOLDM_VAE, TINY_AUDIO_VAE, AutoencoderKL
 from ..models.vocoder import AUDIOLDM_HIFIGAN, TINY_HIFIGAN, HifiGan
 from ..output.media import encode_audio
 from ..output.processor import make_result
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 from ..schedulers import get_scheduler
 from .graphs import GraphCache
 from ..utils import stable_seed
@@ -175,7 +176,7 @@ def _sub(d, name):
 def load_audioldm(model_name: str, device: str) -> AudioLDM:
     tiny = model_name.lower().startswith("tiny")
     return cache().get(("audioldm", model_name, device),
-                       lambda: AudioLDM(device, tiny=tiny, weights_dir=find_weights(model_name),
+                       lambda: AudioLDM(device, tiny=tiny, weights_dir=ensure_weights(model_name),
                                         seed=stable_seed(model_name)))
 
 

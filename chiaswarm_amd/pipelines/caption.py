@@ -42,7 +42,8 @@ from ..models.blip import BLIP_BASE, BLIP_LARGE, TINY_BLIP, BlipCaptioner, BlipC
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.wordpiece import WordPiece
 from ..output.processor import make_text_result
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 
 MODEL_TYPES = {"BlipForConditionalGeneration": "caption", "BlipForQuestionAnswering": "vqa", "GitForCausalLM": "git",
                "Blip2ForConditionalGeneration": "blip2", "InstructBlipForConditionalGeneration": "blip2",
@@ -96,7 +97,7 @@ def load_git(model_name: str, device: str):
     def make():
         from ..models.git import GitCaptioner, convert_hf_git
 
-        w = find_weights(model_name)
+        w = ensure_weights(model_name)
         cfg = _git_config(model_name, w)
         dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
         with torch.device(device):
@@ -123,7 +124,7 @@ def load_blip2(model_name: str, device: str):
         from ..models.hf_config import component_config
         from ..models.tokenizer import ByteBPETokenizer
 
-        w = find_weights(model_name)
+        w = ensure_weights(model_name)
         raw = component_config(w, "") if w else None
         if raw is not None and "qformer_config" in raw:
             cfg = Blip2Config.from_hf(raw)
@@ -193,7 +194,7 @@ def load_vitgpt2(model_name: str, device: str):
         from ..models.tokenizer import ByteBPETokenizer
         from ..models.vit_gpt2 import TINY_VIT_GPT2, VIT_GPT2, VitGpt2Captioner, VitGpt2Config, convert_hf_vit_gpt2
 
-        w = find_weights(model_name)
+        w = ensure_weights(model_name)
         raw = component_config(w, "") if w else None
         if raw is not None and "encoder" in raw and "decoder" in raw:
             cfg = VitGpt2Config.from_hf(raw, component_config(w, "", "preprocessor_config.json"))
@@ -227,7 +228,7 @@ def load_captioner(model_name: str, device: str, task: str = "caption"):
         return load_vitgpt2(model_name, device)
 
     def make():
-        w = find_weights(model_name)
+        w = ensure_weights(model_name)
         cfg = _config(model_name, w)
         dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
         cls = BlipVQA if task == "vqa" else BlipCaptioner

@@ -15,7 +15,8 @@ from PIL import Image
 
 from ..models.controlnet import ControlNetModel
 from ..models.layers import init_random_fast_, prepare_model
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 from ..utils import stable_seed
 
 
@@ -83,7 +84,7 @@ class ControlNetRunner:
 
 def load_controlnet(name: str, pipe, device_identifier: str, revision: str = "main") -> ControlNetRunner:
     def make():
-        w = find_weights(name, revision)
+        w = ensure_weights(name, revision)
         cfg, kw = pipe.unet.cfg, {}
         from ..models.hf_config import component_config, controlnet_config
 

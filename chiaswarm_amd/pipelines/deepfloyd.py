@@ -29,7 +29,8 @@ from ..models.if_unet import IF_I_XL, IF_II_L, TINY_IF_I, TINY_IF_II, IFUNet
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.t5 import T5_XXL, TINY_T5, T5Encoder, T5Tokenizer
 from ..output.processor import OutputProcessor
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 from ..schedulers import get_scheduler
 from .graphs import GraphCache
 from .upscale import load_x4_upscaler
@@ -154,8 +155,8 @@ class IFCascade:
 def load_if(model_name: str, device: str) -> IFCascade:
     tiny = model_name.lower().startswith("tiny")
     return cache().get(("if", model_name, device),
-                       lambda: IFCascade(device, tiny=tiny, weights_dir=find_weights(model_name),
-                                         stage2_dir=find_weights("DeepFloyd/IF-II-L-v1.0")))
+                       lambda: IFCascade(device, tiny=tiny, weights_dir=ensure_weights(model_name),
+                                         stage2_dir=ensure_weights("DeepFloyd/IF-II-L-v1.0")))
 
 
 def diffusion_if_callback(device_identifier, model_name, **kwargs):

@@ -19,6 +19,7 @@ import torch
 
 from ..output.processor import OutputProcessor
 from ..runtime.model_cache import cache, find_weights
+from ..runtime.provision import ensure_weights
 from ..schedulers import get_scheduler
 from .sd import StableDiffusion, resolve_family
 from ..utils import stable_seed
@@ -71,10 +72,34 @@ def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "mai
     raise ValueError(f"pipeline class {cls} is not implemented by the Stable Diffusion callback of this worker")
 
 
+def safety_checker_dir(weights_dir: str | None) -> str | None:
+    """Weights of the NSFW checker this pipeline runs (the reference runs the
+    pipeline's own ``safety_checker`` component and aggregates
+    ``nsfw_content_detected``, swarm/diffusion/diffusion_func.py:98-111):
+    the checkpoint's own ``safety_checker/`` when its model_index.json lists
+    one (SD1.x layouts), else a separately provisioned
+    CompVis/stable-diffusion-safety-checker; None when neither exists (a
+    random tower would be meaningless)."""
+    import json
+
+    from ..runtime.provision import has_weights
+
+    if weights_dir and os.path.exists(os.path.join(weights_dir, "model_index.json")):
+        with open(os.path.join(weights_dir, "model_index.json")) as f:
+            entry = json.load(f).get("safety_checker")
+        own = os.path.join(weights_dir, "safety_checker")
+        if isinstance(entry, (list, tuple)) and entry and entry[0] and has_weights(own):
+            return own
+    sw = find_weights("CompVis/stable-diffusion-safety-checker")
+    return sw if has_weights(sw) else None
+
+
 def load_sd(model_name: str, device_identifier: str, revision: str = "main", controlnet_name: str | None = None,
             controlnet_revision: str = "main") -> StableDiffusion:
     def make():
-        w = find_weights(model_name, revision)
+        # fetched on a miss like from_pretrained; no weights -> WeightsMissing
+        # (non-fatal job error), random-init only under SDAAS_ALLOW_RANDOM=1
+        w = ensure_weights(model_name, revision)
         # architecture from the checkpoint's own model_index.json / config.json
         # files (the reference's from_pretrained); name presets only without them
         return StableDiffusion(resolve_family(model_name, w), device=device_identifier, weights_dir=w,
@@ -82,10 +107,8 @@ def load_sd(model_name: str, device_identifier: str, revision: str = "main", con
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)
     if not hasattr(pipe, "_safety_probed"):
-        # the NSFW checker runs when its weights are available locally (a random
-        # tower would be meaningless); SDAAS_SAFETY=0 disables it
         pipe._safety_probed = True
-        sw = find_weights("CompVis/stable-diffusion-safety-checker")
+        sw = safety_checker_dir(find_weights(model_name, revision))
         if sw and os.environ.get("SDAAS_SAFETY", "1") != "0":
             from ..models.safety import load_safety_checker
 
@@ -155,6 +178,7 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
     # all images from one generator stream (swarm/gpu/device.py:35-41).
     image_range = kwargs.pop("_image_range", None)
     return_images = bool(kwargs.pop("_return_images", False))
+    ensure_weights(model_name, revision)  # provisioned before the class is read from its model_index.json
     pcls = pipeline_class_for(pipeline_type, model_name, revision)
     if pcls in UPSCALE_CLASSES:
         if split is not None or image_range is not None:

@@ -18,7 +18,8 @@ from PIL import Image
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.rrdbnet import TINY_RRDB, RRDBNet
 from ..output.processor import OutputProcessor
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 
 
 # the original ESRGAN repo's RRDB_ESRGAN_x4.pth names -> BasicSR / Real-ESRGAN names
@@ -51,7 +52,7 @@ def load_esrgan(model_name: str, device: str):
 
         tiny = model_name.lower().startswith("tiny")
         dt = torch.bfloat16 if str(device).startswith("cuda") else torch.float32
-        w = find_weights(model_name) or (model_name if os.path.isfile(model_name) else None)
+        w = model_name if os.path.isfile(model_name) else ensure_weights(model_name)
         sd = esrgan_state_dict(w) if w else None
         kw = dict(TINY_RRDB) if tiny else {}
         if sd is not None:  # geometry from the checkpoint: block count, width, growth

@@ -33,7 +33,8 @@ from ..models.weights import tokenizer_dir
 from ..models.kunet import LATENT_X2_K, TINY_X2_K, KUNet2DConditionModel
 from ..models.unet import TINY_X4, X4_UPSCALER, UNet2DConditionModel
 from ..models.vae import SD_VAE, TINY_VAE, AutoencoderKL, VAEConfig
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 from ..schedulers import get_scheduler
 from .graphs import GraphCache
 
@@ -233,14 +234,14 @@ class X4Upscaler(_Base):
 def load_latent_upscaler(device: str, model_name: str = "stabilityai/sd-x2-latent-upscaler") -> LatentUpscaler:
     tiny = model_name.startswith("tiny")
     return cache().get(("x2", model_name, str(device)),
-                       lambda: LatentUpscaler(device, tiny=tiny, weights_dir=find_weights(model_name)))
+                       lambda: LatentUpscaler(device, tiny=tiny, weights_dir=ensure_weights(model_name)))
 
 
 def load_x4_upscaler(device: str, model_name: str = "stabilityai/stable-diffusion-x4-upscaler",
                      tiny: bool | None = None) -> X4Upscaler:
     tiny = model_name.startswith("tiny") if tiny is None else tiny
     return cache().get(("x4", model_name, str(device), tiny),
-                       lambda: X4Upscaler(device, tiny=tiny, weights_dir=find_weights(model_name)))
+                       lambda: X4Upscaler(device, tiny=tiny, weights_dir=ensure_weights(model_name)))
 
 
 def upscale_images(images, device_identifier, prompt, generator=None, num_inference_steps=20,

@@ -29,7 +29,8 @@ from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
 from ..output.media import frames_to_video, read_video_frames
 from ..output.processor import image_to_buffer, make_result
-from ..runtime.model_cache import cache, find_weights
+from ..runtime.model_cache import cache
+from ..runtime.provision import ensure_weights
 from ..schedulers import batch_randn, get_scheduler
 from .graphs import GraphCache
 
@@ -41,7 +42,7 @@ class TextToVideo:
         ucfg = unet3d.TINY_T2V if tiny else unet3d.T2V
         tcfg = clip_mod.TINY_TEXT if tiny else clip_mod.OPENCLIP_H
         vcfg = vae_mod.TINY_VAE if tiny else vae_mod.SD_VAE
-        w = find_weights(model_name)
+        w = ensure_weights(model_name)
         self.sched_config = {}
         if w:  # the checkpoint's own configs (the reference: from_pretrained, swarm/video/tx2vid.py:24-30)
             from ..models import hf_config as hc

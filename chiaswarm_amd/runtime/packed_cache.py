@@ -40,7 +40,7 @@ def fingerprint(src_dir: str, module: torch.nn.Module) -> str:
     h.update(f"{__framework_version__}|{type(module).__name__}".encode())
     p = next(module.parameters(), None)
     h.update(str(p.dtype if p is not None else None).encode())
-    for f in sorted(Path(src_dir).glob("*.safetensors")):
+    for f in sorted(list(Path(src_dir).glob("*.safetensors")) + list(Path(src_dir).glob("*.bin"))):
         st = f.stat()
         h.update(f"{f.name}|{st.st_size}|{st.st_mtime_ns}".encode())
     return h.hexdigest()

@@ -1,7 +1,12 @@
 """Manual smoke jobs (reference: swarm/test.py:7-77 — canned job dicts run
 through the real ``do_work`` on device 0; prints "ok" or the error).
 
-    python -m swarm.test [sd|txt2audio|vid2vid|txt2vid|bark|if|tiny] [--cpu]
+    python -m swarm.test [sd|txt2audio|vid2vid|txt2vid|bark|if|tiny] [--cpu] [--synthetic]
+
+Models are provisioned like any job (fetched on a miss, runtime/provision.py);
+``--synthetic`` runs seeded random-init weights of the same architecture
+instead (SDAAS_ALLOW_RANDOM=1, no fetch) — a plumbing check on a box without
+checkpoints.  The "tiny" job always runs synthetic.
 """
 from __future__ import annotations
 
@@ -46,7 +51,13 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("job", nargs="?", default="sd", choices=sorted(JOBS))
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--synthetic", action="store_true", help="random-init weights, no fetch")
     a = ap.parse_args(argv)
+    if a.synthetic or a.job == "tiny":
+        import os
+
+        os.environ["SDAAS_ALLOW_RANDOM"] = "1"
+        os.environ["SDAAS_OFFLINE"] = "1"
     asyncio.run(run_test(JOBS[a.job], a.cpu))
 
 

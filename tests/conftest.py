@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# the suite runs synthetic (random-init) models of the real architectures and
+# has no network: tests of the provisioning contract unset these themselves
+os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -25,7 +25,10 @@ def test_prepare_models_fetches_with_revision_variant_and_safe_patterns(tmp_path
         calls.append((repo, revision, allow_patterns, ignore_patterns, token))
         if repo == "org/c":
             raise OSError("offline")
-        return f"/cache/{repo}"
+        d = tmp_path / "cache" / repo
+        d.mkdir(parents=True, exist_ok=True)
+        (d / "model.fp16.safetensors").write_bytes(b"x")  # a safetensors repo: one fetch, no pickles
+        return str(d)
 
     try:
         s = Settings()
@@ -38,7 +41,7 @@ def test_prepare_models_fetches_with_revision_variant_and_safe_patterns(tmp_path
     assert calls[0][1] == "fp16" and "*.fp16.safetensors" in calls[0][2] and calls[0][4] == "hf_x"
     assert "*.bin" in calls[0][3] and "*.ckpt" in calls[0][3]
     by = {r["model_name"]: r for r in rep}
-    assert by["org/a"]["weights"] == "/cache/org/a" and by["org/a"]["fetched"]
+    assert by["org/a"]["weights"] == str(tmp_path / "cache" / "org" / "a") and by["org/a"]["fetched"]
     assert "fetch_error" in by["org/c"] and by["org/c"]["weights"].startswith("synthetic")
     assert by["org/b"]["weights"].startswith("synthetic")
     assert os.path.exists(os.path.join(str(tmp_path), "models.json"))

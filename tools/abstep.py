@@ -4,6 +4,13 @@ runtime kernel knobs, each arm captured in its own graph, arms interleaved:
 
     python tools/abstep.py --arms gn0,gn1024,gnmax --rounds 5
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import os
 import statistics

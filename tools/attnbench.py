@@ -56,6 +56,19 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
+    if a.probe == 128:
+        import ctypes
+        n = 256 * 8 * 8
+        buf = (ctypes.c_ulonglong * n)()
+        _lib.load().csk_attn_fa_dbg(buf, n)
+        import numpy as np
+        arr = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, 8).astype(np.float64)
+        units = arr[:, 0, 7].sum()
+        names = ["vmcnt-wait", "barrier", "dma-issue", "qk+exp+pack", "pv-wait+mfma", "rowmax+rescale"]
+        tot = arr[:, :, :6].sum(axis=(0, 1))
+        per = tot / (units * 8)
+        print("phase cycles per unit per wave:", {k: round(v, 1) for k, v in zip(names, per)},
+              "sum", round(per.sum(), 1), "seg ends", arr[:, 0, 6].sum())
     print(f"fa {a.fa} probe {a.probe} w {a.workers} attn32 {a.attn32} variant {a.variant} split {a.split} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: "
           f"{ms * 1000:.1f} us  "
           f"{4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")

@@ -14,6 +14,13 @@ Prints one JSON line per config (images/s, p50 latency ms).
 """
 from __future__ import annotations
 
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import json
 import os

@@ -8,6 +8,13 @@ the kernels run back to back as in the hipGraph (durations are device time).
     rocprofv3 --kernel-trace -d OUT -o cp -- python tools/callprof.py --record OUT/calls.json
     python tools/callprof.py --db OUT/.../cp_results.db --calls OUT/calls.json
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import collections
 import glob

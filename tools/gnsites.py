@@ -5,6 +5,13 @@ separate statistics pass, by shape:
 
     python tools/gnsites.py
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import collections
 import os
 import sys

@@ -7,6 +7,13 @@ hipGraph-replayed UNet step to price launch bubbles:
     rocprofv3 --kernel-trace -d /tmp/kt -o k -- python tools/abstep.py --rounds 1 --iters 3
     python tools/graph_gaps.py /tmp/kt/k_results.db --marker timestep_emb
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import sqlite3
 

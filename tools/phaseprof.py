@@ -2,6 +2,13 @@
 """Fine-grained host/device timing of the pre-denoise part of an SD2.1 job
 (tokenize, text encoder, cross-attention K/V, noise), each bracketed by a
 device sync, to find host overhead outside the hipGraph-replayed steps."""
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import os
 import sys
 import time

@@ -5,6 +5,13 @@ events (synchronised, so launch gaps are excluded):
 
     python tools/stepshapes.py [--batch 8] [--iters 3] [--json out.json]
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import collections
 import json

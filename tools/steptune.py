@@ -19,6 +19,13 @@ accepted change, so a run cut short still leaves its progress:
 
     python tools/steptune.py --budget 900 --out gpurun_out/tune_step.json
 """
+import os as _os
+
+# synthetic (random-init) weights of the real architectures: there are no
+# checkpoints on the bench / profiling boxes (runtime/provision.py)
+_os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1")
+_os.environ.setdefault("SDAAS_OFFLINE", "1")
+
 import argparse
 import json
 import os
