@@ -51,6 +51,15 @@ import torch
 
 METRIC = ("images/sec (whole node) SD2.1 512×512 50-step txt2img at 1/2/4/8 MI355X; "
           "p50 job latency")
+# BASELINE.json configs this script drives: (family, resolution, denoise steps, images per GPU, metric, model label)
+CONFIGS = {
+    "sd21": ("sd21", 512, 50, 4, METRIC,
+             "SD2.1 (stable-diffusion-2-1-base arch: UNet 865.9M + OpenCLIP-H 340.4M + VAE 83.7M)"),
+    # config #3: SDXL-base 1024², 30 steps, DP batch 8 across 8 GPUs = one image per rank
+    "sdxl": ("sdxl", 1024, 30, 1, "images/sec (whole node) SDXL-base 1024×1024 30-step txt2img, DP batch 1 per "
+             "MI355X (BASELINE config #3: DP batch 8 across 8); p50 job latency",
+             "SDXL-base 1.0 (stable-diffusion-xl-base-1.0 arch: UNet 2567M + CLIP-L + OpenCLIP-bigG + VAE)"),
+}
 
 
 def parse():
@@ -58,15 +67,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4, help="images per GPU per job")
-    ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--denoise-steps", type=int, default=50)
-    ap.add_argument("--family", default="sd21")
+    ap.add_argument("--config", default="sd21", choices=sorted(CONFIGS),
+                    help="BASELINE config: sd21 (headline, config #2) or sdxl (config #3); "
+                         "--batch / --res / --denoise-steps / --family override its values")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU per job")
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--denoise-steps", type=int, default=None)
+    ap.add_argument("--family", default=None)
     ap.add_argument("--impl", default="hip", choices=["hip", "reference"])
     ap.add_argument("--guidance", type=float, default=7.5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None)
-    return ap.parse_args()
+    a = ap.parse_args()
+    fam, res, steps, batch, _, _ = CONFIGS[a.config]
+    a.family = a.family or fam
+    a.res = a.res or res
+    a.denoise_steps = a.denoise_steps or steps
+    a.batch = a.batch or batch
+    return a
 
 
 def _free_port() -> int:
@@ -80,8 +98,10 @@ def _free_port() -> int:
 def spawn_ranks(args) -> int:
     """``--gpus N`` > 1 without a torchrun environment: start N rank processes
     of this script (before this process touches the GPU), forward rank 0's
-    JSON line and return the worst exit code.  A rank that fails takes the
-    others down (process group), so the run ends instead of hanging."""
+    JSON line and return the worst exit code.  Every child is polled: as soon
+    as ANY rank exits non-zero the others are terminated (a survivor blocked in
+    a collective would otherwise wait out the process-group timeout), and the
+    failing rank is named on stderr."""
     import subprocess
 
     port = _free_port()
@@ -92,12 +112,20 @@ def spawn_ranks(args) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc = 0
     try:
-        for p in procs:
-            rc = max(rc, abs(p.wait()))
-            if rc:
+        while any(p.poll() is None for p in procs):
+            bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode not in (None, 0)]
+            if bad:
+                r, code = bad[0]
+                print(f"bench: rank {r} exited with {code}; terminating the other ranks", file=sys.stderr, flush=True)
                 for q in procs:
                     if q.poll() is None:
                         q.terminate()
+                deadline = time.monotonic() + 20
+                while time.monotonic() < deadline and any(q.poll() is None for q in procs):
+                    time.sleep(0.1)
+                break
+            time.sleep(0.2)
+        rc = max(abs(p.returncode) if p.returncode is not None else 1 for p in procs)
     finally:
         for q in procs:
             if q.poll() is None:
@@ -133,7 +161,7 @@ def main():
     pipe = StableDiffusion(args.family, device=device, seed=1234)
     if args.no_graphs:
         pipe.use_graphs = False
-    load_s, load_bytes = load_through_checkpoint(pipe, rank, world)
+    load_s, load_bytes, load_read_s, load_gather_s = load_through_checkpoint(pipe, rank, world)
 
     prompts = ["a photograph of an astronaut riding a horse", "a watercolor fox in a snowy forest",
                "a cyberpunk city street at night, neon", "a bowl of ramen, studio lighting"]
@@ -178,7 +206,12 @@ def main():
     comm.barrier()
     if on_gpu:
         torch.cuda.synchronize()
-    elapsed = comm.max_over_ranks(time.perf_counter() - t0)
+    mine = time.perf_counter() - t0
+    elapsed = comm.max_over_ranks(mine)
+    per_rank = [mine]
+    if comm.is_dist():
+        per_rank = [None] * world
+        torch.distributed.all_gather_object(per_rank, mine)
     p50_gpu = comm.max_over_ranks(statistics.median(lat))
     while len(done) < len(futs):  # done-callbacks run on the pool's reader thread
         time.sleep(0.001)
@@ -189,7 +222,7 @@ def main():
     if rank == 0:
         phase = {k: round(1000 * statistics.median([t[k] for t in timings]), 2) for k in timings[0]}
         rec = {
-            "metric": METRIC,
+            "metric": CONFIGS[args.config][4],
             "value": round(ips, 4),
             "unit": "images/s",
             "n_gpus": world,
@@ -202,8 +235,9 @@ def main():
             "dtype": "bf16" if on_gpu else "fp32",
             "data": "synthetic prompts, random-init weights (no checkpoints offline)",
             "config": {
-                "model": ("SD2.1 (stable-diffusion-2-1-base arch: UNet 865.9M + OpenCLIP-H 340.4M + VAE 83.7M)"
-                          if args.family == "sd21" else f"{args.family} (not the headline config)"),
+                "model": (CONFIGS[args.config][5] if args.family == CONFIGS[args.config][0]
+                          else f"{args.family} (not the {args.config} config)"),
+                "bench_config": args.config,
                 "global_batch": args.batch * world,
                 "seq_len": (args.res // 8) ** 2,
                 "parallelism": f"dp{world}",
@@ -218,9 +252,12 @@ def main():
             "p50_job_latency_note": "job start -> result envelope (JPEG/base64/sha256) done",
             "p50_gpu_latency_ms": round(1000 * p50_gpu, 1),
             "world_size": world,
+            "ms_per_step_per_rank": [round(1000 * t / args.steps, 2) for t in per_rank],
             "dist_backend": torch.distributed.get_backend() if comm.is_dist() else None,
             "phase_ms_median": phase,
             "model_load_s": round(load_s, 2),
+            "model_load_read_s": round(load_read_s, 3),
+            "model_load_all_gather_s": round(load_gather_s, 3),
             "load_bytes_read_per_rank": load_bytes,
             "load_path": f"safetensors dir -> sharded byte-range reads + {'RCCL' if on_gpu else 'gloo'} all_gather" if world > 1 else
                          "safetensors dir -> local read",
@@ -235,7 +272,8 @@ def load_through_checkpoint(pipe, rank, world):
     """Write the pipeline's weights once as safetensors (rank 0, /dev/shm), then
     load them on every rank through models/weights.load_component inside
     ``collective_loading`` (sharded reads + all_gather with N > 1).  Returns
-    (seconds, bytes this rank read from the files)."""
+    (seconds, bytes this rank read from the files, read seconds, all_gather
+    seconds) — the last two max over ranks, 0 for the all_gather without one."""
     import shutil
     import tempfile
 
@@ -249,6 +287,8 @@ def load_through_checkpoint(pipe, rank, world):
         [("text_encoder" if i == 0 else f"text_encoder_{i + 1}", m, None) for i, m in enumerate(pipe.text_encoders)]
     base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
     root = os.path.join(base, f"chiaswarm_bench_{os.getuid()}_{os.environ.get('MASTER_PORT', os.getpid())}")
+    if os.environ.get("SDAAS_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank dying during the load
+        raise SystemExit(f"bench: rank {rank} failing on purpose (SDAAS_BENCH_FAIL_RANK)")
     if rank == 0:
         for sub, m, _ in parts:
             os.makedirs(os.path.join(root, sub), exist_ok=True)
@@ -259,22 +299,29 @@ def load_through_checkpoint(pipe, rank, world):
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     nbytes = 0
+    read_s = gather_s = 0.0
     with comm.collective_loading():
         for sub, m, ren in parts:
+            t1 = time.perf_counter()
             load_component(m, root, sub, ren)
             if comm.collective_load_active() and sharded.LAST_READER is not None:
                 nbytes += sharded.LAST_READER.read_bytes
+                read_s += sharded.LAST_READER.read_s
+                gather_s += sharded.LAST_READER.gather_s
             else:
+                read_s += time.perf_counter() - t1
+            if not (comm.collective_load_active() and sharded.LAST_READER is not None):
                 nbytes += sum(os.path.getsize(f) for f in sharded.safetensors_files(os.path.join(root, sub)))
             prepare_model(m)  # re-pack for the kernels (fused QKV, NHWC conv weights ...)
     pipe.invalidate_graphs()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     load_s = comm.max_over_ranks(time.perf_counter() - t0)
+    read_s, gather_s = comm.max_over_ranks(read_s), comm.max_over_ranks(gather_s)
     comm.barrier()
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
-    return load_s, nbytes
+    return load_s, nbytes, read_s, gather_s
 
 
 if __name__ == "__main__":

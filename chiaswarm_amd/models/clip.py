@@ -36,6 +36,7 @@ OPENCLIP_H = CLIPTextConfig()  # SD2.x text encoder (23 layers kept)
 OPENCLIP_BIGG = CLIPTextConfig(hidden_size=1280, intermediate_size=5120, num_layers=32, num_heads=20,
                                projection_dim=1280)
 TINY_TEXT = CLIPTextConfig(vocab_size=1000, hidden_size=32, intermediate_size=64, num_layers=2, num_heads=2)
+TINY_TEXT_G = dataclasses.replace(TINY_TEXT, projection_dim=32)  # second (pooled) encoder of tiny-xl
 
 
 class _SelfAttn(Prepared):

@@ -72,6 +72,14 @@ TINY = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
                   down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
                   up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"),
                   num_heads=(2, 2), cross_attention_dim=32, sample_size=8)
+# SDXL structure at test size: text_time add-embedding, two text encoders
+# (32 + 32 context, pooled projection 32), deeper transformer stack below
+TINY_XL = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
+                     down_block_types=("DownBlock2D", "CrossAttnDownBlock2D"),
+                     up_block_types=("CrossAttnUpBlock2D", "UpBlock2D"),
+                     num_heads=(2, 2), transformer_layers_per_block=(1, 2), cross_attention_dim=64,
+                     addition_embed_type="text_time", addition_time_embed_dim=8,
+                     projection_class_embeddings_input_dim=32 + 6 * 8, sample_size=8)
 
 # AudioLDM (cvssp/audioldm-*): 8-channel mel latents, CLAP embedding as a
 # concatenated class embedding, attention blocks whose "cross" attention runs on

@@ -70,6 +70,8 @@ class _Reader:
     def __init__(self):
         self.read_names: list[str] = []
         self.read_bytes = 0
+        self.read_s = 0.0    # host time in this rank's byte-range reads + H2D copies
+        self.gather_s = 0.0  # time in the all_gather (device-synchronised on GPUs)
 
     def read(self, path: str, start: int, meta) -> torch.Tensor:
         dt, shape, (b, e) = meta
@@ -117,6 +119,10 @@ def sharded_state_dict(files: list[str], dtype: torch.dtype, device, reader: _Re
             for _, _, name, meta in items:
                 out[name] = torch.empty(meta[1], dtype=odt, device=device)
             continue
+        import time
+
+        on_gpu = getattr(torch.device(device), "type", "cpu") == "cuda"
+        t0 = time.perf_counter()
         mine = torch.zeros(shard, dtype=odt, device=device)
         off = 0
         for p, start, name, meta in items:
@@ -127,7 +133,14 @@ def sharded_state_dict(files: list[str], dtype: torch.dtype, device, reader: _Re
             reader.read_names.append(name)
             off += t.numel()
         full = torch.empty(shard * world, dtype=odt, device=device)
+        if on_gpu:
+            torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
         dist.all_gather_into_tensor(full, mine, group=group)
+        if on_gpu:
+            torch.cuda.synchronize(device)
+        reader.read_s += t1 - t0
+        reader.gather_s += time.perf_counter() - t1
         offs = [r * shard for r in range(world)]
         for _, _, name, meta in items:
             r = owner[name]

@@ -37,6 +37,10 @@ SD_CLASSES = {
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
 }
 UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
+# job kwargs the SD callback consumes itself (the rest go to the pipeline call)
+_CALLBACK_KEYS = {"model_name", "scheduler_type", "pipeline_type", "upscale", "textual_inversion", "lora",
+                  "cross_attention_scale", "revision", "variant", "outputs", "content_type", "controlnet_model_name",
+                  "controlnet_revision", "save_preprocessed_input", "_image_range", "_return_images", "_split"}
 
 
 def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
@@ -55,6 +59,27 @@ def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
     if "latent-upscaler" in n:
         return "StableDiffusionLatentUpscalePipeline"
     return None
+
+
+def refuse_unsupported_checkpoint(model_name: str, revision: str = "main"):
+    """A fatal ValueError for checkpoints whose pipeline geometry has no path
+    here: the SDXL refiner (``requires_aesthetics_score``: aesthetic-score
+    ``time_ids``, ``text_encoder_2`` only).  The reference builds whatever
+    class the hive names (swarm/diffusion/diffusion_func.py:41-46); running a
+    refiner through the base SDXL path would silently produce wrong images."""
+    import json
+
+    w = find_weights(model_name, revision)
+    path = os.path.join(w, "model_index.json") if w else None
+    if not path or not os.path.exists(path):
+        return
+    with open(path) as f:
+        idx = json.load(f)
+    te = idx.get("text_encoder")
+    no_te1 = te is None or (isinstance(te, (list, tuple)) and not any(te))
+    if idx.get("requires_aesthetics_score") or (no_te1 and idx.get("text_encoder_2")):
+        raise ValueError(f"{model_name}: SDXL refiner checkpoints (aesthetic-score time ids, text_encoder_2 only) "
+                         "are not implemented by this worker")
 
 
 def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "main") -> str:
@@ -179,6 +204,7 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
     image_range = kwargs.pop("_image_range", None)
     return_images = bool(kwargs.pop("_return_images", False))
     ensure_weights(model_name, revision)  # provisioned before the class is read from its model_index.json
+    refuse_unsupported_checkpoint(model_name, revision)
     pcls = pipeline_class_for(pipeline_type, model_name, revision)
     if pcls in UPSCALE_CLASSES:
         if split is not None or image_range is not None:
@@ -348,6 +374,17 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
     reproduce the job's solo images exactly.  Returns (artifacts, config) per job."""
     import torch
 
+    import inspect
+
+    # the solo path forwards every kwarg it does not consume to the pipeline
+    # call, which raises TypeError on unknown ones: same check here, per job,
+    # before any GPU work (the batcher then runs the jobs one by one and each
+    # gets its own error envelope)
+    call_keys = set(inspect.signature(StableDiffusion.__call__).parameters) - {"self", "unexpected"}
+    for kw in jobs:
+        bad = sorted(k for k in kw if k not in call_keys and k not in _CALLBACK_KEYS and k not in _DROP)
+        if bad:
+            raise TypeError(f"batched job: unexpected keyword arguments {bad}")
     k0 = jobs[0]
     model_name = k0["model_name"]
     pipe = load_sd(model_name, device_identifier, k0.get("revision", "main"))
@@ -375,6 +412,7 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
     p = pipe(prompt=prompts, negative_prompt=negs, num_inference_steps=steps,
              guidance_scale=float(k0.get("guidance_scale", 7.5)), height=height, width=width,
              latents=torch.cat(lat, 0).contiguous(), scheduler=sched,
+             eta=float(k0.get("eta") or 0.0),  # batch key: every job of the batch has this eta
              generator=gens)  # per-job / per-image sampler noise
     outs, i = [], 0
     for kw, n in zip(jobs, counts):

@@ -55,6 +55,10 @@ def load_esrgan(model_name: str, device: str):
         w = model_name if os.path.isfile(model_name) else ensure_weights(model_name)
         sd = esrgan_state_dict(w) if w else None
         kw = dict(TINY_RRDB) if tiny else {}
+        if sd is not None and not ("conv_first.weight" in sd and "body.0.rdb1.conv1.weight" in sd):
+            # e.g. SRVGGNetCompact (realesr-general-x4v3: body.N.weight, no conv_first)
+            raise ValueError(f"{model_name}: not an x4 RRDBNet checkpoint (no conv_first / body.0.rdb1 weights); "
+                             "only the RRDBNet Real-ESRGAN architecture is supported")
         if sd is not None:  # geometry from the checkpoint: block count, width, growth
             kw["nb"] = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"body\.(\d+)\.", k)] if m)
             kw["nf"] = int(sd["conv_first.weight"].shape[0])

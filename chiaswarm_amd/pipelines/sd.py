@@ -101,6 +101,8 @@ FAMILIES = {
     "sdxl": Family("sdxl", unet_mod.SDXL, vae_mod.SDXL_VAE, [clip_mod.CLIP_L, clip_mod.OPENCLIP_BIGG],
                    default_size=1024, pipeline_class="StableDiffusionXLPipeline"),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
+    "tiny-xl": Family("tiny-xl", unet_mod.TINY_XL, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT, clip_mod.TINY_TEXT_G],
+                      default_size=64, pipeline_class="StableDiffusionXLPipeline"),
 }
 
 

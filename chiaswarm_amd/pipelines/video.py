@@ -124,7 +124,10 @@ def txt2vid_diffusion_callback(device_identifier, model_name, **kwargs):
     kwargs.pop("revision", None)
     kwargs.pop("variant", None)
     pipe = load_t2v(model_name, device_identifier)
-    frames = pipe(scheduler=get_scheduler(scheduler_type), **kwargs)
+    # the checkpoint's own scheduler config + Karras sigmas (reference:
+    # scheduler_type.from_config(pipeline.scheduler.config, use_karras_sigmas=True),
+    # swarm/video/tx2vid.py:32-34)
+    frames = pipe(scheduler=get_scheduler(scheduler_type, **pipe.sched_config), **kwargs)
     video, ct = frames_to_video(frames, 8, content_type)
     from PIL import Image
 

@@ -20,7 +20,7 @@ from .. import __version__
 
 # kwargs (after jobs.router.format_args) that must be equal across a batch
 KEY_FIELDS = ("model_name", "revision", "pipeline_type", "scheduler_type", "num_inference_steps", "guidance_scale",
-              "height", "width", "content_type")
+              "height", "width", "content_type", "eta")
 # kwargs that make a job unbatchable
 SOLO_FIELDS = ("image", "mask_image", "controlnet_model_name", "lora", "textual_inversion", "latents",
                "prompt_embeds", "negative_prompt_embeds")

@@ -135,9 +135,12 @@ class ProcessExecutor:
         # rank-local and joins the next generation when the supervisor regroups
         self.env["WORLD_SIZE"] = "1"
         self.restarts += 1
-        for jid, fut in list(self.pending.items()):  # control messages die with the child
-            if jid.startswith("__") and self.loop is not None:
-                self.pending.pop(jid, None)
+        # everything in flight dies with the child: control messages AND jobs
+        # (a job sent during a regroup that then timed out would otherwise wait
+        # out job_timeout_s on a fresh child that never saw it)
+        for jid, fut in list(self.pending.items()):
+            self.pending.pop(jid, None)
+            if self.loop is not None:
                 self.loop.call_soon_threadsafe(_resolve, fut, (None, "GPU worker restarted"))
         self._start()
 
@@ -267,7 +270,7 @@ def _raw_key(job):
         return None
     return (job.get("model_name"), job.get("height"), job.get("width"), job.get("num_inference_steps"),
             job.get("guidance_scale"), p.get("scheduler_type"), p.get("pipeline_type"), job.get("content_type"),
-            job.get("revision"))
+            job.get("revision"), job.get("eta"))
 
 
 def splittable(job) -> int:
@@ -494,7 +497,11 @@ class Supervisor:
         tasks = [asyncio.ensure_future(e.run(sj)) for e, sj in zip(exs, subs)]
         pending = set(tasks)
         failed_at = None  # when a part first returned an error result
-        grace = float(os.environ.get("SDAAS_SPLIT_GRACE_S", "30"))
+        # a part that FAILED released its peers (pipelines.diffusion._split_failed):
+        # the others finish their own images and return, so the grace only
+        # catches a peer wedged in the transfer — long enough for a healthy
+        # leader still rendering (a crashed part is handled at once below)
+        grace = float(os.environ.get("SDAAS_SPLIT_GRACE_S", "300"))
         while pending:
             done, pending = await asyncio.wait(pending, timeout=grace if failed_at is not None else None,
                                                return_when=asyncio.FIRST_COMPLETED)
@@ -577,6 +584,12 @@ class Supervisor:
                 job = await self.work_queue.get()
             finally:
                 self.idle.discard(ex)
+            rt = self._regroup_task
+            if rt is not None and not rt.done():  # no job into a child that is mid-regroup
+                try:
+                    await asyncio.shield(rt)
+                except Exception as e:  # a failed regroup restarted the children; run anyway
+                    logging.warning(f"regroup failed before a job: {e}")
             batch = self._drain_compatible(job)
             self.busy += len(batch)
             helpers = []

@@ -32,3 +32,39 @@ def test_bench_rejects_world_mismatch():
                         "--family", "tiny", "--steps", "1", "--warmup", "0", "--denoise-steps", "1", "--res", "64",
                         "--batch", "1"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_failing_rank_ends_the_run_fast():
+    """A rank that dies during the model load (the others block in its
+    collective) ends the whole run within seconds, non-zero, naming the rank —
+    not after the 600 s process-group timeout."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["SDAAS_BENCH_FAIL_RANK"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--family", "tiny", "--steps", "1", "--warmup", "0", "--denoise-steps", "1", "--res", "64",
+                        "--batch", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    took = time.monotonic() - t0
+    assert r.returncode != 0
+    # (gloo drops rank 0 too when its peer's socket closes; RCCL would leave it
+    # blocked in the collective until the poll terminates it)
+    assert "failing on purpose" in r.stderr
+    assert took < 60, took  # two interpreter + torch start-ups, then the poll notices at once
+
+
+def test_sdxl_config_two_ranks_cpu():
+    """``--config sdxl`` (BASELINE config #3: SDXL-base 1024², 30 steps, one
+    image per rank) labels its metric / model; here on the tiny SDXL-structured
+    family (text_time add-embedding, two text encoders) over 2 gloo ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "sdxl", "--family", "tiny-xl",
+                        "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--denoise-steps", "2",
+                        "--res", "64"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert "SDXL-base 1024×1024 30-step" in rec["metric"] and rec["config"]["bench_config"] == "sdxl"
+    assert rec["config"]["global_batch"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert len(rec["ms_per_step_per_rank"]) == 2 and max(rec["ms_per_step_per_rank"]) <= rec["ms_per_step"] + 1e-6
+    assert rec["model_load_read_s"] >= 0 and rec["model_load_all_gather_s"] > 0

@@ -202,3 +202,46 @@ def test_sd15_layout_runs_its_own_safety_checker(tmp_path, monkeypatch):
     # a layout without one (SD2.x) falls back to a separately provisioned checker, else none
     shutil.rmtree(sc)
     assert diffusion.safety_checker_dir(d) is None
+
+
+def test_sdxl_refiner_is_a_fatal_error_naming_the_gap(tmp_path):
+    d = tmp_path / "store" / "stabilityai" / "stable-diffusion-xl-refiner-1.0"
+    d.mkdir(parents=True)
+    (d / "model.safetensors").write_bytes(b"x")
+    (d / "model_index.json").write_text(json.dumps({
+        "_class_name": "StableDiffusionXLImg2ImgPipeline", "requires_aesthetics_score": True,
+        "text_encoder": [None, None], "text_encoder_2": ["transformers", "CLIPTextModelWithProjection"]}))
+    r = synchronous_do_work_function({"id": "rf", "model_name": "stabilityai/stable-diffusion-xl-refiner-1.0",
+                                      "prompt": "x", "num_inference_steps": 2}, Device("cpu"))
+    assert r["fatal_error"] is True
+    assert "refiner" in r["pipeline_config"]["error"] and "aesthetic" in r["pipeline_config"]["error"]
+
+
+def test_txt2vid_uses_the_checkpoint_scheduler_config(monkeypatch):
+    """reference: scheduler_type.from_config(pipeline.scheduler.config,
+    use_karras_sigmas=True) (swarm/video/tx2vid.py:32-34)"""
+    import numpy as np
+
+    from chiaswarm_amd.pipelines import video
+
+    seen = {}
+
+    class FakePipe:
+        sched_config = {"beta_schedule": "scaled_linear", "beta_start": 0.00085, "beta_end": 0.012}
+        config = {}
+
+        def __call__(self, scheduler=None, **kw):
+            seen["sched"] = scheduler
+            return [np.zeros((8, 8, 3), np.uint8)] * 2
+
+    real = video.get_scheduler
+
+    def spy(name, **cfg):
+        seen["cfg"] = dict(cfg)
+        return real(name, **cfg)
+
+    monkeypatch.setattr(video, "load_t2v", lambda *a, **k: FakePipe())
+    monkeypatch.setattr(video, "get_scheduler", spy)
+    video.txt2vid_diffusion_callback("cpu", "damo-vilab/text-to-video-ms-1.7b", prompt="x", num_inference_steps=2,
+                                     content_type="video/webm")
+    assert seen["cfg"] == FakePipe.sched_config and seen["sched"] is not None

@@ -110,3 +110,16 @@ def test_pth_checkpoint_weights_only(tmp_path):
     torch.save({"params_ema": {"a": 1}}, tmp_path / "notensors.pth")
     with pytest.raises(CheckpointMismatch):
         read_pth(str(tmp_path / "notensors.pth"))
+
+
+def test_srvgg_checkpoint_is_a_clear_error(tmp_path):
+    """A Real-ESRGAN checkpoint of another architecture (SRVGGNetCompact,
+    realesr-general-x4v3: ``body.N.weight`` only) is refused with a ValueError
+    naming it, not a bare KeyError."""
+    from chiaswarm_amd.pipelines.esrgan import load_esrgan
+
+    sd = {f"body.{i}.weight": torch.zeros(64, 64 if i else 3, 3, 3) for i in range(4)}
+    f = tmp_path / "realesr-general-x4v3.pth"
+    torch.save({"params": sd}, f)
+    with pytest.raises(ValueError, match="not an x4 RRDBNet"):
+        load_esrgan(str(f), "cpu")

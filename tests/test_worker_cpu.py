@@ -219,3 +219,68 @@ def test_every_job_writes_a_structured_log_line(caplog):
     assert [r["id"] for r in recs] == ["L1", "L2"]
     assert recs[0]["status"] == "ok" and recs[0]["seed"] == 9 and recs[0]["seconds"] > 0
     assert recs[1]["status"] == "fatal" and "error" in recs[1]
+
+
+def test_batched_ddim_eta_matches_solo_and_splits_by_eta():
+    """eta is part of the batch key and reaches the batched sampler: a DDIM
+    eta > 0 job gives its solo images when coalesced."""
+    import numpy as np
+
+    from chiaswarm_amd.runtime.batcher import run_jobs
+
+    base = {**TINY, "parameters": {"scheduler_type": "DDIMScheduler"}, "content_type": "image/png"}
+    jobs = [{"id": f"e{i}", **base, "seed": 40 + i, "eta": 1.0} for i in range(2)]
+    jobs.append({"id": "e0eta", **base, "seed": 50})  # eta 0: not coalesced with the eta 1 jobs
+    dev = Device("cpu")
+    batched = run_jobs([dict(j) for j in jobs], dev, max_images=8)
+    assert batched[0]["pipeline_config"].get("batched_with") == 2
+    assert batched[2]["pipeline_config"].get("batched_with", 1) == 1
+    for j, r in zip(jobs[:2], batched[:2]):
+        solo = synchronous_do_work_function(dict(j), dev)
+        a = np.asarray(Image.open(io.BytesIO(base64.b64decode(r["artifacts"]["primary"]["blob"]))), np.int16)
+        b = np.asarray(Image.open(io.BytesIO(base64.b64decode(solo["artifacts"]["primary"]["blob"]))), np.int16)
+        d = np.abs(a - b)
+        assert d.mean() < 0.5 and d.max() <= 24
+
+
+def test_batched_unknown_kwarg_fails_like_solo():
+    """An unknown pipeline kwarg fails the job batched exactly as it does solo
+    (retryable TypeError envelope), and does not sink its batch mates."""
+    from chiaswarm_amd.runtime.batcher import run_jobs
+
+    jobs = [{"id": "k0", **TINY, "seed": 1}, {"id": "k1", **TINY, "seed": 2, "not_a_pipeline_arg": 3}]
+    dev = Device("cpu")
+    out = run_jobs([dict(j) for j in jobs], dev, max_images=8)
+    solo = synchronous_do_work_function(dict(jobs[1]), dev)
+    assert "error" not in out[0]["pipeline_config"]
+    assert "not_a_pipeline_arg" in out[1]["pipeline_config"]["error"]
+    assert out[1]["pipeline_config"]["error"] == solo["pipeline_config"]["error"]
+    assert "fatal_error" not in out[1]
+
+
+def test_restart_fails_every_pending_job():
+    """A child restart (e.g. a regroup that timed out) resolves the futures of
+    jobs already sent to it, not only control messages."""
+    from chiaswarm_amd.runtime.worker import ProcessExecutor
+
+    class _Proc:
+        def kill(self):
+            pass
+
+        def join(self, timeout=None):
+            pass
+
+    async def main():
+        ex = ProcessExecutor.__new__(ProcessExecutor)
+        ex.loop = asyncio.get_running_loop()
+        ex.pending = {"job-1": ex.loop.create_future(), "__regrouped__": ex.loop.create_future()}
+        ex.proc, ex.env, ex.restarts = _Proc(), {}, 0
+        ex._start = lambda: None
+        futs = dict(ex.pending)
+        ex._restart()
+        await asyncio.sleep(0)
+        return {k: f.result() for k, f in futs.items()}, ex.pending
+
+    res, left = asyncio.run(main())
+    assert res == {"job-1": (None, "GPU worker restarted"), "__regrouped__": (None, "GPU worker restarted")}
+    assert left == {}

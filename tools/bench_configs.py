@@ -62,7 +62,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="sdxl,controlnet,esrgan,sd21-b1")
     ap.add_argument("--impl", default="hip")
-    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     ops.set_mode(a.impl)
     ops._lib.load()
