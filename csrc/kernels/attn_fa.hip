@@ -118,7 +118,17 @@ struct FaArgs {
   float* part;      // [G][FA_PART] partial slots
   unsigned* flags;  // [G] published partials (the owner resets them)
   unsigned* err;    // [1] spins that gave up (never expected)
+  unsigned long long* dbg;  // PROBE & 128: per-wave phase cycle sums [G][8 waves][8]
 };
+
+// in-kernel stamp (diagnostic builds only: its lgkmcnt(0) and fences forbid overlaps)
+__device__ __forceinline__ unsigned long long fa_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 template <int PROBE = 0>
 __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
@@ -216,8 +226,10 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   v8s qf[4];
   v16f o[2];
   float mref = 0.f, lsum = 0.f;
-  bool fast = true;  // every row of this wave has m_ref == 0
   const v16f zero16 = {0.f};
+  v16f cneg = zero16;  // -m_ref in every register: the QK^T chain's initial accumulator
+                       // (scores come out relative to the reference: no per-score subtract)
+  unsigned long long ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0, tl = 0;
 
   auto load_q = [&]() {  // this wave's 32 query rows -> B fragments, pre-scaled into log2 units
 #pragma unroll
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
           asm volatile("" ::"v"(kf), "v"(qf[ds]));
           if (ds == 0) s[kt] = zero16 + (float)kt;
         } else {
-          s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], ds == 0 ? zero16 : s[kt], 0, 0, 0);
+          s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], ds == 0 ? cneg : s[kt], 0, 0, 0);
         }
       }
     }
@@ -261,24 +273,32 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     return vmax3(__uint_as_float(x[0]), __uint_as_float(x[1]), m);
   };
   // new segment: reference for its first tile's scores (row max mb)
-  auto seg_init = [&](float mb) {
+  // (the segment's first scores s were computed with cneg = 0)
+  auto seg_init = [&](float mb, v16f (&s)[2]) {
     mref = (mb > FA_THR_HI || mb < FA_THR_LO) ? mb : 0.f;
     lsum = 0.f;
     o[0] = zero16;
     o[1] = zero16;
-    fast = __all(mref == 0.f);
+    if (__any(mref != 0.f)) {
+      s[0] -= mref;
+      s[1] -= mref;
+      cneg = zero16 - mref;
+    }
   };
-  // tile max mb of the NEXT tile arrives while this tile's P is in O: deferred rescale
-  auto rescale = [&](float mb) {
-    const bool up = mb > mref + FA_THR_HI;
+  // the NEXT tile's row max mb (of s - m_ref) arrives while this tile's P is
+  // in O: deferred rescale of O and l, and the next tile's scores re-referenced
+  auto rescale = [&](float mb, v16f (&s)[2]) {
+    const bool up = mb > FA_THR_HI;
     if (__any(up)) {
-      const float mnew = up ? mb : mref;
-      const float alpha = __builtin_amdgcn_exp2f(mref - mnew);
+      const float d = up ? mb : 0.f;  // new reference - old
+      const float alpha = __builtin_amdgcn_exp2f(-d);
       o[0] *= alpha;
       o[1] *= alpha;
       lsum *= alpha;
-      mref = mnew;
-      fast = __all(mref == 0.f);
+      s[0] -= d;
+      s[1] -= d;
+      mref += d;
+      cneg = zero16 - mref;
     }
   };
 
@@ -286,7 +306,10 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   // m_ref), QK^T of unit u+1 into Sn ----
   // NEXT: u + 1 is in the same segment (its QK^T overlaps this unit's softmax)
   auto body = [&](int u, bool nxt, v16f (&Sc)[2], v16f (&Sn)[2]) {
-    // V^T fragments of this unit first (16 asm tr-reads: lo keys +0..3, hi
+    // QK^T of unit u+1 always (branch-free body: at a segment end or the range
+    // end it multiplies the wrong Q or a stale slot and Sn is recomputed / unused)
+    qk(u + 1, Sn);
+    // V^T fragments of this unit (after the K reads of the QK^T above) (16 asm tr-reads: lo keys +0..3, hi
     // +8..11 of each 16-key step, [kt][st][dt]); their latency hides under the
     // QK^T / exp work below and one lgkmcnt wait naming them precedes the PV
     const unsigned vs = lds0 + (unsigned)((u & (FA_NSLOT - 1)) * FA_SLOT);
@@ -300,9 +323,6 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     fa_tr<2 * 2048>(vl[1][0][1], va01); fa_tr<2 * 2048>(vh[1][0][1], va11);
     fa_tr<3 * 2048>(vl[1][1][0], va00); fa_tr<3 * 2048>(vh[1][1][0], va10);
     fa_tr<3 * 2048>(vl[1][1][1], va01); fa_tr<3 * 2048>(vh[1][1][1], va11);
-    // QK^T of unit u+1 always (branch-free body: at a segment end or the range
-    // end it multiplies the wrong Q or a stale slot and Sn is recomputed / unused)
-    qk(u + 1, Sn);
     // exp (scores -> P), in place
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -330,6 +350,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
                             pack2(Sc[kt][o8 + 4], Sc[kt][o8 + 5]), pack2(Sc[kt][o8 + 6], Sc[kt][o8 + 7])));
       }
     // PV: O^T += V^T P^T
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph3 += t - tl; tl = t; }
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(vl[0][0][0]), "+v"(vh[0][0][0]), "+v"(vl[0][0][1]), "+v"(vh[0][0][1]),
                    "+v"(vl[0][1][0]), "+v"(vh[0][1][0]), "+v"(vl[0][1][1]), "+v"(vh[0][1][1]),
@@ -349,8 +370,10 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st], o[dt], 0, 0, 0);
           }
         }
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph4 += t - tl; tl = t; }
     const float mb = rowmax(Sn);
-    if (nxt) rescale(mb);
+    if (nxt) rescale(mb, Sn);
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph5 += t - tl; tl = t; }
   };
 
   // ---- epilogues ----
@@ -443,10 +466,11 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   v16f sA[2], sB[2];
   load_q();
   qk(u0, sA);
-  seg_init(rowmax(sA));
+  seg_init(rowmax(sA), sA);
 
   // ---- main loop over units, two per trip (the score registers swap roles) ----
   auto unit = [&](int u, v16f (&Sc)[2], v16f (&Sn)[2]) {
+    if constexpr ((PROBE & 128) != 0) tl = fa_stamp();
     // unit u+1's tiles (K for the QK^T below or the next segment's first QK^T,
     // V for the next unit) landed in every wave's LDS image
     // DMA(u+2) — 2 instructions, issued after DMA(u+1) and after any Q DMA issued
@@ -455,21 +479,19 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
       if (u + 2 < u1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph0 += t - tl; tl = t; }
     if constexpr ((PROBE & 16) == 0) fa_barrier();
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph1 += t - tl; tl = t; }
     // next segment's Q: its DMA goes out once this segment's Q has been read
     if (seg_hi < u1 && q_for != seg_hi && seg_hi <= u + FA_LEAD) {
       dma_q(seg_hi / T);
       q_for = seg_hi;
     }
     if (u + FA_LEAD < u1) dma_unit(u + FA_LEAD);
-    if (!fast) {  // some row of this wave moved its reference off 0 (rare): subtract it here
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) Sc[kt][i] -= mref;
-    }
+    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph2 += t - tl; tl = t; }
     body(u, u + 1 < seg_hi, Sc, Sn);
     if (u + 1 < seg_hi) return;
+    if constexpr ((PROBE & 128) != 0) ph6 += 1;  // segment ends
     // ---- segment [seg_lo, seg_hi) of block blk ends here ----
     const int blk = u / T;
     const bool owns_first = seg_lo == blk * T;
@@ -488,12 +510,20 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     }
     wait_issue(q_end);  // own wave's Q region (K of unit u+1 was waited for above)
     load_q();
+    cneg = zero16;
     qk(u + 1, Sn);
-    seg_init(rowmax(Sn));
+    seg_init(rowmax(Sn), Sn);
   };
   for (int u = u0; u < u1; u += 2) {
     unit(u, sA, sB);
     if (u + 1 < u1) unit(u + 1, sB, sA);
+  }
+  if constexpr ((PROBE & 128) != 0) {
+    if (lane == 0) {
+      unsigned long long* d = a.dbg + ((size_t)w * FA_WAVES + wv) * 8;
+      d[0] = ph0; d[1] = ph1; d[2] = ph2; d[3] = ph3; d[4] = ph4; d[5] = ph5; d[6] = ph6;
+      d[7] = (unsigned long long)(u1 - u0);
+    }
   }
 }
 
@@ -502,6 +532,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
 // ---------------------------------------------------------------------------
 static float* g_fa_part = nullptr;
 static unsigned* g_fa_flags = nullptr;  // [G] flags + [1] error counter
+static unsigned long long* g_fa_dbg = nullptr;  // [G][8][8] phase stamps (probe 128)
 static int g_fa_workers = 0;
 static int g_fa_min_skv = 512;  // csk_set_attn_fa_min_skv (tests: 128)
 
@@ -536,7 +567,15 @@ CSK_API int csk_attn_fa_init() {
   if (e != hipSuccess) return (int)e;
   e = hipMalloc(&g_fa_flags, (size_t)(g_fa_workers + 1) * sizeof(unsigned));
   if (e != hipSuccess) return (int)e;
+  e = hipMalloc(&g_fa_dbg, (size_t)g_fa_workers * FA_WAVES * 8 * sizeof(unsigned long long));
+  if (e != hipSuccess) return (int)e;
   return (int)hipMemset(g_fa_flags, 0, (size_t)(g_fa_workers + 1) * sizeof(unsigned));
+}
+
+// probe 128: copy the per-wave phase cycle sums of the last launch ([G][8][8])
+CSK_API int csk_attn_fa_dbg(unsigned long long* out, int n) {
+  if (!g_fa_dbg) return (int)hipErrorNotInitialized;
+  return (int)hipMemcpy(out, g_fa_dbg, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
 }
 
 CSK_API int csk_attn_fa_errors(unsigned* out) {
@@ -583,6 +622,7 @@ CSK_API int csk_attention_fa(void* o, const void* q, const void* k, const void* 
   a.part = g_fa_part;
   a.flags = g_fa_flags;
   a.err = g_fa_flags + g_fa_workers;
+  a.dbg = g_fa_dbg;
   int G = g_fa_workers;
   if (workers > 0 && workers < G) G = workers;
   if (G > a.U) G = a.U;
@@ -595,6 +635,7 @@ CSK_API int csk_attention_fa(void* o, const void* q, const void* k, const void* 
     case 64: attn_fa_kernel<66><<<G, 512, 0, stream>>>(a); break;      // no K/V DMA (and no waits)
     case 76: attn_fa_kernel<66 + 12><<<G, 512, 0, stream>>>(a); break; // ... and no MFMAs
     case 77: attn_fa_kernel<66 + 13><<<G, 512, 0, stream>>>(a); break; // ... and no exp
+    case 128: attn_fa_kernel<128><<<G, 512, 0, stream>>>(a); break;    // phase stamps
     default: attn_fa_kernel<0><<<G, 512, 0, stream>>>(a); break;
   }
   return (int)hipGetLastError();
