@@ -182,6 +182,9 @@ class PipelineSpec:
     scheduler: dict
     components: dict
     tokenizer_pad: list  # per tokenizer: the pad token string (None: not declared)
+    text_names: tuple = ("text_encoder",)  # component directory of each text encoder
+    requires_aesthetics_score: bool = False  # SDXL refiner: aesthetic score in the time ids
+    force_zeros_for_empty_prompt: bool = False  # SDXL: no negative prompt -> zero negative embeddings
 
 
 def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
@@ -192,9 +195,11 @@ def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
     if idx is None:
         return None
     comps = {k: v for k, v in idx.items() if not k.startswith("_") and isinstance(v, (list, tuple)) and v[0]}
-    for need in ("unet", "vae", "text_encoder"):
+    for need in ("unet", "vae"):
         if need not in comps:
             raise UnsupportedConfig(f"{weights_dir}: model_index.json has no {need!r} component")
+    if "text_encoder" not in comps and "text_encoder_2" not in comps:
+        raise UnsupportedConfig(f"{weights_dir}: model_index.json has no 'text_encoder' component")
     ucfg = component_config(weights_dir, "unet")
     vcfg = component_config(weights_dir, "vae")
     if ucfg is None or vcfg is None:
@@ -203,6 +208,7 @@ def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
         raise UnsupportedConfig(f"unet: {ucfg['_class_name']} is not a UNet2DConditionModel")
     text = []
     pads = []
+    names = []
     for i, sub in enumerate(("text_encoder", "text_encoder_2")):
         if sub not in comps:
             continue
@@ -218,14 +224,18 @@ def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
             if cls not in tc["architectures"]:
                 tc["architectures"] = list(tc["architectures"]) + [cls]
         text.append(clip_text_config(tc, sub))
+        names.append(sub)
         tok = "tokenizer" if i == 0 else "tokenizer_2"
         sp = component_config(weights_dir, tok, "special_tokens_map.json") or {}
         tk = component_config(weights_dir, tok, "tokenizer_config.json") or {}
         pad = sp.get("pad_token", tk.get("pad_token"))
         pads.append(pad.get("content") if isinstance(pad, dict) else pad)
     sched = component_config(weights_dir, "scheduler", "scheduler_config.json") or {}
-    return PipelineSpec(idx.get("_class_name", "DiffusionPipeline"), unet_config(ucfg), vae_config(vcfg), text,
-                        sched, comps, pads)
+    cls = idx.get("_class_name", "DiffusionPipeline")
+    # diffusers' StableDiffusionXL*Pipeline constructors default this to True
+    fz = bool(idx.get("force_zeros_for_empty_prompt", str(cls).startswith("StableDiffusionXL")))
+    return PipelineSpec(cls, unet_config(ucfg), vae_config(vcfg), text, sched, comps, pads, tuple(names),
+                        bool(idx.get("requires_aesthetics_score", False)), fz)
 
 
 def controlnet_config(cfg: dict, what: str = "controlnet") -> tuple[UNetConfig, dict]:

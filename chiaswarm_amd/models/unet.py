@@ -72,6 +72,14 @@ TINY = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
                   down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
                   up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"),
                   num_heads=(2, 2), cross_attention_dim=32, sample_size=8)
+# stabilityai/stable-diffusion-xl-refiner-1.0: bigG context only (1280), pooled
+# 1280 + 5 aesthetic-score time ids x 256 = 2560
+SDXL_REFINER = UNetConfig(
+    block_out_channels=(384, 768, 1536, 1536),
+    down_block_types=("DownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D", "DownBlock2D"),
+    up_block_types=("UpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "UpBlock2D"),
+    num_heads=(6, 12, 24, 24), transformer_layers_per_block=4, cross_attention_dim=1280,
+    addition_embed_type="text_time", projection_class_embeddings_input_dim=2560, sample_size=128)
 # SDXL structure at test size: text_time add-embedding, two text encoders
 # (32 + 32 context, pooled projection 32), deeper transformer stack below
 TINY_XL = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
@@ -80,6 +88,7 @@ TINY_XL = UNetConfig(block_out_channels=(32, 64), layers_per_block=1,
                      num_heads=(2, 2), transformer_layers_per_block=(1, 2), cross_attention_dim=64,
                      addition_embed_type="text_time", addition_time_embed_dim=8,
                      projection_class_embeddings_input_dim=32 + 6 * 8, sample_size=8)
+TINY_XL_REFINER = dataclasses.replace(TINY_XL, cross_attention_dim=32, projection_class_embeddings_input_dim=32 + 5 * 8)
 
 # AudioLDM (cvssp/audioldm-*): 8-channel mel latents, CLAP embedding as a
 # concatenated class embedding, attention blocks whose "cross" attention runs on

@@ -213,8 +213,11 @@ def load_sd_weights(pipe, weights_dir: str) -> bool:
     use_cache = os.environ.get("SDAAS_PACKED_CACHE", "1") != "0" and not comm.collective_load_active()
     key = hashlib.sha1(os.path.abspath(weights_dir).encode()).hexdigest()[:16]
     parts = [("unet", pipe.unet, None), ("vae", pipe.vae, _VAE_RENAMES)]
-    for i, te in enumerate(pipe.text_encoders):
-        parts.append(("text_encoder" if i == 0 else f"text_encoder_{i + 1}", te, None))
+    fam = getattr(pipe, "family", None)
+    tnames = fam.text_components if fam is not None else \
+        ["text_encoder" if i == 0 else f"text_encoder_{i + 1}" for i in range(len(pipe.text_encoders))]
+    for name, te in zip(tnames, pipe.text_encoders):
+        parts.append((name, te, None))
     present = [sub for sub, _, _ in parts if weight_files(os.path.join(weights_dir, sub))[1]]
     if not present:
         return False

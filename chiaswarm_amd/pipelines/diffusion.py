@@ -61,27 +61,6 @@ def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
     return None
 
 
-def refuse_unsupported_checkpoint(model_name: str, revision: str = "main"):
-    """A fatal ValueError for checkpoints whose pipeline geometry has no path
-    here: the SDXL refiner (``requires_aesthetics_score``: aesthetic-score
-    ``time_ids``, ``text_encoder_2`` only).  The reference builds whatever
-    class the hive names (swarm/diffusion/diffusion_func.py:41-46); running a
-    refiner through the base SDXL path would silently produce wrong images."""
-    import json
-
-    w = find_weights(model_name, revision)
-    path = os.path.join(w, "model_index.json") if w else None
-    if not path or not os.path.exists(path):
-        return
-    with open(path) as f:
-        idx = json.load(f)
-    te = idx.get("text_encoder")
-    no_te1 = te is None or (isinstance(te, (list, tuple)) and not any(te))
-    if idx.get("requires_aesthetics_score") or (no_te1 and idx.get("text_encoder_2")):
-        raise ValueError(f"{model_name}: SDXL refiner checkpoints (aesthetic-score time ids, text_encoder_2 only) "
-                         "are not implemented by this worker")
-
-
 def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "main") -> str:
     """The class this job runs as: the hive-named class, or — for the generic
     ``DiffusionPipeline`` — the checkpoint's own (reference:
@@ -204,7 +183,6 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
     image_range = kwargs.pop("_image_range", None)
     return_images = bool(kwargs.pop("_return_images", False))
     ensure_weights(model_name, revision)  # provisioned before the class is read from its model_index.json
-    refuse_unsupported_checkpoint(model_name, revision)
     pcls = pipeline_class_for(pipeline_type, model_name, revision)
     if pcls in UPSCALE_CLASSES:
         if split is not None or image_range is not None:
@@ -399,7 +377,7 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
         n = max(1, int(kw.get("num_images_per_prompt", 1) or 1))
         counts.append(n)
         prompts += [kw.get("prompt", "")] * n
-        negs += [kw.get("negative_prompt") or ""] * n
+        negs += [kw.get("negative_prompt")] * n  # None: SDXL zero negative embeddings, else ""
         g = kw["generator"]
         # same per-image seeding as diffusion_callback (image j of a job: seed + j)
         jg = [(g, n)] if n == 1 else [(torch.Generator(device=g.device).manual_seed((g.initial_seed() + j) % (1 << 63)), 1)

@@ -52,6 +52,24 @@ class Family:
     # whichever sampler a job names (diffusers ``from_config``)
     sched_config: dict = dataclasses.field(default_factory=dict)
     from_config: bool = False  # built from the checkpoint's config files (else a named preset)
+    # component directory of each text encoder (the SDXL refiner has text_encoder_2 only)
+    text_names: tuple | None = None
+    # SDXL refiner: (orig_h, orig_w, crop_top, crop_left, aesthetic_score) time ids
+    # (diffusers StableDiffusionXLImg2ImgPipeline, requires_aesthetics_score=True)
+    aesthetics: bool = False
+    # SDXL: a job without a negative prompt gets ZERO negative embeddings (and
+    # pooled), not the encoding of "" (diffusers force_zeros_for_empty_prompt)
+    force_zeros: bool = False
+
+    @property
+    def text_components(self) -> list:
+        if self.text_names:
+            return list(self.text_names)
+        return ["text_encoder" if i == 0 else f"text_encoder_{i + 1}" for i in range(len(self.text))]
+
+    @property
+    def tokenizer_components(self) -> list:
+        return [n.replace("text_encoder", "tokenizer") for n in self.text_components]
 
     @property
     def is_xl(self) -> bool:  # SDXL conditioning: pooled text embeds + size/crop time ids
@@ -77,13 +95,17 @@ class Family:
         if pcls in ("DiffusionPipeline", "StableDiffusionPipeline") and spec.unet.in_channels == 9:
             pcls = "StableDiffusionInpaintPipeline"
         if spec.unet.addition_embed_type == "text_time" and not pcls.startswith("StableDiffusionXL"):
-            pcls = "StableDiffusionXLPipeline"
+            pcls = "StableDiffusionXLImg2ImgPipeline" if spec.requires_aesthetics_score else \
+                "StableDiffusionXLPipeline"
         pad0 = spec.tokenizer_pad[0] if spec.tokenizer_pad else None
+        xl = spec.unet.addition_embed_type == "text_time"
         return cls(name=name, unet=spec.unet, vae=spec.vae, text=list(spec.text),
-                   pad_with_eos=pad0 is None or pad0 == "<|endoftext|>",
+                   pad_with_eos=(pad0 is None or pad0 == "<|endoftext|>") and spec.text_names[:1] == ("text_encoder",),
                    default_size=int(spec.unet.sample_size) * 2 ** (len(spec.vae.block_out_channels) - 1),
                    prediction_type=sk.pop("prediction_type", "epsilon"), pipeline_class=pcls, sched_config=sk,
-                   from_config=True)
+                   from_config=True, text_names=tuple(spec.text_names),
+                   aesthetics=xl and spec.requires_aesthetics_score,
+                   force_zeros=xl and spec.force_zeros_for_empty_prompt)
 
 
 # Named presets: random-init runs (bench, smoke) and directories without config files
@@ -99,10 +121,16 @@ FAMILIES = {
     "pix2pix": Family("pix2pix", unet_mod.PIX2PIX, vae_mod.SD_VAE, [clip_mod.CLIP_L],
                       pipeline_class="StableDiffusionInstructPix2PixPipeline"),
     "sdxl": Family("sdxl", unet_mod.SDXL, vae_mod.SDXL_VAE, [clip_mod.CLIP_L, clip_mod.OPENCLIP_BIGG],
-                   default_size=1024, pipeline_class="StableDiffusionXLPipeline"),
+                   default_size=1024, pipeline_class="StableDiffusionXLPipeline", force_zeros=True),
+    "sdxl-refiner": Family("sdxl-refiner", unet_mod.SDXL_REFINER, vae_mod.SDXL_VAE, [clip_mod.OPENCLIP_BIGG],
+                           pad_with_eos=False, default_size=1024, pipeline_class="StableDiffusionXLImg2ImgPipeline",
+                           text_names=("text_encoder_2",), aesthetics=True),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
     "tiny-xl": Family("tiny-xl", unet_mod.TINY_XL, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT, clip_mod.TINY_TEXT_G],
-                      default_size=64, pipeline_class="StableDiffusionXLPipeline"),
+                      default_size=64, pipeline_class="StableDiffusionXLPipeline", force_zeros=True),
+    "tiny-xl-refiner": Family("tiny-xl-refiner", unet_mod.TINY_XL_REFINER, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT_G],
+                              pad_with_eos=False, default_size=64, pipeline_class="StableDiffusionXLImg2ImgPipeline",
+                              text_names=("text_encoder_2",), aesthetics=True),
 }
 
 
@@ -115,6 +143,8 @@ def family_for_model(model_name: str) -> str:
         return "tiny"
     if "instruct-pix2pix" in n:
         return "pix2pix"
+    if "xl" in n and "refiner" in n:
+        return "sdxl-refiner"
     if "xl" in n:
         return "sdxl"
     if "inpaint" in n and ("2-" in n or "2." in n):
@@ -177,20 +207,19 @@ class StableDiffusion:
 
             if load_sd_weights(self, weights_dir):
                 self.weights_source = str(weights_dir)
-        names = ["unet", "vae"] + ["text_encoder" if i == 0 else f"text_encoder_{i + 1}"
-                                   for i in range(len(self.text_encoders))]
+        names = ["unet", "vae"] + fam.text_components
         for name, m in zip(names, [self.unet, self.vae] + self.text_encoders):
             if name not in self.prepared:  # loaded components were packed (or read packed) already
                 prepare_model(m)
         from ..models.weights import CheckpointMismatch, tokenizer_dir
 
         # tokenizer/ (+ tokenizer_2/ for SDXL, whose OpenCLIP-bigG tokenizer pads with "!")
-        tdirs = [tokenizer_dir(weights_dir, "tokenizer" if i == 0 else f"tokenizer_{i + 1}")
-                 for i in range(len(fam.text))]
+        tnames = fam.tokenizer_components
+        tdirs = [tokenizer_dir(weights_dir, t) for t in tnames]
         if self.weights_source != "random-init" and None in tdirs:
             # real text-encoder weights fed hash-fallback token ids = a random prompt
             raise CheckpointMismatch(f"{weights_dir}: tokenizer files (vocab.json / merges.txt) missing for "
-                                     f"{['tokenizer' if i == 0 else f'tokenizer_{i + 1}' for i, d in enumerate(tdirs) if d is None]}")
+                                     f"{[t for t, d in zip(tnames, tdirs) if d is None]}")
         self.tokenizers = [CLIPTokenizer(tdirs[i], 77, pad_with_eos=fam.pad_with_eos and i == 0,
                                          vocab_size=c.vocab_size)
                            for i, c in enumerate(fam.text)]
@@ -260,9 +289,17 @@ class StableDiffusion:
         ctx, added, _ = self.encode(prompts, negatives, cfg, with_kv=False)
         return ctx, added
 
-    def _time_ids(self, b, h, w, device):
-        # (orig_h, orig_w, crop_top, crop_left, target_h, target_w)
-        return torch.tensor([[h, w, 0, 0, h, w]] * b, dtype=torch.float32, device=device)
+    def _time_ids(self, b, h, w, device, aesthetic=None, n_neg=0):
+        """SDXL micro-conditioning rows: (orig_h, orig_w, crop_top, crop_left,
+        target_h, target_w); the refiner's (orig_h, orig_w, crop_top, crop_left,
+        aesthetic_score), the first ``n_neg`` (CFG negative) rows with the
+        negative score (diffusers StableDiffusionXLImg2ImgPipeline._get_add_time_ids)."""
+        if aesthetic is not None:
+            pos, neg = aesthetic
+            rows = [[h, w, 0, 0, neg if i < n_neg else pos] for i in range(b)]
+        else:
+            rows = [[h, w, 0, 0, h, w]] * b
+        return torch.tensor(rows, dtype=torch.float32, device=device)
 
     def _phase_sync(self):
         """Phase timings are device time: sync at phase boundaries (a ~10 us
@@ -427,6 +464,8 @@ class StableDiffusion:
                  num_images_per_prompt=1, height=None, width=None, generator=None, image=None,
                  mask_image=None, strength=0.8, image_guidance_scale=None, scheduler=None,
                  controlnet_conditioning_scale=1.0, output_type="pil", latents=None, eta=0.0, **unexpected):
+        aesthetic = (float(unexpected.pop("aesthetic_score", 6.0)),
+                     float(unexpected.pop("negative_aesthetic_score", 2.5))) if self.family.aesthetics else None
         if unexpected:  # the diffusers call raises on unknown kwargs too (a retryable job error)
             raise TypeError(f"{self.family.pipeline_class}.__call__() got unexpected keyword arguments "
                             f"{sorted(unexpected)}")
@@ -435,12 +474,14 @@ class StableDiffusion:
         prompts = prompt if isinstance(prompt, list) else [prompt]
         prompts = [p for p in prompts for _ in range(num_images_per_prompt)]
         b = len(prompts)
-        neg = negative_prompt if negative_prompt is not None else ""
-        negs = neg if isinstance(neg, list) else [neg] * b
+        negs = negative_prompt if isinstance(negative_prompt, list) else [negative_prompt] * b
         if len(negs) != b:
             negs = [negs[0]] * b
         is_pix2pix = self.family.is_pix2pix
         cfg = guidance_scale > 1.0 or is_pix2pix
+        # rows without a negative prompt (None): SDXL zeroes their embeddings
+        zero_neg = [i for i, n in enumerate(negs) if n is None] if (cfg and self.family.force_zeros) else []
+        negs = [n if n is not None else "" for n in negs]
         sched = scheduler or get_scheduler("DPMSolverMultistepScheduler", **self.family.scheduler_kwargs())
         sched.prediction_type = self.family.prediction_type
         if eta and sched.accepts_eta:  # diffusers forwards eta only to samplers whose step takes it (DDIM)
@@ -466,13 +507,23 @@ class StableDiffusion:
             with trace_range("text_encode"):
                 ctx, added, cross_kv = self.encode(prompts, negs, cfg)
             cross_kv = list(cross_kv)
+            if zero_neg:
+                # SDXL force_zeros_for_empty_prompt: zero negative context and
+                # pooled embedding; their cross-attention K/V (bias only) are
+                # rewritten into the text graph's static outputs
+                rows = torch.tensor(zero_neg, device=ctx.device)
+                ctx = ctx.index_fill(0, rows, 0)
+                if added is not None and added.get("text_embeds") is not None:
+                    added["text_embeds"] = added["text_embeds"].index_fill(0, rows, 0)
+                for dst, src in zip(cross_kv, self.unet.encode_context(ctx)):
+                    dst.copy_(src)
         # K/V are the text graph's static outputs (rewritten in place per request)
         self._kv_static = (not is_pix2pix) and self.use_graphs and hasattr(self, "_text_graphs") and \
             ops.get_mode() == "hip" and ops._lib.available()
         self._req = getattr(self, "_req", 0) + 1
         if added is not None:
             nrep = ctx.shape[0] // b
-            added["time_ids"] = self._time_ids(nrep * b, height, width, self.device)
+            added["time_ids"] = self._time_ids(nrep * b, height, width, self.device, aesthetic, b if cfg else 0)
         self._phase_sync()
         timings["text_encode"] = time.perf_counter() - t0
 

@@ -36,7 +36,7 @@ FIX = os.path.join(os.path.dirname(__file__), "fixtures", "hf_configs")
 SD_MODELS = ["runwayml--stable-diffusion-v1-5", "runwayml--stable-diffusion-inpainting",
              "stabilityai--stable-diffusion-2-1-base", "stabilityai--stable-diffusion-2-1",
              "stabilityai--stable-diffusion-2-inpainting", "stabilityai--stable-diffusion-xl-base-1.0",
-             "timbrooks--instruct-pix2pix"]
+             "stabilityai--stable-diffusion-xl-refiner-1.0", "timbrooks--instruct-pix2pix"]
 
 
 def _j(*p):
@@ -139,8 +139,10 @@ def _tiny_unet(cfg, xdim, n_text_pool=0):
         cfg["transformer_layers_per_block"] = [min(t, 2) for t in cfg["transformer_layers_per_block"]]
     cfg["layers_per_block"] = 1
     if cfg.get("addition_embed_type") == "text_time":
+        # 6 size / crop ids (base) or 5 with the aesthetic score (refiner) next to the pooled 1280
+        n_ids = (cfg["projection_class_embeddings_input_dim"] - 1280) // cfg["addition_time_embed_dim"]
         cfg["addition_time_embed_dim"] = 8
-        cfg["projection_class_embeddings_input_dim"] = n_text_pool + 6 * 8
+        cfg["projection_class_embeddings_input_dim"] = n_text_pool + n_ids * 8
     if cfg.get("class_embed_type") == "simple_projection":
         cfg["projection_class_embeddings_input_dim"] = 32
     return cfg
@@ -192,16 +194,16 @@ def _tiny_sd_dir(name, root):
     idx = _j(name, "model_index.json")
     _write_json(os.path.join(dst, "model_index.json"), idx)
     shutil.copytree(os.path.join(src, "scheduler"), os.path.join(dst, "scheduler"))
-    texts = [s for s in ("text_encoder", "text_encoder_2") if s in idx]
+    texts = [s for s in ("text_encoder", "text_encoder_2") if s in idx and idx[s][0]]
     eos = None
     pool = 0
     for i, sub in enumerate(texts):
-        tok = "tokenizer" if i == 0 else "tokenizer_2"
+        tok = sub.replace("text_encoder", "tokenizer")
         vocab = _tokenizer(os.path.join(dst, tok), _j(name, tok, "special_tokens_map.json"))
         eos = vocab["<|endoftext|>"]
         tc = _tiny_text(_j(name, sub, "config.json"), eos)
         _write_json(os.path.join(dst, sub, "config.json"), tc)
-        m = clip_mod.CLIPTextModel(hc.clip_text_config(tc if i == 0 else dict(
+        m = clip_mod.CLIPTextModel(hc.clip_text_config(tc if sub == "text_encoder" else dict(
             tc, architectures=[idx[sub][1]])))
         init_random_(m, seed=i)
         _save_st(m, os.path.join(dst, sub), "model.safetensors")
@@ -234,7 +236,7 @@ def test_sd_family_loads_strictly_and_steps(tmp_path, name, monkeypatch):
     assert all(getattr(r, "complete", True) for r in pipe.load_reports.values()), pipe.load_reports
     assert pipe.config["_class_name"] == fam.pipeline_class
     kw = {}
-    if fam.unet.in_channels != 4:  # inpaint (9) / pix2pix (8): image-conditioned
+    if fam.unet.in_channels != 4 or fam.aesthetics:  # inpaint (9) / pix2pix (8) / refiner: image-conditioned
         kw["image"] = Image.new("RGB", (64, 64), (120, 30, 200))
         if fam.unet.in_channels == 9:
             kw["mask_image"] = Image.new("L", (64, 64), 255)

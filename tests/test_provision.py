@@ -204,17 +204,56 @@ def test_sd15_layout_runs_its_own_safety_checker(tmp_path, monkeypatch):
     assert diffusion.safety_checker_dir(d) is None
 
 
-def test_sdxl_refiner_is_a_fatal_error_naming_the_gap(tmp_path):
-    d = tmp_path / "store" / "stabilityai" / "stable-diffusion-xl-refiner-1.0"
-    d.mkdir(parents=True)
-    (d / "model.safetensors").write_bytes(b"x")
-    (d / "model_index.json").write_text(json.dumps({
-        "_class_name": "StableDiffusionXLImg2ImgPipeline", "requires_aesthetics_score": True,
-        "text_encoder": [None, None], "text_encoder_2": ["transformers", "CLIPTextModelWithProjection"]}))
-    r = synchronous_do_work_function({"id": "rf", "model_name": "stabilityai/stable-diffusion-xl-refiner-1.0",
-                                      "prompt": "x", "num_inference_steps": 2}, Device("cpu"))
-    assert r["fatal_error"] is True
-    assert "refiner" in r["pipeline_config"]["error"] and "aesthetic" in r["pipeline_config"]["error"]
+def test_sdxl_refiner_runs_with_aesthetic_time_ids(tmp_path, monkeypatch):
+    """stable-diffusion-xl-refiner-1.0 layout (text_encoder_2 only,
+    requires_aesthetics_score): img2img through the refiner UNet with
+    (h, w, crop, crop, aesthetic score) time ids, negative rows at the negative
+    score (diffusers StableDiffusionXLImg2ImgPipeline; parity unpinned: no
+    diffusers here)."""
+    from PIL import Image
+
+    from chiaswarm_amd.pipelines.sd import StableDiffusion, resolve_family
+    from tests.test_hf_config import _tiny_sd_dir
+
+    d = _tiny_sd_dir("stabilityai--stable-diffusion-xl-refiner-1.0", str(tmp_path / "store"))
+    fam = resolve_family("stabilityai/stable-diffusion-xl-refiner-1.0", d)
+    assert fam.aesthetics and not fam.force_zeros and fam.text_components == ["text_encoder_2"]
+    assert fam.pipeline_class == "StableDiffusionXLImg2ImgPipeline"
+    pipe = StableDiffusion(fam, device="cpu", weights_dir=d)
+    tid = pipe._time_ids(4, 64, 48, "cpu", (7.0, 2.0), 2)
+    assert tid.tolist() == [[64, 48, 0, 0, 2.0]] * 2 + [[64, 48, 0, 0, 7.0]] * 2
+    img = Image.new("RGB", (64, 64), (120, 30, 200))
+    kw = dict(prompt="a fox", image=img, strength=0.5, num_inference_steps=2, guidance_scale=5.0,
+              output_type="latent")
+    a = pipe(**kw, generator=torch.Generator().manual_seed(0)).latents
+    b = pipe(**kw, aesthetic_score=2.0, generator=torch.Generator().manual_seed(0)).latents
+    assert torch.isfinite(a).all() and not torch.equal(a, b)  # the score reaches the UNet
+    assert pipe.config["_class_name"] == "StableDiffusionXLImg2ImgPipeline"
+
+
+def test_aesthetic_score_is_refiner_only():
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    pipe = StableDiffusion("tiny-xl", device="cpu")
+    with pytest.raises(TypeError, match="aesthetic_score"):
+        pipe(prompt="x", num_inference_steps=1, aesthetic_score=6.0, output_type="latent")
+
+
+def test_sdxl_empty_negative_prompt_is_zero_embeddings():
+    """diffusers force_zeros_for_empty_prompt (SDXL base): no negative prompt
+    -> zero negative context / pooled, unlike an explicit "" negative."""
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    kw = dict(prompt="x", num_inference_steps=2, guidance_scale=5.0, output_type="latent", height=64, width=64)
+    for fam, differs in (("tiny-xl", True), ("tiny", False)):
+        pipe = StableDiffusion(fam, device="cpu")
+        a = pipe(**kw, generator=torch.Generator().manual_seed(1)).latents
+        b = pipe(**kw, negative_prompt="", generator=torch.Generator().manual_seed(1)).latents
+        assert torch.equal(a, b) != differs, fam
+        # per row: a batch mixing jobs with and without negatives (diffusion_batch)
+        c = pipe(**dict(kw, prompt=["x", "x"]), negative_prompt=[None, ""],
+                 generator=[(torch.Generator().manual_seed(1), 1), (torch.Generator().manual_seed(1), 1)]).latents
+        assert torch.allclose(c[0], a[0], rtol=1e-4, atol=1e-3) and torch.allclose(c[1], b[0], rtol=1e-4, atol=1e-3)
 
 
 def test_txt2vid_uses_the_checkpoint_scheduler_config(monkeypatch):
