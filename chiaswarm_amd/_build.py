@@ -19,6 +19,7 @@ import argparse
 import concurrent.futures as cf
 import glob
 import hashlib
+import re
 import os
 import shutil
 import subprocess
@@ -67,18 +68,72 @@ def source_digest(debug: bool = False) -> str:
     return h.hexdigest()[:16]
 
 
+# ---- assembly lint: hazards hipcc does not pad around inline asm ----------
+# A transcendental VALU op (v_exp / v_log / v_rcp / v_rsq / v_sqrt) needs one
+# wait state before a VALU reads its result (CDNA3/4 trans forwarding hazard).
+# hipcc pads its own readers, not an inline-asm reader (common.h vadd / vmax3),
+# and a schedule that puts one right behind the v_exp reads the pre-exp value:
+# the persistent attention's row sums went wrong this way in one build.
+_TRANS = re.compile(r"^\s*(v_(?:exp|log|rcp|rsq|sqrt)_f(?:32|16)\w*)\s+(v\d+)")
+# profiling variants (wrong results by design) are exempt
+_LINT_EXEMPT = (re.compile(r"attn_fa_kernelILi[1-9]"), re.compile(r"attn32_kernelILi1ELi[1-9]"))
+
+
+def lint_asm(text: str) -> list:
+    """(function, line, trans op, reader) of every trans result read by the
+    very next instruction."""
+    out, func, prev = [], "", None
+    for n, line in enumerate(text.split("\n"), 1):
+        t = line.strip()
+        if re.match(r"^_Z\w*:", line):
+            func, prev = line.split(":")[0], None
+            continue
+        if not t or t.startswith((";", ".")) or t.endswith(":"):
+            continue
+        if prev is not None and t.startswith("v_"):
+            parts = t.split(None, 1)
+            srcs = parts[1].split(",")[1:] if len(parts) > 1 else []
+            if any(re.search(r"\b%s\b" % prev[1], x) for x in srcs):
+                out.append((func, n, prev[0], t))
+        m = _TRANS.match(line)
+        prev = (t, m.group(2)) if m else None
+    return [h for h in out if not any(e.search(h[0]) for e in _LINT_EXEMPT)]
+
+
+def _lint(src: str, fl: list, dig: str) -> None:
+    name = os.path.splitext(os.path.basename(src))[0]
+    ok = os.path.join(BUILD, f"{name}.{dig}.lint")
+    if os.path.exists(ok):
+        return
+    asm = os.path.join(BUILD, f"{name}.{dig}.s")
+    cmd = [hipcc(), *[f for f in fl if f != "-fPIC"], "-I", SRC, "-S", "--cuda-device-only", src, "-o", asm]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc -S failed for {src}:\n{r.stderr}")
+    with open(asm) as f:
+        hits = lint_asm(f.read())
+    os.remove(asm)
+    if hits:
+        msg = "\n".join(f"  {fn} (.s line {n}): {a}  ->  {b}" for fn, n, a, b in hits[:10])
+        raise RuntimeError(f"{src}: transcendental result read by the next (inline-asm) instruction — "
+                           f"use vadd_t / an s_nop:\n{msg}")
+    open(ok, "w").close()
+
+
 def _compile(src: str, force: bool, debug: bool = False) -> str:
     name = os.path.splitext(os.path.basename(src))[0]
     fl = flags(debug)
     dig = _digest(src, " ".join(fl))
     obj = os.path.join(BUILD, f"{name}.{dig}.o")
     if os.path.exists(obj) and not force:
+        _lint(src, fl, dig)
         return obj
     cmd = [hipcc(), *fl, "-I", SRC, "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     os.replace(obj + ".tmp", obj)
+    _lint(src, fl, dig)
     return obj
 
 

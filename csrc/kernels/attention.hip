@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const AttnArgs a) {
         for (int r = 0; r < 4; ++r) s[kt][qt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][qt][r], sl2, -mnew));
       float l4[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) l4[r] = vadd(vadd(s[0][qt][r], s[1][qt][r]), vadd(s[2][qt][r], s[3][qt][r]));
+      for (int r = 0; r < 4; ++r) l4[r] = vadd(vadd_t(s[0][qt][r], s[1][qt][r]), vadd_t(s[2][qt][r], s[3][qt][r]));
       lrow[qt] = lrow[qt] * alpha + vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3]));
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) oacc[dt][qt] *= alpha;
@@ -491,9 +491,9 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_pipe_kernel(const AttnArgs
         // 4 independent single-instruction chains (no v_pk_add_f32 beside MFMAs)
         float l4[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) l4[r] = vadd(sc[0][qt][r], sc[1][qt][r]);
+        for (int r = 0; r < 4; ++r) l4[r] = vadd_t(sc[0][qt][r], sc[1][qt][r]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) l4[r] = vadd(l4[r], vadd(sc[2][qt][r], sc[3][qt][r]));
+        for (int r = 0; r < 4; ++r) l4[r] = vadd(l4[r], vadd_t(sc[2][qt][r], sc[3][qt][r]));
         lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
       }
 #pragma unroll
@@ -826,10 +826,10 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         float l4[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          l4[c] = vadd(sc[0][qt][c], sc[0][qt][c + 4]);
-          l4[c] = vadd(l4[c], vadd(sc[0][qt][c + 8], sc[0][qt][c + 12]));
-          l4[c] = vadd(l4[c], vadd(sc[1][qt][c], sc[1][qt][c + 4]));
-          l4[c] = vadd(l4[c], vadd(sc[1][qt][c + 8], sc[1][qt][c + 12]));
+          l4[c] = vadd_t(sc[0][qt][c], sc[0][qt][c + 4]);  // (exp results: trans-hazard-safe adds)
+          l4[c] = vadd(l4[c], vadd_t(sc[0][qt][c + 8], sc[0][qt][c + 12]));
+          l4[c] = vadd(l4[c], vadd_t(sc[1][qt][c], sc[1][qt][c + 4]));
+          l4[c] = vadd(l4[c], vadd_t(sc[1][qt][c + 8], sc[1][qt][c + 12]));
         }
         lrow[qt] = vadd(lrow[qt], vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
       }

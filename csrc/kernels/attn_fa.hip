@@ -22,13 +22,19 @@
 //     reaches it last) acquires, merges and stores (cdna_hip_programming.md
 //     §6 Guideline 16; the owner resets the flag; bounded spins).
 //   * K / V tiles arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
-//     instruction: each wave moves 8 K rows + 8 V rows per tile) into a 4-slot
-//     ring, three units ahead and across query-block seams; the XOR swizzle of
+//     instruction: each wave moves 8 K rows + 8 V rows per tile) into an 8-slot
+//     ring, five units ahead and across query-block seams; the XOR swizzle of
 //     the LDS image (kv_off32 of attention.hip: conflict-free for the K
 //     ds_read_b128 and the V ds_read_b64_tr_b16 patterns) is carried by the
 //     per-lane SOURCE address.  Q arrives the same way into a per-wave region.
 //     Waits are counted (`s_waitcnt vmcnt(n)` from a scalar issue counter),
-//     barriers raw: one barrier per key tile.
+//     barriers raw: one barrier per TWO key tiles (the waves drift apart by up
+//     to a tile between barriers, which spreads their DMA issue and MFMA
+//     phases; 4-slot ring with a barrier per tile: 243-248 us, this: 234 us at
+//     B8 H5 S4096).
+//   * Inline-asm adds of exp results use vadd_t (one wait state: the trans
+//     forwarding hazard hipcc does not pad before inline asm); _build.py lints
+//     the assembly for any trans result read by the next instruction.
 //   * Every LDS address is a per-lane base fixed at kernel entry plus a
 //     compile-time offset (the ring slot is one scalar add).
 //   * Per wave: 32 query rows.  S^T = K Q^T and O^T = V^T P^T on
@@ -52,10 +58,15 @@ namespace {
 constexpr int FA_WAVES = 8;
 constexpr int FA_ROWS = FA_WAVES * 32;  // query rows per block
 constexpr int FA_SLOT = 16384;          // one 64-key tile: K (8 KiB) + V (8 KiB)
-constexpr int FA_NSLOT = 4;             // K/V ring slots (unit v -> slot v & 3)
-constexpr int FA_LEAD = 3;              // units of K/V DMA in flight ahead of the compute
-constexpr int FA_Q_OFF = FA_NSLOT * FA_SLOT;
-constexpr int FA_LDS = FA_Q_OFF + FA_WAVES * 4096;  // + one 32-row Q region per wave
+constexpr int FA_NSLOT = 8;             // K/V ring slots (unit v -> slot v & 7)
+constexpr int FA_LEAD = 5;              // units of K/V DMA in flight ahead of the compute
+constexpr int FA_BE = 2;                // one workgroup barrier every FA_BE units
+// WAR: DMA(v) (issued at unit v - LEAD, after that unit's barrier or the one
+// before it) overwrites unit v - NSLOT's slot, whose last reader (its PV) ran
+// before that barrier
+static_assert(FA_NSLOT >= FA_LEAD + FA_BE, "ring too short for the barrier spacing");
+static_assert(FA_LEAD > FA_BE, "a barrier must find the next FA_BE units' DMA issued");
+static_assert((FA_NSLOT & (FA_NSLOT - 1)) == 0, "slot index is a mask");
 constexpr int FA_PART = FA_WAVES * 9 * 64 * 4;      // floats per worker slot: 8 waves x 9 float4 x 64 lanes
 constexpr float FA_THR_HI = 64.f;  // move m_ref when a tile's row max exceeds it by this (log2 units)
 constexpr float FA_THR_LO = -40.f; // first-tile row max below m_ref + this: m_ref = that max
@@ -132,7 +143,11 @@ __device__ __forceinline__ unsigned long long fa_stamp() {
 
 template <int PROBE = 0>
 __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[FA_LDS];
+  // (probe 256: the 4-slot ring of the first version, a barrier every unit)
+  constexpr int NSLOT = (PROBE & 256) ? 4 : FA_NSLOT;
+  constexpr int LEAD = (PROBE & 256) ? 3 : FA_LEAD;
+  constexpr int QOFF = NSLOT * FA_SLOT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[QOFF + FA_WAVES * 4096];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
@@ -148,14 +163,14 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   const int lr = lane >> 3;                        // row of the 8-row DMA piece
   const int kvrow = 8 * wv + lr;                   // tile row this lane's DMA piece fetches
   const int kvch = (lane & 7) ^ fa_f(kvrow);       // source chunk that lands in this lane's slot
-  const int k_lane = kvrow * a.sks + kvch * 8;  // element offsets
-  const int v_lane = kvrow * a.svs + kvch * 8;
+  const unsigned k_lane = (unsigned)(kvrow * a.sks + kvch * 8) * 2u;  // byte offsets (32-bit: saddr + voffset)
+  const unsigned v_lane = (unsigned)(kvrow * a.svs + kvch * 8) * 2u;
   int q_lane[4];                                   // Q piece i: local row 8 i + lr
 #pragma unroll
   for (int i = 0; i < 4; ++i) q_lane[i] = ((lane & 7) ^ fa_f(8 * i + lr)) * 8;
   const unsigned kv_dst = (unsigned)wv * 1024u;    // this wave's 1 KiB of a K or V tile
   const unsigned lds0 = (unsigned)(size_t)(fa_lptr_t)(void*)smem;  // LDS byte address of the array
-  const unsigned q_base = FA_Q_OFF + (unsigned)wv * 4096u;
+  const unsigned q_base = QOFF + (unsigned)wv * 4096u;
   unsigned koff[4];  // K / Q fragment (row r, chunk 2 ds + hh) byte offsets
 #pragma unroll
   for (int ds = 0; ds < 4; ++ds) koff[ds] = (unsigned)(r * 128 + (((2 * ds + hh) ^ fa_f(r)) << 4));
@@ -187,9 +202,9 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     d_h = bh - d_b * a.H;
   }
   auto dma_unit = [&](int v) {  // v == the next unit in order
-    const bf16_t* kb = a.k + (size_t)(d_b * a.skb + d_h * a.skh) + (size_t)(d_tile * 64 * a.sks);
-    const bf16_t* vb = a.v + (size_t)(d_b * a.svb + d_h * a.svh) + (size_t)(d_tile * 64 * a.svs);
-    unsigned char* dst = smem + (v & (FA_NSLOT - 1)) * FA_SLOT + kv_dst;
+    const char* kb = (const char*)(a.k + (size_t)(d_b * a.skb + d_h * a.skh) + (size_t)(d_tile * 64 * a.sks));
+    const char* vb = (const char*)(a.v + (size_t)(d_b * a.svb + d_h * a.svh) + (size_t)(d_tile * 64 * a.svs));
+    unsigned char* dst = smem + (v & (NSLOT - 1)) * FA_SLOT + kv_dst;
     if (!(PROBE & 64) || v < u0 + 2) {
       __builtin_amdgcn_global_load_lds((fa_gptr_t)(kb + k_lane), (fa_lptr_t)dst, 16, 0, 0);
       __builtin_amdgcn_global_load_lds((fa_gptr_t)(vb + v_lane), (fa_lptr_t)(dst + 8192), 16, 0, 0);
@@ -243,7 +258,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     }
   };
   auto qk = [&](int v, v16f (&s)[2]) {  // S^T of unit v's keys (its K tile is in LDS)
-    const unsigned char* kb = smem + (v & (FA_NSLOT - 1)) * FA_SLOT;
+    const unsigned char* kb = smem + (v & (NSLOT - 1)) * FA_SLOT;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
@@ -312,7 +327,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     // V^T fragments of this unit (after the K reads of the QK^T above) (16 asm tr-reads: lo keys +0..3, hi
     // +8..11 of each 16-key step, [kt][st][dt]); their latency hides under the
     // QK^T / exp work below and one lgkmcnt wait naming them precedes the PV
-    const unsigned vs = lds0 + (unsigned)((u & (FA_NSLOT - 1)) * FA_SLOT);
+    const unsigned vs = lds0 + (unsigned)((u & (NSLOT - 1)) * FA_SLOT);
     const unsigned va00 = vs + voff[0][0], va01 = vs + voff[0][1], va10 = vs + voff[1][0], va11 = vs + voff[1][1];
     v4s vl[2][2][2], vh[2][2][2];
     fa_tr<0 * 2048>(vl[0][0][0], va00); fa_tr<0 * 2048>(vh[0][0][0], va10);
@@ -333,10 +348,10 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     float l4[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      l4[c] = vadd(Sc[0][c], Sc[0][c + 4]);
-      l4[c] = vadd(l4[c], vadd(Sc[0][c + 8], Sc[0][c + 12]));
-      l4[c] = vadd(l4[c], vadd(Sc[1][c], Sc[1][c + 4]));
-      l4[c] = vadd(l4[c], vadd(Sc[1][c + 8], Sc[1][c + 12]));
+      l4[c] = vadd_t(Sc[0][c], Sc[0][c + 4]);  // (exp results: trans-hazard-safe adds)
+      l4[c] = vadd(l4[c], vadd_t(Sc[0][c + 8], Sc[0][c + 12]));
+      l4[c] = vadd(l4[c], vadd_t(Sc[1][c], Sc[1][c + 4]));
+      l4[c] = vadd(l4[c], vadd_t(Sc[1][c + 8], Sc[1][c + 12]));
     }
     lsum = vadd(lsum, vadd(vadd(l4[0], l4[1]), vadd(l4[2], l4[3])));
     v8s pf[2][2];
@@ -460,7 +475,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   int seg_hi = min(u1, (u0 / T + 1) * T);            // one past its last
   int q_for = u0;                                    // segment start whose Q DMA was issued last
   dma_q(u0 / T);
-  for (int v = u0; v < min(u1, u0 + FA_LEAD); ++v) dma_unit(v);
+  for (int v = u0; v < min(u1, u0 + LEAD); ++v) dma_unit(v);
   wait_issue(max(q_end, dma_u0));
   fa_barrier();
   v16f sA[2], sB[2];
@@ -469,25 +484,29 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   seg_init(rowmax(sA), sA);
 
   // ---- main loop over units, two per trip (the score registers swap roles) ----
-  auto unit = [&](int u, v16f (&Sc)[2], v16f (&Sn)[2]) {
+  // BAR: a barrier unit (every FA_BE-th from u0).  Its barrier publishes units
+  // u+1 .. u+FA_BE (K for the QK^Ts, V for the PVs up to the next barrier):
+  // each wave first waits for its own share of them; the DMA units issued after
+  // u+FA_BE (2 instructions each, any Q DMA issued among them only makes the
+  // wait stricter) may stay in flight
+  auto unit = [&](auto bar_c, int u, v16f (&Sc)[2], v16f (&Sn)[2]) {
+    constexpr bool BAR = decltype(bar_c)::value;
     if constexpr ((PROBE & 128) != 0) tl = fa_stamp();
-    // unit u+1's tiles (K for the QK^T below or the next segment's first QK^T,
-    // V for the next unit) landed in every wave's LDS image
-    // DMA(u+2) — 2 instructions, issued after DMA(u+1) and after any Q DMA issued
-    // before it — may stay in flight; without it (range end) nothing may
-    if constexpr ((PROBE & 2) == 0) {
-      if (u + 2 < u1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (BAR) {
+      if constexpr ((PROBE & 2) == 0) {
+        if (u + LEAD <= u1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (LEAD - FA_BE - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph0 += t - tl; tl = t; }
+      if constexpr ((PROBE & 16) == 0) fa_barrier();
+      if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph1 += t - tl; tl = t; }
     }
-    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph0 += t - tl; tl = t; }
-    if constexpr ((PROBE & 16) == 0) fa_barrier();
-    if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph1 += t - tl; tl = t; }
     // next segment's Q: its DMA goes out once this segment's Q has been read
-    if (seg_hi < u1 && q_for != seg_hi && seg_hi <= u + FA_LEAD) {
+    if (seg_hi < u1 && q_for != seg_hi && seg_hi <= u + LEAD) {
       dma_q(seg_hi / T);
       q_for = seg_hi;
     }
-    if (u + FA_LEAD < u1) dma_unit(u + FA_LEAD);
+    if (u + LEAD < u1) dma_unit(u + LEAD);
     if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph2 += t - tl; tl = t; }
     body(u, u + 1 < seg_hi, Sc, Sn);
     if (u + 1 < seg_hi) return;
@@ -514,9 +533,13 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     qk(u + 1, Sn);
     seg_init(rowmax(Sn), Sn);
   };
+  static_assert(FA_BE == 2, "the unrolled loop below pairs one barrier unit with one plain unit");
   for (int u = u0; u < u1; u += 2) {
-    unit(u, sA, sB);
-    if (u + 1 < u1) unit(u + 1, sB, sA);
+    unit(std::true_type{}, u, sA, sB);
+    if (u + 1 < u1) {
+      if constexpr ((PROBE & (32 | 256)) != 0) unit(std::true_type{}, u + 1, sB, sA);  // (probe: a barrier every unit)
+      else unit(std::false_type{}, u + 1, sB, sA);
+    }
   }
   if constexpr ((PROBE & 128) != 0) {
     if (lane == 0) {
@@ -632,6 +655,8 @@ CSK_API int csk_attention_fa(void* o, const void* q, const void* k, const void* 
     case 4: attn_fa_kernel<4><<<G, 512, 0, stream>>>(a); break;
     case 8: attn_fa_kernel<8><<<G, 512, 0, stream>>>(a); break;
     case 16: attn_fa_kernel<16><<<G, 512, 0, stream>>>(a); break;
+    case 32: attn_fa_kernel<32><<<G, 512, 0, stream>>>(a); break;
+    case 256: attn_fa_kernel<256><<<G, 512, 0, stream>>>(a); break;
     case 64: attn_fa_kernel<66><<<G, 512, 0, stream>>>(a); break;      // no K/V DMA (and no waits)
     case 76: attn_fa_kernel<66 + 12><<<G, 512, 0, stream>>>(a); break; // ... and no MFMAs
     case 77: attn_fa_kernel<66 + 13><<<G, 512, 0, stream>>>(a); break; // ... and no exp

@@ -77,6 +77,16 @@ __device__ __forceinline__ float vadd(float a, float b) {
   asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// vadd for operands that may be FRESH transcendental results (v_exp / v_rcp ...):
+// CDNA3/4 need one wait state between a trans op and a VALU reading its result
+// (trans forwarding hazard) and hipcc pads none before an inline-asm reader —
+// a plain vadd scheduled right behind its v_exp reads the pre-exp value.
+// (_build.py lints every kernel's assembly for that adjacency.)
+__device__ __forceinline__ float vadd_t(float a, float b) {
+  float r;
+  asm("s_nop 0\n\tv_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 // MFMA result -> inline-asm reader: hipcc pads no wait states for an asm
 // statement (cdna_hip_programming.md §5.7 item 2), and the softmax's vmax3
 // reads score accumulators straight out of the matrix cores.  This nop

@@ -94,6 +94,7 @@ def analyse(db, calls_path, out_json=""):
     sep_idx = sep_idx[-n:]  # the recorded calls are the last n separated groups
     agg = collections.OrderedDict()
     per_kernel = collections.defaultdict(float)
+    torch_kernels = collections.defaultdict(float)
     prev = sep_idx[0] - 1
     # the group of call k: the kernels between separator k-1 and separator k
     first = sep_idx[0]
@@ -112,7 +113,11 @@ def analyse(db, calls_path, out_json=""):
         a[0] += 1
         a[1] += us
         for nm, s, e in ks:
-            a[3][nm.split("(")[0][:60]] += 1
+            short = nm.split("(")[0][:60]
+            if "at::native" in nm:  # torch kernels between libcsk calls: name them fully
+                short = nm.replace("(anonymous namespace)::", "")[:160]
+                torch_kernels[(label, short)] += (e - s) / 1e3
+            a[3][short] += 1
             per_kernel[nm.split("(")[0][:70]] += (e - s) / 1e3
     iters = meta.get("iters", 1)
     print(f"{n} calls over {iters} step(s): {total / iters / 1e3:.3f} ms device time per step")
@@ -123,6 +128,10 @@ def analyse(db, calls_path, out_json=""):
               f"[{', '.join(f'{k}' for k in kn)}]")
         out.append({"op": label, "tile": tile, "calls_per_step": cnt // iters, "us_each": round(us / cnt, 2),
                     "us_per_step": round(us / iters, 1), "tflops": round(tf, 1), "kernels": list(kn)})
+    if torch_kernels:
+        print("torch (at::native) kernels launched before these libcsk calls (us per step):")
+        for (label, nm), us in sorted(torch_kernels.items(), key=lambda kv: -kv[1]):
+            print(f"  {us / iters:8.1f} us  before {label}:  {nm}")
     if out_json:
         with open(out_json, "w") as f:
             json.dump({"ms_per_step": total / iters / 1e3, "rows": out}, f, indent=1)
