@@ -105,6 +105,8 @@ sig("csk_xattn_block", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_
 sig("csk_attention_fa", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p)
 sig("csk_set_attn_fa", c_int)
+sig("csk_set_gemm_sk_workers", c_int)
+sig("csk_gemm_sk_errors", c_void_p)
 sig("csk_attn_fa_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)

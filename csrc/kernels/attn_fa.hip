@@ -324,6 +324,9 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     // QK^T of unit u+1 always (branch-free body: at a segment end or the range
     // end it multiplies the wrong Q or a stale slot and Sn is recomputed / unused)
     qk(u + 1, Sn);
+    if constexpr ((PROBE & 512) != 0) {  // (A/B: the K / V DMA issued behind the QK^T MFMAs:
+      if (u + LEAD < u1) dma_unit(u + LEAD);  //  248-252 vs 230-233 us at B8 H5 S4096, profiles/attn_fa_r5b.txt)
+    }
     // V^T fragments of this unit (after the K reads of the QK^T above) (16 asm tr-reads: lo keys +0..3, hi
     // +8..11 of each 16-key step, [kt][st][dt]); their latency hides under the
     // QK^T / exp work below and one lgkmcnt wait naming them precedes the PV
@@ -506,7 +509,9 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
       dma_q(seg_hi / T);
       q_for = seg_hi;
     }
-    if (u + LEAD < u1) dma_unit(u + LEAD);
+    if constexpr ((PROBE & 512) == 0) {
+      if (u + LEAD < u1) dma_unit(u + LEAD);
+    }
     if constexpr ((PROBE & 128) != 0) { const auto t = fa_stamp(); ph2 += t - tl; tl = t; }
     body(u, u + 1 < seg_hi, Sc, Sn);
     if (u + 1 < seg_hi) return;
@@ -657,6 +662,7 @@ CSK_API int csk_attention_fa(void* o, const void* q, const void* k, const void* 
     case 16: attn_fa_kernel<16><<<G, 512, 0, stream>>>(a); break;
     case 32: attn_fa_kernel<32><<<G, 512, 0, stream>>>(a); break;
     case 256: attn_fa_kernel<256><<<G, 512, 0, stream>>>(a); break;
+    case 512: attn_fa_kernel<512><<<G, 512, 0, stream>>>(a); break;
     case 64: attn_fa_kernel<66><<<G, 512, 0, stream>>>(a); break;      // no K/V DMA (and no waits)
     case 76: attn_fa_kernel<66 + 12><<<G, 512, 0, stream>>>(a); break; // ... and no MFMAs
     case 77: attn_fa_kernel<66 + 13><<<G, 512, 0, stream>>>(a); break; // ... and no exp

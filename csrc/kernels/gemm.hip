@@ -483,6 +483,7 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
       !((tile >= 11 && tile <= 29) || tile == 36))
     return (int)hipErrorInvalidValue;
   if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
+  if (tile >= 40 && tile <= 43) ksplit = 1;  // stream-K tiles split K themselves
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
@@ -504,7 +505,13 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else tile = 4;
   }
   int err;
-  if (tile >= 31 && tile <= 34) {  // 8-wave phased / ring tiles (gemm8p.hip); 40+: gemm_glds.hip
+  if (tile >= 40 && tile <= 43) {  // stream-K (gemm_sk.hip); same-geometry LDS-DMA tile where it declines
+    err = csk_gemm_sk_launch(a, tile, CONV, s);
+    if (err == (int)hipErrorNotSupported) {
+      static const int fallback[4] = {13, 12, 14, 14};
+      err = csk_gemm_glds_launch(a, fallback[tile - 40], 1, CONV, s);
+    }
+  } else if (tile >= 31 && tile <= 34) {  // 8-wave phased / ring tiles (gemm8p.hip); 40+: gemm_glds.hip
     err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
     if (err == (int)hipErrorNotSupported) {
       // the fallback must write the GN-statistics segments the host sized gn_part
@@ -604,7 +611,8 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36) && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
+  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36 || (tile >= 40 && tile <= 43)) &&
+                         g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
     if (!rows) return (int)hipErrorInvalidValue;

@@ -1156,3 +1156,4 @@ __host__ __forceinline__ int gn_seg_for() {
 
 int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);
 int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);
+int csk_gemm_sk_launch(const GemmArgs& a, int tile, bool conv, hipStream_t s);
