@@ -72,6 +72,7 @@ constexpr float FA_THR_HI = 64.f;  // move m_ref when a tile's row max exceeds i
 constexpr float FA_THR_LO = -40.f; // first-tile row max below m_ref + this: m_ref = that max
 
 typedef __attribute__((address_space(3))) v4s fa_lds_v4s;
+typedef unsigned int fa_u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const void* fa_gptr_t;
 typedef __attribute__((address_space(3))) void* fa_lptr_t;
 
@@ -415,23 +416,27 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
         }
     }
   };
-  auto slot_ptr = [&](int worker) { return a.part + (size_t)worker * FA_PART + (size_t)wv * 9 * 64 * 4; };
+  // Hand-off without fences (cdna_hip_programming.md Guideline 16 R1; an
+  // agent-scope fence costs ~1.7 us): the partial is stored write-through
+  // (sc1) and drained before the flag's atomic store; the owner polls relaxed
+  // and reads the partial with sc1 loads.
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, G * FA_PART * (int)sizeof(float), 0x00020000);
+  auto slot_off = [&](int worker) { return (worker * FA_PART + wv * 9 * 64 * 4) * (int)sizeof(float); };
   auto publish = [&]() {  // contributor: partial (O, m_ref, l) of this worker's first block piece
-    float* p = slot_ptr(w);
+    const int so = slot_off(w);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(p + ((dt * 4 + g) * 64 + lane) * 4) =
-            make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
-    *reinterpret_cast<float4*>(p + (8 * 64 + lane) * 4) = make_float4(mref, lsum, 0.f, 0.f);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.flags + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(fa_u4, make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3])),
+            prs, ((dt * 4 + g) * 64 + lane) * 16, so, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fa_u4, make_float4(mref, lsum, 0.f, 0.f)), prs,
+                                           (8 * 64 + lane) * 16, so, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    fa_barrier();
+    if (tid == 0) __hip_atomic_store(a.flags + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto merge = [&](int blk_end) {  // owner: every worker whose range starts inside this block
     if (tid == 0) {
@@ -445,20 +450,21 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
           }
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: the loads below are sc1)
+    fa_barrier();
     for (int j = w + 1; j < G && (int)((long long)U * j / G) < blk_end; ++j) {
-      const float* p = a.part + (size_t)j * FA_PART + (size_t)wv * 9 * 64 * 4;
-      const float4 ml = *reinterpret_cast<const float4*>(p + (8 * 64 + lane) * 4);
+      const int so = slot_off(j);
+      const float4 ml =
+          __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, (8 * 64 + lane) * 16, so, 16));
       const float mn = fmaxf(mref, ml.x);
       const float ca = __builtin_amdgcn_exp2f(mref - mn), cb = __builtin_amdgcn_exp2f(ml.x - mn);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 x = *reinterpret_cast<const float4*>(p + ((dt * 4 + g) * 64 + lane) * 4);
+          const float4 x = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(prs, ((dt * 4 + g) * 64 + lane) * 16, so, 16));
           o[dt][4 * g] = o[dt][4 * g] * ca + x.x * cb;
           o[dt][4 * g + 1] = o[dt][4 * g + 1] * ca + x.y * cb;
           o[dt][4 * g + 2] = o[dt][4 * g + 2] * ca + x.z * cb;
@@ -467,7 +473,8 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
       lsum = lsum * ca + ml.y * cb;
       mref = mn;
     }
-    __syncthreads();  // every wave has read the slots before they are released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fa_barrier();  // every wave has read the slots before they are released
     if (tid == 0)
       for (int j = w + 1; j < G && (int)((long long)U * j / G) < blk_end; ++j)
         __hip_atomic_store(a.flags + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

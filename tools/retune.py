@@ -39,6 +39,30 @@ def run_model(name, dev):
         p.use_graphs = False
         g = torch.Generator(device=dev).manual_seed(0)
         p(prompt="tune", num_inference_steps=2, height=size, width=size, num_images_per_prompt=batch, generator=g)
+    elif name == "esrgan":  # Real-ESRGAN x4plus, 512 -> 2048 (config #5): RRDB convs at 512^2, up-convs
+        import numpy as np
+        from PIL import Image
+
+        from chiaswarm_amd.pipelines.esrgan import load_esrgan, upscale_x4
+
+        net = load_esrgan("xinntao/RealESRGAN_x4plus", str(dev))
+        img = Image.fromarray((np.random.default_rng(0).random((512, 512, 3)) * 255).astype(np.uint8))
+        upscale_x4(net, img)
+    elif name == "controlnet":  # SD1.5 + ControlNet-canny 512^2 (config #4), batch 1 and 4
+        import numpy as np
+        from PIL import Image
+
+        from chiaswarm_amd.controlnet.preprocess import image_to_canny
+        from chiaswarm_amd.pipelines.controlnet import load_controlnet
+        from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+        p = StableDiffusion("sd15", device=dev, seed=0)
+        p.controlnet = load_controlnet("lllyasviel/control_v11p_sd15_canny", p, str(dev))
+        p.use_graphs = False
+        img = image_to_canny(Image.fromarray((np.random.default_rng(0).random((512, 512, 3)) * 255).astype(np.uint8)))
+        g = torch.Generator(device=dev)
+        for n in (1, 4):
+            p(prompt="tune", image=img, num_inference_steps=2, num_images_per_prompt=n, generator=g.manual_seed(0))
     else:
         raise SystemExit(f"unknown model {name}")
 
