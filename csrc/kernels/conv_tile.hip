@@ -1,0 +1,263 @@
+// Persistent halo-tile 3x3 convolution for narrow outputs (Cout = 32): the
+// Real-ESRGAN dense-block convs (north-star config #5; RRDBNet
+// conv1..conv4 of every residual dense block, 276 of the 345 convs of an x4
+// upscale).
+//
+// Why: the implicit-GEMM conv (gemm_glds.hip / gemm.hip) stages an A tile per
+// K-step per tap — each input pixel crosses L2 -> LDS nine times — and with
+// N = 32 output channels every staged A byte feeds only 32 FLOP.  The four
+// Cout = 32 convs ran at 290-420 TF/s bound by the LDS-DMA fill
+// (profiles/esrgan_kernels_r5a.txt).  Here a workgroup owns an 8 x 32 pixel
+// output tile and stages its (8+2) x (32+2) input halo ONCE per 32-channel
+// chunk; the nine taps read it at a pixel offset, so A crosses L2 -> LDS
+// ~1.33x instead of 9x and per chunk a workgroup issues 48 LDS-DMA
+// instructions for 4.7 MFLOP (the 128x32 implicit GEMM: ~190).
+//
+// Structure (MI355X-first):
+//   * persistent: one 512-thread workgroup per CU walks tiles w, w + G, ...;
+//     the (tile, chunk) units form ONE LDS-DMA stream through a 3-stage ring
+//     (two chunks in flight), so the next tile's first chunks land during this
+//     tile's last chunk and its register-direct epilogue (no LDS in the
+//     epilogue: the ring stays live).  Counted `vmcnt` waits, raw barriers.
+//   * LDS images are row-major, 64 B (one 32-channel chunk) per halo pixel or
+//     (tap, cout) weight row, the four 16-byte channel groups XOR-swizzled by
+//     row so the 16 lanes of an MFMA fragment hit distinct bank quads; one
+//     LDS-DMA instruction fills 16 rows (16 x 64 contiguous source bytes; a
+//     first version that filled 64 pixels of one group per instruction touched
+//     64 cache lines per 1 KB: 33.6-58.4 us against 26.7-43.9 us now);
+//     out-of-image halo pixels read the zero page.
+//
+// Measured (tools/convtilebench.py, 512^2, profiles/conv_tile_r5.txt): 64 /
+// 96 / 128 / 160 -> 32 in 26.7 / 33.4 / 38.0 / 43.9 us (362-551 TF/s) against
+// 38.7 / 54.7 / 62.5 / 87.7 us for the tuned implicit GEMM; Real-ESRGAN x4
+// 512 -> 2048 29.3 -> 24.2 ms.  Cout = 64 convs stay on the implicit GEMM
+// (twice the reuse per staged byte: 680 TF/s for the 192 -> 64 conv5).
+//   * wave w computes tile row w (32 px = 2 MFMA row fragments) x 32 outputs
+//     with v_mfma_f32_16x16x32_bf16 (B . A order: row-layout accumulators, a
+//     lane holds one pixel's 4 consecutive outputs -> 8-byte stores).
+//   * input / output are channel slices of wider NHWC buffers (pixel strides
+//     lda / ldc): the dense block's concat is never materialised.
+#include "gemm_common.h"
+
+namespace {
+
+constexpr int CT_N = 32;                   // output channels
+constexpr int CT_TH = 8, CT_TW = 32;       // output tile
+constexpr int CT_HW = CT_TW + 2, CT_HH = CT_TH + 2;
+constexpr int CT_HPX = CT_HH * CT_HW;      // 340 halo pixels
+constexpr int CT_HSLOT = 384;              // halo pixel slots: 24 DMA instructions of 16 pixels
+constexpr int CT_HALO = CT_HSLOT * 64;     // bytes per stage ([pixel][4 x 16 B])
+constexpr int CT_WROWS = 384;              // 9 taps x 32 outputs = 288 rows, padded to 24 instructions
+constexpr int CT_WGT = CT_WROWS * 64;      // bytes per stage ([tap x cout][4 x 16 B])
+constexpr int CT_STAGE = CT_HALO + CT_WGT;
+constexpr int CT_S = 3;                    // ring stages (two chunks in flight)
+constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per chunk (3)
+constexpr int CT_WI = CT_WROWS / 16 / 8;   // weight DMA instructions per wave per chunk (3)
+
+// 16-byte slot of channel group g (of 4) in LDS row r (a pixel or a (tap, cout)
+// row of 64 B): XOR-swizzled so the 16 lanes of an MFMA fragment (16
+// consecutive rows, one group) hit 16 distinct bank quads
+__device__ __forceinline__ int ct_slot(int r, int g) { return g ^ ((r >> 2) & 3); }
+
+struct ConvTileArgs {
+  const bf16_t* x;     // [B][H][W] pixels, pixel stride lda, channels [0, Cin)
+  const bf16_t* w;     // packed [32][3][3][Cin]
+  const bf16_t* bias;  // [32] or null
+  bf16_t* y;           // [B][H][W] pixels, pixel stride ldc, channels [0, 32)
+  const bf16_t* zero;  // zero page (LDS-DMA source for padding)
+  int B, H, W, Cin, lda, ldc, act;
+  int tiles_x, tiles_y, ntiles;
+};
+
+typedef __attribute__((address_space(1))) const void* ct_gptr_t;
+typedef __attribute__((address_space(3))) void* ct_lptr_t;
+
+__device__ __forceinline__ void ct_dma(const bf16_t* src, unsigned char* dst) {
+  __builtin_amdgcn_global_load_lds((ct_gptr_t)src, (ct_lptr_t)dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void ct_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[CT_S * CT_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int w = xcd_remap(blockIdx.x, G);
+  const int my_tiles = w < a.ntiles ? (a.ntiles - 1 - w) / G + 1 : 0;
+  const int nc = a.Cin / 32;  // 32-channel chunks per tile
+  const int U = my_tiles * nc;
+  if (U == 0) return;
+  const int H = a.H, W = a.W;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- weight DMA (tile-independent): instruction k = wv * 3 + i writes rows
+  // 16 k .. 16 k + 15 (lane L: row 16 k + L / 4, LDS slot L % 4) ----
+  const bf16_t* wsrc[CT_WI];
+#pragma unroll
+  for (int i = 0; i < CT_WI; ++i) {
+    const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * 32 + output channel
+    const int tap = row >> 5, co = row & 31;
+    const int g = (lane & 3) ^ ((row >> 2) & 3);  // source channel group landing in this lane's slot
+    wsrc[i] = row < 9 * CT_N ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
+  }
+  // ---- halo DMA: instruction k = wv * 3 + i writes halo pixels 16 k .. 16 k + 15 ----
+  const bf16_t* hsrc[CT_HI];
+  int d_tile = w, d_c = 0, d_s = 0;  // next unit to issue: tile, chunk, ring stage
+  auto set_halo = [&]() {
+    const int b = d_tile / (a.tiles_x * a.tiles_y);
+    const int rem = d_tile - b * (a.tiles_x * a.tiles_y);
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+#pragma unroll
+    for (int i = 0; i < CT_HI; ++i) {
+      const int hp = (wv * CT_HI + i) * 16 + (lane >> 2);
+      const int hy = hp / CT_HW, hx = hp - hy * CT_HW;
+      const int iy = ty * CT_TH - 1 + hy, ix = tx * CT_TW - 1 + hx;
+      const bool ok = hp < CT_HPX && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const int g = (lane & 3) ^ ((hp >> 2) & 3);
+      hsrc[i] = ok ? a.x + ((size_t)(b * H + iy) * W + ix) * a.lda + g * 8 : a.zero;
+    }
+  };
+  set_halo();
+  auto issue = [&]() {
+    unsigned char* st = smem + d_s * CT_STAGE;
+    const int co = d_c * 32;  // channel offset of this chunk
+#pragma unroll
+    for (int i = 0; i < CT_HI; ++i) ct_dma(hsrc[i] + co, st + (wv * CT_HI + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < CT_WI; ++i) ct_dma(wsrc[i] + co, st + CT_HALO + (wv * CT_WI + i) * 1024);
+    d_s = d_s + 1 == CT_S ? 0 : d_s + 1;
+    if (++d_c == nc) {
+      d_c = 0;
+      d_tile += G;
+      if (d_tile < a.ntiles) set_halo();
+    }
+  };
+
+  v4f acc[2][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+  float bias[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = a.bias ? bf2f(a.bias[j * 16 + fq * 4 + r]) : 0.f;
+
+  auto epilogue = [&](int tile) {
+    const int b = tile / (a.tiles_x * a.tiles_y);
+    const int rem = tile - b * (a.tiles_x * a.tiles_y);
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    const int y = ty * CT_TH + wv;
+    if (y >= H) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int x = tx * CT_TW + i * 16 + fr;
+      if (x >= W) continue;
+      bf16_t* op = a.y + ((size_t)(b * H + y) * W + x) * a.ldc;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[i][j][r] + bias[j][r]);
+        uint2 wd;
+        wd.x = pack2(v[0], v[1]);
+        wd.y = pack2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(op + j * 16 + fq * 4) = wd;
+      }
+    }
+  };
+
+  // ---- prologue: two units in flight ----
+  issue();
+  if (U > 1) issue();
+  int c = 0, s = 0, tile = w;
+  for (int u = 0; u < U; ++u) {
+    // unit u landed once at most one younger unit (CT_HI + CT_WI instructions) is in flight
+    if (u + 1 < U) ct_vmcnt<CT_HI + CT_WI>();
+    else ct_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < U) issue();
+    const unsigned char* hb = smem + s * CT_STAGE;
+    const unsigned char* wb = hb + CT_HALO;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = ky * 3 + kx;
+        v8s af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int hp = (wv + ky) * CT_HW + i * 16 + fr + kx;
+          af[i] = *reinterpret_cast<const v8s*>(hb + hp * 64 + ct_slot(hp, fq) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = tap * CT_N + j * 16 + fr;
+          bfr[j] = *reinterpret_cast<const v8s*>(wb + row * 64 + ct_slot(row, fq) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    s = s + 1 == CT_S ? 0 : s + 1;
+    if (++c == nc) {
+      epilogue(tile);
+      zero_acc();
+      c = 0;
+      tile += G;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static int g_ct_cus = 0;
+
+// 1 when csk_conv_tile takes this conv: 3x3 / stride 1 / pad 1, Cout = 32,
+// Cin % 32 == 0 (<= 64 chunks), 16-byte aligned pixel strides
+CSK_API int csk_conv_tile_ok(int B, int H, int W, int Cin, int Cout, int lda, int ldc) {
+  return B > 0 && H > 0 && W > 0 && Cout == CT_N && Cin % 32 == 0 && Cin >= 32 && Cin <= 2048 && lda >= Cin &&
+         lda % 8 == 0 && ldc >= Cout && ldc % 4 == 0 && (long long)B * H * W * lda < (1ll << 31) &&
+         (long long)B * H * W * ldc < (1ll << 31);
+}
+
+// y[..., :32] = act(conv3x3(x[..., :Cin]) + bias), NHWC with pixel strides lda / ldc
+CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bias, int B, int H, int W, int Cin,
+                          int lda, int ldc, int act, hipStream_t stream) {
+  if (!csk_conv_tile_ok(B, H, W, Cin, CT_N, lda, ldc) || !csk_zero_ptr()) return (int)hipErrorInvalidValue;
+  if ((((size_t)x) & 15) || (((size_t)y) & 7) || (((size_t)wp) & 15)) return (int)hipErrorInvalidValue;
+  if ((size_t)(Cin + 64) * sizeof(bf16_t) > (size_t)csk_zero_bytes()) return (int)hipErrorInvalidValue;
+  if (!g_ct_cus) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    g_ct_cus = cus > 0 ? cus : 256;
+  }
+  ConvTileArgs a;
+  a.x = (const bf16_t*)x;
+  a.w = (const bf16_t*)wp;
+  a.bias = (const bf16_t*)bias;
+  a.y = (bf16_t*)y;
+  a.zero = csk_zero_ptr();
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.lda = lda; a.ldc = ldc; a.act = act;
+  a.tiles_x = (W + CT_TW - 1) / CT_TW;
+  a.tiles_y = (H + CT_TH - 1) / CT_TH;
+  a.ntiles = B * a.tiles_x * a.tiles_y;
+  const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
+  conv_tile_kernel<<<G, 512, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
