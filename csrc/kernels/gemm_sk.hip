@@ -45,6 +45,7 @@
 namespace {
 
 constexpr int SK_MAX_ELEMS = 128 * 64;  // fp32 accumulators per worker slot (largest tile)
+typedef unsigned int sk_u4 __attribute__((ext_vector_type(4)));
 
 struct SkArgs {
   float* part;      // [G][BM * BN] partial accumulators
@@ -146,21 +147,23 @@ __global__ __launch_bounds__(256, OCC) void gemm_sk_kernel(const GemmArgs args, 
   zero_acc();
 
   // ---- fixup ----
-  float* const my_part = sk.part + (size_t)w * SK_MAX_ELEMS;
+  // fence-free hand-off (cdna_hip_programming.md Guideline 16 R1; an agent
+  // fence costs ~1.7 us): partials stored write-through (sc1) and drained
+  // before the flag's atomic store; the owner polls relaxed, reads them sc1
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)sk.part, 0, G * SK_MAX_ELEMS * (int)sizeof(float), 0x00020000);
   auto publish = [&]() {  // contributor: this worker's first (partial) tile piece
+    const int so = w * SK_MAX_ELEMS * (int)sizeof(float);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        *reinterpret_cast<float4*>(my_part + ((i * NT + j) * 256 + tid) * 4) =
-            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also drains the ring: once per worker)
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sk.flags + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(sk_u4, make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3])), prs,
+            ((i * NT + j) * 256 + tid) * 16, so, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave (also drains the ring: once per worker)
+    sk_barrier();
+    if (tid == 0) __hip_atomic_store(sk.flags + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto merge = [&](int tile_end) {  // owner: every worker whose range starts inside the tile
     if (tid == 0) {
@@ -174,23 +177,25 @@ __global__ __launch_bounds__(256, OCC) void gemm_sk_kernel(const GemmArgs args, 
           }
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: the loads below are sc1)
     sk_barrier();
     for (int j = w + 1; j < G && (int)((long long)U * j / G) < tile_end; ++j) {
-      const float* p = sk.part + (size_t)j * SK_MAX_ELEMS;
+      const int so = j * SK_MAX_ELEMS * (int)sizeof(float);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jj = 0; jj < NT; ++jj) {
-          const float4 x = reinterpret_cast<const float4*>(p)[(i * NT + jj) * 256 + tid];
+          const float4 x = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(prs, ((i * NT + jj) * 256 + tid) * 16, so, 16));
           acc[i][jj][0] += x.x;
           acc[i][jj][1] += x.y;
           acc[i][jj][2] += x.z;
           acc[i][jj][3] += x.w;
         }
     }
-    sk_barrier();  // (the slot loads were consumed above: every wave has read them)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sk_barrier();  // every wave has read the slots before they are released
     if (tid == 0)
       for (int j = w + 1; j < G && (int)((long long)U * j / G) < tile_end; ++j)
         __hip_atomic_store(sk.flags + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
