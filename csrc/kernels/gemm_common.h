@@ -559,8 +559,8 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
                 const float g0 = lnr[i] * (acc[i][2 * f + 1][r] - lnm[i] * cq[1][r]) + bq[1][r];
                 const float h1 = lnr[i] * (acc[i][2 * f + 2][r] - lnm[i] * cq[2][r]) + bq[2][r];
                 const float g1 = lnr[i] * (acc[i][2 * f + 3][r] - lnm[i] * cq[3][r]) + bq[3][r];
-                x[r] = h0 * gelu_f(g0);
-                y[r] = h1 * gelu_f(g1);
+                x[r] = h0 * gelu_geglu(g0);
+                y[r] = h1 * gelu_geglu(g1);
               }
               float o[8];
               const int col = ob + sw_pair(x, y, f, fq, o);
@@ -878,7 +878,7 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
         float g[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          g[r] = (rs * (acc[i][j][r] - mu * ch_s[r]) + bh[r]) * gelu_f(rs * (acc[i][j + 1][r] - mu * cg_s[r]) + bg[r]);
+          g[r] = (rs * (acc[i][j][r] - mu * ch_s[r]) + bh[r]) * gelu_geglu(rs * (acc[i][j + 1][r] - mu * cg_s[r]) + bg[r]);
         *reinterpret_cast<float4*>(cs + (row - pr0) * LDC_S + oc) = make_float4(g[0], g[1], g[2], g[3]);
       }
     }
@@ -912,7 +912,7 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WTM + i * 16 + fq * 4 + r;
           cs[(row - pr0) * LDC_S + oc] =
-              (lnfix(acc[i][j][r], row, j) + bh) * gelu_f(lnfix(acc[i][j + 1][r], row, j + 1) + bg);
+              (lnfix(acc[i][j][r], row, j) + bh) * gelu_geglu(lnfix(acc[i][j + 1][r], row, j + 1) + bg);
         }
       }
   } else {
