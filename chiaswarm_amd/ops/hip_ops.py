@@ -58,7 +58,7 @@ def _gn_seg(tile, split, rows_per_b, M, code, N=8):
     bm, bn = tuning.TILES.get(tile, (0, 0))
     if code == 3 or bm == 0 or rows_per_b <= 0:
         return 0
-    if split != 1:
+    if split > 1:  # (split < 0, the in-kernel fixup, writes the tile's own segments)
         if not SPLITK_GN:
             return 0
         s = SPLITK_GN_SEG
@@ -68,6 +68,17 @@ def _gn_seg(tile, split, rows_per_b, M, code, N=8):
     seg = bm * bn // 256 if GN_FINE else bm
     band = bm // tuning.EPI_WM.get(tile, 2) if (bm > 128 or bn == 160) else bm  # epilogue row band (epi_passes)
     return min(seg, band)
+
+
+def _ws(split, M, N, device):
+    """fp32 split-K workspace: [split][M][N] for the reduce kernel; split < 0
+    (in-kernel fixup, gemm_common.h splitk_fixup) stores whole padded tiles, at
+    most (M + 255) x (N + 255) outputs per split for every tile geometry"""
+    if split > 1:
+        return torch.empty(split * M * N, dtype=torch.float32, device=device)
+    if split < 0:
+        return torch.empty(-split * (M + 255) * (N + 255), dtype=torch.float32, device=device)
+    return None
 
 
 def _gn_part(M, N, seg, device):
@@ -107,6 +118,7 @@ sig("csk_attention_fa", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c
 sig("csk_set_attn_fa", c_int)
 sig("csk_set_gemm_sk_workers", c_int)
 sig("csk_gemm_sk_errors", c_void_p)
+sig("csk_gemm_slk_launches", c_void_p)
 sig("csk_attn_fa_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)
@@ -202,11 +214,15 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
     lda, ldb = a2.stride(0), w.stride(0)
 
     def run(tile, split, part=None):
-        ws = torch.empty(split * M * N, dtype=torch.float32, device=a2.device) if split > 1 else None
+        ws = _ws(split, M, N, a2.device)
         _lib.call("csk_gemm", _p(out), _p(a2), _p(w), _p(bias), None, _p(residual),
                   M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
+    if tile == 44 and (ln is not None or row_stats or gn_rows or code == 3):
+        tile = 14  # the sliced-K tile has none of these epilogues (gemm_slk.hip): 64x64 one-tile kernel
+    if split < 0 and not (11 <= tile <= 29 or tile == 36):
+        split = 1  # the in-kernel fixup exists in the LDS-DMA tiles only
     if ln is not None or row_stats:
         if split > 1:  # the split-K reduce has no LN / row-statistics epilogue
             tile, split = (19 if N <= 1280 else 20), 1
@@ -382,7 +398,7 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     code = ACT[act]
 
     def run(tile, split, part=None):
-        ws = torch.empty(split * M * Cout, dtype=torch.float32, device=x.device) if split > 1 else None
+        ws = _ws(split, M, Cout, x.device)
         _lib.call("csk_conv2d_ex", _p(out), _p(x), _p(wp), _p(bias), _p(bias2d), b2s, _p(residual),
                   B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
                   float(out_scale), int(dilation), _p(part), tile, split, _p(ws), _s())

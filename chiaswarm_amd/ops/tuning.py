@@ -38,7 +38,9 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # 64x160 2-stage (fewest L2->LDS bytes per output of the 64-row tiles)
          36: (64, 160),
          # stream-K (gemm_sk.hip): one persistent workgroup per CU, K-steps spread evenly, in-kernel fixup
-         40: (64, 128), 41: (128, 64), 42: (64, 64), 43: (64, 64)}
+         40: (64, 128), 41: (128, 64), 42: (64, 64), 43: (64, 64),
+         # sliced-K (gemm_slk.hip): the 8 waves of a 64x64 tile split its K-steps (small-M grids)
+         44: (64, 64)}
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
 # cannot exceed that band (hip_ops._gn_seg mirrors gemm_common.h gn_seg_for)
@@ -105,7 +107,9 @@ def candidates(M, N, K):
             continue
         if tile >= 31 and K % 64:
             continue
-        if tile >= 40:  # stream-K tiles: A/B only (gemm_sk.hip MEASURED STANDING)
+        if 40 <= tile <= 43:  # stream-K tiles: A/B only (gemm_sk.hip MEASURED STANDING)
+            continue
+        if tile == 44:  # sliced-K: A/B only (gemm_slk.hip MEASURED STANDING)
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)
@@ -114,6 +118,8 @@ def candidates(M, N, K):
             if split == 16 and ntiles > 64:
                 continue
             out.append((tile, split))
+            if split > 1 and (11 <= tile <= 29 or tile == 36):
+                out.append((tile, -split))  # the same split with the in-kernel fixup (no reduce launch)
     return out
 
 

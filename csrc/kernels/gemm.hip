@@ -470,6 +470,8 @@ CSK_API int csk_set_gn_lds(int v) {
   return 0;
 }
 
+int csk_gemm_slk_launch(const GemmArgs& a, bool conv, hipStream_t s);  // gemm_slk.hip
+
 template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
@@ -482,10 +484,18 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   if ((a.act == ACT_PROBE_NO_EPILOGUE || a.act == ACT_PROBE_NO_STORE || a.act == ACT_PROBE_NO_A) &&
       !((tile >= 11 && tile <= 29) || tile == 36))
     return (int)hipErrorInvalidValue;
-  if (ksplit > 1 && a.act == ACT_GEGLU) ksplit = 1;
-  if (tile >= 40 && tile <= 43) ksplit = 1;  // stream-K tiles split K themselves
+  // ksplit < 0: split -ksplit ways with the in-kernel fixup (LDS-DMA tiles only:
+  // the last split of each tile runs the full epilogue, so GEGLU / LN / row and
+  // GN statistics work as unsplit; the host sizes GN segments for the tile)
+  const bool fixup = ksplit < 0;
+  if (fixup) {
+    if (!((tile >= 11 && tile <= 29) || tile == 36) || !a.ws || a.attn_kv) return (int)hipErrorInvalidValue;
+    ksplit = -ksplit;
+  }
+  if (ksplit > 1 && a.act == ACT_GEGLU && !fixup) ksplit = 1;
+  if (tile >= 40 && tile <= 44) ksplit = 1;  // stream-K / sliced-K tiles split K themselves
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
-  if ((a.ln_part || a.row_part) && (ksplit > 1 || tile == 0)) return (int)hipErrorInvalidValue;
+  if ((a.ln_part || a.row_part) && ((ksplit > 1 && !fixup) || tile == 0)) return (int)hipErrorInvalidValue;
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
   if (ksplit > 1) {
     if (!a.ws) return (int)hipErrorInvalidValue;
@@ -497,6 +507,11 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     a.kchunk = a.K;
     ksplit = 1;
   }
+  if (fixup && ksplit > 1) {  // gemm_glds.hip launch_glds: per-tile counters, no reduce kernel
+    a.fx_ws = a.ws;
+    const int err = csk_gemm_glds_launch(a, tile, ksplit, CONV, s);
+    return err;
+  }
   if (tile == 0) {  // heuristic: wide tiles for big problems, narrow-N tiles for Cout <= 64
     const long long t128 = (long long)((a.M + 127) / 128) * ((a.N + 127) / 128);
     if (a.N <= 32) tile = 5;
@@ -505,7 +520,10 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else tile = 4;
   }
   int err;
-  if (tile >= 40 && tile <= 43) {  // stream-K (gemm_sk.hip); same-geometry LDS-DMA tile where it declines
+  if (tile == 44) {  // sliced-K small-M tile (gemm_slk.hip); the 64x64 LDS-DMA tile where it declines
+    err = csk_gemm_slk_launch(a, CONV, s);
+    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, 14, 1, CONV, s);
+  } else if (tile >= 40 && tile <= 43) {  // stream-K (gemm_sk.hip); same-geometry LDS-DMA tile where it declines
     err = csk_gemm_sk_launch(a, tile, CONV, s);
     if (err == (int)hipErrorNotSupported) {
       static const int fallback[4] = {13, 12, 14, 14};
@@ -611,7 +629,7 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36 || (tile >= 40 && tile <= 43)) &&
+  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36 || (tile >= 40 && tile <= 44)) &&
                          g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;

@@ -118,6 +118,13 @@ struct GemmArgs {
   const bf16_t* attn_kv_end;
   int attn_skv;
   float attn_sl2;  // softmax scale * log2(e)
+  // in-kernel split-K fixup (gemm_glds.hip, tuning split < 0): the fx_split
+  // workgroups of an output tile each publish their fp32 partial to
+  // fx_ws[tile][split] and bump fx_cnt[tile]; the last one sums the partials in
+  // split order and runs the normal epilogue (every fusion of the unsplit tile)
+  float* fx_ws;
+  unsigned* fx_cnt;
+  int fx_split;
 };
 
 #define ZERO_BYTES (128 * 1024)  // the LDS-DMA zero page (gemm_glds.hip: csk_init)
@@ -426,6 +433,70 @@ __device__ __forceinline__ void gemm_attn_epilogue(const GemmArgs& args, v4f (&a
 // kernel prologue (ln_merge_tile); a reference to a fixed-size array so the
 // values stay in registers (a pointer that may be null made hipcc keep the
 // array in scratch)
+typedef unsigned int fx_u4 __attribute__((ext_vector_type(4)));
+
+// In-kernel split-K fixup: true in the ONE workgroup of the tile that arrives
+// last, with acc = sum of every split's partial in split order (deterministic
+// whichever workgroup is last); false in the others, which are done.
+// Fence-free hand-off (cdna_hip_programming.md Guideline 16 R1, as
+// gemm_sk.hip): partials stored write-through (sc1) and drained before the
+// counter's atomic; the last arriver reads them all back sc1.  Each thread stores
+// and reloads its own accumulator registers (16 B per lane per fragment: no
+// layout math, fully coalesced).  The last arriver re-zeroes the counter for
+// the next launch that uses it (gemm_glds.hip fixup_counters).
+template <int MT, int NT, int NTHR>
+__device__ __forceinline__ bool splitk_fixup(const GemmArgs& args, v4f (&acc)[MT][NT], int tile, int split,
+                                             int* flag) {
+  constexpr int SLOT = MT * NT * NTHR * 16;  // bytes per split partial
+  const int tid = threadIdx.x, ns = args.fx_split;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(args.fx_ws + (size_t)tile * ns * (SLOT / 4)), 0, ns * SLOT, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fx_u4, acc[i][j]), rs, ((i * NT + j) * NTHR + tid) * 16,
+                                             split * SLOT, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(args.fx_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(ns - 1);
+    if (last) __hip_atomic_store(args.fx_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __syncthreads();  // every wave has read the flag before the epilogue reuses its LDS word
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: the loads below are sc1)
+  // every partial (this workgroup's own too) re-read in split order: a
+  // deterministic sum with no second accumulator array live (the 128x160 and
+  // 256-row tiles are at their register limit)
+  // split 0 straight into acc (all fragments in flight), then the others in
+  // groups of 4 fragments (16 temporaries), adding in split order
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      acc[i][j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * NT + j) * NTHR + tid) * 16, 0, 16));
+  constexpr int NF = MT * NT, G = 4;
+  for (int z = 1; z < ns; ++z) {
+#pragma unroll
+    for (int f0 = 0; f0 < NF; f0 += G) {
+      v4f t[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (f0 + g < NF)
+          t[g] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, ((f0 + g) * NTHR + tid) * 16, z * SLOT, 16));
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (f0 + g < NF) acc[(f0 + g) / NT][(f0 + g) % NT] += t[g];
+    }
+  }
+  return true;
+}
+
 template <int BM, int BN, int WM, int WN, bool RAW = false, int EP = 1, int NTHR = 256, bool SW = false,
           bool ATTN = false>
 __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc)[BM / WM / 16][BN / WN / 16],

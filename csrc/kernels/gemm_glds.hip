@@ -23,6 +23,9 @@
 //     running channel offset never leaves it, so no per-step select is needed.
 #include "gemm_common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 static bf16_t* g_zero = nullptr;
 
 template <int N>
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int split = blockIdx.y;
   const int kbeg = split * args.kchunk;
-  const int kend = args.ws ? min(K, kbeg + args.kchunk) : K;
+  const int kend = (args.ws || args.fx_cnt) ? min(K, kbeg + args.kchunk) : K;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   const int lrow = lane >> 3;                 // row within the 8-row DMA group
@@ -254,6 +257,11 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     }
   }
   __syncthreads();
+  if (args.fx_cnt) {  // in-kernel split-K: only the tile's last-arriving split continues, with the full sum
+    // (the flag borrows the drained ring's first word: no extra LDS, which would
+    // cost the 32 KB / 80 KB tiles a workgroup slot per CU)
+    if (!splitk_fixup<MT, NT, 256>(args, acc, t, split, reinterpret_cast<int*>(smem))) return;
+  }
   if (args.act == ACT_PROBE_NO_EPILOGUE || args.act == ACT_PROBE_NO_A) {  // profiling probes: main loop only
     float sum = 0.f;
 #pragma unroll
@@ -266,6 +274,41 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
   gemm_epilogue_ln<BM, BN, WM, WN, false, EP, 256, true, ATTN>(args, acc, smem, m0, n0, split, lnrow, lnlane, lnl);
 }
 
+// Counters of the in-kernel split-K fixup (one per output tile, zero between
+// launches: the tile's last workgroup re-zeroes its own).  Launches on one
+// stream never overlap, so every eager launch on a stream shares that stream's
+// block; a launch captured into a hipGraph may replay beside other streams'
+// work, so each captured launch gets counters of its own, bump-allocated from a
+// ring that wraps only after 2^24 tiles (~2,000 UNet-step captures: two graph
+// replays would have to run concurrently across that distance to collide).
+static constexpr int FX_STREAM_CNT = 1 << 16;     // tiles per launch (M x N <= 2^28 outputs at 64x64)
+static constexpr int FX_GRAPH_CNT = 1 << 24;      // 64 MB of counters for captured launches
+static unsigned* g_fx_graph = nullptr;
+static long long g_fx_graph_used = 0;
+static std::mutex g_fx_mu;
+static std::unordered_map<hipStream_t, unsigned*> g_fx_stream;
+
+static unsigned* fixup_counters(hipStream_t s, int tiles) {
+  if (tiles > FX_STREAM_CNT) return nullptr;
+  std::lock_guard<std::mutex> lk(g_fx_mu);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) return nullptr;
+  if (st != hipStreamCaptureStatusNone) {
+    if (!g_fx_graph) return nullptr;
+    if (g_fx_graph_used + tiles > FX_GRAPH_CNT) g_fx_graph_used = 0;
+    unsigned* p = g_fx_graph + g_fx_graph_used;
+    g_fx_graph_used += (tiles + 63) / 64 * 64;
+    return p;
+  }
+  auto it = g_fx_stream.find(s);
+  if (it != g_fx_stream.end()) return it->second;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, FX_STREAM_CNT * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, FX_STREAM_CNT * sizeof(unsigned)) != hipSuccess) return nullptr;
+  g_fx_stream[s] = p;
+  return p;
+}
+
 template <int BM, int BN, int WM, int WN, int S>
 static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s) {
   GemmArgs a = a0;
@@ -274,6 +317,12 @@ static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s)
   // FAST staging: K-steps never straddle a tap / the K tail, and every running
   // offset stays inside the zero page
   const int span = ksplit > 1 ? a.kchunk : a.K;
+  if (a.fx_ws) {  // in-kernel split-K fixup: a zeroed counter per output tile
+    a.fx_cnt = fixup_counters(s, tiles);
+    if (!a.fx_cnt) return (int)hipErrorOutOfMemory;
+    a.fx_split = ksplit;
+    a.ws = nullptr;
+  }
   const bool fast = (conv ? (a.Cin % BK == 0) : (a.K % BK == 0)) && a.K % BK == 0 &&
                     (size_t)(span + 2 * BK) * sizeof(bf16_t) <= ZERO_BYTES &&
                     (!conv || (size_t)(a.Cin + BK) * sizeof(bf16_t) <= ZERO_BYTES);
@@ -308,6 +357,10 @@ CSK_API int csk_init() {
   hipError_t e = hipMalloc(&g_zero, ZERO_BYTES);
   if (e != hipSuccess) return (int)e;
   e = hipMemset(g_zero, 0, ZERO_BYTES);
+  if (e != hipSuccess) return (int)e;
+  e = hipMalloc(&g_fx_graph, (size_t)FX_GRAPH_CNT * sizeof(unsigned));
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(g_fx_graph, 0, (size_t)FX_GRAPH_CNT * sizeof(unsigned));
   if (e != hipSuccess) return (int)e;
   e = (hipError_t)csk_attn_fa_init();
   if (e != hipSuccess) return (int)e;

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--missing", action="store_true", help="only keys the table has no entry for (new shapes)")
     ap.add_argument("--all-tiles", action="store_true", help="every candidate, not the shortlist")
     ap.add_argument("--only-tiles", default="", help="comma list: try only these tiles (e.g. a new kernel)")
+    ap.add_argument("--fixup", action="store_true",
+                    help="only in-kernel split-K fixup candidates (split < 0) near each key's current entry")
     ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG doubles the images: 8 = 4 images, 2 = 1)")
     ap.add_argument("--latent", type=int, default=64, help="latent side (64 = 512 px)")
     ap.add_argument("--model", default="sd21", choices=("sd21", "sdxl"),
@@ -127,6 +129,10 @@ def main():
         only = {int(v) for v in a.only_tiles.split(",") if v}
         cands = [c for c in tuning.candidates(M, N, K) if (a.all_tiles or c[0] in SHORTLIST) and c != tuple(cur)
                  and (not only or c[0] in only)]
+        if a.fixup:  # the current tile with every fixup split, and the current split's fixup on the 64-wide tiles
+            cs = abs(int(cur[1]))
+            cands = [c for c in cands if c[1] < 0 and (c[0] == int(cur[0]) or (cs > 1 and c[1] == -cs
+                                                                                 and c[0] in (14, 18, 12)))]
         best_c, best_t = None, base
         for c in cands:
             if time.time() - t_start > a.budget:

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from chiaswarm_amd import ops  # noqa: E402
-from chiaswarm_amd.ops import _lib  # noqa: E402
+from chiaswarm_amd.ops import _lib, hip_ops  # noqa: E402
 from chiaswarm_amd.ops.hip_ops import _p, _s  # noqa: E402
 
 CONVS = ["8,64,64,320,320", "8,64,64,640,320", "8,64,64,960,320", "8,32,32,640,640", "8,32,32,1280,640",
@@ -67,7 +67,7 @@ def main():
                         gpart=gpart, up=up, Ho=Ho, Wo=Wo):
                     if sw is not None:
                         _lib.call("csk_set_sw_odd", sw)
-                    ws = torch.empty(split * B * Ho * Wo * Cout, dtype=torch.float32, device=dev) if split > 1 else None
+                    ws = hip_ops._ws(split, B * Ho * Wo, Cout, dev)
                     _lib.call("csk_conv2d", _p(y), _p(x), _p(wp), None, None, None, B, H, W, Cin, Cout, 3, 3, 1, 1, 1,
                               Ho, Wo, up, Cin, Cout, 0, act, 1.0, 1, _p(gpart) if gn else None, tile, split, _p(ws),
                               _s())
@@ -92,7 +92,7 @@ def main():
             for probe, res in variants:
                 def run(tile, split, x=x, w=w, y=y, yfull=yfull, M=M, N=N, K=K, no=no, geglu=geglu, probe=probe, res=res,
                         r=r):
-                    ws = torch.empty(split * M * N, dtype=torch.float32, device=dev) if split > 1 else None
+                    ws = hip_ops._ws(split, M, N, dev)
                     # a probe is not a GEGLU epilogue: full-width output buffer and row stride
                     out, ldo = (yfull, N) if probe else (y, no)
                     _lib.call("csk_gemm", _p(out), _p(x), _p(w), None, None, _p(r) if (res and not probe) else None, M,
