@@ -221,7 +221,7 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
     if tile == 44 and (ln is not None or row_stats or gn_rows or code == 3):
         tile = 14  # the sliced-K tile has none of these epilogues (gemm_slk.hip): 64x64 one-tile kernel
-    if split < 0 and not (11 <= tile <= 29 or tile == 36):
+    if split < 0 and tile not in tuning.GLDS:
         split = 1  # the in-kernel fixup exists in the LDS-DMA tiles only
     if ln is not None or row_stats:
         if split > 1:  # the split-K reduce has no LN / row-statistics epilogue

@@ -41,6 +41,7 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          40: (64, 128), 41: (128, 64), 42: (64, 64), 43: (64, 64),
          # sliced-K (gemm_slk.hip): the 8 waves of a 64x64 tile split its K-steps (small-M grids)
          44: (64, 64)}
+GLDS = frozenset(range(11, 30)) | {36}  # gemm_glds.hip tiles (in-kernel split-K fixup)
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
 # cannot exceed that band (hip_ops._gn_seg mirrors gemm_common.h gn_seg_for)
@@ -118,7 +119,7 @@ def candidates(M, N, K):
             if split == 16 and ntiles > 64:
                 continue
             out.append((tile, split))
-            if split > 1 and (11 <= tile <= 29 or tile == 36):
+            if split > 1 and tile in GLDS:
                 out.append((tile, -split))  # the same split with the in-kernel fixup (no reduce launch)
     return out
 

@@ -472,6 +472,9 @@ CSK_API int csk_set_gn_lds(int v) {
 
 int csk_gemm_slk_launch(const GemmArgs& a, bool conv, hipStream_t s);  // gemm_slk.hip
 
+// the LDS-DMA tiles of gemm_glds.hip (csk_gemm_glds_launch)
+static inline bool glds_tile(int t) { return (t >= 11 && t <= 29) || t == 36; }
+
 template <bool CONV>
 static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.zero = csk_zero_ptr();
@@ -482,14 +485,14 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   // any other kernel would run them as a plain full-width epilogue — into a
   // caller's GEGLU-sized (N/2) output that is an out-of-bounds write
   if ((a.act == ACT_PROBE_NO_EPILOGUE || a.act == ACT_PROBE_NO_STORE || a.act == ACT_PROBE_NO_A) &&
-      !((tile >= 11 && tile <= 29) || tile == 36))
+      !glds_tile(tile))
     return (int)hipErrorInvalidValue;
   // ksplit < 0: split -ksplit ways with the in-kernel fixup (LDS-DMA tiles only:
   // the last split of each tile runs the full epilogue, so GEGLU / LN / row and
   // GN statistics work as unsplit; the host sizes GN segments for the tile)
   const bool fixup = ksplit < 0;
   if (fixup) {
-    if (!((tile >= 11 && tile <= 29) || tile == 36) || !a.ws || a.attn_kv) return (int)hipErrorInvalidValue;
+    if (!glds_tile(tile) || !a.ws || a.attn_kv) return (int)hipErrorInvalidValue;
     ksplit = -ksplit;
   }
   if (ksplit > 1 && a.act == ACT_GEGLU && !fixup) ksplit = 1;
@@ -629,7 +632,7 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = ((tile >= 11 && tile <= 29) || tile == 36 || (tile >= 40 && tile <= 44)) &&
+  const bool in_kernel = (glds_tile(tile) || (tile >= 40 && tile <= 44)) &&
                          g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;

@@ -33,6 +33,7 @@ __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+
 // waves per SIMD the register budget must allow: the 128x160 tile runs two
 // workgroups per CU (its 74 KB ring), so <= 256 registers per lane; 64x160 too
 // (unconstrained it took 271 and one workgroup per CU)
@@ -41,7 +42,7 @@ constexpr int glds_min_waves() {
   return (BN == 160 && BM <= 128) ? 2 : 1;
 }
 
-template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST, bool ATTN = false>
+template <int BM, int BN, int WM, int WN, int S, bool CONV, bool FAST, bool ATTN = false, bool FX = false>
 __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_kernel(const GemmArgs args) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int split = blockIdx.y;
   const int kbeg = split * args.kchunk;
-  const int kend = (args.ws || args.fx_cnt) ? min(K, kbeg + args.kchunk) : K;
+  const int kend = (args.ws || FX) ? min(K, kbeg + args.kchunk) : K;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   const int lrow = lane >> 3;                 // row within the 8-row DMA group
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(256, (glds_min_waves<BM, BN>())) void gemm_glds_ker
     }
   }
   __syncthreads();
-  if (args.fx_cnt) {  // in-kernel split-K: only the tile's last-arriving split continues, with the full sum
+  if constexpr (FX) {  // in-kernel split-K: only the tile's last-arriving split continues, with the full sum
     // (the flag borrows the drained ring's first word: no extra LDS, which would
     // cost the 32 KB / 80 KB tiles a workgroup slot per CU)
     if (!splitk_fixup<MT, NT, 256>(args, acc, t, split, reinterpret_cast<int*>(smem))) return;
@@ -336,6 +337,12 @@ static int launch_glds(const GemmArgs& a0, int ksplit, bool conv, hipStream_t s)
       return (int)hipErrorInvalidValue;
     }
   }
+  if (a.fx_cnt) {  // a separate instance: the unsplit kernels keep their code (measured 1 % of the step)
+    if (!fast) return (int)hipErrorInvalidValue;
+    if (conv) gemm_glds_kernel<BM, BN, WM, WN, S, true, true, false, true><<<grid, 256, 0, s>>>(a);
+    else gemm_glds_kernel<BM, BN, WM, WN, S, false, true, false, true><<<grid, 256, 0, s>>>(a);
+    return (int)hipGetLastError();
+  }
   if (conv) {
     if (fast) gemm_glds_kernel<BM, BN, WM, WN, S, true, true><<<grid, 256, 0, s>>>(a);
     else gemm_glds_kernel<BM, BN, WM, WN, S, true, false><<<grid, 256, 0, s>>>(a);
@@ -408,6 +415,8 @@ int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hi
     // Its 3-stage sibling (one workgroup per CU: exactly 256 tiles at M2048 N1280)
     // was slower than 64x64 there (19.7 vs 14.8 us, profiles/tilebench_64x160_r6m.txt)
     case 36: return launch_glds<64, 160, 2, 2, 2>(a, ksplit, conv, s);
+    // (deep rings, S = 5..8 at 64x64 / 128x64 / 64x128, were measured and dropped:
+    // never faster in the step or in graph-timed isolation, profiles/tilebench_graph_deep_r5.txt)
     default: return (int)hipErrorInvalidValue;
   }
 }

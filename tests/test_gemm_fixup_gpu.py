@@ -42,7 +42,7 @@ class _Force:
 
 
 @pytest.mark.parametrize("tile", [14, 18, 11, 12, 26, 36])
-@pytest.mark.parametrize("split", [-2, -4, -8])
+@pytest.mark.parametrize("split", [1, -2, -4, -8])
 @pytest.mark.parametrize("M,N,K", [(128, 1280, 1280), (512, 640, 5120), (130, 200, 1024)])
 def test_fixup_matches_fp32(gpu, tile, split, M, N, K):
     torch.manual_seed(M + N + K + tile - split)

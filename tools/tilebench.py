@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--only", default="", help="conv|gemm")
     ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
     ap.add_argument("--res", action="store_true", help="GEMMs also with a residual input (epilogue load)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time hipGraph replays of --iters launches (no host launch cost: small kernels)")
     ap.add_argument("--gemms", default="", help="';'-separated 'M,N,K' list overriding the GEMM shapes")
     ap.add_argument("--convs", default="", help="';'-separated 'B,H,W,Cin,Cout' list overriding the conv shapes")
     ap.add_argument("--gn", action="store_true", help="convs also emitting fused GroupNorm statistics (64-row segments)")
@@ -110,11 +112,28 @@ def main():
             except Exception as e:  # noqa: BLE001
                 print(f"  {name}: tile {t} split {s} unsupported ({str(e)[:60]})", flush=True)
         torch.cuda.synchronize()
+        graphs = {}
+        if a.graph:
+            for t, s in arms:
+                st = torch.cuda.Stream()
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    run(t, s)
+                torch.cuda.current_stream().wait_stream(st)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(a.iters):
+                        run(t, s)
+                graphs[(t, s)] = g
+            torch.cuda.synchronize()
         for _ in range(a.rounds):
             for t, s in arms:
                 ev[0].record()
-                for _ in range(a.iters):
-                    run(t, s)
+                if a.graph:
+                    graphs[(t, s)].replay()
+                else:
+                    for _ in range(a.iters):
+                        run(t, s)
                 ev[1].record()
                 ev[1].synchronize()
                 res.setdefault((t, s), []).append(ev[0].elapsed_time(ev[1]) * 1e3 / a.iters)
