@@ -242,3 +242,31 @@ def recv_images(src: int):
     if hdr[0] < 0:
         return None, False
     return recv_tensor(tuple(hdr[:4]), torch.uint8, src, dev), bool(hdr[4])
+
+
+# -- CFG-parallel (runtime/worker.py: a one-image CFG job on two idle GPUs; each
+#    rank evaluates one CFG half of the UNet batch and they swap predictions)
+def cfg_handshake(peer: int, ok: bool = True) -> bool:
+    """Both parts of a CFG-parallel job exchange a ready flag before the first
+    step; a part that failed before its denoise loop sends ``ok=False``
+    (pipelines.diffusion._split_failed) so its peer raises instead of waiting
+    on predictions that never come.  Returns the peer's flag."""
+    dev = group_device()
+    mine = torch.tensor([1 if ok else -1], dtype=torch.int64, device=dev)
+    other = torch.empty_like(mine)
+    for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, mine, peer), dist.P2POp(dist.irecv, other, peer)]):
+        r.wait()
+    return int(other.item()) > 0
+
+
+def exchange_cfg_half(e: torch.Tensor, peer: int, half: int) -> torch.Tensor:
+    """This rank's noise prediction for its CFG half <-> the peer's (one
+    send + one receive, posted together): returns [uncond; cond] on e's device.
+    SD 512 px batch 1: 32 KB per step over xGMI."""
+    dev = group_device()
+    mine = e.contiguous() if e.device == dev else e.to(dev).contiguous()
+    other = torch.empty_like(mine)
+    for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, mine, peer), dist.P2POp(dist.irecv, other, peer)]):
+        r.wait()
+    full = torch.cat((mine, other) if half == 0 else (other, mine), 0)
+    return full if full.device == e.device else full.to(e.device)

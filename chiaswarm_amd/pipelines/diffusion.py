@@ -144,14 +144,16 @@ def _apply_textual_inversion(pipe, ti, model_name):
 
 
 def diffusion_callback(device_identifier, model_name, **kwargs):
-    split = kwargs.pop("_split", None)  # {"role": "leader", "peers": [rank, ...]} | {"role": "helper", "leader": r}
+    # {"role": "leader", "peers": [rank, ...]} | {"role": "helper", "leader": r} (image split) |
+    # {"role": "cfg", "peer": r, "half": 0 | 1} (CFG-parallel: half 1 returns only an ack)
+    split = kwargs.pop("_split", None)
     state = {"transferred": False}
     try:
         return _diffusion(device_identifier, model_name, split, state, **kwargs)
     except BaseException:
         # ANY failure of a split part (load, adapters, scheduler, arguments, the
         # pipeline) before its transfer started: release the peers blocked on it
-        if not state["transferred"]:
+        if not state["transferred"] and not state.get("cfg", {}).get("started"):
             _split_failed(split)
         raise
 
@@ -209,7 +211,15 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
         sched = get_scheduler(scheduler_type, **pipe.family.scheduler_kwargs())
         load_s = time.perf_counter() - t0
         helper = split is not None and split.get("role") == "helper"
-        p = pipe(scheduler=sched, **dict(kwargs, output_type="uint8_device" if helper else "pil"))
+        cfg_part = split is not None and split.get("role") == "cfg"
+        if cfg_part:
+            if kwargs.get("image") is not None or int(kwargs.get("num_images_per_prompt", 1) or 1) != 1:
+                raise ValueError("CFG-parallel parts are one-image txt2img jobs")
+            # the pipeline marks "started" after its handshake: a failure after that
+            # must not send a second handshake into the peer's prediction exchange
+            kwargs["cfg_split"] = state["cfg"] = {"peer": int(split["peer"]), "half": int(split["half"])}
+        out_type = "uint8_device" if helper else ("latent" if cfg_part and int(split["half"]) == 1 else "pil")
+        p = pipe(scheduler=sched, **dict(kwargs, output_type=out_type))
     finally:
         from ..models.lora import unload_lora, unload_textual_inversion
 
@@ -225,6 +235,10 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
         config["nsfw"] = True
 
     images = p.images
+    if cfg_part and int(split["half"]) == 1:  # the peer (half 0) decodes and answers the job
+        return {}, {"_split_ack": 1}
+    if cfg_part:
+        config["cfg_parallel"] = 2
     if helper:  # a split part: uint8 images straight to the leader's GPU over the process group
         from ..parallel import comm
 
@@ -316,7 +330,9 @@ def _split_failed(split):
     from ..parallel import comm
 
     try:
-        if split.get("role") == "helper":
+        if split.get("role") == "cfg":
+            comm.cfg_handshake(int(split["peer"]), ok=False)
+        elif split.get("role") == "helper":
             comm.send_images(None, int(split["leader"]))
         else:
             for r in split.get("peers", []):

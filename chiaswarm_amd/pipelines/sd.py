@@ -308,10 +308,11 @@ class StableDiffusion:
             torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------
-    def _unet_eval(self, x_in, t, cross_kv, added, cc=None, dup=False):
+    def _unet_eval(self, x_in, t, cross_kv, added, cc=None, dup=False, tag=None):
         """One denoiser evaluation.  ``cc``: a ControlNet request context — on
         the graph path the ControlNet encoder copy, its zero convs (fused with
-        the skip adds) and the UNet are ONE captured hipGraph."""
+        the skip adds) and the UNet are ONE captured hipGraph.  ``tag``: part of
+        the graph key (a CFG-parallel half binds different static K/V rows)."""
         share = bool(getattr(self, "_kv_static", False))
         if (not self.use_graphs or ops.get_mode() != "hip" or not ops._lib.available()
                 or self.device.type != "cuda"):
@@ -320,7 +321,7 @@ class StableDiffusion:
             return self.unet(x_in, tt, cross_kv=cross_kv, added_cond=added, control=control,
                              cfg_dup=dup and cc is None)
         key = (x_in.shape, added is not None, len(cross_kv), share, dup,
-               None if cc is None else (id(cc.model), cc.scale, tuple(cc.cond_emb.shape)))
+               None if cc is None else (id(cc.model), cc.scale, tuple(cc.cond_emb.shape)), tag)
         g = self._graphs.get(key)
         if g is None:
             g = (_UNetGraph(self.unet, x_in, cross_kv, added, share_kv=share, cfg_dup=dup) if cc is None else
@@ -331,18 +332,30 @@ class StableDiffusion:
     @torch.no_grad()
     def denoise(self, latents, sched: Scheduler, cross_kv, guidance, added=None, generator=None,
                 image_latents=None, image_guidance=None, mask=None, masked_latents=None,
-                init_latents=None, noise=None, control=None):
+                init_latents=None, noise=None, control=None, cfg_split=None):
         """Sampler loop on NHWC fp32 latents.
 
         * guidance > 1 -> CFG batch [uncond, cond] (pix2pix: [cond, uncond-img, uncond]);
         * ``image_latents`` concatenated on channels (pix2pix / inpaint-9ch);
-        * ``mask``/``init_latents`` -> legacy (4-channel) inpaint blending.
+        * ``mask``/``init_latents`` -> legacy (4-channel) inpaint blending;
+        * ``cfg_split`` = {"peer": rank, "half": 0 | 1}: CFG-parallel, this rank
+          evaluates one CFG half and swaps predictions with its peer each step.
         """
         b = latents.shape[0]
         cfg = guidance > 1.0
         three_way = image_guidance is not None
         nrep = 3 if three_way else (2 if cfg else 1)
         x = latents
+        if cfg_split is not None:
+            from ..parallel import comm
+
+            ok = comm.cfg_handshake(int(cfg_split["peer"]))
+            cfg_split["started"] = True
+            if not ok:
+                raise RuntimeError("CFG-parallel: the peer part failed before its denoise loop")
+            if nrep == 2 and image_latents is None and mask is None and control is None:
+                return self._denoise_cfg_split(x, sched, cross_kv, guidance, added, generator, cfg_split)
+            # (not splittable: both parts run the whole CFG batch, identical results)
         if mask is None and self._loop_ok():
             table = sched.loop_table()
             if table is not None and len(table[0]) > 0:
@@ -379,6 +392,31 @@ class StableDiffusion:
                 i = min(sched.step_index, sched.n - 1)
                 known = init_latents if sched.step_index >= sched.n else sched.add_noise(init_latents, noise, i)
                 x = known * (1 - mask) + x * mask
+        return x
+
+    def _denoise_cfg_split(self, x, sched, cross_kv, guidance, added, generator, split):
+        """CFG-parallel sampler loop: rank ``half`` runs the UNet on its rows
+        of the CFG batch (0: uncond, 1: cond) at batch b, the two predictions are
+        swapped over the process group (comm.exchange_cfg_half), and both parts
+        apply the identical guidance + scheduler update, so their latents stay
+        bit-identical without further traffic.  SURVEY §2.6 "CFG-parallel"."""
+        from ..parallel import comm
+
+        peer, h = int(split["peer"]), int(split["half"])
+        b = x.shape[0]
+        kv = [t[h * b:(h + 1) * b] for t in cross_kv]
+        add_h = {k: v[h * b:(h + 1) * b] for k, v in added.items()} if added is not None else None
+        while sched.step_index < sched.n:
+            t = sched.current_t()
+            xi = (x * sched.current_scale()).to(self.dtype)
+            e = comm.exchange_cfg_half(self._unet_eval(xi, t, kv, add_h, tag=("cfg", h)), peer, h)
+            coeffs = sched.fused_coeffs()
+            if coeffs is not None and ops.use_hip(x):
+                nz = batch_randn(x.shape, generator, x.device) if coeffs.D != 0.0 else None
+                x = ops.sched_step(e, x, sched, coeffs, guidance, nz)
+            else:
+                e_u, e_c = e.float().chunk(2)
+                x = sched.step(e_u + guidance * (e_c - e_u), x, generator)
         return x
 
     def _loop_ok(self) -> bool:
@@ -463,7 +501,8 @@ class StableDiffusion:
     def __call__(self, prompt="", negative_prompt=None, num_inference_steps=30, guidance_scale=7.5,
                  num_images_per_prompt=1, height=None, width=None, generator=None, image=None,
                  mask_image=None, strength=0.8, image_guidance_scale=None, scheduler=None,
-                 controlnet_conditioning_scale=1.0, output_type="pil", latents=None, eta=0.0, **unexpected):
+                 controlnet_conditioning_scale=1.0, output_type="pil", latents=None, eta=0.0, cfg_split=None,
+                 **unexpected):
         aesthetic = (float(unexpected.pop("aesthetic_score", 6.0)),
                      float(unexpected.pop("negative_aesthetic_score", 2.5))) if self.family.aesthetics else None
         if unexpected:  # the diffusers call raises on unknown kwargs too (a retryable job error)
@@ -579,7 +618,8 @@ class StableDiffusion:
         with trace_range("denoise"):
             x = self.denoise(x, sched, cross_kv, guidance_scale, added, generator,
                              image_latents=image_latents, image_guidance=img_guid,
-                             mask=mask_t, init_latents=init_latents, noise=noise, control=control)
+                             mask=mask_t, init_latents=init_latents, noise=noise, control=control,
+                             cfg_split=cfg_split)
             self._phase_sync()
         timings["denoise"] = time.perf_counter() - t1
         if output_type == "latent":

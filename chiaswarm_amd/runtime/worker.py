@@ -281,6 +281,19 @@ def splittable(job) -> int:
     return n if n >= 2 else 0
 
 
+def cfg_splittable(job) -> bool:
+    """A one-image CFG txt2img job whose two CFG halves may run on two idle
+    GPUs (CFG-parallel, SURVEY §2.6: lower latency for the common batch-1 job)."""
+    if _raw_key(job) is None or not str(job.get("content_type", "image/jpeg")).startswith("image/"):
+        return False
+    if int(job.get("num_images_per_prompt", 1) or 1) != 1:
+        return False
+    p = job.get("parameters") or {}
+    if "pix2pix" in str(p.get("pipeline_type", "")).lower():
+        return False
+    return float(job.get("guidance_scale", 7.5) or 0.0) > 1.0
+
+
 def _ranges(n, k):
     q, r = divmod(n, k)
     out, lo = [], 0
@@ -347,6 +360,7 @@ class Supervisor:
         self.busy = 0
         self.results_submitted = 0
         self.splits = 0
+        self.cfg_splits = 0  # one-image jobs run CFG-parallel on two GPUs
         self.stop = asyncio.Event()
         self.locks = {id(ex): asyncio.Lock() for ex in self.executors}
         # executors whose device_worker is parked on the work queue: only these
@@ -413,8 +427,11 @@ class Supervisor:
         if not getattr(self.settings, "split_jobs", True) or len(self.executors) < 2:
             return []
         n = splittable(job)
-        if n < 2:
-            return []
+        if n < 2:  # one image: its two CFG halves on two GPUs (needs the process group)
+            if not (getattr(self.settings, "cfg_parallel", True) and cfg_splittable(job) and self.group_ok()
+                    and hasattr(ex, "kill")):
+                return []
+            n = 2
         helpers = []
         for other in self.executors:
             if len(helpers) + 1 >= n:
@@ -436,6 +453,8 @@ class Supervisor:
         seed = job.get("seed")
         if seed is None:
             seed = random.SystemRandom().randrange(0, 2 ** 63 - 1)
+        if n < 2:  # claimed for CFG-parallel (_claim_helpers)
+            return await self._run_cfg_split(job, exs[:2], seed)
         if self.group_ok() and all(hasattr(e, "kill") for e in exs):
             return await self._run_split_group(job, exs, n, seed)
         subs = []
@@ -482,8 +501,6 @@ class Supervisor:
         CPU children), then encodes the one envelope itself.  A part whose child
         dies leaves its peers blocked in a transfer, so the other parts' children
         are killed too (each restarts; the group re-forms when idle)."""
-        from .generator import _error_result
-
         jid = job.get("id")
         rngs = _ranges(n, len(exs))
         ranks = [e.group["rank"] for e in exs]
@@ -493,6 +510,28 @@ class Supervisor:
             lo, hi = rngs[i]
             subs.append(dict(job, id=f"{jid}#{i}", seed=seed, num_images_per_prompt=hi - lo, _image_range=[lo, hi],
                              _split={"role": "helper", "leader": ranks[0]}))
+        return await self._await_parts(job, exs, subs, seed)
+
+    async def _run_cfg_split(self, job, exs, seed) -> dict:
+        """CFG-parallel: both parts run the whole job with the same seed; part 0
+        evaluates the unconditional half of every UNet step, part 1 the
+        conditional half, and they swap predictions each step over the process
+        group (pipelines.sd._denoise_cfg_split).  Part 0 decodes and answers."""
+        jid = job.get("id")
+        r0, r1 = (e.group["rank"] for e in exs)
+        subs = [dict(job, id=jid, seed=seed, _split={"role": "cfg", "peer": r1, "half": 0}),
+                dict(job, id=f"{jid}#cfg", seed=seed, _split={"role": "cfg", "peer": r0, "half": 1})]
+        out = await self._await_parts(job, exs, subs, seed)
+        if out.get("artifacts"):
+            self.cfg_splits += 1
+        return out
+
+    async def _await_parts(self, job, exs, subs, seed) -> dict:
+        """Run the parts of a group split; the first part answers the job, the
+        others must return a ``_split_ack``."""
+        from .generator import _error_result
+
+        jid = job.get("id")
         restarts0 = [e.restarts for e in exs]
         tasks = [asyncio.ensure_future(e.run(sj)) for e, sj in zip(exs, subs)]
         pending = set(tasks)

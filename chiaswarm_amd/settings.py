@@ -28,10 +28,12 @@ class Settings:
     preload: str = ""           # comma list of models every GPU loads at startup (sharded RCCL read)
     distributed: bool = True    # per-GPU processes form one process group (RCCL over xGMI)
     split_jobs: bool = True     # a multi-image txt2img job may use several idle GPUs
+    cfg_parallel: bool = True   # a one-image CFG txt2img job may run its two CFG halves on two idle GPUs
 
     def __init__(self):
         for k in ("huggingface_token", "log_level", "log_filename", "sdaas_token", "sdaas_uri", "worker_name",
-                  "gpus", "max_batch", "cache_gb", "model_dir", "preload", "distributed", "split_jobs"):
+                  "gpus", "max_batch", "cache_gb", "model_dir", "preload", "distributed", "split_jobs",
+                  "cfg_parallel"):
             setattr(self, k, getattr(type(self), k))
 
 
@@ -57,6 +59,7 @@ def load_settings() -> Settings:
     settings.preload = str(d.get("preload", ""))
     settings.distributed = bool(d.get("distributed", True))
     settings.split_jobs = bool(d.get("split_jobs", True))
+    settings.cfg_parallel = bool(d.get("cfg_parallel", True))
 
     settings.sdaas_token = os.getenv("SDAAS_TOKEN", settings.sdaas_token)
     settings.sdaas_uri = os.getenv("SDAAS_URI", settings.sdaas_uri)
@@ -68,6 +71,7 @@ def load_settings() -> Settings:
     settings.preload = os.getenv("SDAAS_PRELOAD", settings.preload)
     settings.distributed = os.getenv("SDAAS_DIST", "1" if settings.distributed else "0") != "0"
     settings.split_jobs = os.getenv("SDAAS_SPLIT_JOBS", "1" if settings.split_jobs else "0") != "0"
+    settings.cfg_parallel = os.getenv("SDAAS_CFG_PARALLEL", "1" if settings.cfg_parallel else "0") != "0"
     return settings
 
 
