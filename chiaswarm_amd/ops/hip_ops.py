@@ -107,6 +107,7 @@ sig("csk_debug_selftest", c_int, c_void_p)  # CSK_DEBUG builds: one deliberate r
 sig("csk_set_gn_lds", c_int)
 sig("csk_set_sw_odd", c_int)
 sig("csk_set_epi_band", c_int)
+sig("csk_set_epi_nt", c_int)
 sig("csk_set_skr_unroll", c_int)
 sig("csk_set_short_kv_variant", c_int)
 sig("csk_set_short_kv_rows", c_int)

@@ -460,6 +460,11 @@ CSK_API int csk_set_sw_odd(int v) {
   g_sw_odd = v;
   return 0;
 }
+int g_epi_nt = 0;  // tools/abstep.py arms nt0 / nt1 / nt2: non-temporal direct-epilogue stores (/ residual loads)
+CSK_API int csk_set_epi_nt(int v) {
+  g_epi_nt = v;
+  return 0;
+}
 int g_epi_band = 1;  // tools/abstep.py arms band0 / band1: LDS-staged epilogue band path off / on
 CSK_API int csk_set_epi_band(int v) {
   g_epi_band = v;
@@ -481,6 +486,7 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
   a.gn_lds = g_gn_lds;
   a.sw_odd = g_sw_odd;
   a.epi_band = g_epi_band;
+  a.epi_nt = g_epi_nt;
   // profiling probes (act 97-99) exist only in the LDS-DMA tiles (gemm_glds.hip);
   // any other kernel would run them as a plain full-width epilogue — into a
   // caller's GEGLU-sized (N/2) output that is an out-of-bounds write

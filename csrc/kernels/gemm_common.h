@@ -91,6 +91,7 @@ struct GemmArgs {
   int gn_lds;  // 1: GroupNorm statistics through the LDS epilogue even where the direct one can (A/B knob)
   int sw_odd;  // 1: row-layout tiles with an odd fragment count (160 wide) use the direct epilogue (A/B knob)
   int epi_band;  // 1: LDS-staged epilogue stores through the compile-time band path (A/B knob, default 1)
+  int epi_nt;    // 1: the direct epilogue's C stores (2: and residual loads) are non-temporal (A/B knob)
   // fused LayerNorm of the INPUT rows (SURVEY K11 folded into K9/K10): the
   // weight was pre-multiplied by gamma (W' = W diag(gamma)), the bias holds
   // b + W beta, and the epilogue applies
@@ -673,8 +674,15 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
           for (int i = 0; i < MT; ++i) {
             const int m = m0 + wm * WTM + i * 16 + fr;
             rpre[i] = make_uint4(0, 0, 0, 0);
-            if (ROOMY && args.res && col < outN && m < M)
-              rpre[i] = *reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + col);
+            if (ROOMY && args.res && col < outN && m < M) {
+              const uint4* rp = reinterpret_cast<const uint4*>(args.res + (size_t)m * args.ldr + col);
+              if (args.epi_nt >= 2) {
+                const fx_u4 v = __builtin_nontemporal_load(reinterpret_cast<const fx_u4*>(rp));
+                rpre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+              } else {
+                rpre[i] = *rp;
+              }
+            }
           }
           if (b2u && col < outN) b2pre = *reinterpret_cast<const uint4*>(args.bias2d + (size_t)(m0 / args.rows_per_b) * args.ldb2 + col);
           if (col < outN) {
@@ -731,7 +739,13 @@ __device__ __forceinline__ void gemm_epilogue_ln(const GemmArgs& args, v4f (&acc
                 gq[r] = __builtin_fmaf(o[r], o[r], gq[r]);
               }
             }
-            *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
+            if (args.epi_nt) {
+              const uint4 pv = pack8(o);
+              __builtin_nontemporal_store(fx_u4{pv.x, pv.y, pv.z, pv.w},
+                                          reinterpret_cast<fx_u4*>(args.C + (size_t)m * args.ldc + col));
+            } else {
+              *reinterpret_cast<uint4*>(args.C + (size_t)m * args.ldc + col) = pack8(o);
+            }
           }
           if (gnp) {
             // the 16 lanes of a 16-row group (fr) hold the same 8 columns

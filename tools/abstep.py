@@ -29,6 +29,9 @@ def apply_arm(arm):
         ops.SIDE_STREAM = arm == "side1"
     elif arm in ("swodd0", "swodd1"):  # 160-wide tiles: LDS (0) / direct row-layout (1) epilogue
         _lib.call("csk_set_sw_odd", int(arm == "swodd1"))
+    elif arm in ("nt0", "nt1", "nt2"):  # direct epilogue: plain / non-temporal C stores (/ + residual loads);
+        # measured: nt1 +0.23 ms, nt2 +0.30 ms per CFG-8 step (the consumer's reads miss the MALL), default 0
+        _lib.call("csk_set_epi_nt", int(arm[2:]))
     elif arm in ("band0", "band1"):  # LDS-staged epilogue: generic loop (0) / compile-time band path (1)
         _lib.call("csk_set_epi_band", int(arm == "band1"))
     elif arm in ("gnd0", "gnd1"):  # GN statistics in the direct (gnd0) / LDS (gnd1) epilogue

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--only", default="", help="conv|gemm")
     ap.add_argument("--probe", action="store_true", help="GEMMs also without their epilogue (act 99)")
     ap.add_argument("--res", action="store_true", help="GEMMs also with a residual input (epilogue load)")
+    ap.add_argument("--nt", type=int, default=0, help="csk_set_epi_nt for this run (non-temporal direct-epilogue stores)")
     ap.add_argument("--graph", action="store_true",
                     help="time hipGraph replays of --iters launches (no host launch cost: small kernels)")
     ap.add_argument("--gemms", default="", help="';'-separated 'M,N,K' list overriding the GEMM shapes")
@@ -43,6 +44,8 @@ def main():
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
+    _lib.load()
+    _lib.call("csk_set_epi_nt", a.nt)
     tiles = [int(t) for t in a.tiles.split(",")]
     splits = [int(s) for s in a.splits.split(",")]
     jobs = []
