@@ -120,6 +120,7 @@ sig("csk_set_attn_fa", c_int)
 sig("csk_set_gemm_sk_workers", c_int)
 sig("csk_gemm_sk_errors", c_void_p)
 sig("csk_gemm_slk_launches", c_void_p)
+sig("csk_gemm_pst_launches", c_void_p)
 sig("csk_attn_fa_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)

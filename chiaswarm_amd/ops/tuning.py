@@ -40,7 +40,9 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # stream-K (gemm_sk.hip): one persistent workgroup per CU, K-steps spread evenly, in-kernel fixup
          40: (64, 128), 41: (128, 64), 42: (64, 64), 43: (64, 64),
          # sliced-K (gemm_slk.hip): the 8 waves of a 64x64 tile split its K-steps (small-M grids)
-         44: (64, 64)}
+         44: (64, 64),
+         # persistent, ring across output tiles (gemm_pst.hip): short-K GEMMs whose epilogue overlaps the next tile's loads
+         50: (128, 64), 51: (64, 64), 52: (128, 128), 53: (64, 128)}
 GLDS = frozenset(range(11, 30)) | {36}  # gemm_glds.hip tiles (in-kernel split-K fixup)
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
@@ -112,11 +114,15 @@ def candidates(M, N, K):
             continue
         if tile == 44:  # sliced-K: A/B only (gemm_slk.hip MEASURED STANDING)
             continue
+        if tile >= 50 and K % 64:
+            continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)
             if split > 1 and (ntiles >= 512 or K // 64 < 4 * split):
                 continue
             if split == 16 and ntiles > 64:
+                continue
+            if tile >= 50 and split != 1:  # the persistent tiles do not split K
                 continue
             out.append((tile, split))
             if split > 1 and tile in GLDS:
