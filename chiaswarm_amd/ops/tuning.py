@@ -114,15 +114,13 @@ def candidates(M, N, K):
             continue
         if tile == 44:  # sliced-K: A/B only (gemm_slk.hip MEASURED STANDING)
             continue
-        if tile >= 50 and K % 64:
+        if tile >= 50:  # persistent tiles: A/B only (gemm_pst.hip MEASURED STANDING)
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)
             if split > 1 and (ntiles >= 512 or K // 64 < 4 * split):
                 continue
             if split == 16 and ntiles > 64:
-                continue
-            if tile >= 50 and split != 1:  # the persistent tiles do not split K
                 continue
             out.append((tile, split))
             if split > 1 and tile in GLDS:

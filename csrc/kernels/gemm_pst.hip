@@ -20,6 +20,15 @@
 // of gemm_common.h and must not touch LDS (the ring is live): the launcher
 // admits only shapes whose epilogue takes that path (no GN / LN / row
 // statistics, aligned vectors), others get hipErrorNotSupported.
+//
+// MEASURED STANDING (profiles/tilebench_graph_pst_r5.txt, graph-timed): slower
+// than the one-tile kernels everywhere — M32768 N320 K320 22.1 us (128x64,
+// 3 workgroups per CU) / 25.9 us (3-stage, 2 per CU) vs 19.2 us for tile 19;
+// M8192 N640 K640 20.1 vs 15.3 us.  The one-tile grid already overlaps one
+// workgroup's epilogue with the others' main loops (3-5 resident per CU) and
+// its dynamic dispatch balances better than the static tile walk, which also
+// drains the epilogue's stores at the next counted wait.  Kept for A/B; the
+// tuner does not propose tiles 50-53.
 #include "gemm_common.h"
 
 namespace {

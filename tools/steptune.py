@@ -39,7 +39,7 @@ import torch  # noqa: E402
 from chiaswarm_amd import ops  # noqa: E402
 from chiaswarm_amd.ops import _lib, tuning  # noqa: E402
 
-SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 33, 15, 27, 28, 29, 36, 50, 51, 52, 53)
+SHORTLIST = (11, 13, 14, 18, 19, 20, 26, 12, 17, 31, 32, 33, 15, 27, 28, 29, 36)
 
 
 def main():
