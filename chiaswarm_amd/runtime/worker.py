@@ -424,9 +424,11 @@ class Supervisor:
     async def _claim_helpers(self, job, ex) -> list:
         """Idle executors for a split, claimed synchronously: an executor in
         ``self.idle`` has no waiter on its lock, so ``acquire`` returns at once."""
-        if not getattr(self.settings, "split_jobs", True) or len(self.executors) < 2:
+        if len(self.executors) < 2:
             return []
         n = splittable(job)
+        if n >= 2 and not getattr(self.settings, "split_jobs", True):
+            return []
         if n < 2:  # one image: its two CFG halves on two GPUs (needs the process group)
             if not (getattr(self.settings, "cfg_parallel", True) and cfg_splittable(job) and self.group_ok()
                     and hasattr(ex, "kill")):
