@@ -342,9 +342,10 @@ def _pix_stride(t):
 # Persistent halo-tile conv for 3x3 / stride-1 / Cout = 32 (csrc/kernels/conv_tile.hip:
 # the Real-ESRGAN dense-block convs); CSK_CONV_TILE=0 keeps the implicit GEMM
 sig("csk_conv_tile_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
-sig("csk_conv_tile", c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_void_p)
+sig("csk_conv_tile", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_int, c_float, c_void_p)
 CONV_TILE = os.environ.get("CSK_CONV_TILE", "1") == "1"
+CONV_TILE64 = os.environ.get("CSK_CONV_TILE64", "0") == "1"  # the Cout = 64 instance (A/B)
 CONV_TILE_STATS = [0]  # calls (tests assert the kernel ran)
 
 
@@ -409,11 +410,14 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     if kh != kw or dilation != 1:
         key += f":{kw}:{dilation}"
     if (CONV_TILE and kh == 3 and kw == 3 and stride == 1 and (pt, pl, pb, pr) == (1, 1, 1, 1) and dilation == 1
-            and not up2x and residual is None and bias2d is None and out_scale == 1.0 and not gn_stats
-            and code in (0, 2, 5, 6, 8, 9) and _lib.call_int("csk_conv_tile_ok", B, H, W, Cin, Cout, xs, ys) > 0
+            and not up2x and bias2d is None and not gn_stats
+            and code in (0, 2, 5, 6, 8, 9) and (Cout == 32 or CONV_TILE64)
+            and (residual is None or (rs % 4 == 0 and residual.data_ptr() % 8 == 0))
+            and _lib.call_int("csk_conv_tile_ok", B, H, W, Cin, Cout, xs, ys) > 0
             and x.data_ptr() % 16 == 0 and out.data_ptr() % 8 == 0 and wp.data_ptr() % 16 == 0):
         # narrow-output 3x3 (the Real-ESRGAN dense-block convs): persistent halo-tile kernel
-        _lib.call("csk_conv_tile", _p(out), _p(x), _p(wp), _p(bias), B, H, W, Cin, xs, ys, code, _s())
+        _lib.call("csk_conv_tile", _p(out), _p(x), _p(wp), _p(bias), _p(residual), B, H, W, Cin, Cout, xs, ys, rs,
+                  code, float(out_scale), _s())
         CONV_TILE_STATS[0] += 1
         return out
     tile, split = tuning.choose(key, M, Cout, K, run)

@@ -1,4 +1,4 @@
-// Persistent halo-tile 3x3 convolution for narrow outputs (Cout = 32): the
+// Persistent halo-tile 3x3 convolution for narrow outputs (Cout = 32 / 64): the
 // Real-ESRGAN dense-block convs (north-star config #5; RRDBNet
 // conv1..conv4 of every residual dense block, 276 of the 345 convs of an x4
 // upscale).
@@ -41,18 +41,24 @@
 
 namespace {
 
-constexpr int CT_N = 32;                   // output channels
 constexpr int CT_TH = 8, CT_TW = 32;       // output tile
 constexpr int CT_HW = CT_TW + 2, CT_HH = CT_TH + 2;
 constexpr int CT_HPX = CT_HH * CT_HW;      // 340 halo pixels
 constexpr int CT_HSLOT = 384;              // halo pixel slots: 24 DMA instructions of 16 pixels
 constexpr int CT_HALO = CT_HSLOT * 64;     // bytes per stage ([pixel][4 x 16 B])
-constexpr int CT_WROWS = 384;              // 9 taps x 32 outputs = 288 rows, padded to 24 instructions
-constexpr int CT_WGT = CT_WROWS * 64;      // bytes per stage ([tap x cout][4 x 16 B])
-constexpr int CT_STAGE = CT_HALO + CT_WGT;
-constexpr int CT_S = 3;                    // ring stages (two chunks in flight)
 constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per chunk (3)
-constexpr int CT_WI = CT_WROWS / 16 / 8;   // weight DMA instructions per wave per chunk (3)
+
+// per output width NOUT (32 or 64): weight rows 9 x NOUT padded to whole
+// 8-wave x 16-row DMA rounds, ring depth (3 stages at 32: 144 KB; 2 at 64: 128 KB)
+template <int NOUT>
+struct CtGeo {
+  static constexpr int WROWS = (9 * NOUT + 127) / 128 * 128;  // 384 / 640
+  static constexpr int WGT = WROWS * 64;                      // bytes per stage ([tap x cout][4 x 16 B])
+  static constexpr int STAGE = CT_HALO + WGT;
+  static constexpr int S = NOUT == 32 ? 3 : 2;
+  static constexpr int WI = WROWS / 16 / 8;                   // weight DMA instructions per wave per chunk (3 / 5)
+  static constexpr int NF = NOUT / 16;                        // output fragments per pixel row
+};
 
 // 16-byte slot of channel group g (of 4) in LDS row r (a pixel or a (tap, cout)
 // row of 64 B): XOR-swizzled so the 16 lanes of an MFMA fragment (16
@@ -61,11 +67,13 @@ __device__ __forceinline__ int ct_slot(int r, int g) { return g ^ ((r >> 2) & 3)
 
 struct ConvTileArgs {
   const bf16_t* x;     // [B][H][W] pixels, pixel stride lda, channels [0, Cin)
-  const bf16_t* w;     // packed [32][3][3][Cin]
-  const bf16_t* bias;  // [32] or null
-  bf16_t* y;           // [B][H][W] pixels, pixel stride ldc, channels [0, 32)
+  const bf16_t* w;     // packed [NOUT][3][3][Cin]
+  const bf16_t* bias;  // [NOUT] or null
+  bf16_t* y;           // [B][H][W] pixels, pixel stride ldc, channels [0, NOUT)
   const bf16_t* zero;  // zero page (LDS-DMA source for padding)
-  int B, H, W, Cin, lda, ldc, act;
+  const bf16_t* res;   // [B][H][W] pixels, pixel stride ldr, or null: y = act(conv + bias) * out_scale + res
+  int B, H, W, Cin, lda, ldc, act, ldr;
+  float out_scale;
   int tiles_x, tiles_y, ntiles;
 };
 
@@ -83,7 +91,10 @@ __device__ __forceinline__ void ct_vmcnt() {
 
 }  // namespace
 
+template <int NOUT>
 __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
+  using Geo = CtGeo<NOUT>;
+  constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF;
   __shared__ __attribute__((aligned(16))) unsigned char smem[CT_S * CT_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,10 +112,10 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
   const bf16_t* wsrc[CT_WI];
 #pragma unroll
   for (int i = 0; i < CT_WI; ++i) {
-    const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * 32 + output channel
-    const int tap = row >> 5, co = row & 31;
+    const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * NOUT + output channel
+    const int tap = row / NOUT, co = row % NOUT;
     const int g = (lane & 3) ^ ((row >> 2) & 3);  // source channel group landing in this lane's slot
-    wsrc[i] = row < 9 * CT_N ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
+    wsrc[i] = row < 9 * NOUT ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
   }
   // ---- halo DMA: instruction k = wv * 3 + i writes halo pixels 16 k .. 16 k + 15 ----
   const bf16_t* hsrc[CT_HI];
@@ -139,17 +150,17 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     }
   };
 
-  v4f acc[2][2];
+  v4f acc[2][NF];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NF; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
-  float bias[2][4];
+  float bias[NF][4];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < NF; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[j][r] = a.bias ? bf2f(a.bias[j * 16 + fq * 4 + r]) : 0.f;
 
@@ -164,11 +175,19 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
       const int x = tx * CT_TW + i * 16 + fr;
       if (x >= W) continue;
       bf16_t* op = a.y + ((size_t)(b * H + y) * W + x) * a.ldc;
+      const bf16_t* rp = a.res ? a.res + ((size_t)(b * H + y) * W + x) * a.ldr : nullptr;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NF; ++j) {
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[i][j][r] + bias[j][r]);
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[i][j][r] + bias[j][r]) * a.out_scale;
+        if (rp) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(rp + j * 16 + fq * 4);
+          v[0] += __uint_as_float(rr.x << 16);
+          v[1] += __uint_as_float(rr.x & 0xffff0000u);
+          v[2] += __uint_as_float(rr.y << 16);
+          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+        }
         uint2 wd;
         wd.x = pack2(v[0], v[1]);
         wd.y = pack2(v[2], v[3]);
@@ -177,17 +196,18 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     }
   };
 
-  // ---- prologue: two units in flight ----
-  issue();
-  if (U > 1) issue();
+  // ---- prologue: S - 1 units in flight ----
+#pragma unroll
+  for (int k = 0; k < CT_S - 1; ++k)
+    if (k < U) issue();
   int c = 0, s = 0, tile = w;
   for (int u = 0; u < U; ++u) {
-    // unit u landed once at most one younger unit (CT_HI + CT_WI instructions) is in flight
-    if (u + 1 < U) ct_vmcnt<CT_HI + CT_WI>();
+    // unit u landed once at most S - 2 younger units (CT_HI + CT_WI instructions each) are in flight
+    if (CT_S == 3 && u + 1 < U) ct_vmcnt<CT_HI + CT_WI>();
     else ct_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (u + 2 < U) issue();
+    if (u + CT_S - 1 < U) issue();
     const unsigned char* hb = smem + s * CT_STAGE;
     const unsigned char* wb = hb + CT_HALO;
 #pragma unroll
@@ -195,21 +215,21 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const int tap = ky * 3 + kx;
-        v8s af[2], bfr[2];
+        v8s af[2], bfr[NF];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int hp = (wv + ky) * CT_HW + i * 16 + fr + kx;
           af[i] = *reinterpret_cast<const v8s*>(hb + hp * 64 + ct_slot(hp, fq) * 16);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int row = tap * CT_N + j * 16 + fr;
+        for (int j = 0; j < NF; ++j) {
+          const int row = tap * NOUT + j * 16 + fr;
           bfr[j] = *reinterpret_cast<const v8s*>(wb + row * 64 + ct_slot(row, fq) * 16);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NF; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     s = s + 1 == CT_S ? 0 : s + 1;
@@ -227,19 +247,23 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 // ---------------------------------------------------------------------------
 static int g_ct_cus = 0;
 
-// 1 when csk_conv_tile takes this conv: 3x3 / stride 1 / pad 1, Cout = 32,
-// Cin % 32 == 0 (<= 64 chunks), 16-byte aligned pixel strides
+// 1 when csk_conv_tile takes this conv: 3x3 / stride 1 / pad 1, Cout = 32 or
+// 64, Cin % 32 == 0 (<= 64 chunks), 16-byte aligned pixel strides
 CSK_API int csk_conv_tile_ok(int B, int H, int W, int Cin, int Cout, int lda, int ldc) {
-  return B > 0 && H > 0 && W > 0 && Cout == CT_N && Cin % 32 == 0 && Cin >= 32 && Cin <= 2048 && lda >= Cin &&
+  return B > 0 && H > 0 && W > 0 && (Cout == 32 || Cout == 64) && Cin % 32 == 0 && Cin >= 32 && Cin <= 2048 && lda >= Cin &&
          lda % 8 == 0 && ldc >= Cout && ldc % 4 == 0 && (long long)B * H * W * lda < (1ll << 31) &&
          (long long)B * H * W * ldc < (1ll << 31);
 }
 
-// y[..., :32] = act(conv3x3(x[..., :Cin]) + bias), NHWC with pixel strides lda / ldc
-CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bias, int B, int H, int W, int Cin,
-                          int lda, int ldc, int act, hipStream_t stream) {
-  if (!csk_conv_tile_ok(B, H, W, Cin, CT_N, lda, ldc) || !csk_zero_ptr()) return (int)hipErrorInvalidValue;
+// y[..., :Cout] = act(conv3x3(x[..., :Cin]) + bias) * out_scale (+ res[..., :Cout]), NHWC with
+// pixel strides lda / ldc / ldr (res may be null)
+CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bias, const void* res, int B, int H,
+                          int W, int Cin, int Cout, int lda, int ldc, int ldr, int act, float out_scale,
+                          hipStream_t stream) {
+  if (!csk_conv_tile_ok(B, H, W, Cin, Cout, lda, ldc) || !csk_zero_ptr()) return (int)hipErrorInvalidValue;
   if ((((size_t)x) & 15) || (((size_t)y) & 7) || (((size_t)wp) & 15)) return (int)hipErrorInvalidValue;
+  if (res && ((((size_t)res) & 7) || ldr < Cout || ldr % 4 || (long long)B * H * W * ldr >= (1ll << 31)))
+    return (int)hipErrorInvalidValue;
   if ((size_t)(Cin + 64) * sizeof(bf16_t) > (size_t)csk_zero_bytes()) return (int)hipErrorInvalidValue;
   if (!g_ct_cus) {
     int dev = 0, cus = 0;
@@ -253,11 +277,14 @@ CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bi
   a.bias = (const bf16_t*)bias;
   a.y = (bf16_t*)y;
   a.zero = csk_zero_ptr();
+  a.res = (const bf16_t*)res;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.lda = lda; a.ldc = ldc; a.act = act;
+  a.ldr = ldr; a.out_scale = out_scale;
   a.tiles_x = (W + CT_TW - 1) / CT_TW;
   a.tiles_y = (H + CT_TH - 1) / CT_TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
   const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
-  conv_tile_kernel<<<G, 512, 0, stream>>>(a);
+  if (Cout == 64) conv_tile_kernel<64><<<G, 512, 0, stream>>>(a);
+  else conv_tile_kernel<32><<<G, 512, 0, stream>>>(a);
   return (int)hipGetLastError();
 }

@@ -19,15 +19,17 @@ def rel_err(y, ref):
 @pytest.mark.parametrize("B,H,W", [(1, 64, 64), (1, 37, 50), (2, 16, 96), (1, 8, 32), (3, 9, 33)])
 @pytest.mark.parametrize("Cin", [32, 64, 96, 160])
 @pytest.mark.parametrize("act", [None, "lrelu"])
-def test_conv_tile_matches_fp32(gpu, B, H, W, Cin, act):
-    torch.manual_seed(B * 100 + H + W + Cin)
-    C = 192  # dense buffer: input = channels [0, Cin), output = channels [Cin, Cin + 32) when they fit
-    buf = (torch.randn(B, H, W, C + 32, device=gpu)).to(torch.bfloat16)
+@pytest.mark.parametrize("Cout", [32, 64])
+def test_conv_tile_matches_fp32(gpu, B, H, W, Cin, act, Cout, monkeypatch):
+    torch.manual_seed(B * 100 + H + W + Cin + Cout)
+    monkeypatch.setattr(hip_ops, "CONV_TILE64", True)
+    C = 192  # dense buffer: input = channels [0, Cin), output = channels [C, C + Cout)
+    buf = (torch.randn(B, H, W, C + Cout, device=gpu)).to(torch.bfloat16)
     x = buf[..., :Cin]
-    out = buf[..., C:C + 32]
-    w = (torch.randn(32, Cin, 3, 3, device=gpu) * (9 * Cin) ** -0.5).to(torch.bfloat16)
+    out = buf[..., C:C + Cout]
+    w = (torch.randn(Cout, Cin, 3, 3, device=gpu) * (9 * Cin) ** -0.5).to(torch.bfloat16)
     wp = ops.pack_conv_weight(w)
-    bias = torch.randn(32, device=gpu).to(torch.bfloat16)
+    bias = torch.randn(Cout, device=gpu).to(torch.bfloat16)
     keep = buf[..., :C].clone()
     before = hip_ops.CONV_TILE_STATS[0]
     y = ops.conv2d(x, wp, bias, act=act, out=out)
@@ -57,3 +59,29 @@ def test_conv_tile_rrdb_block_matches_gemm_path(gpu):
     finally:
         hip_ops.CONV_TILE = True
     assert rel_err(a.cpu(), b.cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("Cout", [32, 64])
+def test_conv_tile_residual_out_scale(gpu, Cout, monkeypatch):
+    """RRDB conv5: act-free conv * 0.2 + x (residual a channel slice of the dense buffer)."""
+    monkeypatch.setattr(hip_ops, "CONV_TILE64", True)
+    torch.manual_seed(Cout)
+    B, H, W, Cin = 1, 40, 70, 192
+    buf = torch.randn(B, H, W, Cin, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, device=gpu) * (9 * Cin) ** -0.5).to(torch.bfloat16)
+    wp = ops.pack_conv_weight(w)
+    bias = torch.randn(Cout, device=gpu).to(torch.bfloat16)
+    res = buf[..., :Cout]
+    out = torch.empty(B, H, W, Cout, device=gpu, dtype=torch.bfloat16)
+    before = hip_ops.CONV_TILE_STATS[0]
+    y = ops.conv2d(buf, wp, bias, residual=res, out_scale=0.2, out=out)
+    assert hip_ops.CONV_TILE_STATS[0] == before + 1
+    ref = ops._ref_conv2d(buf.float().cpu(), wp.float().cpu(), bias.float().cpu(), 1, 1, res.float().cpu(), False,
+                          None, None, 0.2)
+    assert rel_err(y.cpu(), ref) < 1e-2
+
+
+def test_conv_tile64_rrdb_block_matches_gemm_path(gpu, monkeypatch):
+    """A whole RRDB with the Cout = 64 instance (conv5 with its fused * 0.2 + x) == the implicit GEMM."""
+    monkeypatch.setattr(hip_ops, "CONV_TILE64", True)
+    test_conv_tile_rrdb_block_matches_gemm_path(gpu)

@@ -18,18 +18,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shapes", default="", help="';'-separated hw,cin,cout (default: the four Cout = 32 convs)")
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
-    buf = torch.randn(1, a.hw, a.hw, 224, device=dev).to(torch.bfloat16)
+    shapes = ([tuple(map(int, t.split(","))) for t in a.shapes.split(";")] if a.shapes
+              else [(a.hw, c, 32) for c in (64, 96, 128, 160)])
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    for cin in (64, 96, 128, 160):
-        wp = ops.pack_conv_weight((torch.randn(32, cin, 3, 3, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16))
-        b = torch.randn(32, device=dev).to(torch.bfloat16)
+    hip_ops.CONV_TILE64 = True
+    for hw, cin, cout in shapes:
+        buf = torch.randn(1, hw, hw, 192 + cout, device=dev).to(torch.bfloat16)
+        wp = ops.pack_conv_weight((torch.randn(cout, cin, 3, 3, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16))
+        b = torch.randn(cout, device=dev).to(torch.bfloat16)
         res = {}
         for tile in (True, False):
             hip_ops.CONV_TILE = tile
-            run = lambda: ops.conv2d(buf[..., :cin], wp, b, act="lrelu", out=buf[..., 192:224])  # noqa: E731
+            run = lambda: ops.conv2d(buf[..., :cin], wp, b, act="lrelu", out=buf[..., 192:192 + cout])  # noqa: E731
             run()
             torch.cuda.synchronize()
             best = 1e9
@@ -41,10 +45,12 @@ def main():
                 ev[1].synchronize()
                 best = min(best, ev[0].elapsed_time(ev[1]) * 1e3 / a.iters)
             res[tile] = best
-        fl = 2.0 * a.hw * a.hw * 32 * 9 * cin
-        print(f"conv {a.hw}x{a.hw} {cin}->32: halo-tile {res[True]:7.1f} us ({fl / res[True] / 1e6:6.1f} TF/s)   "
+        del buf
+        fl = 2.0 * hw * hw * cout * 9 * cin
+        print(f"conv {hw}x{hw} {cin}->{cout}: halo-tile {res[True]:7.1f} us ({fl / res[True] / 1e6:6.1f} TF/s)   "
               f"implicit GEMM {res[False]:7.1f} us ({fl / res[False] / 1e6:6.1f} TF/s)", flush=True)
     hip_ops.CONV_TILE = True
+    hip_ops.CONV_TILE64 = False
 
 
 if __name__ == "__main__":
