@@ -30,8 +30,10 @@
 // Measured (tools/convtilebench.py, 512^2, profiles/conv_tile_r5.txt): 64 /
 // 96 / 128 / 160 -> 32 in 26.7 / 33.4 / 38.0 / 43.9 us (362-551 TF/s) against
 // 38.7 / 54.7 / 62.5 / 87.7 us for the tuned implicit GEMM; Real-ESRGAN x4
-// 512 -> 2048 29.3 -> 24.2 ms.  Cout = 64 convs stay on the implicit GEMM
-// (twice the reuse per staged byte: 680 TF/s for the 192 -> 64 conv5).
+// 512 -> 2048 29.3 -> 24.2 ms.  The Cout = 64 instance (2-stage ring: 64 KB
+// stages) with the fused "* 0.2 + x" epilogue of conv5: 192 -> 64 77.9 vs 96.6
+// us, 64 -> 64 at 1024^2 / 2048^2 133 / 522 vs 158 / 622 us
+// (profiles/conv_tile64_r5.txt).
 //   * wave w computes tile row w (32 px = 2 MFMA row fragments) x 32 outputs
 //     with v_mfma_f32_16x16x32_bf16 (B . A order: row-layout accumulators, a
 //     lane holds one pixel's 4 consecutive outputs -> 8-byte stores).
