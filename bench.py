@@ -259,8 +259,10 @@ def main():
             "model_load_read_s": round(load_read_s, 3),
             "model_load_all_gather_s": round(load_gather_s, 3),
             "load_bytes_read_per_rank": load_bytes,
-            "load_path": f"safetensors dir -> sharded byte-range reads + {'RCCL' if on_gpu else 'gloo'} all_gather" if world > 1 else
-                         "safetensors dir -> local read",
+            "model_load_read_GBps": round(load_bytes / max(load_read_s, 1e-9) / 1e9, 2),
+            "load_path": (f"safetensors dir -> native sharded byte-range reads (csrc/host/csk_io.cpp) + "
+                          f"{'RCCL' if on_gpu else 'gloo'} all_gather of the raw bytes" if world > 1 else
+                          "safetensors dir -> native threaded pread + pinned-ring H2D (csrc/host/csk_io.cpp)"),
         }
         print(json.dumps(rec), flush=True)
     pool.shutdown()

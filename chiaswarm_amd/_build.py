@@ -137,7 +137,47 @@ def _compile(src: str, force: bool, debug: bool = False) -> str:
     return obj
 
 
+HOST_SRC = os.path.join(ROOT, "csrc", "host")
+OUT_IO = os.path.join(ROOT, "chiaswarm_amd", "lib", "libcskio.so")
+
+
+def io_digest() -> str:
+    h = hashlib.sha256(b"cskio-v1")
+    for f in sorted(glob.glob(os.path.join(HOST_SRC, "*.cpp"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_io(force: bool = False, verbose: bool = True) -> str:
+    """``libcskio.so``: the host-side native checkpoint reader
+    (``csrc/host/csk_io.cpp``: threaded pread into a pinned staging ring +
+    hipMemcpyAsync).  Plain host C++ against the HIP runtime, built with g++."""
+    dig = io_digest()
+    stamp = OUT_IO + ".src"
+    if os.path.exists(OUT_IO) and not force and os.path.exists(stamp) and open(stamp).read().strip() == dig:
+        return OUT_IO
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if not cxx:
+        raise RuntimeError("no host C++ compiler for csrc/host")
+    srcs = sorted(glob.glob(os.path.join(HOST_SRC, "*.cpp")))
+    cmd = [cxx, "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           *srcs, "-o", OUT_IO + ".tmp", f"-L{rocm}/lib", "-lamdhip64", "-lpthread", f"-Wl,-rpath,{rocm}/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host library build failed:\n{r.stderr}")
+    os.replace(OUT_IO + ".tmp", OUT_IO)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    if verbose:
+        print(f"[csk] built {OUT_IO} from {len(srcs)} host sources")
+    return OUT_IO
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool = False) -> str:
+    build_io(force, verbose)
     out = OUT_DEBUG if debug else OUT
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(os.path.dirname(out), exist_ok=True)

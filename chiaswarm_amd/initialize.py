@@ -78,6 +78,24 @@ def _has_safetensors(path) -> bool:
     return bool(path) and bool(glob.glob(os.path.join(str(path), "**", "*.safetensors"), recursive=True))
 
 
+def _components_without_safetensors(path) -> list:
+    """Component sub-directories of a fetched repo (those with a config.json,
+    or the repo root itself) that hold no safetensors weights: their weights
+    exist only as pickled ``.bin`` files, which from_pretrained would read."""
+    import glob
+    import os
+
+    if not path:
+        return []
+    root = str(path)
+    out = []
+    for cfg in sorted(glob.glob(os.path.join(root, "*", "config.json")) + [os.path.join(root, "config.json")]):
+        d = os.path.dirname(cfg)
+        if os.path.exists(cfg) and not glob.glob(os.path.join(d, "*.safetensors")):
+            out.append(os.path.relpath(d, root))
+    return out
+
+
 def fetch(name: str, revision: str = "main", variant: str | None = None, token=None, downloader=None) -> str:
     """Download (or re-validate) one model into the HF cache; returns its path.
     Safetensors first; a repo that ships only pickled ``pytorch_model.bin`` /
@@ -91,6 +109,14 @@ def fetch(name: str, revision: str = "main", variant: str | None = None, token=N
                       token=tok)
     if not _has_safetensors(path):
         path = downloader(name, revision=revision, allow_patterns=BIN_ALLOW,
+                          ignore_patterns=[p for p in IGNORE if p != "*.bin"], token=tok)
+        return path
+    # per component: one that ships only pytorch_model.bin (e.g. a text_encoder
+    # beside a safetensors unet) gets its .bin fetched too
+    missing = _components_without_safetensors(path)
+    if missing:
+        pats = [f"{c}/*.bin" if c != "." else "*.bin" for c in missing]
+        path = downloader(name, revision=revision, allow_patterns=pats,
                           ignore_patterns=[p for p in IGNORE if p != "*.bin"], token=tok)
     return path
 

@@ -364,36 +364,10 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = Conv2d(cin, cout, 1, padding=0) if cin != cout else None
         self.out_channels = cout
 
-    def _halo_ok(self, x, x2=None) -> bool:
-        return (ops.use_hip(x) and self.norm1.weight.dim() == 1 and self.conv1.kernel_size == (3, 3)
-                and self.conv1.stride == (1, 1) and self.conv1.padding == (1, 1) and ops.conv_halo_ok(x, self.conv1, x2))
-
-    def _forward_halo(self, x, x2, temb_proj, sc_fn):
-        """norm1 -> conv1 -> norm2 -> conv2 with both GroupNorm(+SiLU)s applied
-        inside the halo convs' LDS tiles (csrc/kernels/conv_halo.hip): the two
-        GroupNorm apply passes (a full read + write of the activation each) are
-        gone; the producers' epilogue statistics are finalized per (sample,
-        group) by a tiny kernel.  Returns None when the statistics are missing."""
-        n1, n2 = self.norm1, self.norm2
-        st1 = ops.gn_finalize(x, n1.num_groups, n1.eps, x2)
-        if st1 is None:
-            return None
-        sc = sc_fn()
-        h = ops.conv_halo(x, self.conv1, bias2d=temb_proj, gn=(st1, n1.weight, n1.bias, n1.num_groups, True), x2=x2)
-        st2 = ops.gn_finalize(h, n2.num_groups, n2.eps) if ops.conv_halo_ok(h, self.conv2) else None
-        if st2 is None:
-            return self.conv2(self.norm2(h, silu=True), residual=sc, gn_stats=True)
-        return ops.conv_halo(h, self.conv2, residual=sc, gn=(st2, n2.weight, n2.bias, n2.num_groups, True))
-
     def forward(self, x, temb_proj=None):
         """``temb_proj``: this block's [B, Cout] time projection (already
         computed by the model's batched time-embedding GEMM).  A 1x1 shortcut
         runs on a side stream, overlapping norm1 / conv1 / norm2."""
-        if self._halo_ok(x):
-            y = self._forward_halo(x, None, temb_proj,
-                                   lambda: self.conv_shortcut(x) if self.conv_shortcut is not None else x)
-            if y is not None:
-                return y
         sc = x
         with ops.side_branch(x) as br:
             if self.conv_shortcut is not None:
@@ -411,18 +385,6 @@ class ResnetBlock2D(nn.Module):
         (the concat cost a full read + write of both tensors per up-block
         ResNet)."""
         sc_conv = self.conv_shortcut
-        if (sc_conv is not None and sc_conv.kernel_size == (1, 1) and a.shape[-1] % 64 == 0 and a.is_contiguous()
-                and b.is_contiguous() and self._halo_ok(a, b)):
-            w = sc_conv.weight.view(sc_conv.out_channels, sc_conv.in_channels)
-            ca = a.shape[-1]
-
-            def shortcut():
-                s1 = ops.gemm(a, w[:, :ca])
-                return ops.gemm(b, w[:, ca:], sc_conv.bias, residual=s1)
-
-            y = self._forward_halo(a, b, temb_proj, shortcut)
-            if y is not None:
-                return y
         hn = None
         if ops.use_hip(a) and sc_conv is not None and sc_conv.kernel_size == (1, 1) and self.norm1.weight.dim() == 1:
             hn = ops.group_norm_cat(a, b, self.norm1.weight, self.norm1.bias, self.norm1.num_groups,

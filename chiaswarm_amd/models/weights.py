@@ -78,8 +78,12 @@ def weight_files(d: str) -> tuple:
     return ("bin", bins) if bins else ("", [])
 
 
-def _read_dir(d: str) -> dict:
-    from safetensors.torch import load_file
+def _read_dir(d: str, device="cpu") -> dict:
+    """Tensors of a component directory.  Safetensors go through the native
+    reader (runtime/fastload.py: one threaded read of each file's data region
+    straight to ``device``; tensors are views of it); ``.bin`` files through
+    the weights-only unpickler on the host."""
+    from ..runtime.fastload import load_file
 
     out = {}
     kind, files = weight_files(d)
@@ -95,7 +99,7 @@ def _read_dir(d: str) -> dict:
     if fp16 and len(fp16) < len(files):
         files = [f for f in files if f not in fp16]
     for f in files:
-        out.update(load_file(f, device="cpu"))
+        out.update(load_file(f, device=device))
     return out
 
 
@@ -119,14 +123,16 @@ def read_weights(path: str) -> dict:
     """State dict of a directory (``*.safetensors``, else a single ``*.pth`` /
     ``*.pt``) or of one file of either format."""
     if os.path.isdir(path):
-        if weight_files(path)[1] and not glob.glob(os.path.join(path, "*.pth")):
+        kind, files = weight_files(path)
+        # safetensors always win; a .pth is read only where there are none
+        if kind == "safetensors" or (files and not glob.glob(os.path.join(path, "*.pth"))):
             return _read_dir(path)
         pth = sorted(glob.glob(os.path.join(path, "*.pth")) + glob.glob(os.path.join(path, "*.pt")))
         if len(pth) != 1:
             raise CheckpointMismatch(f"{path}: expected *.safetensors or exactly one *.pth, found {pth}")
         return read_pth(pth[0])
     if path.endswith(".safetensors"):
-        from safetensors.torch import load_file
+        from ..runtime.fastload import load_file
 
         return load_file(path, device="cpu")
     return read_pth(path)
@@ -184,7 +190,8 @@ def read_checkpoint(d: str, like: torch.nn.Module | None = None) -> dict:
         if dev is not None and getattr(dev, "type", dev) == "cuda" and torch.distributed.get_backend() == "gloo":
             dev = "cpu"
         return sharded_state_dict(safetensors_files(d), dt, dev)
-    return _read_dir(d)
+    p = next(like.parameters(), None) if like is not None else None
+    return _read_dir(d, p.device if p is not None else "cpu")
 
 
 def load_component(module, weights_dir: str, sub: str, renames=None, **kw) -> LoadReport | None:

@@ -204,34 +204,6 @@ def layer_norm_gemm(x, norm, w, bias, folded, act=None, residual=None, row_stats
                 row_stats=row_stats)
 
 
-def conv_halo_ok(x: torch.Tensor, conv, x2=None) -> bool:
-    """The halo 3x3 conv kernel (csrc/kernels/conv_halo.hip) takes ``conv`` on
-    ``x`` (or on the channel concat [x | x2]) on the HIP path."""
-    if not use_hip(x) or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1):
-        return False
-    from . import hip_ops
-
-    return hip_ops.conv_halo_ok(x, conv._wp(), x2)
-
-
-def gn_finalize(x, groups, eps, x2=None):
-    """(mean, rstd) [B, G, 2] of x (or of [x | x2]) from the producers' fused
-    epilogue statistics, or None (HIP path)."""
-    from . import hip_ops
-
-    return hip_ops.gn_finalize(x, groups, eps, x2)
-
-
-def conv_halo(x, conv, bias2d=None, residual=None, gn=None, x2=None, gn_stats=True):
-    """conv(act(GroupNorm(x))) through the halo kernel (``gn = (stat, gamma,
-    beta, groups, silu)``); ``conv`` is the Conv2d module (its packed weight and
-    bias)."""
-    from . import hip_ops
-
-    return hip_ops.conv_halo(x, conv._wp(), conv.bias, bias2d=bias2d, residual=residual, gn=gn, x2=x2,
-                             gn_stats=gn_stats)
-
-
 def qattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
     """The query projection of this cross-attention can carry the attention in
     its epilogue (HIP path; head dim 64, <= 80 context tokens)."""

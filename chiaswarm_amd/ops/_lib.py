@@ -31,7 +31,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 DEBUG = os.environ.get("CSK_DEBUG", "") not in ("", "0")
 LIB_PATH = os.environ.get("CSK_LIB_PATH") or os.path.join(LIB_DIR, "libcsk_debug.so" if DEBUG else "libcsk.so")
 # translation units that export csk_debug_read_<tu> / csk_debug_clear_<tu> in debug builds
-DEBUG_TUS = ("gemm", "gemm_glds", "gemm8p", "attention", "attention_wide", "xattn", "conv_halo")
+DEBUG_TUS = ("gemm", "gemm_glds", "gemm8p", "attention", "attention_wide", "xattn")
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

@@ -117,10 +117,6 @@ sig("csk_xattn_block", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_
 sig("csk_attention_fa", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p)
 sig("csk_set_attn_fa", c_int)
-sig("csk_set_gemm_sk_workers", c_int)
-sig("csk_gemm_sk_errors", c_void_p)
-sig("csk_gemm_slk_launches", c_void_p)
-sig("csk_gemm_pst_launches", c_void_p)
 sig("csk_attn_fa_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("csk_attention_split", c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64), c_int, c_int, c_int, c_int,
     c_int, c_float, c_int, c_void_p, c_void_p, c_void_p)
@@ -221,8 +217,6 @@ def gemm(a2, w, bias=None, residual=None, act=None, out=None, gn_rows=0, ln=None
                   M, N, K, lda, ldb, n_out, n_out, 1, code, 1.0, _p(part), tile, split, _p(ws), _s())
 
     tile, split = tuning.choose(f"g:{M}:{N}:{K}:{code}", M, N, K, run)
-    if tile == 44 and (ln is not None or row_stats or gn_rows or code == 3):
-        tile = 14  # the sliced-K tile has none of these epilogues (gemm_slk.hip): 64x64 one-tile kernel
     if split < 0 and tile not in tuning.GLDS:
         split = 1  # the in-kernel fixup exists in the LDS-DMA tiles only
     if ln is not None or row_stats:
@@ -613,6 +607,23 @@ def attn_fa_errors() -> int:
     return int(out.value)
 
 
+sig("csk_attn_fa_reset")
+
+
+def attn_fa_health() -> bool:
+    """Per-job check of the stream-K attention's merge protocol (called by
+    runtime/device.py after every GPU job).  A spin that gave up means a late
+    contributor may publish into a slot after its owner released it, so the
+    partials of every later launch are suspect: the kernel is switched off for
+    this process, its flags are zeroed, and False is returned (the caller fails
+    the job and drops the captured graphs, which still launch the kernel)."""
+    if attn_fa_errors() == 0:
+        return True
+    set_attn_fa(False)
+    _lib.call("csk_attn_fa_reset")
+    return False
+
+
 ATTN32 = True  # mirrors the library's csk_set_attn32 (set_attn32): the split-KV path runs attn32_kernel only
 
 
@@ -818,105 +829,6 @@ def xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats
     out = y.view(x.shape)
     if rp is not None:
         out._csk_rows = (rp, 1, C)
-    return out
-
-
-# ---------------------------------------------------------------------------
-# Halo-tiled 3x3 conv with the input GroupNorm(+SiLU) applied in its LDS halo
-# (csrc/kernels/conv_halo.hip): the ResNet norm -> conv pairs without the
-# GroupNorm apply pass.
-sig("csk_gn_finalize", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p)
-sig("csk_conv_halo_supported", c_int, c_int, c_int, c_int, c_int)
-sig("csk_conv_halo_gn_seg", c_int)
-sig("csk_conv_halo", c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-    c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-    c_int, c_void_p)
-# Off by default: measured slower than the tuned implicit-GEMM conv + GroupNorm
-# apply on every UNet shape (profiles/halobench_r6f.txt: 64x64 320->320 at CFG
-# batch 8: halo 132 us / halo+GN 187 us vs conv 77.5 us + apply 20 us) — one
-# workgroup per CU with four waves has no second workgroup to hide the
-# per-step barrier and LDS latency, and the in-LDS GroupNorm transform
-# (2.1x halo x 2 column tiles of the elements, SiLU's two transcendentals)
-# is not overlapped with the matrix cores.  CSK_CONV_HALO=1 enables it.
-CONV_HALO = os.environ.get("CSK_CONV_HALO", "0") == "1"
-HALO_STATS = [0, 0]  # [fused GroupNorm + conv calls, conv calls] (tests)
-
-
-def gn_finalize(x, groups, eps, x2=None):
-    """(mean, rstd) per (sample, group) [B, G, 2] fp32 of x (or of the channel
-    concat [x | x2]) from the producers' fused epilogue statistics
-    (``_csk_gn``); None if they are missing or incompatible."""
-    sa = getattr(x, "_csk_gn", None)
-    if sa is None:
-        return None
-    B, C1 = x.shape[0], x.shape[-1]
-    P = x.numel() // (B * C1)
-    part2, C = None, C1
-    seg = sa[1]
-    if x2 is not None:
-        sb = getattr(x2, "_csk_gn", None)
-        if sb is None or sb[1] != seg or x2.shape[:-1] != x.shape[:-1]:
-            return None
-        part2, C = sb[0], C1 + x2.shape[-1]
-    if C % groups or P % seg:
-        return None
-    stat = torch.empty((B, groups, 2), dtype=torch.float32, device=x.device)
-    _lib.call("csk_gn_finalize", _p(stat), _p(sa[0]), _p(part2), C1, seg, B, P, C, groups, float(eps), _s())
-    return stat
-
-
-def conv_halo_ok(x, wp, x2=None) -> bool:
-    if not CONV_HALO or x.dim() != 4:
-        return False
-    B, H, W, Ca = x.shape
-    Cin = Ca + (x2.shape[-1] if x2 is not None else 0)
-    return (wp.dim() == 4 and wp.shape[1:] == (3, 3, Cin) and (x2 is None or Ca % 64 == 0)
-            and _lib.call_int("csk_conv_halo_supported", B, H, W, Cin, wp.shape[0]) > 0)
-
-
-def conv_halo(x, wp, bias=None, bias2d=None, residual=None, gn=None, x2=None, act=None, out_scale=1.0,
-              gn_stats=True):
-    """3x3 / stride 1 / pad 1 NHWC conv of ``x`` (or of the concat [x | x2]),
-    optionally of GroupNorm(+SiLU)(input): ``gn = (stat, gamma, beta, groups,
-    silu)`` with ``stat`` from ``gn_finalize``.  ``gn_stats``: the output
-    carries ``_csk_gn`` statistics for the next GroupNorm."""
-    _bf16(x, "conv_halo.x")
-    _bf16(wp, "conv_halo.w")
-    x = x.contiguous()
-    B, H, W, Ca = x.shape
-    lda2 = 0
-    if x2 is not None:
-        _bf16(x2, "conv_halo.x2")
-        x2 = x2.contiguous()
-        lda2 = x2.shape[-1]
-    Cin = Ca + lda2
-    Cout = wp.shape[0]
-    out = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
-    b2s = 0
-    if bias2d is not None:
-        _bf16(bias2d, "conv_halo.bias2d")
-        if bias2d.stride(1) != 1 or bias2d.data_ptr() % 16 or bias2d.stride(0) % 8:
-            bias2d = bias2d.contiguous()
-        b2s = bias2d.stride(0) if B > 1 else Cout
-    if residual is not None:
-        _bf16(residual, "conv_halo.residual")
-        residual = residual.contiguous()
-    seg = _lib.call_int("csk_conv_halo_gn_seg", W) if gn_stats else 0
-    part = _gn_part(B * H * W, Cout, seg, x.device) if seg and (H * W) % seg == 0 else None
-    stat = gamma = beta = None
-    groups, silu = 1, 0
-    if gn is not None:
-        stat, gamma, beta, groups, silu = gn
-        _bf16(gamma, "conv_halo.gamma")
-        _bf16(beta, "conv_halo.beta")
-    HALO_STATS[1] += 1
-    HALO_STATS[0] += gn is not None
-    _lib.call("csk_conv_halo", _p(out), _p(x), Ca, _p(x2), lda2, Ca, _p(wp.contiguous()), _p(bias), _p(bias2d), b2s,
-              _p(residual), B, H, W, Cin, Cout, ACT[act], float(out_scale), _p(part), _p(stat),
-              _p(None if gamma is None else gamma.contiguous()), _p(None if beta is None else beta.contiguous()),
-              int(groups), int(bool(silu)), _s())
-    if part is not None:
-        out._csk_gn = (part, seg)
     return out
 
 

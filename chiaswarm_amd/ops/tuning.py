@@ -36,13 +36,7 @@ TILES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 32), 6
          # 8-wave 256x160 3-stage ring (gemm8p.hip gemm8r_kernel): 0.0102 B/FLOP, 256 tiles at the 64x64 level
          33: (256, 160), 34: (256, 128),
          # 64x160 2-stage (fewest L2->LDS bytes per output of the 64-row tiles)
-         36: (64, 160),
-         # stream-K (gemm_sk.hip): one persistent workgroup per CU, K-steps spread evenly, in-kernel fixup
-         40: (64, 128), 41: (128, 64), 42: (64, 64), 43: (64, 64),
-         # sliced-K (gemm_slk.hip): the 8 waves of a 64x64 tile split its K-steps (small-M grids)
-         44: (64, 64),
-         # persistent, ring across output tiles (gemm_pst.hip): short-K GEMMs whose epilogue overlaps the next tile's loads
-         50: (128, 64), 51: (64, 64), 52: (128, 128), 53: (64, 128)}
+         36: (64, 160)}
 GLDS = frozenset(range(11, 30)) | {36}  # gemm_glds.hip tiles (in-kernel split-K fixup)
 # waves along M of the tiles whose epilogue stages one wave-row band at a time
 # (gemm_common.h epi_passes: BM > 128 or BN == 160); the GN-statistics segment
@@ -109,12 +103,6 @@ def candidates(M, N, K):
         if tile in (2, 6, 12, 17, 19, 22, 24, 29) and N > 1280:
             continue
         if tile >= 31 and K % 64:
-            continue
-        if 40 <= tile <= 43:  # stream-K tiles: A/B only (gemm_sk.hip MEASURED STANDING)
-            continue
-        if tile == 44:  # sliced-K: A/B only (gemm_slk.hip MEASURED STANDING)
-            continue
-        if tile >= 50:  # persistent tiles: A/B only (gemm_pst.hip MEASURED STANDING)
             continue
         ntiles = -(-M // bm) * -(-N // bn)
         for split in (1, 2, 4, 8, 16):  # 16: the 8x8-level convs (M = 512 rows, K = 11520 / 23040)

@@ -27,16 +27,18 @@ def env_rank():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
-def init_distributed(backend: str | None = None, timeout_s: int = 600):
+def init_distributed(backend: str | None = None, timeout_s: int = 600, force: bool = False):
     """Initialise the process group from torchrun env vars (one rank per GPU).
 
     With ``SDAAS_STORE_PORT`` set (the worker's GPU children) the rendezvous is
     the TCPStore the SUPERVISOR hosts (runtime/worker.py), namespaced by the
     group generation ``SDAAS_GROUP_GEN``: the store outlives any GPU child, so
     a crashed rank 0 takes no surviving rank's store with it, and a re-formed
-    group (a new generation) never reads a stale key of the old one."""
+    group (a new generation) never reads a stale key of the old one.
+    ``force``: form the group even at world size 1 (the GPU test of the RCCL
+    paths, tests/test_rccl_gpu.py)."""
     rank, local_rank, world = env_rank()
-    if world <= 1:
+    if world <= 1 and not force:
         return rank, local_rank, world
     if dist.is_initialized():
         return rank, local_rank, world
@@ -108,7 +110,7 @@ def collective_load_active() -> bool:
 
 
 def barrier():
-    if is_dist():
+    if dist.is_available() and dist.is_initialized():
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
@@ -215,7 +217,7 @@ def recv_tensor(shape, dtype, src: int, device) -> torch.Tensor:
 
 def group_device():
     """Where this rank's collective tensors live: its GPU under RCCL, host under gloo."""
-    if is_dist() and dist.get_backend() == "nccl":
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 

@@ -58,10 +58,32 @@ class Device:
             seed = int(seed)
             kwargs["generator"] = torch.Generator(device=self.identifier()).manual_seed(seed)
             artifacts, pipeline_config = func(self.identifier(), model_name, **kwargs)
+            self._health_check()
             pipeline_config["seed"] = seed
             return artifacts, pipeline_config
         finally:
             self.mutex.release()
+
+    def _health_check(self):
+        """Fail the job (non-fatal: the hive reissues it) when a kernel's
+        in-launch hand-off protocol reported a timeout during it (the
+        persistent attention's merge, csrc/kernels/attn_fa.hip): the kernel is
+        off for this process from now on and every resident model — whose
+        captured graphs still launch it — is dropped."""
+        if self.is_cpu:
+            return
+        from ..ops import _lib
+
+        if _lib._LIB is None:  # the HIP library never ran in this process
+            return
+        from ..ops import hip_ops
+
+        if not hip_ops.attn_fa_health():
+            from .model_cache import cache
+
+            cache().clear()
+            raise RuntimeError("persistent attention merge timed out on this GPU; the kernel is disabled for this "
+                               "process and the job must be retried")
 
     def run_batch(self, func, kwargs_list):
         """Batched variant (runtime.batcher): every job gets its own seeded
@@ -82,6 +104,7 @@ class Device:
                 kw["generator"] = torch.Generator(device=self.identifier()).manual_seed(seed)
                 jobs.append(kw)
             outs = func(self.identifier(), jobs)
+            self._health_check()
             for (_, cfg), seed in zip(outs, seeds):
                 cfg["seed"] = seed
             return outs

@@ -74,6 +74,19 @@ class ModelCache:
     def keys(self):
         return list(self._items)
 
+    def clear(self):
+        """Drop every resident bundle (and with them their captured hipGraphs)."""
+        with self._lock:
+            self._items.clear()
+            self._sizes.clear()
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                torch.cuda.empty_cache()
+        except Exception:
+            pass
+
 
 _CACHE: ModelCache | None = None
 

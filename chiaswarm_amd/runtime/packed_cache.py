@@ -82,23 +82,23 @@ def load(module: torch.nn.Module, path: Path, fp: str) -> bool:
     """Fill ``module`` from the cache; False (module untouched) if absent/stale."""
     if not path.is_file():
         return False
-    from safetensors import safe_open
-
     from ..models.weights import load_into
+    from . import fastload
 
     p0 = next(module.parameters())
-    with safe_open(str(path), framework="pt", device="cpu") as f:
-        meta = f.metadata() or {}
-        if meta.get("fingerprint") != fp:
-            return False
-        keys = list(f.keys())
-        params = {k[3:]: f.get_tensor(k) for k in keys if k.startswith("p::")}
-        extra = {k[3:]: f.get_tensor(k) for k in keys if k.startswith("x::")}
+    meta = fastload.read_metadata(str(path))
+    if meta.get("fingerprint") != fp:
+        return False
+    # one native read of the whole file onto the module's device (fastload)
+    tensors = fastload.load_file(str(path), device=p0.device)
+    params = {k[3:]: v for k, v in tensors.items() if k.startswith("p::")}
+    extra = {k[3:]: v for k, v in tensors.items() if k.startswith("x::")}
     load_into(module, params, name=str(path.name))
     mods = dict(module.named_modules())
     for key, t in extra.items():
         name, attr = key.split("::", 1)
-        setattr(mods[name], attr, t.to(p0.device))
+        # own storage: a view would pin the whole file buffer (params included) in HBM
+        setattr(mods[name], attr, t.clone() if t.device == p0.device else t.to(p0.device))
     for key, v in json.loads(meta.get("lists", "{}")).items():
         name, attr = key.split("::", 1)
         setattr(mods[name], attr, None if v is None else list(v))

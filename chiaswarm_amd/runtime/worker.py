@@ -523,14 +523,18 @@ class Supervisor:
         r0, r1 = (e.group["rank"] for e in exs)
         subs = [dict(job, id=jid, seed=seed, _split={"role": "cfg", "peer": r1, "half": 0}),
                 dict(job, id=f"{jid}#cfg", seed=seed, _split={"role": "cfg", "peer": r0, "half": 1})]
-        out = await self._await_parts(job, exs, subs, seed)
+        # lockstep: a part that failed mid-loop leaves its peer blocked in the
+        # per-step exchange, so the survivor is killed at once (no grace)
+        out = await self._await_parts(job, exs, subs, seed, lockstep=True)
         if out.get("artifacts"):
             self.cfg_splits += 1
         return out
 
-    async def _await_parts(self, job, exs, subs, seed) -> dict:
+    async def _await_parts(self, job, exs, subs, seed, lockstep: bool = False) -> dict:
         """Run the parts of a group split; the first part answers the job, the
-        others must return a ``_split_ack``."""
+        others must return a ``_split_ack``.  ``lockstep``: the parts exchange
+        data every step (CFG-parallel), so once one part has failed the others
+        can only be waiting on it: they are killed without a grace period."""
         from .generator import _error_result
 
         jid = job.get("id")
@@ -556,7 +560,8 @@ class Supervisor:
             # (pipelines.diffusion._split_failed), so survivors still pending
             # after the grace period are wedged on the transfer: restart them
             # rather than leave queued sends a later split could match
-            if crashed or (failed_at is not None and pending and time.monotonic() - failed_at >= grace):
+            if crashed or (failed_at is not None and pending and
+                           (lockstep or time.monotonic() - failed_at >= grace)):
                 for e, t in zip(exs, tasks):
                     if not t.done():
                         e.kill()

@@ -28,7 +28,7 @@ class Settings:
     preload: str = ""           # comma list of models every GPU loads at startup (sharded RCCL read)
     distributed: bool = True    # per-GPU processes form one process group (RCCL over xGMI)
     split_jobs: bool = True     # a multi-image txt2img job may use several idle GPUs
-    cfg_parallel: bool = True   # a one-image CFG txt2img job may run its two CFG halves on two idle GPUs
+    cfg_parallel: bool = False  # opt-in: a one-image CFG txt2img job may run its two CFG halves on two idle GPUs (UNet at batch 1 per half: not bit-identical to the solo batch-2 run)
 
     def __init__(self):
         for k in ("huggingface_token", "log_level", "log_filename", "sdaas_token", "sdaas_uri", "worker_name",
@@ -59,7 +59,7 @@ def load_settings() -> Settings:
     settings.preload = str(d.get("preload", ""))
     settings.distributed = bool(d.get("distributed", True))
     settings.split_jobs = bool(d.get("split_jobs", True))
-    settings.cfg_parallel = bool(d.get("cfg_parallel", True))
+    settings.cfg_parallel = bool(d.get("cfg_parallel", False))
 
     settings.sdaas_token = os.getenv("SDAAS_TOKEN", settings.sdaas_token)
     settings.sdaas_uri = os.getenv("SDAAS_URI", settings.sdaas_uri)

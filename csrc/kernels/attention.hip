@@ -603,10 +603,10 @@ __device__ __forceinline__ int kv_off32(int row, int chunk) {
 // PROBE (profiling builds, wrong results by design; variants 31/32/34/38):
 // 1 = no exp, 2 = no K/V global loads past the first two blocks, 4 = no PV
 // MFMAs, 8 = no QK^T MFMAs
-// TRICKS (A/B, csk_set_attn32(1 + TRICKS)): 1 = the -mu offset as one MFMA from
-// a zero accumulator instead of 32 register moves per block; 2 = the row sum
-// on an all-ones O^T tile of the PV chain instead of 32 VALU adds per block
-template <int QB, int PROBE = 0, int TRICKS = 0>
+// Measured and removed (round 4): the -mu offset as one MFMA from a zero
+// accumulator, and the row sum on an all-ones O^T tile of the PV chain — both
+// slower than the register moves / VALU adds they replaced.
+template <int QB, int PROBE = 0>
 __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const AttnArgs a) {
   constexpr int DP = 64, CPR = DP / 8, KB = 64;
   constexpr int QROWS = QB * 32 * 4;
@@ -648,30 +648,18 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
       qf[qt][ds] = __builtin_bit_cast(v8s, pack8(f));
     }
   v16f oacc[2][QB];  // O^T d-tile dt: query r, d = dt*32 + (i & 3) + 8 (i >> 2) + 4 hh
-  // row sums ride on the PV MFMAs: an all-ones A operand makes every row of this
-  // O^T tile the query's sum of P over the keys (replaces 32 VALU adds per block)
-  v16f osum[QB];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][qt][i] = 0.f;
-  float mrow[QB], lrow[QB];  // running max (log2 units); this lane's partial row sum (TRICKS & 2: osum)
+  float mrow[QB], lrow[QB];  // running max (log2 units); this lane's partial row sum
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
     mrow[qt] = -1e30f;
     lrow[qt] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) osum[qt][i] = 0.f;
   }
-  constexpr short BF_ONE = 0x3F80;
-  const v8s ones8 = {BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE, BF_ONE};
-  // -mu enters the QK^T chain as one extra MFMA from a zero accumulator (no
-  // per-block 32-register init): A = [1, 1, 0..] in k-slots 0-1 of every key
-  // row, B = [-mu_hi, -mu_lo, 0..] (bf16 hi/lo split, exact in the fp32 sum)
-  const v8s kmu = hh == 0 ? v8s{BF_ONE, BF_ONE, 0, 0, 0, 0, 0, 0} : v8s{0, 0, 0, 0, 0, 0, 0, 0};
-  const v16f zero16 = {0.f};
 
   int kv_end = Skv;
   if (a.causal) {
@@ -716,31 +704,14 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   // scores of one 64-key block: s[kt][qt] = S^T of keys kt*32.. (issued with offset -mu)
   auto qk = [&](int buf, v16f (&s)[2][QB], float (&mu)[QB]) {
     const bf16_t* ks = smem + buf * 2 * TILE;
-    v8s qmu[QB];
 #pragma unroll
-    for (int qt = 0; qt < QB; ++qt) {
-      const float m = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
-      if constexpr ((TRICKS & 1) != 0) {
-        const bf16_t hi = f2bf(m);
-        const bf16_t lo = f2bf(m - bf2f(hi));
-        mu[qt] = bf2f(hi) + bf2f(lo);  // the value the MFMA subtracts, exactly
-        qmu[qt] = hh == 0 ? v8s{(short)(hi ^ 0x8000), (short)(lo ^ 0x8000), 0, 0, 0, 0, 0, 0}
-                          : v8s{0, 0, 0, 0, 0, 0, 0, 0};
-      } else {
-        mu[qt] = m;
-      }
-    }
+    for (int qt = 0; qt < QB; ++qt) mu[qt] = mrow[qt] > -1e29f ? mrow[qt] : 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int qt = 0; qt < QB; ++qt) {
-        if constexpr ((TRICKS & 1) != 0) {
-          s[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kmu, qmu[qt], zero16, 0, 0, 0);
-        } else {
+      for (int qt = 0; qt < QB; ++qt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
-        }
-      }
+        for (int i = 0; i < 16; ++i) s[kt][qt][i] = -mu[qt];
 #pragma unroll
       for (int ds = 0; ds < ((PROBE & 8) ? 0 : 4); ++ds) {
         const v8s kf = *reinterpret_cast<const v8s*>(ks + kv_off32(kt * 32 + r, 2 * ds + hh));
@@ -804,7 +775,6 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
         const float alpha = __builtin_amdgcn_exp2f(mrow[qt] - mnew);
         mrow[qt] = mnew;
         lrow[qt] *= alpha;
-        if constexpr ((TRICKS & 2) != 0) osum[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) oacc[dt][qt] *= alpha;
       }
@@ -821,7 +791,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
 #pragma unroll
           for (int i = 0; i < 16; ++i) sc[kt][qt][i] = __builtin_amdgcn_exp2f(sc[kt][qt][i]);
       }
-      if constexpr ((TRICKS & 2) == 0) {
+      {
         // 4 independent single-instruction add chains (no v_pk_add_f32 beside MFMAs)
         float l4[4];
 #pragma unroll
@@ -867,8 +837,6 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
               asm volatile("" ::"v"(vf), "v"(pf[kt][st][qt]));
             } else {
               oacc[dt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][st][qt], oacc[dt][qt], 0, 0, 0);
-              if ((TRICKS & 2) != 0 && dt == 1)  // the row-sum tile of this k-step
-                osum[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones8, pf[kt][st][qt], osum[qt], 0, 0, 0);
             }
           }
         }
@@ -885,8 +853,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
     const size_t rows = (size_t)a.B * a.H * a.Sq;
 #pragma unroll
     for (int qt = 0; qt < QB; ++qt) {
-      float l = osum[qt][0];
-      if constexpr ((TRICKS & 2) == 0) l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
+      const float l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
       const int qi = q0 + qt * 32 + r;
       if (qi >= a.Sq) continue;
       const size_t row = (size_t)ks * rows + (size_t)bh * a.Sq + qi;
@@ -905,8 +872,7 @@ __global__ __launch_bounds__(256, (QB == 1 ? 2 : 1)) void attn32_kernel(const At
   bf16_t* op = a.o + b * a.sob + h * a.soh;
 #pragma unroll
   for (int qt = 0; qt < QB; ++qt) {
-    float l = osum[qt][0];
-    if constexpr ((TRICKS & 2) == 0) l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
+    const float l = lrow[qt] + __shfl_xor(lrow[qt], 32, 64);
     const float inv = l > 0.f ? 1.0f / l : 0.f;
     const int qi = q0 + qt * 32 + r;
     if (qi >= a.Sq) continue;
@@ -1189,12 +1155,7 @@ CSK_API int csk_attention(void* o, const void* q, const void* k, const void* v, 
     }
     if (variant == 20) {  // 32x32x16 MFMA kernel, 128 query rows per workgroup
       const dim3 g32(B * H * ((Sq + 127) / 128));
-      switch (g_attn32) {
-        case 2: attn32_kernel<1, 0, 1><<<g32, 256, 0, stream>>>(a); break;
-        case 3: attn32_kernel<1, 0, 2><<<g32, 256, 0, stream>>>(a); break;
-        case 4: attn32_kernel<1, 0, 3><<<g32, 256, 0, stream>>>(a); break;
-        default: attn32_kernel<1><<<g32, 256, 0, stream>>>(a); break;
-      }
+      attn32_kernel<1><<<g32, 256, 0, stream>>>(a);
       return (int)hipGetLastError();
     }
     if (variant >= 2 || (variant == 0 && Skv > 128)) {

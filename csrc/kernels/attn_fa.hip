@@ -618,6 +618,25 @@ CSK_API int csk_attn_fa_errors(unsigned* out) {
   return (int)hipMemcpy(out, g_fa_flags + g_fa_workers, sizeof(unsigned), hipMemcpyDeviceToHost);
 }
 
+// After a merge spin gave up (csk_attn_fa_errors > 0) a late contributor may
+// still set its flag after the owner cleared it, and the next launch that uses
+// that slot would read a stale partial.  The host therefore disables the
+// kernel for the process (csk_set_attn_fa(0), hip_ops.attn_fa_health) and
+// zeroes every flag and the counter here — outside any graph capture, with the
+// device idle (synchronous memset).
+CSK_API int csk_attn_fa_reset() {
+  if (!g_fa_flags) return (int)hipErrorNotInitialized;
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(g_fa_flags, 0, (size_t)(g_fa_workers + 1) * sizeof(unsigned));
+}
+
+// test hook: pretend n merge spins gave up (tests/test_attn_fa_gpu.py)
+CSK_API int csk_attn_fa_inject_errors(unsigned n) {
+  if (!g_fa_flags) return (int)hipErrorNotInitialized;
+  return (int)hipMemcpy(g_fa_flags + g_fa_workers, &n, sizeof(unsigned), hipMemcpyHostToDevice);
+}
+
 // 1 when csk_attention_fa takes this shape
 CSK_API int csk_attn_fa_ok(int B, int H, int Sq, int Skv, int D, int causal, int has_kv_len) {
   if (!g_fa_enabled || D != 64 || causal || has_kv_len || !g_fa_part) return 0;

@@ -475,9 +475,6 @@ CSK_API int csk_set_gn_lds(int v) {
   return 0;
 }
 
-int csk_gemm_slk_launch(const GemmArgs& a, bool conv, hipStream_t s);  // gemm_slk.hip
-int csk_gemm_pst_launch(const GemmArgs& a, int tile, bool conv, hipStream_t s);  // gemm_pst.hip
-
 // the LDS-DMA tiles of gemm_glds.hip (csk_gemm_glds_launch)
 static inline bool glds_tile(int t) { return (t >= 11 && t <= 29) || t == 36; }
 
@@ -503,7 +500,6 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     ksplit = -ksplit;
   }
   if (ksplit > 1 && a.act == ACT_GEGLU && !fixup) ksplit = 1;
-  if ((tile >= 40 && tile <= 44) || (tile >= 50 && tile <= 53)) ksplit = 1;  // stream-K / sliced-K / persistent tiles: no split
   if (a.gn_part && (a.act == ACT_GEGLU || tile == 0)) return (int)hipErrorInvalidValue;
   if ((a.ln_part || a.row_part) && ((ksplit > 1 && !fixup) || tile == 0)) return (int)hipErrorInvalidValue;
   if (a.row_part && a.act == ACT_GEGLU) return (int)hipErrorInvalidValue;
@@ -530,22 +526,9 @@ static int dispatch(GemmArgs a, int tile, int ksplit, hipStream_t s) {
     else tile = 4;
   }
   int err;
-  if (tile >= 50 && tile <= 53) {  // persistent cross-tile ring (gemm_pst.hip); same-geometry one-tile kernel where it declines
-    err = csk_gemm_pst_launch(a, tile, CONV, s);
-    if (err == (int)hipErrorNotSupported) {
-      static const int fallback[4] = {12, 14, 11, 13};
-      err = csk_gemm_glds_launch(a, fallback[tile - 50], 1, CONV, s);
-    }
-  } else if (tile == 44) {  // sliced-K small-M tile (gemm_slk.hip); the 64x64 LDS-DMA tile where it declines
-    err = csk_gemm_slk_launch(a, CONV, s);
-    if (err == (int)hipErrorNotSupported) err = csk_gemm_glds_launch(a, 14, 1, CONV, s);
-  } else if (tile >= 40 && tile <= 43) {  // stream-K (gemm_sk.hip); same-geometry LDS-DMA tile where it declines
-    err = csk_gemm_sk_launch(a, tile, CONV, s);
-    if (err == (int)hipErrorNotSupported) {
-      static const int fallback[4] = {13, 12, 14, 14};
-      err = csk_gemm_glds_launch(a, fallback[tile - 40], 1, CONV, s);
-    }
-  } else if (tile >= 31 && tile <= 34) {  // 8-wave phased / ring tiles (gemm8p.hip); 40+: gemm_glds.hip
+  // (stream-K, sliced-K and persistent cross-tile tiles 40-44 / 50-53 were built,
+  // measured slower in round 5 and removed: README "Measured and removed")
+  if (tile >= 31 && tile <= 34) {  // 8-wave phased / ring tiles (gemm8p.hip)
     err = csk_gemm8p_launch(a, tile, ksplit, CONV, s);
     if (err == (int)hipErrorNotSupported) {
       // the fallback must write the GN-statistics segments the host sized gn_part
@@ -645,8 +628,7 @@ CSK_API int csk_gemm_ln(void* C, const void* A, const void* W, const void* bias,
   if (M == 0 || N == 0) return 0;
   // the LDS-DMA tiles merge the row statistics themselves (gemm_common.h
   // ln_merge_tile); the others read them from a merge kernel launched first
-  const bool in_kernel = (glds_tile(tile) || (tile >= 40 && tile <= 44) || (tile >= 50 && tile <= 53)) &&
-                         g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
+  const bool in_kernel = glds_tile(tile) && g_ln_in_kernel;  // 21-26 remap to LDS-DMA tiles
   if (ln_part && !in_kernel) {  // (mean, rstd) per input row into the tail of the partials workspace' sibling
     float* rows = (float*)ln_rowbuf;
     if (!rows) return (int)hipErrorInvalidValue;

@@ -439,8 +439,7 @@ typedef unsigned int fx_u4 __attribute__((ext_vector_type(4)));
 // In-kernel split-K fixup: true in the ONE workgroup of the tile that arrives
 // last, with acc = sum of every split's partial in split order (deterministic
 // whichever workgroup is last); false in the others, which are done.
-// Fence-free hand-off (cdna_hip_programming.md Guideline 16 R1, as
-// gemm_sk.hip): partials stored write-through (sc1) and drained before the
+// Fence-free hand-off (cdna_hip_programming.md Guideline 16 R1): partials stored write-through (sc1) and drained before the
 // counter's atomic; the last arriver reads them all back sc1.  Each thread stores
 // and reloads its own accumulator registers (16 B per lane per fragment: no
 // layout math, fully coalesced).  The last arriver re-zeroes the counter for
@@ -1241,4 +1240,3 @@ __host__ __forceinline__ int gn_seg_for() {
 
 int csk_gemm_glds_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);
 int csk_gemm8p_launch(const GemmArgs& a, int tile, int ksplit, bool conv, hipStream_t s);
-int csk_gemm_sk_launch(const GemmArgs& a, int tile, bool conv, hipStream_t s);

@@ -357,7 +357,6 @@ const bf16_t* csk_zero_ptr() { return g_zero; }
 int csk_zero_bytes() { return ZERO_BYTES; }
 
 extern "C" int csk_attn_fa_init();  // attn_fa.hip: the stream-K attention's merge workspace
-extern "C" int csk_gemm_sk_init();  // gemm_sk.hip: the stream-K GEMM's fixup workspace
 
 CSK_API int csk_init() {
   if (g_zero) return 0;
@@ -369,9 +368,7 @@ CSK_API int csk_init() {
   if (e != hipSuccess) return (int)e;
   e = hipMemset(g_fx_graph, 0, (size_t)FX_GRAPH_CNT * sizeof(unsigned));
   if (e != hipSuccess) return (int)e;
-  e = (hipError_t)csk_attn_fa_init();
-  if (e != hipSuccess) return (int)e;
-  return csk_gemm_sk_init();
+  return csk_attn_fa_init();
 }
 
 int csk_gemm_glds_launch(const GemmArgs& a0, int tile, int ksplit, bool conv, hipStream_t s) {

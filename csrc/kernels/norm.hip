@@ -649,24 +649,6 @@ CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, 
                               eps, silu, affine_bstride, stream);
 }
 
-// Finalize only: (mean, rstd) per (sample, group) from fused epilogue partials
-// (part over x's C1 channels, part2 over x2's C - C1; part2 null: one tensor),
-// for a consumer that applies the GroupNorm itself (conv_halo.hip).
-CSK_API int csk_gn_finalize(void* stat, const void* part, const void* part2, int C1, int seg_rows, int B, int P,
-                            int C, int G, float eps, hipStream_t stream) {
-  if (C % G != 0 || seg_rows <= 0 || P % seg_rows != 0 || (part2 && (C1 <= 0 || C1 >= C)))
-    return (int)hipErrorInvalidValue;
-  if (!part2) C1 = C;
-  const int nseg = P / seg_rows;
-  if (nseg * (C / G) > g_gn_wg_min)
-    gn_finalize_part_wg_kernel<<<B * G, 256, 0, stream>>>((const float*)part, (float*)stat, B, C, G, nseg, seg_rows,
-                                                          eps, (const float*)part2, C1);
-  else
-    gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
-        (const float*)part, (float*)stat, B, C, G, nseg, seg_rows, eps, (const float*)part2, C1);
-  CSK_CHECK_LAUNCH();
-}
-
 // part: B*nchunk*G*3 floats followed by B*G*2 floats of final stats
 // x2 / C1: optional second input (channel concat [x | x2] read in place, x has C1 channels)
 CSK_API int csk_group_norm(void* y, const void* x, const void* x2, int C1, void* part, const void* gamma,

@@ -4,6 +4,7 @@ stream-K split can produce (forced with small worker counts: one block cut into
 2..many pieces, pieces of 1 tile), strided fused-QKV views, the deferred
 rescale (logits far above the lazy reference) and far-negative rows."""
 import math
+import ctypes
 
 import pytest
 import torch
@@ -122,3 +123,28 @@ def test_attn_fa_graph_replay(gpu):
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_attn_fa_timeout_disables_kernel_and_fails_job(gpu):
+    """A merge spin that gave up (simulated: csk_attn_fa_inject_errors) turns the
+    kernel off for the process, zeroes its flags and fails the job through
+    the device wrapper (a stale flag must never be merged later)."""
+    from chiaswarm_amd.ops import _lib
+    from chiaswarm_amd.runtime.device import Device
+
+    q, k, v = (torch.randn(1, 1024, 2, 64, device=gpu).bfloat16() for _ in range(3))
+    assert hip_ops.attn_fa_ok(1, 2, 1024, 1024, 64)
+    assert hip_ops.attn_fa_health()
+    lib = _lib.load()
+    try:
+        assert lib.csk_attn_fa_inject_errors(ctypes.c_uint(3)) == 0
+        dev = Device(0)
+        with pytest.raises(RuntimeError, match="persistent attention"):
+            dev(lambda ident, name, **kw: ({}, {}), model_name="x", seed=1)
+        assert not hip_ops.attn_fa_ok(1, 2, 1024, 1024, 64)
+        assert hip_ops.attn_fa_errors() == 0
+        y = hip_ops.attention(q, k, v, 0.125)  # the fallback kernel serves the shape
+        assert rel_err(y.cpu(), _ref(q, k, v, 0.125)) < 1.5e-2
+    finally:
+        hip_ops.set_attn_fa(True)
+    assert hip_ops.attn_fa_ok(1, 2, 1024, 1024, 64)

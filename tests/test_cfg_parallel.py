@@ -135,6 +135,7 @@ def test_supervisor_runs_one_image_job_cfg_parallel(sdaas_root):
         s.sdaas_uri, s.sdaas_token = hive.base, "t"
         s.preload = "tiny/sd"
         s.max_batch = 1
+        s.cfg_parallel = True  # opt-in (settings.py)
 
         async def main():
             sup = Supervisor(s, executors=exs)

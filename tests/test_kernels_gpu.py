@@ -238,14 +238,13 @@ def test_attention_spike_rescale(gpu, variant):
     assert rel_err(y.cpu(), _attn_ref(q, k, v, 0.125, False)) < 1.5e-2
 
 
-@pytest.mark.parametrize("a32", [1, 2, 3, 4])
+@pytest.mark.parametrize("a32", [1])
 @pytest.mark.parametrize("B,Sq,Skv,H,D,causal,spike", [(2, 1024, 1024, 5, 64, False, False),
                                                         (1, 300, 517, 3, 64, False, True),
                                                         (2, 77, 77, 4, 64, True, False)])
-def test_attn32_trick_variants(gpu, a32, B, Sq, Skv, H, D, causal, spike):
-    """The attn32 A/B variants (csk_set_attn32 2-5: -mu as an MFMA, row sum on
-    the PV chain, both) against fp32, incl. a causal mask
-    and rescale spikes."""
+def test_attn32_kernel(gpu, a32, B, Sq, Skv, H, D, causal, spike):
+    """The 32x32x16 attention kernel (variant 20) against fp32, incl. a causal
+    mask and rescale spikes."""
     from chiaswarm_amd.ops import _lib
 
     q, k, v = (rnd(B, s, H, D, dev=gpu) for s in (Sq, Skv, Skv))

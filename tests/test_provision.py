@@ -117,6 +117,43 @@ def test_bin_only_repo_fetches_pickles_second(tmp_path):
     assert "*.ckpt" in calls[1][1] and "*.pth" in calls[1][1]
 
 
+def test_mixed_repo_fetches_bin_for_the_component_without_safetensors(tmp_path):
+    """the .bin fallback is decided per component — a safetensors
+    unet beside a text_encoder that ships only pytorch_model.bin gets that
+    component's .bin fetched (and only that)."""
+    from chiaswarm_amd.initialize import fetch
+
+    calls = []
+
+    def fake(repo, revision=None, allow_patterns=None, ignore_patterns=None, token=None):
+        calls.append(tuple(allow_patterns))
+        d = tmp_path / repo
+        for comp in ("unet", "text_encoder"):
+            (d / comp).mkdir(parents=True, exist_ok=True)
+            (d / comp / "config.json").write_text("{}")
+        (d / "unet" / "diffusion_pytorch_model.safetensors").write_bytes(b"x")
+        if any(p.endswith(".bin") for p in allow_patterns):
+            (d / "text_encoder" / "pytorch_model.bin").write_bytes(b"x")
+        return str(d)
+
+    path = fetch("org/mixed", downloader=fake)
+    assert len(calls) == 2 and calls[1] == ("text_encoder/*.bin",)
+    assert (tmp_path / "org/mixed" / "text_encoder" / "pytorch_model.bin").exists()
+    assert path.endswith("org/mixed")
+
+
+def test_safetensors_win_over_a_stray_pth(tmp_path):
+    """a .pth beside safetensors never replaces them."""
+    from safetensors.torch import save_file
+
+    from chiaswarm_amd.models.weights import read_weights
+
+    save_file({"w": torch.ones(3)}, str(tmp_path / "model.safetensors"))
+    torch.save({"w": torch.zeros(3)}, str(tmp_path / "old.pth"))
+    torch.save({"w": torch.zeros(3)}, str(tmp_path / "older.pth"))
+    assert torch.equal(read_weights(str(tmp_path))["w"], torch.ones(3))
+
+
 def test_bin_weights_load_like_safetensors(tmp_path):
     """diffusers / transformers ``*.bin`` component weights go through the
     weights-only unpickler and load strictly, same tensors as safetensors."""

@@ -1,7 +1,9 @@
 """Sharded checkpoint distribution over a process group (gloo on CPU here,
-RCCL on the GPU node): every rank reads only its byte ranges, one all_gather
-assembles the model, and every rank ends with bitwise-identical weights equal
-to a plain full read.  World sizes 2 and 4."""
+RCCL on the GPU node): every rank reads only its 1/world byte range of the
+checkpoint's data regions (the native reader, runtime/fastload.py), one
+all_gather of the raw bytes assembles the model, and every rank ends with
+bitwise-identical weights equal to a plain full read.  World sizes 2 and 4.
+Also: ``fastload.load_file`` is bitwise equal to ``safetensors.load_file``."""
 import os
 import socket
 
@@ -48,7 +50,7 @@ def _worker(rank, world, port, d, q):
         with comm.collective_loading():
             rep = load_component(m, d, "text_encoder")
         rd = sharded.LAST_READER
-        q.put((rank, rep.complete, sorted(rd.read_names), rd.read_bytes,
+        q.put((rank, rep.complete, list(rd.ranges), rd.read_bytes,
                {k: v.float().numpy().copy() for k, v in m.state_dict().items()}))  # by value, not shared fds
         # outside the context the same call is rank-local (no collective)
         m2 = clip.CLIPTextModel(clip.TINY_TEXT)
@@ -75,14 +77,59 @@ def test_sharded_load_reads_only_own_share(tmp_path, world):
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
-    names = [set(r[2]) for r in res]
     assert all(r[1] for r in res)
-    for i in range(world):  # disjoint shares that together cover every tensor
-        for j in range(i + 1, world):
-            assert not names[i] & names[j]
-    assert set().union(*names) == set(ref)
-    assert all(len(n) > 0 for n in names)
+    # the ranks' byte ranges are disjoint and together cover every data byte of every file
+    from chiaswarm_amd.runtime.fastload import read_header
+
+    covered = {}
+    for r in res:
+        for path, b, e in r[2]:
+            covered.setdefault(path, []).append((b, e))
+    for path, rngs in covered.items():
+        rngs.sort()
+        start, _ = read_header(path)
+        assert rngs[0][0] == start and rngs[-1][1] == os.path.getsize(path)
+        for (_, e0), (b1, _) in zip(rngs, rngs[1:]):
+            assert e0 == b1
+    assert len(covered) == 2
+    assert all(r[3] > 0 for r in res)
+    assert sum(r[3] for r in res) < total  # headers are never part of a share
     assert max(r[3] for r in res) < 0.75 * total  # nobody read (close to) the whole checkpoint
     for r in res:  # bitwise equal on every rank, and equal to a plain full read
         for k, v in r[4].items():
             assert torch.equal(torch.from_numpy(v), ref[k].float()), k
+
+
+@pytest.mark.parametrize("native", ["1", "0"])
+def test_fastload_bitwise_equal_to_safetensors(tmp_path, monkeypatch, native):
+    """The native reader (and its pure-Python fallback) returns exactly the
+    tensors safetensors.load_file does, mixed dtypes and odd sizes included,
+    for files larger than one 16 MiB staging chunk."""
+    from safetensors.torch import load_file
+
+    from chiaswarm_amd.runtime import fastload
+
+    monkeypatch.setattr(fastload, "_LIB", None)
+    monkeypatch.setenv("CSK_IO_NATIVE", native)
+    g = torch.Generator().manual_seed(0)
+    sd = {"big": torch.randn(5 << 20, generator=g),  # 20 MiB fp32: two chunks
+          "odd_bf16": torch.randn(7, 13, generator=g).bfloat16(),
+          "half": torch.randn(3, 5, generator=g).half(),
+          "ids": torch.arange(11, dtype=torch.int64),
+          "flag": torch.tensor([True, False, True]),
+          "empty": torch.empty(0, 4)}
+    path = str(tmp_path / "m.safetensors")
+    save_file(sd, path)
+    ref = load_file(path)
+    got = fastload.load_file(path)
+    assert (fastload.lib() is not None) == (native == "1" and os.path.exists(fastload.LIB_PATH))
+    assert set(got) == set(ref)
+    for k in ref:
+        assert got[k].dtype == ref[k].dtype and got[k].shape == ref[k].shape, k
+        assert torch.equal(got[k], ref[k]), k
+    # a byte range straight into a host tensor
+    start, hdr = fastload.read_header(path)
+    b, e = hdr["big"][2]
+    out = torch.empty(e - b, dtype=torch.uint8)
+    fastload.read_range(path, start + b, out)
+    assert torch.equal(out.view(torch.float32), sd["big"])

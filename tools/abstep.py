@@ -72,7 +72,7 @@ def apply_arm(arm):
         ops.LN_FUSE = arm == "lnon"
     elif arm in ("lnk0", "lnk1"):  # fused-LN row statistics: merge kernel (0) / in the consumer prologue (1)
         _lib.call("csk_set_ln_in_kernel", int(arm == "lnk1"))
-    elif arm.startswith("a32t"):  # attn32 variant: csk_set_attn32 value (1 default, 2-5 TRICKS 1-4)
+    elif arm.startswith("a32t"):  # attn32 on/off: csk_set_attn32 value (0 off, 1 default)
         _lib.call("csk_set_attn32", int(arm[4:]))
     elif arm in ("a32off", "a32on"):  # D = 64 self-attention: 16x16x32 pipelined / 32x32x16 kernel
         hip_ops.set_attn32(arm == "a32on")

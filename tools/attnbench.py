@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--shape", default="8,4096,4096,5,64")
     ap.add_argument("--short-kv", type=int, default=-1, help="Skv <= 128 kernel: 1 plain, 2 pipelined, 3 K/V-resident")
     ap.add_argument("--kv-rows", type=int, default=0, help="K/V-resident kernel rows per workgroup (0 auto)")
-    ap.add_argument("--attn32", type=int, default=1, help="csk_set_attn32 value (0 off, 1 default, 2-4 TRICKS A/B)")
+    ap.add_argument("--attn32", type=int, default=1, help="csk_set_attn32 value (0 off, 1 default)")
     ap.add_argument("--split", type=int, default=0, help="force this many key splits (attention_split); 0: the op's rule")
     ap.add_argument("--fa", type=int, default=1, help="persistent stream-K d=64 kernel (attn_fa.hip) on / off")
     ap.add_argument("--workers", type=int, default=0, help="attn_fa workers (0: one per CU)")

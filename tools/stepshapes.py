@@ -37,10 +37,6 @@ def flops_of(name, a):
     if name == "csk_attention":
         B, H, Sq, Skv, D = a[5:10]
         return f"attn B{B} H{H} Sq{Sq} Skv{Skv} D{D}", 4.0 * B * H * Sq * Skv * D, None
-    if name == "csk_conv_halo":
-        B, H, W, Cin, Cout = a[11:16]
-        gn = a[19] is not None
-        return (f"halo conv B{B} {H}x{W} {Cin}->{Cout}{' +GN' if gn else ''}", 2.0 * B * H * W * Cout * 9 * Cin, None)
     if name == "csk_xattn_block":
         M, C, rpb, Bc, Skv = a[9:14]
         return (f"xattn block M{M} C{C} Skv{Skv}", 2.0 * M * C * C * 2 + 4.0 * M * Skv * C, None)
