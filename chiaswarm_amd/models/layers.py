@@ -225,13 +225,31 @@ class GEGLU(Prepared):
         return ops.gemm(x, self.wp, self.bp, act="geglu")
 
 
-class FeedForward(nn.Module):
+class FeedForward(Prepared):
     """diffusers FeedForward(GEGLU): keys ff.net.0.proj / ff.net.2."""
 
     def __init__(self, dim, mult=4):
         super().__init__()
         inner = dim * mult
+        self.inner = inner
         self.net = nn.ModuleList([GEGLU(dim, inner), nn.Identity(), Linear(inner, dim)])
+
+    def prepare(self):
+        """Packed weights of the fused FF kernel (csrc/kernels/ff.hip), C = 320
+        only (the blocks it serves)."""
+        p, d = self.net[0].proj, self.net[2]
+        if p.weight.shape[1] != 320:
+            self.ff_w1p = self.ff_b1p = self.ff_w2p = None
+            return
+        self.ff_w1p, self.ff_b1p, self.ff_w2p = ops.pack_ff_fused(
+            p.weight.detach(), None if p.bias is None else p.bias.detach(), d.weight.detach())
+
+    def fused_weights(self):
+        w = getattr(self, "ff_w1p", None)
+        p = self.net[0].proj.weight
+        if (w is None and p.shape[1] == 320) or (w is not None and (w.device != p.device or w.dtype != p.dtype)):
+            self.prepare()
+        return getattr(self, "ff_w1p", None), getattr(self, "ff_b1p", None), getattr(self, "ff_w2p", None)
 
     def forward(self, x, residual=None):
         return self.net[2](self.net[0](x), residual=residual)
@@ -300,6 +318,13 @@ class BasicTransformerBlock(nn.Module):
             if dup:
                 q, x = ops.dup2(q), ops.dup2(x)
             x = a2.attend_q(q, kv, ctx if ctx is not None else x, residual=x, row_stats=hip)
+        if hip and not row_stats and ops.ff_fusable(x, ff.inner):
+            # LN3 + GEGLU + down-projection + residual in ONE kernel
+            # (csrc/kernels/ff.hip): the [M, 4C] intermediate never reaches HBM
+            w1p, b1p, w2p = ff.fused_weights()
+            if w1p is not None:
+                return ops.ff_fused(x, self.norm3.weight, self.norm3.bias, w1p, b1p, w2p, ff.net[2].bias,
+                                    self.norm3.eps)
         g = ff.net[0]
         g.ensure()
         fus = ops.ln_fusable(x)

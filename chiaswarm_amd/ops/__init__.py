@@ -246,6 +246,64 @@ def _ref_gemm_attn(xn, w, bias, kv, scale):
     return (att @ v.transpose(1, 2)).transpose(1, 2).reshape(b, s, c).to(xn.dtype)
 
 
+# the 16-column block order of the fused FF's W2 (csrc/kernels/ff.hip: a lane's
+# 8 GEGLU results are intermediates {4h + j, 8 + 4h + j})
+_FF_PERM = (0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15)
+
+
+def pack_ff_fused(w1, b1, w2):
+    """Weights of the fused feed-forward kernel from the diffusers GEGLU
+    projection ``w1`` [2I, C] (+ ``b1`` [2I]; value rows first, gate rows second)
+    and the down-projection ``w2`` [C, I]: (w1p [I/16, 32, C], b1p [I/16, 32]
+    fp32, w2p [C, I])."""
+    two_i, c = w1.shape
+    inner = two_i // 2
+    t = inner // 16
+    w1p = torch.stack((w1[:inner].reshape(t, 16, c), w1[inner:].reshape(t, 16, c)), 1).reshape(t, 32, c)
+    b1p = None
+    if b1 is not None:
+        b1p = torch.stack((b1[:inner].reshape(t, 16), b1[inner:].reshape(t, 16)), 1).reshape(t, 32).float()
+    perm = torch.tensor(_FF_PERM, device=w2.device)
+    w2p = w2.reshape(w2.shape[0], t, 16).index_select(2, perm).reshape(w2.shape[0], inner)
+    return w1p.contiguous(), (None if b1p is None else b1p.contiguous()), w2p.contiguous()
+
+
+def ff_fusable(x: torch.Tensor, inner: int) -> bool:
+    """The fused feed-forward kernel takes this block (HIP path, C = 320)."""
+    if not use_hip(x) or x.dim() != 3:
+        return False
+    from . import hip_ops
+
+    return hip_ops.ff_fused_ok(x, inner)
+
+
+def ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps):
+    """x + FF(LayerNorm(x)) with a GEGLU feed-forward; one HIP kernel, or the
+    fp32 reference composition of the packed weights."""
+    if use_hip(x):
+        from . import hip_ops
+
+        return hip_ops.ff_geglu(x, gamma, beta, w1p, b1p, w2p, b2, eps)
+    return _ref_ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps)
+
+
+def _ref_ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps):
+    """fp32 reference from the packed weights (unpacks them): LayerNorm, GEGLU
+    with the exact GELU, down-projection, bias, residual."""
+    t, _, c = w1p.shape
+    inner = 16 * t
+    xf = x.float()
+    h = torch.nn.functional.layer_norm(xf, (c,), gamma.float(), None if beta is None else beta.float(), eps)
+    w1 = torch.cat((w1p[:, :16].reshape(inner, c), w1p[:, 16:].reshape(inner, c)), 0).float()
+    b1 = None if b1p is None else torch.cat((b1p[:, :16].reshape(inner), b1p[:, 16:].reshape(inner)), 0).float()
+    vg = torch.nn.functional.linear(h, w1, b1)
+    hid = vg[..., :inner] * torch.nn.functional.gelu(vg[..., inner:])
+    inv = torch.argsort(torch.tensor(_FF_PERM))
+    w2 = w2p.reshape(c, t, 16)[:, :, inv.to(w2p.device)].reshape(c, inner).float()
+    y = torch.nn.functional.linear(hid, w2, None if b2 is None else b2.float())
+    return (xf + y).to(x.dtype)
+
+
 def xattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
     """The fused cross-attention sub-block kernel takes this block (HIP path)."""
     if not use_hip(x):

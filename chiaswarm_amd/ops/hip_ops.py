@@ -832,5 +832,50 @@ def xattn_block(x, wq, colsum, bq, kv, wo, bo, eps, scale, rows_per_b, row_stats
     return out
 
 
+# Fused feed-forward (csrc/kernels/ff.hip): LN3 + GEGLU + down-projection +
+# residual in one kernel at C = 320; the [M, 4C] intermediate stays on chip.
+sig("csk_ff_geglu_ok", c_int, c_int, c_int)
+sig("csk_ff_geglu", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+    c_int, c_float, c_void_p)
+sig("csk_set_ff_probe", c_int)
+# below this many rows (CFG batch 2 at 64x64: 8192) the 128-row workgroups
+# leave most CUs idle and the two tuned GEMMs win (tools/ffbench.py)
+FF_MIN_ROWS = int(os.environ.get("CSK_FF_MIN_ROWS", "16384"))
+FF_FUSED = os.environ.get("CSK_FF_FUSED", "1") == "1"
+
+
+def ff_fused_ok(x, inner: int) -> bool:
+    C = x.shape[-1]
+    M = x.numel() // C
+    return (FF_FUSED and x.dtype == torch.bfloat16 and M >= FF_MIN_ROWS
+            and _lib.call_int("csk_ff_geglu_ok", M, C, inner) == 1)
+
+
+def ff_geglu(x, gamma, beta, w1p, b1p, w2p, b2, eps):
+    """y = x + W2 GEGLU(W1 LayerNorm(x) + b1) + b2 in ONE kernel (C = 320).
+    Weights packed by ``ops.pack_ff_fused``: w1p [I/16, 32, C] bf16 (16 value
+    rows, then the 16 gate rows of the same intermediates), b1p [I/16, 32] fp32,
+    w2p [C, I] bf16 with every 16-column block ordered 0-3, 8-11, 4-7, 12-15."""
+    for t, n in ((x, "x"), (gamma, "gamma"), (w1p, "w1p"), (w2p, "w2p")):
+        _bf16(t, "ff_geglu." + n)
+    C = x.shape[-1]
+    M = x.numel() // C
+    inner = w2p.shape[1]
+    x2 = x.reshape(M, C)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    y = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+    if beta is not None:
+        _bf16(beta, "ff_geglu.beta")
+    if b2 is not None:
+        _bf16(b2, "ff_geglu.b2")
+    if b1p is not None and b1p.dtype != torch.float32:
+        raise ValueError("ff_geglu: b1p must be fp32")
+    _lib.call("csk_ff_geglu", _p(y), _p(x2), _p(gamma.contiguous()), _p(None if beta is None else beta.contiguous()),
+              _p(w1p.contiguous()), _p(None if b1p is None else b1p.contiguous()), _p(w2p.contiguous()),
+              _p(None if b2 is None else b2.contiguous()), M, C, inner, float(eps), _s())
+    return y.view(x.shape)
+
+
 sig("csk_set_xattn_probe", c_int)
 sig("csk_set_xattn_waves", c_int)
