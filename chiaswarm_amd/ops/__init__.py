@@ -251,21 +251,60 @@ def _ref_gemm_attn(xn, w, bias, kv, scale):
 _FF_PERM = (0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15)
 
 
+def _ff_keys(device):
+    """16-byte chunk swizzles of the fused FF's LDS images (ff.hip): a W1
+    sub-image row r [32][64] holds logical chunk pos ^ ((r & 7) ^ ((r >> 3) & 1))
+    at position pos; a W2 tile row [32][32], pos ^ ((r >> 2) & 3)."""
+    r = torch.arange(32, device=device)
+    k1 = (r & 7) ^ ((r >> 3) & 1)
+    k2 = (r >> 2) & 3
+    p8, p4 = torch.arange(8, device=device), torch.arange(4, device=device)
+    return p8[None, :] ^ k1[:, None], p4[None, :] ^ k2[:, None]  # [32, 8], [32, 4]
+
+
 def pack_ff_fused(w1, b1, w2):
     """Weights of the fused feed-forward kernel from the diffusers GEGLU
     projection ``w1`` [2I, C] (+ ``b1`` [2I]; value rows first, gate rows second)
-    and the down-projection ``w2`` [C, I]: (w1p [I/16, 32, C], b1p [I/16, 32]
-    fp32, w2p [C, I])."""
+    and the down-projection ``w2`` [C, I], laid out in global memory exactly as
+    the kernel's LDS images (swizzle included), so every LDS-DMA piece is one
+    contiguous 1 KB run:
+      w1p [I/16, C/64, 32, 64]: W1 tile t = 16 value rows + the 16 gate rows of
+          intermediates 16t.., as C/64 swizzled [32][64] sub-images;
+      b1p [I/16, 32] fp32 (same row order);
+      w2p [I/32, C/32, 32, 32]: per 32 intermediates, one swizzled [32][32]
+          image per 32 output rows, columns in 16-blocks ordered 0-3, 8-11, 4-7, 12-15."""
     two_i, c = w1.shape
     inner = two_i // 2
     t = inner // 16
-    w1p = torch.stack((w1[:inner].reshape(t, 16, c), w1[inner:].reshape(t, 16, c)), 1).reshape(t, 32, c)
+    k8, k4 = _ff_keys(w1.device)
+    w1t = torch.stack((w1[:inner].reshape(t, 16, c), w1[inner:].reshape(t, 16, c)), 1).reshape(t, 32, c // 64, 8, 8)
+    w1p = torch.gather(w1t, 3, k8[None, :, None, :, None].expand(t, 32, c // 64, 8, 8))  # pos <- logical chunk
+    w1p = w1p.permute(0, 2, 1, 3, 4).reshape(t, c // 64, 32, 64)
     b1p = None
     if b1 is not None:
         b1p = torch.stack((b1[:inner].reshape(t, 16), b1[inner:].reshape(t, 16)), 1).reshape(t, 32).float()
     perm = torch.tensor(_FF_PERM, device=w2.device)
-    w2p = w2.reshape(w2.shape[0], t, 16).index_select(2, perm).reshape(w2.shape[0], inner)
+    w2q = w2.reshape(c, t, 16).index_select(2, perm).reshape(c // 32, 32, inner // 32, 4, 8)
+    w2p = torch.gather(w2q, 3, k4[None, :, None, :, None].expand(c // 32, 32, inner // 32, 4, 8))
+    w2p = w2p.permute(2, 0, 1, 3, 4).reshape(inner // 32, c // 32, 32, 32)
     return w1p.contiguous(), (None if b1p is None else b1p.contiguous()), w2p.contiguous()
+
+
+def unpack_ff_fused(w1p, b1p, w2p):
+    """Inverse of ``pack_ff_fused``: (w1 [2I, C], b1 [2I] or None, w2 [C, I])."""
+    t, si = w1p.shape[0], w1p.shape[1]
+    c, inner = 64 * si, 16 * t
+    k8, k4 = _ff_keys(w1p.device)
+    inv8, inv4 = torch.argsort(k8, 1), torch.argsort(k4, 1)
+    x = w1p.reshape(t, si, 32, 8, 8).permute(0, 2, 1, 3, 4)  # [t, r, si, pos, e]
+    x = torch.gather(x, 3, inv8[None, :, None, :, None].expand(t, 32, si, 8, 8)).reshape(t, 32, c)
+    w1 = torch.cat((x[:, :16].reshape(inner, c), x[:, 16:].reshape(inner, c)), 0)
+    b1 = None if b1p is None else torch.cat((b1p[:, :16].reshape(inner), b1p[:, 16:].reshape(inner)), 0)
+    nc, no = w2p.shape[0], w2p.shape[1]
+    y = w2p.reshape(nc, no, 32, 4, 8).permute(1, 2, 0, 3, 4)  # [o, r, c, pos, e]
+    y = torch.gather(y, 3, inv4[None, :, None, :, None].expand(no, 32, nc, 4, 8)).reshape(c, inner // 16, 16)
+    w2 = y[:, :, torch.argsort(torch.tensor(_FF_PERM, device=w2p.device))].reshape(c, inner)
+    return w1, b1, w2
 
 
 def ff_fusable(x: torch.Tensor, inner: int) -> bool:
@@ -290,17 +329,13 @@ def ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps):
 def _ref_ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps):
     """fp32 reference from the packed weights (unpacks them): LayerNorm, GEGLU
     with the exact GELU, down-projection, bias, residual."""
-    t, _, c = w1p.shape
-    inner = 16 * t
+    w1, b1, w2 = unpack_ff_fused(w1p, b1p, w2p)
+    c, inner = w2.shape
     xf = x.float()
     h = torch.nn.functional.layer_norm(xf, (c,), gamma.float(), None if beta is None else beta.float(), eps)
-    w1 = torch.cat((w1p[:, :16].reshape(inner, c), w1p[:, 16:].reshape(inner, c)), 0).float()
-    b1 = None if b1p is None else torch.cat((b1p[:, :16].reshape(inner), b1p[:, 16:].reshape(inner)), 0).float()
-    vg = torch.nn.functional.linear(h, w1, b1)
+    vg = torch.nn.functional.linear(h, w1.float(), None if b1 is None else b1.float())
     hid = vg[..., :inner] * torch.nn.functional.gelu(vg[..., inner:])
-    inv = torch.argsort(torch.tensor(_FF_PERM))
-    w2 = w2p.reshape(c, t, 16)[:, :, inv.to(w2p.device)].reshape(c, inner).float()
-    y = torch.nn.functional.linear(hid, w2, None if b2 is None else b2.float())
+    y = torch.nn.functional.linear(hid, w2.float(), None if b2 is None else b2.float())
     return (xf + y).to(x.dtype)
 
 

@@ -853,14 +853,14 @@ def ff_fused_ok(x, inner: int) -> bool:
 
 def ff_geglu(x, gamma, beta, w1p, b1p, w2p, b2, eps):
     """y = x + W2 GEGLU(W1 LayerNorm(x) + b1) + b2 in ONE kernel (C = 320).
-    Weights packed by ``ops.pack_ff_fused``: w1p [I/16, 32, C] bf16 (16 value
-    rows, then the 16 gate rows of the same intermediates), b1p [I/16, 32] fp32,
-    w2p [C, I] bf16 with every 16-column block ordered 0-3, 8-11, 4-7, 12-15."""
+    Weights packed by ``ops.pack_ff_fused`` (the kernel's LDS images, swizzle
+    included): w1p [I/16, C/64, 32, 64] bf16, b1p [I/16, 32] fp32,
+    w2p [I/32, C/32, 32, 32] bf16."""
     for t, n in ((x, "x"), (gamma, "gamma"), (w1p, "w1p"), (w2p, "w2p")):
         _bf16(t, "ff_geglu." + n)
     C = x.shape[-1]
     M = x.numel() // C
-    inner = w2p.shape[1]
+    inner = 32 * w2p.shape[0]
     x2 = x.reshape(M, C)
     if not x2.is_contiguous():
         x2 = x2.contiguous()

@@ -41,9 +41,11 @@ struct FfArgs {
   const bf16_t* x;      // [M][C]: LayerNorm input and residual
   const bf16_t* gamma;  // [C] LN3 weight
   const bf16_t* beta;   // [C] LN3 bias (or null)
-  const bf16_t* w1;     // [I/16][32][C]: per 16 intermediates 16 value rows, then their 16 gate rows
+  const bf16_t* w1;     // [I/16][C/64][32][64]: per 16 intermediates 16 value rows, then their 16 gate
+                        // rows, as swizzled [32][64] sub-images (ops.pack_ff_fused)
   const float* b1;      // [I/16][32] fp32, same row order (or null)
-  const bf16_t* w2;     // [C][I], inside every 16-column block ordered 0-3, 8-11, 4-7, 12-15
+  const bf16_t* w2;     // [I/32][C/32][32][32]: swizzled [32 out rows][32 intermediates] images, every
+                        // 16-column block ordered 0-3, 8-11, 4-7, 12-15
   const bf16_t* b2;     // [C] (or null)
   bf16_t* y;            // [M][C]
   const bf16_t* x_end;  // CSK_DEBUG bounds
@@ -114,29 +116,25 @@ __global__ __launch_bounds__(FF_WAVES * 64, 1) void ff_geglu_kernel(const FfArgs
   const int nchunk = I / 32;
   const int nslots = 3 * nchunk;
 
-  // ---- LDS-DMA of ring slot t (every wave issues FF_PPW pieces) ----
-  auto dma_slot = [&](int t) {
+  // ---- LDS-DMA: this wave's piece i (of FF_PPW) of ring slot t ----
+  auto dma_piece = [&](int t, int i) {
     bf16_t* base = ring + (t % FF_NSLOT) * FF_SLOT;
-    const int c = t / 3, kind = t % 3;
+    const int c = t / 3, kind = t - 3 * c;
+    const int p = wid + FF_WAVES * i;
+    // the packed weights ARE the slot images (ops.pack_ff_fused): a slot is
+    // one contiguous 20 KB run, piece p its p-th KB
+    const bf16_t* src = (kind < 2 ? a.w1 + (size_t)(2 * c + kind) * FF_SLOT : a.w2 + (size_t)c * FF_SLOT) +
+                        512 * p + 8 * lane;
+    CSK_DCHECK(src + 8 <= (kind < 2 ? a.w1_end : a.w2_end), 91, t, I);
+    __builtin_amdgcn_global_load_lds((ff_gptr_t)src, (ff_lptr_t)(base + 512 * p), 16, 0, 0);
+  };
+  auto dma_slot = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < FF_PPW; ++i) {
-      const int p = wid + FF_WAVES * i;
-      const bf16_t* src;
-      if (kind < 2) {  // W1 tile 2c + kind: sub-image p / 4, rows 8 (p % 4) ..
-        const int tt = 2 * c + kind, si = p >> 2, r = 8 * (p & 3) + (lane >> 3), pos = lane & 7;
-        src = a.w1 + ((size_t)(tt * 32 + r) * C + 64 * si + 8 * (pos ^ at_key(r)));
-        CSK_DCHECK(src + 8 <= a.w1_end, 91, tt, I);
-      } else {  // W2 slice: output tile p / 2, rows 16 (p % 2) .., 32 intermediates from 32 c
-        const int o = p >> 1, r = 16 * (p & 1) + (lane >> 2), pos = lane & 3;
-        src = a.w2 + ((size_t)(32 * o + r) * I + 32 * c + 8 * (pos ^ ((r >> 2) & 3)));
-        CSK_DCHECK(src + 8 <= a.w2_end, 92, c, I);
-      }
-      __builtin_amdgcn_global_load_lds((ff_gptr_t)src, (ff_lptr_t)(base + 512 * p), 16, 0, 0);
-    }
+    for (int i = 0; i < FF_PPW; ++i) dma_piece(t, i);
   };
 
   // ---- prologue: the rows, b1, then six slots in flight while the rows normalise ----
-  constexpr int LEAD = FF_NSLOT - 1;
+  constexpr int LEAD = FF_NSLOT - 2;  // slots issued before the first barrier
   uint4 xu[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
@@ -196,20 +194,26 @@ __global__ __launch_bounds__(FF_WAVES * 64, 1) void ff_geglu_kernel(const FfArgs
 #pragma unroll
     for (int i = 0; i < 16; ++i) out[o][i] = 0.f;
 
-  // slot t has landed for every wave and slot t - 1 is free: own pieces of t
-  // waited for (the slots issued after it stay in flight), LDS reads of t - 1
-  // retired, then one barrier
-  auto enter_slot = [&](int t) {
+  // Ring protocol (7 slots, one barrier per PAIR of slots): the barrier in
+  // front of an even slot s waits for this wave's pieces of s and s + 1
+  // (slots s + 2 .. s + 4 stay in flight: vmcnt(15)) and retires its LDS
+  // reads; after it every wave is done with s - 2 and s - 1, so slot u issues
+  // the DMA of slot u + 5 into ring position (u - 2) % 7, one piece after every
+  // fourth MFMA (the issue cost hides under the matrix pipe).
+  auto enter_pair = [&](int t) {
     if constexpr ((PROBE & 4) == 0) {
-      if (t + LEAD - 1 < nslots) ff_vmcnt<FF_PPW * (LEAD - 1)>();
+      if (t + 4 < nslots) ff_vmcnt<FF_PPW * 3>();
       else ff_vmcnt<0>();
     } else {
       ff_vmcnt<0>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto dma_hook = [&](int t, int k) {  // after MFMA k of slot t: piece k / 4 of slot t + 5
     if constexpr ((PROBE & 4) == 0) {
-      if (t + LEAD < nslots) dma_slot(t + LEAD);  // into slot (t - 1) % NSLOT, just released
+      if ((k & 3) == 3 && t + 5 < nslots) dma_piece(t + 5, k >> 2);
     }
   };
 
@@ -228,22 +232,39 @@ __global__ __launch_bounds__(FF_WAVES * 64, 1) void ff_geglu_kernel(const FfArgs
   auto slot_base = [&](int t) -> unsigned {
     return ring0 + (unsigned)(((PROBE & 4) ? (t % 3) : (t % FF_NSLOT)) * FF_SLOT * 2);
   };
-  constexpr int D = 4;  // fragment reads in flight ahead of the MFMA that consumes them
+  constexpr int D = 6;  // fragment reads in flight ahead of the MFMA that consumes them
+  constexpr int GAT = 2;  // the previous tile's GEGLU runs after this MFMA of the next slot
 
-  // acc = b1 rows of W1 tile tt + W1 tile (slot t) x^T: 20 MFMAs
-  auto w1_tile = [&](int t, int tt, v16f& acc) {
+  // GEGLU in-lane: H of intermediates {4h + j, 8 + 4h + j} as one B fragment.
+  // Accumulator slot j = 4q + r: value rows q = 0, 1; their gates sit 16 rows
+  // (two q) further.  bq (b1 of the tile) was read in the tile's own slot and
+  // has arrived (every read of that slot was waited for): the empty asm only
+  // keeps its uses behind that wait.
+  auto geglu = [&](v16f& acc, v4f (&bq)[4]) -> v8s {
+    asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+    mfma_fence16(acc, acc);
+    float hv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = acc[j] + bq[j >> 2][j & 3];
+      const float g = acc[j + 8] + bq[2 + (j >> 2)][j & 3];
+      if constexpr ((PROBE & 2) != 0) hv[j] = v + g;
+      else hv[j] = v * gelu_geglu(g);
+    }
+    return __builtin_bit_cast(v8s, pack8(hv));
+  };
+
+  // acc = W1 tile tt (slot t) x^T: 20 MFMAs; bq <- b1 of the tile.  `pend`
+  // (if set): the previous tile's GEGLU, run after MFMA GAT of this slot.
+  auto w1_tile = [&](int t, int tt, v16f& acc, v4f (&bq)[4], v16f* pacc, v4f (*pbq)[4], v8s* pout) {
     const unsigned sb = slot_base(t);
-    v4f bq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ff_ldf(bq[q], b1base + (unsigned)((tt * 32 + 8 * q) * 4));
     v8s wf[KS];
 #pragma unroll
     for (int ks = 0; ks < D; ++ks) ff_ld(wf[ks], sb + w1o[ks & 3] + (unsigned)((ks >> 2) * 4096));
-    ff_waitf<D>(bq);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[4 * q + r] = bq[q][r];
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       ff_wait(ks + D - 1 < KS ? D - 1 : KS - 1 - ks, wf[ks]);
@@ -253,28 +274,18 @@ __global__ __launch_bounds__(FF_WAVES * 64, 1) void ff_geglu_kernel(const FfArgs
         const int k1 = ks + D;
         ff_ld(wf[k1], sb + w1o[k1 & 3] + (unsigned)((k1 >> 2) * 4096));
       }
+      dma_hook(t, ks);
+      if (ks == GAT && pacc) *pout = geglu(*pacc, *pbq);
     }
   };
 
-  // GEGLU of a W1 tile's accumulators (b1 already in them), in-lane: H of
-  // intermediates {4h + j, 8 + 4h + j} as one B fragment.  Accumulator slot
-  // j = 4q + r: value rows q = 0, 1; their gates sit 16 rows (two q) further.
-  auto geglu = [&](v16f& acc) -> v8s {
-    mfma_fence16(acc, acc);
-    float hv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if constexpr ((PROBE & 2) != 0) hv[j] = acc[j] + acc[j + 8];
-      else hv[j] = acc[j] * gelu_geglu(acc[j + 8]);
-    }
-    return __builtin_bit_cast(v8s, pack8(hv));
-  };
-
-  // out^T += W2 slice (slot t) [H_a; H_b]^T: 2 k-steps x 10 output tiles
-  auto w2_slice = [&](int t, const v8s& ha, const v8s& hb) {
+  // out^T += W2 slice (slot t) [H_a; H_b]^T: 2 k-steps x 10 output tiles;
+  // H_b = GEGLU(acc_b) is formed after MFMA GAT (the first 10 need only H_a)
+  auto w2_slice = [&](int t, const v8s& ha, v16f& acc_b, v4f (&bqb)[4]) {
     const unsigned sb = slot_base(t);
     constexpr int NR = 2 * NOT;
     v8s wf[NR];
+    v8s hb;
 #pragma unroll
     for (int i = 0; i < D; ++i) ff_ld(wf[i], sb + w2o[i / NOT] + (unsigned)((i % NOT) * 2048));
 #pragma unroll
@@ -287,20 +298,26 @@ __global__ __launch_bounds__(FF_WAVES * 64, 1) void ff_geglu_kernel(const FfArgs
         const int i1 = i + D;
         ff_ld(wf[i1], sb + w2o[i1 / NOT] + (unsigned)((i1 % NOT) * 2048));
       }
+      dma_hook(t, i);
+      if (i == GAT) hb = geglu(acc_b, bqb);
     }
   };
 
-  for (int c = 0; c < nchunk; ++c) {
-    const int t0 = 3 * c;
+  // two chunks (6 slots, 3 pairs) per trip: barriers in front of t, t + 2, t + 4
+  for (int c = 0; c < nchunk; c += 2) {
+    const int t = 3 * c;
     v16f acc_a, acc_b;
-    enter_slot(t0);
-    w1_tile(t0, 2 * c, acc_a);
-    enter_slot(t0 + 1);
-    const v8s ha = geglu(acc_a);  // VALU beside tile b's MFMAs
-    w1_tile(t0 + 1, 2 * c + 1, acc_b);
-    enter_slot(t0 + 2);
-    const v8s hb = geglu(acc_b);  // beside the first k-step's MFMAs
-    w2_slice(t0 + 2, ha, hb);
+    v4f bqa[4], bqb[4];
+    v8s ha;
+    enter_pair(t);
+    w1_tile(t, 2 * c, acc_a, bqa, nullptr, nullptr, nullptr);
+    w1_tile(t + 1, 2 * c + 1, acc_b, bqb, &acc_a, &bqa, &ha);
+    enter_pair(t + 2);
+    w2_slice(t + 2, ha, acc_b, bqb);
+    w1_tile(t + 3, 2 * c + 2, acc_a, bqa, nullptr, nullptr, nullptr);
+    enter_pair(t + 4);
+    w1_tile(t + 4, 2 * c + 3, acc_b, bqb, &acc_a, &bqa, &ha);
+    w2_slice(t + 5, ha, acc_b, bqb);
   }
 
   // ---- epilogue: + b2 + residual x; accumulator rows 32 o + 8 q + 4 h + r of row `row` ----
@@ -341,7 +358,7 @@ CSK_API int csk_set_ff_probe(int p) {
 
 // 1 when csk_ff_geglu takes this shape
 CSK_API int csk_ff_geglu_ok(int M, int C, int I) {
-  return (C == 320 && I > 0 && I % 32 == 0 && I <= FF_IMAX && M > 0) ? 1 : 0;
+  return (C == 320 && I > 0 && I % 64 == 0 && I <= FF_IMAX && M > 0) ? 1 : 0;  // chunk pairs
 }
 
 // y[M][C] = x + W2 GEGLU(W1 LN(x) + b1) + b2 (weights packed by ops.pack_ff_fused).

@@ -48,7 +48,10 @@ def rel_err(y, ref):
 def test_pack_roundtrip_cpu():
     blk, x = _setup("cpu", torch.float32)
     w1p, b1p, w2p = blk.ff.fused_weights()
-    assert w1p.shape == (80, 32, 320) and b1p.shape == (80, 32) and w2p.shape == (320, 1280)
+    assert w1p.shape == (80, 5, 32, 64) and b1p.shape == (80, 32) and w2p.shape == (40, 10, 32, 32)
+    w1, b1, w2 = ops.unpack_ff_fused(w1p, b1p, w2p)
+    p = blk.ff.net[0].proj
+    assert torch.equal(w1, p.weight) and torch.equal(b1, p.bias) and torch.equal(w2, blk.ff.net[2].weight)
     y = ops._ref_ff_fused(x, blk.norm3.weight, blk.norm3.bias, w1p, b1p, w2p, blk.ff.net[2].bias, blk.norm3.eps)
     ref = _unfused(x, blk)
     assert torch.allclose(y, ref, atol=1e-4, rtol=1e-4), (y - ref).abs().max()
