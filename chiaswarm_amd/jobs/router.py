@@ -24,6 +24,7 @@ PIPELINE_TYPES = {
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
     "StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline", "AudioLDMPipeline",
     "TextToVideoSDPipeline", "VideoToVideoSDPipeline", "IFPipeline", "IFSuperResolutionPipeline",
+    "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
 }
 # real diffusers classes with no implementation here: a fatal error naming the
 # class (never silently run as plain SD)

@@ -198,7 +198,8 @@ def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
     for need in ("unet", "vae"):
         if need not in comps:
             raise UnsupportedConfig(f"{weights_dir}: model_index.json has no {need!r} component")
-    if "text_encoder" not in comps and "text_encoder_2" not in comps:
+    if "text_encoder" not in comps and "text_encoder_2" not in comps and "image_encoder" not in comps:
+        # (StableDiffusionImageVariationPipeline conditions on a CLIP image encoder instead)
         raise UnsupportedConfig(f"{weights_dir}: model_index.json has no 'text_encoder' component")
     ucfg = component_config(weights_dir, "unet")
     vcfg = component_config(weights_dir, "vae")

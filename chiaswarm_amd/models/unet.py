@@ -114,6 +114,9 @@ X4_UPSCALER = UNetConfig(
     up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
     num_heads=8, cross_attention_dim=1024, num_class_embeds=1000, sample_size=128)
 TINY_X4 = dataclasses.replace(TINY, in_channels=7, num_class_embeds=1000)
+# stabilityai/stable-diffusion-2-depth: latents + 1 depth channel (512 px, epsilon)
+DEPTH_SD2 = dataclasses.replace(SD21, in_channels=5)
+TINY_DEPTH = dataclasses.replace(TINY, in_channels=5)
 
 CONFIGS = {"sd15": SD15, "sd21": SD21, "sd21-v": SD21_V, "sdxl": SDXL, "pix2pix": PIX2PIX,
            "sd2-inpaint": INPAINT_SD2, "sd15-inpaint": INPAINT_SD15, "tiny": TINY}

@@ -35,7 +35,12 @@ SD_CLASSES = {
     "StableDiffusionInpaintPipeline", "StableDiffusionInpaintPipelineLegacy", "StableDiffusionControlNetPipeline",
     "StableDiffusionControlNetImg2ImgPipeline", "StableDiffusionInstructPix2PixPipeline",
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
+    "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
 }
+# checkpoints whose own class must win over a generic requested one (the
+# router defaults an image job to StableDiffusionImg2ImgPipeline; these
+# architectures cannot run as that class)
+_OWN_CLASS = {"StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline"}
 UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
 # job kwargs the SD callback consumes itself (the rest go to the pipeline call)
 _CALLBACK_KEYS = {"model_name", "scheduler_type", "pipeline_type", "upscale", "textual_inversion", "lora",
@@ -54,6 +59,10 @@ def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
         with open(os.path.join(w, "model_index.json")) as f:
             return json.load(f).get("_class_name")
     n = model_name.lower()
+    if "image-variations" in n or (n.startswith("tiny/") and "variation" in n):
+        return "StableDiffusionImageVariationPipeline"
+    if "stable-diffusion-2-depth" in n or (n.startswith("tiny/") and "depth" in n):
+        return "StableDiffusionDepth2ImgPipeline"
     if "x4-upscaler" in n:
         return "StableDiffusionUpscalePipeline"
     if "latent-upscaler" in n:
@@ -69,7 +78,11 @@ def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "mai
     cls = str(pipeline_type or "DiffusionPipeline")
     if cls == "DiffusionPipeline":
         ck = checkpoint_class(model_name, revision)
-        if ck in UPSCALE_CLASSES or (ck is not None and ck not in SD_CLASSES):
+        if ck in UPSCALE_CLASSES or (ck is not None and ck not in SD_CLASSES) or ck in _OWN_CLASS:
+            cls = ck
+    elif cls in ("StableDiffusionPipeline", "StableDiffusionImg2ImgPipeline"):
+        ck = checkpoint_class(model_name, revision)
+        if ck in _OWN_CLASS:
             cls = ck
     if cls in SD_CLASSES or cls in UPSCALE_CLASSES:
         return cls
@@ -106,8 +119,12 @@ def load_sd(model_name: str, device_identifier: str, revision: str = "main", con
         w = ensure_weights(model_name, revision)
         # architecture from the checkpoint's own model_index.json / config.json
         # files (the reference's from_pretrained); name presets only without them
-        return StableDiffusion(resolve_family(model_name, w), device=device_identifier, weights_dir=w,
-                               seed=stable_seed(model_name))
+        fam = resolve_family(model_name, w)
+        if fam.is_image_variation:
+            from .variants import ImageVariation
+
+            return ImageVariation(fam, device=device_identifier, weights_dir=w, seed=stable_seed(model_name))
+        return StableDiffusion(fam, device=device_identifier, weights_dir=w, seed=stable_seed(model_name))
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)
     if not hasattr(pipe, "_safety_probed"):

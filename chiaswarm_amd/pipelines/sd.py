@@ -80,6 +80,14 @@ class Family:
         return self.pipeline_class == "StableDiffusionInstructPix2PixPipeline" or (
             self.unet.in_channels == 8 and self.pipeline_class != "StableDiffusionInpaintPipeline")
 
+    @property
+    def is_depth(self) -> bool:  # StableDiffusionDepth2ImgPipeline: latents + 1 depth channel
+        return self.unet.in_channels == 5
+
+    @property
+    def is_image_variation(self) -> bool:  # CLIP image embedding as the only context token
+        return self.pipeline_class == "StableDiffusionImageVariationPipeline"
+
     def scheduler_kwargs(self) -> dict:
         kw = dict(self.sched_config)
         kw["prediction_type"] = self.prediction_type
@@ -125,7 +133,18 @@ FAMILIES = {
     "sdxl-refiner": Family("sdxl-refiner", unet_mod.SDXL_REFINER, vae_mod.SDXL_VAE, [clip_mod.OPENCLIP_BIGG],
                            pad_with_eos=False, default_size=1024, pipeline_class="StableDiffusionXLImg2ImgPipeline",
                            text_names=("text_encoder_2",), aesthetics=True),
+    # StableDiffusionDepth2ImgPipeline (stabilityai/stable-diffusion-2-depth) and
+    # StableDiffusionImageVariationPipeline (lambdalabs/sd-image-variations-diffusers:
+    # no text encoder, CLIP ViT-L/14 image embedding as the context): pipelines/variants.py
+    "sd2-depth": Family("sd2-depth", unet_mod.DEPTH_SD2, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H], pad_with_eos=False,
+                        pipeline_class="StableDiffusionDepth2ImgPipeline"),
+    "sd15-imagevar": Family("sd15-imagevar", unet_mod.SD15, vae_mod.SD_VAE, [],
+                            pipeline_class="StableDiffusionImageVariationPipeline"),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
+    "tiny-depth": Family("tiny-depth", unet_mod.TINY_DEPTH, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64,
+                         pipeline_class="StableDiffusionDepth2ImgPipeline"),
+    "tiny-imagevar": Family("tiny-imagevar", unet_mod.TINY, vae_mod.TINY_VAE, [], default_size=64,
+                            pipeline_class="StableDiffusionImageVariationPipeline"),
     "tiny-xl": Family("tiny-xl", unet_mod.TINY_XL, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT, clip_mod.TINY_TEXT_G],
                       default_size=64, pipeline_class="StableDiffusionXLPipeline", force_zeros=True),
     "tiny-xl-refiner": Family("tiny-xl-refiner", unet_mod.TINY_XL_REFINER, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT_G],
@@ -140,7 +159,11 @@ def family_for_model(model_name: str) -> str:
     checkpoint is built from its own config files (``resolve_family``)."""
     n = model_name.lower()
     if n.startswith("tiny/") or n == "tiny":
-        return "tiny"
+        return "tiny-depth" if "depth" in n else ("tiny-imagevar" if "variation" in n else "tiny")
+    if "image-variations" in n:
+        return "sd15-imagevar"
+    if "stable-diffusion-2-depth" in n:
+        return "sd2-depth"
     if "instruct-pix2pix" in n:
         return "pix2pix"
     if "xl" in n and "refiner" in n:
@@ -188,6 +211,7 @@ class StableDiffusion:
     def __init__(self, family: "str | Family", device="cpu", dtype=None, seed=0, weights_dir=None,
                  with_encoder=True, controlnet=None):
         self.family = FAMILIES[family] if isinstance(family, str) else family
+        self.weights_dir = weights_dir
         self.device = torch.device(device)
         if dtype is None:
             dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
@@ -502,7 +526,7 @@ class StableDiffusion:
                  num_images_per_prompt=1, height=None, width=None, generator=None, image=None,
                  mask_image=None, strength=0.8, image_guidance_scale=None, scheduler=None,
                  controlnet_conditioning_scale=1.0, output_type="pil", latents=None, eta=0.0, cfg_split=None,
-                 **unexpected):
+                 depth_map=None, **unexpected):
         aesthetic = (float(unexpected.pop("aesthetic_score", 6.0)),
                      float(unexpected.pop("negative_aesthetic_score", 2.5))) if self.family.aesthetics else None
         if unexpected:  # the diffusers call raises on unknown kwargs too (a retryable job error)
@@ -590,6 +614,14 @@ class StableDiffusion:
             if hasattr(sched, "_i"):
                 sched._i = start
             x = sched.add_noise(init_latents, noise, start)
+            if self.family.is_depth:
+                # Depth2Img: the [-1, 1]-normalised depth of the input at latent
+                # size is the UNet's fifth input channel (CFG-duplicated)
+                from .variants import depth_latents
+
+                d = depth_latents(self, image[:1] * b if len(image) < b else image, lh, lw, depth_map)
+                image_latents = torch.cat([d] * (2 if cfg else 1), 0)
+                init_latents = None
             if mask_image is not None:
                 m = np.asarray(mask_image.convert("L").resize((lw, lh), Image.Resampling.NEAREST),
                                dtype=np.float32) / 255.0
