@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--guidance", type=float, default=7.5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--through-supervisor", action="store_true",
+                    help="drive the real serving path: a fake hive -> Supervisor -> per-GPU ProcessExecutor "
+                         "children -> router -> pipeline -> encoder -> result POST")
     a = ap.parse_args()
     fam, res, steps, batch, _, _ = CONFIGS[a.config]
     a.family = a.family or fam
@@ -133,8 +136,98 @@ def spawn_ranks(args) -> int:
     return rc
 
 
+def supervisor_bench(args) -> int:
+    """``--through-supervisor``: the config's jobs through the production
+    serving path (reference loop: swarm/worker.py:113-163) — an in-process fake
+    hive serves them over HTTP, the Supervisor polls it, one ProcessExecutor
+    child per GPU runs router -> pipeline -> JPEG envelope, results are POSTed
+    back.  This process never touches the GPU.  ``value`` = images/s from the
+    first timed poll to the last result POST; p50 = the jobs' own start ->
+    envelope time (pipeline_config timings), as in the direct bench."""
+    import asyncio
+    import tempfile
+
+    root = tempfile.mkdtemp(prefix="csk_supbench_")
+    os.environ.setdefault("SDAAS_ROOT", root)
+    os.environ["SDAAS_TIMINGS"] = "1"
+    from chiaswarm_amd.hive.fake import FakeHive
+    from chiaswarm_amd.runtime.worker import ProcessExecutor, Supervisor, group_envs
+    from chiaswarm_amd.settings import Settings
+
+    fam, res, steps, batch = args.family, args.res, args.denoise_steps, args.batch
+    model = {"sd21": "stabilityai/stable-diffusion-2-1-base", "sdxl": "stabilityai/stable-diffusion-xl-base-1.0",
+             "tiny": "tiny/sd"}.get(fam, fam)
+    prompts = ["a photograph of an astronaut riding a horse", "a watercolor fox in a snowy forest",
+               "a cyberpunk city street at night, neon", "a bowl of ramen, studio lighting"]
+
+    def jobs(n, tag):
+        return [{"id": f"{tag}{i}", "model_name": model, "prompt": prompts[i % 4],
+                 "negative_prompt": "blurry, low quality", "num_inference_steps": steps, "guidance_scale": args.guidance,
+                 "num_images_per_prompt": batch, "height": res, "width": res, "seed": 1000 + i,
+                 "content_type": "image/jpeg", "parameters": {"scheduler_type": "DPMSolverMultistepScheduler"}}
+                for i in range(n)]
+
+    hive = FakeHive().start()
+    st = Settings()
+    st.sdaas_uri, st.sdaas_token = hive.base, "bench"
+    st.preload = model
+    st.max_batch = 1
+    n = args.gpus
+    devs = ["cpu"] * n if args.device == "cpu" else list(range(n))
+    exs = [ProcessExecutor(g, env=e) for g, e in zip(devs, group_envs(n, st))]
+    try:
+        sup = Supervisor(st, executors=exs)
+
+        async def phase(js):
+            hive.jobs = list(js)
+            before = len(hive.results)
+            t0 = time.monotonic()
+            await sup.run(max_polls=1)
+            return t0, hive.results[before:], hive.result_times[before:]
+
+        async def both():
+            await phase(jobs(max(args.warmup, 1) * n, "w"))  # model load, graph capture
+            return await phase(jobs(args.steps * n, "t"))
+
+        t0, results, times = asyncio.run(both())
+    finally:
+        for e in exs:
+            e.close()
+        hive.stop()
+    bad = [r for r in results if not r.get("artifacts") or "error" in (r.get("pipeline_config") or {})]
+    if bad or len(results) != args.steps * n:
+        print(f"bench: {len(bad)} failed / {len(results)} results: "
+              f"{(bad[0].get('pipeline_config') if bad else None)}", file=sys.stderr)
+        return 1
+    elapsed = max(times) - t0
+    lat = [r["pipeline_config"]["timings"]["total"] for r in results if "timings" in r["pipeline_config"]]
+    ips = batch * len(results) / elapsed
+    rec = {
+        "metric": CONFIGS[args.config][4], "value": round(ips, 4), "unit": "images/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if args.device == "cpu" else "bf16",
+        "data": "synthetic prompts, random-init weights (no checkpoints offline)",
+        "config": {"model": (CONFIGS[args.config][5] if fam == CONFIGS[args.config][0]
+                             else f"{fam} (not the {args.config} config)"),
+                   "bench_config": args.config, "global_batch": batch * n,
+                   "seq_len": (res // 8) ** 2, "parallelism": f"dp{n}", "resolution": f"{res}x{res}",
+                   "denoise_steps": steps, "guidance_scale": args.guidance},
+        "path": "fake hive HTTP -> Supervisor -> ProcessExecutor child -> router -> StableDiffusion -> "
+                "JPEG envelope -> POST /api/results",
+        "p50_job_latency_ms": round(1000 * statistics.median(lat), 1) if lat else None,
+        "p50_job_latency_note": "child job start -> result envelope (pipeline_config timings.total)",
+        "result_interarrival_ms_p50": round(1000 * statistics.median(
+            [b - a for a, b in zip(sorted(times), sorted(times)[1:])]), 1) if len(times) > 1 else None,
+    }
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.through_supervisor:
+        return supervisor_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args)
     # result encoders are separate processes, started before this process touches the GPU

@@ -68,3 +68,20 @@ def test_sdxl_config_two_ranks_cpu():
     assert rec["config"]["global_batch"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert len(rec["ms_per_step_per_rank"]) == 2 and max(rec["ms_per_step_per_rank"]) <= rec["ms_per_step"] + 1e-6
     assert rec["model_load_read_s"] >= 0 and rec["model_load_all_gather_s"] > 0
+
+
+def test_bench_through_supervisor_cpu(tmp_path):
+    """``--through-supervisor``: the jobs go fake hive ->
+    Supervisor -> ProcessExecutor child -> router -> pipeline -> envelope ->
+    POST, and the JSON line reports the serving path's images/s and p50."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["SDAAS_ROOT"] = str(tmp_path)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--through-supervisor", "--device", "cpu",
+                        "--family", "tiny", "--steps", "3", "--warmup", "1", "--denoise-steps", "2", "--res", "64",
+                        "--batch", "2"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["p50_job_latency_ms"] > 0
+    assert "Supervisor" in rec["path"] and rec["config"]["global_batch"] == 2
