@@ -186,6 +186,9 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         jid = job.get("id")
         try:
             result = synchronous_do_work_function(job, device)
+            # the device part is done: the supervisor may hand over the next job
+            # while this one's envelope is still being encoded (post)
+            outbox.put((gpu_index, f"__gpu_done__:{jid}", None, None))
             post(jid, result)
         except BaseException as e:  # never let the loop die silently
             outbox.put((gpu_index, jid, None, f"{e}\n{traceback.format_exc()}"))

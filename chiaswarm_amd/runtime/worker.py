@@ -83,6 +83,7 @@ class ProcessExecutor:
         self.ctx = mp.get_context("spawn")
         self.name = f"gpu{gpu_index}"
         self.pending: dict = {}
+        self.gpu_done: dict = {}  # job id -> asyncio.Event set when the child's device part is done
         self.loop = None
         self.restarts = 0
         self.ready = threading.Event()
@@ -118,6 +119,11 @@ class ProcessExecutor:
                 self.ready_info = f"{info.get('desc')} [{_group_str(self.group)}]"
                 self.ready.set()
                 print(f"Started device {self.ready_info}")
+                continue
+            if isinstance(jid, str) and jid.startswith("__gpu_done__:"):
+                ev = self.gpu_done.pop(jid[len("__gpu_done__:"):], None)
+                if ev is not None and self.loop is not None:
+                    self.loop.call_soon_threadsafe(ev.set)
                 continue
             if jid == "__regrouped__" and result is not None:
                 self.group = dict(result)
@@ -186,18 +192,25 @@ class ProcessExecutor:
         self.group = dict(res or {})
         return self.group
 
-    async def run(self, job):
+    async def run(self, job, gpu_done: asyncio.Event | None = None):
+        """Run one job; ``gpu_done`` (optional) is set as soon as the child's
+        device part has finished (its envelope may still be encoding)."""
         from .generator import _error_result
 
         self.loop = asyncio.get_running_loop()
         fut = self.loop.create_future()
         jid = job.get("id")
         self.pending[jid] = fut
+        if gpu_done is not None:
+            self.gpu_done[jid] = gpu_done
         self.inbox.put(job)
         t0 = time.monotonic()
         while True:
             done, _ = await asyncio.wait({fut}, timeout=2.0)
             if done:
+                self.gpu_done.pop(jid, None)
+                if gpu_done is not None:
+                    gpu_done.set()
                 result, err = fut.result()
                 if result is not None:
                     return result
@@ -207,6 +220,9 @@ class ProcessExecutor:
                 why = "crashed" if not self.proc.is_alive() else "timed out"
                 logging.error(f"{self.name} {why} on job {jid}; restarting")
                 self.pending.pop(jid, None)
+                self.gpu_done.pop(jid, None)
+                if gpu_done is not None:
+                    gpu_done.set()
                 self._restart()
                 return _error_result(jid, RuntimeError(f"GPU worker {why}"), job.get("content_type", "image/jpeg"),
                                      False)
@@ -639,6 +655,7 @@ class Supervisor:
             batch = self._drain_compatible(job)
             self.busy += len(batch)
             helpers = []
+            deferred = None  # a single job whose envelope is still encoding in the child
             try:
                 async with lock:  # a split job may hold this executor as a helper
                     if len(batch) == 1:
@@ -646,6 +663,16 @@ class Supervisor:
                         if helpers:
                             self.busy += len(helpers)
                             results = [await self._run_split(job, [ex] + helpers)]
+                        elif isinstance(ex, ProcessExecutor):
+                            # pipelined: the next job goes to the child as soon as this
+                            # one's device part is done; its envelope (JPEG / base64 /
+                            # sha256, encoder processes) finishes meanwhile
+                            ev = asyncio.Event()
+                            deferred = asyncio.ensure_future(ex.run(job, gpu_done=ev))
+                            waiter = asyncio.ensure_future(ev.wait())
+                            await asyncio.wait({deferred, waiter}, return_when=asyncio.FIRST_COMPLETED)
+                            waiter.cancel()
+                            results = []
                         else:
                             results = [await ex.run(job)]
                     else:
@@ -658,8 +685,26 @@ class Supervisor:
             finally:
                 for h in helpers:
                     self.locks[id(h)].release()
-                self.busy -= len(batch) + len(helpers)
-                self.work_queue.task_done()
+                if deferred is None:
+                    self.busy -= len(batch) + len(helpers)
+                    self.work_queue.task_done()
+                else:
+                    asyncio.ensure_future(self._finish_deferred(deferred, job))
+
+    async def _finish_deferred(self, task, job):
+        """Queue the result of a pipelined job once its envelope is ready."""
+        from .generator import _error_result
+
+        try:
+            try:
+                result = await task
+            except Exception as e:
+                logging.exception(e)
+                result = _error_result(job.get("id"), e, job.get("content_type", "image/jpeg"), False)
+            await self.result_queue.put(result)
+        finally:
+            self.busy -= 1
+            self.work_queue.task_done()
 
     async def result_worker(self):
         while True:
