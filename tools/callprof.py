@@ -1,5 +1,7 @@
 #!/usr/bin/env python
-"""Exact per-call kernel time of one SD2.1 UNet step (CFG batch 8, 64x64; or\n``--model sdxl --batch 2``: the SDXL 1024-px CFG-batch-2 step):
+"""Exact per-call kernel time of one SD2.1 UNet step (CFG batch 8, 64x64; or
+``--model sdxl --batch 2``: the SDXL 1024-px CFG-batch-2 step; ``--model
+controlnet``: SD1.5 + ControlNet at 64x64, config #4):
 every libcsk call is followed by a 1-element int32 fill, so in a rocprofv3
 kernel trace the separator kernels split the dispatch stream into calls; the
 calls' shapes are recorded on the host in the same order.  No host syncs, so
@@ -36,13 +38,24 @@ def record(path, batch, iters, dup=True, model="sd21"):
 
     _lib.load()
     dev = torch.device("cuda", 0)
+    if model == "esrgan":  # Real-ESRGAN x4plus 512 -> 2048 (config #5): one upscale per "step"
+        from chiaswarm_amd.models.rrdbnet import RRDBNet
+
+        with torch.device(dev):
+            net = RRDBNet().to(torch.bfloat16).eval().requires_grad_(False)
+        init_random_fast_(net, seed=0)
+        prepare_model(net)
+        img = torch.rand(1, 512, 512, 3, device=dev)
+        return _record_steps(path, iters, lambda: net(img), flops_of, _lib)
     sdxl = model == "sdxl"
-    cfg, lat, cdim = (unet_mod.SDXL, 128, 2048) if sdxl else (unet_mod.SD21, 64, 1024)
+    cn = model == "controlnet"
+    cfg, lat, cdim = ((unet_mod.SDXL, 128, 2048) if sdxl else (unet_mod.SD15, 64, 768) if cn
+                      else (unet_mod.SD21, 64, 1024))
     with torch.device(dev):
         m = unet_mod.UNet2DConditionModel(cfg).to(torch.bfloat16).eval().requires_grad_(False)
     init_random_fast_(m, seed=0)
     prepare_model(m)
-    dup = dup and not sdxl  # SDXL's halves differ in the pooled text embedding (no shared prefix)
+    dup = dup and not sdxl and not cn  # SDXL's halves differ in the pooled text embedding; ControlNet: no prefix
     x = torch.randn(batch // 2 if dup else batch, lat, lat, 4, device=dev).to(torch.bfloat16)
     if dup:  # identical CFG halves and the shared prefix, as in the product loop
         x = torch.cat([x, x])
@@ -50,12 +63,38 @@ def record(path, batch, iters, dup=True, model="sd21"):
     kv = m.encode_context(ctx)
     t = torch.tensor([500.0], device=dev)
     kw = {"cfg_dup": dup}
+    step = None
+    if cn:  # SD1.5 + ControlNet (config #4): the encoder copy + zero convs merged into the skips
+        from chiaswarm_amd.models.controlnet import ControlNetModel
+        from chiaswarm_amd.pipelines.controlnet import ControlFeatures
+
+        with torch.device(dev):
+            cnm = ControlNetModel(cfg).to(torch.bfloat16).eval().requires_grad_(False)
+        init_random_fast_(cnm, seed=1)
+        prepare_model(cnm)
+        with torch.no_grad():
+            cond_emb = cnm.embed_cond(torch.rand(batch, 8 * lat, 8 * lat, 3, device=dev))
+            cn_kv = cnm.encode_context(ctx)
+
+        def step():
+            feats, mid = cnm.features(x, t, cond_emb, cross_kv=cn_kv)
+            return m(x, t, cross_kv=kv, control=ControlFeatures(cnm, feats, mid, 1.0), **kw)
     if sdxl:
         kw["added_cond"] = {"text_embeds": torch.randn(batch, 1280, device=dev).to(torch.bfloat16),
                             "time_ids": torch.tensor([[1024.0, 1024, 0, 0, 1024, 1024]] * batch, device=dev)}
+    if step is None:
+        def step():
+            return m(x, t, cross_kv=kv, **kw)
+    return _record_steps(path, iters, step, flops_of, _lib)
+
+
+def _record_steps(path, iters, step, flops_of, _lib):
+    import torch
+
+    dev = torch.device("cuda", 0)
     with torch.no_grad():
         for _ in range(2):
-            m(x, t, cross_kv=kv, **kw)
+            step()
     torch.cuda.synchronize()
     sep = torch.zeros(1, dtype=torch.int32, device=dev)
     orig = _lib.call
@@ -70,7 +109,7 @@ def record(path, batch, iters, dup=True, model="sd21"):
     _lib.call = wrapped
     with torch.no_grad():
         for _ in range(iters):
-            m(x, t, cross_kv=kv, **kw)
+            step()
     torch.cuda.synchronize()
     _lib.call = orig
     with open(path, "w") as f:
@@ -146,7 +185,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-cfg-dup", action="store_true")
-    ap.add_argument("--model", default="sd21", choices=("sd21", "sdxl"), help="sdxl: 128x128 latents (1024 px)")
+    ap.add_argument("--model", default="sd21", choices=("sd21", "sdxl", "controlnet", "esrgan"),
+                    help="sdxl: 128x128 latents (1024 px); controlnet: SD1.5 + ControlNet (config #4)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if a.record:

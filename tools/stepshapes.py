@@ -40,6 +40,12 @@ def flops_of(name, a):
     if name == "csk_xattn_block":
         M, C, rpb, Bc, Skv = a[9:14]
         return (f"xattn block M{M} C{C} Skv{Skv}", 2.0 * M * C * C * 2 + 4.0 * M * Skv * C, None)
+    if name == "csk_conv_tile":  # persistent halo-tile 3x3 conv (conv_tile.hip)
+        B, H, W, Cin, Cout = a[5:10]
+        return f"conv-tile B{B} {H}x{W} s1 {Cin}->{Cout} k3", 2.0 * B * H * W * Cout * 9 * Cin, None
+    if name == "csk_ff_geglu":  # fused feed-forward (ff.hip)
+        M, C, inner = a[8:11]
+        return f"ff fused M{M} C{C} I{inner}", 2.0 * M * C * 2 * inner + 2.0 * M * inner * C, None
     return name, 0.0, None
 
 
