@@ -721,25 +721,27 @@ def loop_prologue(counter, cur, t_tab, t_out):
     _lib.call("csk_loop_prologue", _p(counter), _p(cur), _p(t_tab), _p(t_out), t_tab.numel(), _s())
 
 
-def sched_loop(e, x, x0prev, noise_tab, cur, coef, x_in, mode):
+def sched_loop(e, x, x0prev, noise_tab, cur, coef, x_in, mode, reps=None):
     """Tail of a device-resident sampler step (elementwise.hip sched_loop_kernel):
     CFG combine (mode 0 none, 1 [u, c], 2 pix2pix [c, i, u]) + the linear update
     with the coefficients of step ``cur`` from the device table ``coef``
     [n, LOOP_COEF_STRIDE] (guidance scales in the row),
     x / x0prev updated in place, the next UNet input written into ``x_in``
-    ([nrep * B, H, W, Cin] bf16, channels 0..3 of every replica)."""
+    ([reps * B, H, W, Cin] bf16, channels 0..3 of every replica; reps defaults
+    to the CFG replica count, 1 for a CFG-parallel half)."""
     _bf16(e, "sched_loop.e")
     _bf16(x_in, "sched_loop.x_in")
     nrep = mode + 1
+    reps = nrep if reps is None else int(reps)
     B, H, W, C = x.shape
     if C != 4 or x.dtype != torch.float32 or not x.is_contiguous() or not x0prev.is_contiguous() \
             or x0prev.shape != x.shape or x0prev.dtype != torch.float32:
         raise ValueError("sched_loop: x / x0prev must be contiguous fp32 [B, H, W, 4]")
     if e.numel() != nrep * x.numel() or not e.is_contiguous():
         raise ValueError(f"sched_loop: model output {tuple(e.shape)} vs {nrep} x {tuple(x.shape)}")
-    if x_in.dim() != 4 or x_in.shape[0] != nrep * B or x_in.shape[1:3] != (H, W) or x_in.shape[3] < 4 \
+    if x_in.dim() != 4 or x_in.shape[0] != reps * B or x_in.shape[1:3] != (H, W) or x_in.shape[3] < 4 \
             or not x_in.is_contiguous():
-        raise ValueError(f"sched_loop: x_in {tuple(x_in.shape)} for {nrep} x {tuple(x.shape)}")
+        raise ValueError(f"sched_loop: x_in {tuple(x_in.shape)} for {reps} x {tuple(x.shape)}")
     if coef.dtype != torch.float32 or coef.dim() != 2 or coef.shape[1] != LOOP_COEF_STRIDE \
             or cur.dtype != torch.int32:
         raise ValueError("sched_loop: coef must be fp32 [n, LOOP_COEF_STRIDE], cur int32")
@@ -747,7 +749,7 @@ def sched_loop(e, x, x0prev, noise_tab, cur, coef, x_in, mode):
                                   noise_tab.numel() != coef.shape[0] * x.numel()):
         raise ValueError("sched_loop: noise table must be fp32 [n, B, H, W, 4]")
     _lib.call("csk_sched_loop", _p(e), _p(x), _p(x0prev), _p(noise_tab), _p(cur), _p(coef), _p(x_in),
-              x_in.shape[3], nrep, B * H * W, mode, _s())
+              x_in.shape[3], reps, B * H * W, mode, _s())
 
 
 def vae_postprocess(img):

@@ -261,6 +261,26 @@ def cfg_handshake(peer: int, ok: bool = True) -> bool:
     return int(other.item()) > 0
 
 
+def exchange_cfg_half_into(e_full: torch.Tensor, peer: int, half: int):
+    """In-place form for the graph-resident CFG-parallel loop: ``e_full``
+    [2B, ...] holds this rank's half in rows [half*B, (half+1)*B); the peer's
+    half is received into the other rows.  On RCCL the send / receive are
+    enqueued on the current stream (their ``wait`` orders the stream, the host
+    never blocks); on gloo the halves go through the host."""
+    b = e_full.shape[0] // 2
+    mine, other = e_full[half * b:(half + 1) * b], e_full[(1 - half) * b:(2 - half) * b]
+    dev = group_device()
+    if dev.type == e_full.device.type:
+        ops = [dist.P2POp(dist.isend, mine, peer), dist.P2POp(dist.irecv, other, peer)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        return
+    m, o = mine.to(dev).contiguous(), torch.empty(other.shape, dtype=other.dtype, device=dev)
+    for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, m, peer), dist.P2POp(dist.irecv, o, peer)]):
+        r.wait()
+    other.copy_(o)
+
+
 def exchange_cfg_half(e: torch.Tensor, peer: int, half: int) -> torch.Tensor:
     """This rank's noise prediction for its CFG half <-> the peer's (one
     send + one receive, posted together): returns [uncond; cond] on e's device.

@@ -430,6 +430,10 @@ class StableDiffusion:
         b = x.shape[0]
         kv = [t[h * b:(h + 1) * b] for t in cross_kv]
         add_h = {k: v[h * b:(h + 1) * b] for k, v in added.items()} if added is not None else None
+        if self._loop_ok():
+            table = sched.loop_table()
+            if table is not None and len(table[0]) > 0:
+                return self._denoise_loop_split(x, sched, table, kv, guidance, add_h, generator, peer, h)
         while sched.step_index < sched.n:
             t = sched.current_t()
             xi = (x * sched.current_scale()).to(self.dtype)
@@ -501,6 +505,58 @@ class StableDiffusion:
         gph.prepare(x_in, cross_kv, added, control, req=getattr(self, "_req", None))
         for _ in range(n):
             gph.graph.replay()
+        sched.step_index = sched.n
+        sched.prev_x0 = L.x0prev.clone()
+        return L.x.clone()
+
+    def _denoise_loop_split(self, x, sched, table, kv, guidance, added, generator, peer, h):
+        """Device-resident CFG-parallel loop: per step ONE replay of this half's
+        step graph [loop prologue, UNet at batch b, its prediction into its rows
+        of the full CFG prediction], the swap with the peer enqueued on the
+        stream (RCCL: no host sync), ONE replay of the update graph
+        [sched_loop: CFG combine + sampler update + the next bf16 input of this
+        half].  Both ranks apply the same update to the same predictions, so
+        their latents stay bit-identical with no further traffic."""
+        from ..parallel import comm
+
+        ts, rows, s0 = table
+        n = len(ts)
+        need_noise = any(r[5] != 0.0 for r in rows)
+        x_in = (x * s0).to(self.dtype)
+        share = False  # this half binds a row slice of the static K/V: own copies
+        cap = max(64, -(-n // 64) * 64)
+        key = ("loop-split", h, x_in.shape, added is not None, len(kv), need_noise)
+        gph = self._graphs.get(key)
+        if gph is not None and gph.loop_cap < n:
+            gph = None
+        if gph is None:
+            spec = _LoopSpec(tuple(x.shape), 1, cap, need_noise, x.device)
+            gph = _SplitStepGraph(self.unet, x_in, kv, added, h, spec, share_kv=share)
+            self._graphs[key] = gph
+        L = gph.loop
+        from ..ops import hip_ops
+
+        coef = torch.zeros((n, hip_ops.LOOP_COEF_STRIDE), dtype=torch.float32)
+        coef[:, :7] = torch.tensor(rows, dtype=torch.float64).float()
+        coef[:, 7] = float(guidance)
+        L.coef[:n].copy_(coef.to(self.device, non_blocking=False))
+        L.t_tab[:n].copy_(torch.tensor(ts, dtype=torch.float32).to(self.device))
+        if need_noise:
+            for i, r in enumerate(rows):
+                if r[5] != 0.0:
+                    L.noise[i].copy_(batch_randn(x.shape, generator, x.device))
+        L.x.copy_(x)
+        if sched.prev_x0 is not None:
+            L.x0prev.copy_(sched.prev_x0)
+        else:
+            L.x0prev.zero_()
+        L.counter.zero_()
+        gph.fill_temb(L.t_tab[:n])
+        gph.prepare(x_in, kv, added, None, req=getattr(self, "_req", None))
+        for _ in range(n):
+            gph.graph.replay()
+            comm.exchange_cfg_half_into(gph.e_full, peer, h)
+            gph.update.replay()
         sched.step_index = sched.n
         sched.prev_x0 = L.x0prev.clone()
         return L.x.clone()
@@ -808,6 +864,43 @@ class _UNetGraph:
 
     def _new_request(self, cc):
         pass
+
+
+class _SplitStepGraph(_UNetGraph):
+    """A CFG-parallel half's sampler step as two hipGraphs around the
+    prediction swap: ``graph`` = [loop prologue, UNet on this half's b rows, its
+    prediction copied into rows [h*b, (h+1)*b) of the static ``e_full``];
+    ``update`` = [sched_loop over the full [u; c] prediction, writing this
+    half's next bf16 input]."""
+
+    def __init__(self, unet, x_in, cross_kv, added, half, loop, share_kv=False):
+        self.half = half
+        b = x_in.shape[0]
+        self.e_full = torch.zeros((2 * b,) + tuple(x_in.shape[1:3]) + (unet.cfg.out_channels,), dtype=x_in.dtype,
+                                  device=x_in.device)
+        super().__init__(unet, x_in, cross_kv, added, share_kv=share_kv, loop=loop)
+        from ..ops import hip_ops
+
+        L = self.loop
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            hip_ops.sched_loop(self.e_full, L.x.clone(), L.x0prev.clone(), L.noise, L.cur, L.coef, self.x.clone(), 1,
+                               reps=1)
+        torch.cuda.current_stream().wait_stream(s)
+        self.update = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.update):
+            hip_ops.sched_loop(self.e_full, L.x, L.x0prev, L.noise, L.cur, L.coef, self.x, 1, reps=1)
+
+    def _fwd(self):
+        from ..ops import hip_ops
+
+        L = self.loop
+        hip_ops.loop_prologue(L.counter, L.cur, L.t_tab, self.t)
+        e = self._unet_fwd()
+        b = self.x.shape[0]
+        self.e_full[self.half * b:(self.half + 1) * b].copy_(e)
+        return e
 
 
 class _ControlUNetGraph(_UNetGraph):

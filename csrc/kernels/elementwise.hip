@@ -254,7 +254,9 @@ __global__ void sched_loop_kernel(const bf16_t* __restrict__ e, float* __restric
 CSK_API int csk_sched_loop(const void* e, void* x, void* x0prev, const void* noise_tab, const void* cur,
                            const void* coef, void* xin, int cin, int nrep, long long npix, int mode,
                            hipStream_t stream) {
-  if (cin < 4 || nrep < 1 || nrep > 3 || npix <= 0 || mode < 0 || mode > 2 || (mode > 0 && mode + 1 != nrep))
+  // nrep = 1 with mode > 0: a CFG-parallel half (pipelines/sd.py _denoise_loop_split) combines the full
+  // prediction but feeds only its own UNet half
+  if (cin < 4 || nrep < 1 || nrep > 3 || npix <= 0 || mode < 0 || mode > 2 || (mode > 0 && nrep != 1 && mode + 1 != nrep))
     return (int)hipErrorInvalidValue;
   sched_loop_kernel<<<ew_grid((size_t)npix / 2 + 1), 256, 0, stream>>>(
       (const bf16_t*)e, (float*)x, (float*)x0prev, (const float*)noise_tab, (const int*)cur, (const float*)coef,
