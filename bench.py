@@ -217,6 +217,9 @@ def supervisor_bench(args) -> int:
                 "JPEG envelope -> POST /api/results",
         "p50_job_latency_ms": round(1000 * statistics.median(lat), 1) if lat else None,
         "p50_job_latency_note": "child job start -> result envelope (pipeline_config timings.total)",
+        "phase_ms_median": {k: round(1000 * statistics.median([r["pipeline_config"]["timings"][k] for r in results
+                                                                if k in r["pipeline_config"].get("timings", {})]), 2)
+                            for k in (results[0]["pipeline_config"].get("timings") or {})},
         "result_interarrival_ms_p50": round(1000 * statistics.median(
             [b - a for a, b in zip(sorted(times), sorted(times)[1:])]), 1) if len(times) > 1 else None,
     }
