@@ -58,10 +58,10 @@ class Conv2d(nn.Conv2d, Prepared):
         return self.wp
 
     def forward(self, x, residual=None, up2x=False, bias2d=None, padding=None, act=None, out_scale=1.0,
-                out=None, gn_stats=False, row_stats=False):  # type: ignore[override]
+                out=None, gn_stats=False, row_stats=False, residual2=None, res_scale=1.0):  # type: ignore[override]
         kh, kw = self.kernel_size
         if (kh == 1 and kw == 1 and self.stride == (1, 1) and not up2x and act is None and out_scale == 1.0
-                and out is None and x.is_contiguous()):
+                and out is None and x.is_contiguous() and residual2 is None and res_scale == 1.0):
             w2 = self.weight.view(self.out_channels, self.in_channels)
             gr = x.shape[1] * x.shape[2] if (gn_stats and bias2d is None and x.dim() == 4) else 0
             y = ops.gemm(x, w2, self.bias, residual=residual, gn_rows=gr, row_stats=row_stats and bias2d is None)
@@ -75,7 +75,7 @@ class Conv2d(nn.Conv2d, Prepared):
             pad = padding
         return ops.conv2d(x, self._wp(), self.bias, self.stride[0], pad, residual=residual,
                           up2x=up2x, bias2d=bias2d, act=act, out_scale=out_scale, out=out,
-                          dilation=max(self.dilation), gn_stats=gn_stats)
+                          dilation=max(self.dilation), gn_stats=gn_stats, residual2=residual2, res_scale=res_scale)
 
 
 class Conv1d(nn.Conv1d, Prepared):

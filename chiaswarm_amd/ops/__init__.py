@@ -416,7 +416,8 @@ def conv_out_size(h, w, kh, kw, stride, padding, up2x=False, dilation=1):
             (w + pl + pr - dilation * (kw - 1) - 1) // stride + 1)
 
 
-def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, dilation=1):
+def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, dilation=1,
+                residual2=None, res_scale=1.0):
     dt = _cdt(x)
     # NHWC tensor viewed as channels-last NCHW: no copies, MIOpen NHWC kernels
     xn = x.to(dt).permute(0, 3, 1, 2)
@@ -436,25 +437,34 @@ def _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, 
     if out_scale != 1.0:
         y = y * out_scale
     if residual is not None:
-        y = y + residual.to(dt)
+        y = y + (residual.to(dt) if res_scale == 1.0 else res_scale * residual.to(dt))
+    if residual2 is not None:
+        y = y + residual2.to(dt)
     return y.to(x.dtype).contiguous()
 
 
 def conv2d(x, wp, bias=None, stride=1, padding=1, residual=None, up2x=False, bias2d=None, act=None,
-           out_scale=1.0, out=None, dilation=1, gn_stats=False):
+           out_scale=1.0, out=None, dilation=1, gn_stats=False, residual2=None, res_scale=1.0, out_u8=False):
     """NHWC conv.  ``wp``: packed [Cout, kh, kw, Cin].  ``up2x`` fuses a
     nearest-neighbour x2 upsample into the input addressing; ``bias2d`` [B, Cout]
     is a per-sample channel bias (ResNet time-embedding add) fused in the
     epilogue; y = act(conv + bias + bias2d) * out_scale + residual.  ``x``,
     ``residual`` and ``out`` may be channel slices of wider NHWC buffers.
     ``gn_stats``: the HIP epilogue also emits the GroupNorm statistics of the
-    output (consumed by ``group_norm`` of that tensor; skips its stats pass)."""
+    output (consumed by ``group_norm`` of that tensor; skips its stats pass).
+    ``residual2`` / ``res_scale``: y = act(...) * out_scale + res_scale *
+    residual + residual2 (Real-ESRGAN's nested "* 0.2 + x" in one epilogue;
+    ``out`` may alias ``residual2``).  ``out_u8``: the output is a uint8 image,
+    round(clamp(y, 0, 1) * 255) (Real-ESRGAN's RGB conv_last)."""
     if use_hip(x):
         from . import hip_ops
 
         return hip_ops.conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation,
-                              gn_stats)
-    y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, dilation)
+                              gn_stats, residual2=residual2, res_scale=res_scale, out_u8=out_u8)
+    y = _ref_conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, dilation,
+                    residual2, res_scale)
+    if out_u8:
+        y = (y.float().clamp(0, 1) * 255).round().to(torch.uint8)
     if out is not None:
         out.copy_(y)
         return out

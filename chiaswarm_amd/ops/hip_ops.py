@@ -333,21 +333,29 @@ def _pix_stride(t):
     return ps
 
 
-# Persistent halo-tile conv for 3x3 / stride-1 / Cout = 32 (csrc/kernels/conv_tile.hip:
-# the Real-ESRGAN dense-block convs); CSK_CONV_TILE=0 keeps the implicit GEMM
-sig("csk_conv_tile_ok", c_int, c_int, c_int, c_int, c_int, c_int, c_int)
-sig("csk_conv_tile", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-    c_int, c_int, c_int, c_float, c_void_p)
+# Persistent halo-tile conv for 3x3 / stride-1 / Cout = 16 / 32 / 64 and < 16
+# (csrc/kernels/conv_tile.hip: the Real-ESRGAN dense-block convs, its x2
+# up-convs and RGB conv_last); CSK_CONV_TILE=0 keeps the implicit GEMM
+sig("csk_conv_tile_ok2", c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int)
+sig("csk_conv_tile2", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_void_p)
 CONV_TILE = os.environ.get("CSK_CONV_TILE", "1") == "1"
 CONV_TILE64 = os.environ.get("CSK_CONV_TILE64", "1") == "1"  # the Cout = 64 instance: 1.2x faster than the GEMM (profiles/conv_tile64_r5.txt)
+# Cout <= 16 (16-wide instance; e.g. the x4 upscaler's 64 -> 3 conv_last at 2048^2) on
+# maps of at least this many output pixels (below it the grid is a fraction of the chip)
+CONV_TILE_NARROW_MIN_PX = int(os.environ.get("CSK_CONV_TILE_NARROW_MIN_PX", str(1 << 18)))
 CONV_TILE_STATS = [0]  # calls (tests assert the kernel ran)
 
 
 def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_scale=1.0, out=None, dilation=1,
-           gn_stats=False):
+           gn_stats=False, residual2=None, res_scale=1.0, out_u8=False):
     """NHWC conv.  ``x``, ``residual`` and ``out`` may be channel-slice views of
     wider NHWC buffers (last dim contiguous): the kernel takes their pixel
-    strides, so dense/concat blocks need no copies."""
+    strides, so dense/concat blocks need no copies.  ``residual2`` /
+    ``res_scale`` (y = ... * out_scale + res_scale * residual + residual2, ``out``
+    may alias ``residual2``) run in the halo-tile kernel's epilogue, elsewhere as
+    one extra pass.  ``out_u8``: uint8 image output round(clamp(y, 0, 1) * 255)
+    (the halo-tile kernel stores it directly for Cout < 16)."""
     from . import conv_out_size, norm_padding
 
     _bf16(x, "conv.x")
@@ -368,6 +376,9 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     wp = wp.contiguous()
     pt, pl, pb, pr = norm_padding(padding)
     Ho, Wo = conv_out_size(H, W, kh, kw, stride, padding, up2x, dilation)
+    if out_u8:
+        return _conv2d_u8(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation,
+                          residual2, res_scale, Ho, Wo)
     if out is None:
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
     ys = _pix_stride(out)
@@ -400,19 +411,40 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
                   B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(bool(up2x)), xs, ys, rs, code,
                   float(out_scale), int(dilation), _p(part), tile, split, _p(ws), _s())
 
+    rs2 = 0
+    if residual2 is not None:
+        if residual2.shape != out.shape:
+            raise ValueError(f"conv2d residual2 {tuple(residual2.shape)} != {tuple(out.shape)}")
+        rs2 = _pix_stride(residual2)
+        if rs2 is None:
+            residual2 = residual2.contiguous()
+            rs2 = Cout
     key = f"c:{B}:{H}:{W}:{Cin}:{Cout}:{kh}:{stride}:{int(bool(up2x))}"
     if kh != kw or dilation != 1:
         key += f":{kw}:{dilation}"
+    narrow = Cout < 16
     if (CONV_TILE and kh == 3 and kw == 3 and stride == 1 and (pt, pl, pb, pr) == (1, 1, 1, 1) and dilation == 1
-            and not up2x and bias2d is None and not gn_stats
-            and code in (0, 2, 5, 6, 8, 9) and (Cout == 32 or CONV_TILE64)
-            and (residual is None or (rs % 4 == 0 and residual.data_ptr() % 8 == 0))
-            and _lib.call_int("csk_conv_tile_ok", B, H, W, Cin, Cout, xs, ys) > 0
-            and x.data_ptr() % 16 == 0 and out.data_ptr() % 8 == 0 and wp.data_ptr() % 16 == 0):
-        # narrow-output 3x3 (the Real-ESRGAN dense-block convs): persistent halo-tile kernel
-        _lib.call("csk_conv_tile", _p(out), _p(x), _p(wp), _p(bias), _p(residual), B, H, W, Cin, Cout, xs, ys, rs,
-                  code, float(out_scale), _s())
+            and bias2d is None and not gn_stats
+            and code in (0, 2, 5, 6, 8, 9)
+            and (Cout == 32 or (Cout == 64 and CONV_TILE64) or (Cout <= 16 and M >= CONV_TILE_NARROW_MIN_PX))
+            and (residual is None or (not narrow and rs % 4 == 0 and residual.data_ptr() % 8 == 0))
+            and (residual2 is None or (not narrow and rs2 % 4 == 0 and residual2.data_ptr() % 8 == 0))
+            and _lib.call_int("csk_conv_tile_ok2", B, Ho, Wo, Cin, Cout, xs, ys, int(bool(up2x))) > 0
+            and x.data_ptr() % 16 == 0 and (narrow or out.data_ptr() % 8 == 0) and wp.data_ptr() % 16 == 0):
+        # narrow-output 3x3 (the Real-ESRGAN convs): persistent halo-tile kernel
+        _lib.call("csk_conv_tile2", _p(out), _p(x), _p(wp), _p(bias), _p(residual), _p(residual2), B, Ho, Wo, Cin,
+                  Cout, xs, ys, rs, rs2, code, float(out_scale), float(res_scale), int(bool(up2x)), 0, _s())
         CONV_TILE_STATS[0] += 1
+        return out
+    if residual2 is not None or res_scale != 1.0:
+        # the implicit GEMM's epilogue has one unscaled residual: conv into a
+        # temporary, then one combining pass (residual2 is read before out is written)
+        y = conv2d(x, wp, bias, stride, padding, None, up2x, bias2d, act, out_scale, None, dilation)
+        if residual is not None:
+            y = torch.add(y, residual, alpha=res_scale) if res_scale != 1.0 else y + residual
+        if residual2 is not None:
+            y = y + residual2
+        out.copy_(y)
         return out
     tile, split = tuning.choose(key, M, Cout, K, run)
     seg = _gn_seg(tile, split, Ho * Wo, M, code, Cout) if gn_stats and ys == Cout else 0
@@ -421,6 +453,38 @@ def conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act=None, out_s
     if part is not None:
         out._csk_gn = (part, seg)
     return out
+
+
+def _conv2d_u8(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, out, dilation, residual2,
+               res_scale, Ho, Wo):
+    """conv2d with a uint8 image output (``out``: None or a contiguous uint8 [B, Ho, Wo, Cout])."""
+    from . import norm_padding
+
+    B, H, W, Cin = x.shape
+    Cout = wp.shape[0]
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), dtype=torch.uint8, device=x.device)
+    if out.dtype != torch.uint8 or out.shape != (B, Ho, Wo, Cout) or not out.is_contiguous():
+        raise ValueError("conv2d out_u8: out must be a contiguous uint8 [B, Ho, Wo, Cout]")
+    xs = _pix_stride(x)
+    if (CONV_TILE and Cout < 16 and residual is None and residual2 is None and bias2d is None and stride == 1
+            and wp.shape[1:3] == (3, 3) and norm_padding(padding) == (1, 1, 1, 1) and dilation == 1
+            and code_ok(act) and B * Ho * Wo >= CONV_TILE_NARROW_MIN_PX and xs is not None
+            and x.data_ptr() % 16 == 0 and wp.is_contiguous() and wp.data_ptr() % 16 == 0
+            and _lib.call_int("csk_conv_tile_ok2", B, Ho, Wo, Cin, Cout, xs, Cout, int(bool(up2x))) > 0):
+        _lib.call("csk_conv_tile2", _p(out), _p(x), _p(wp), _p(bias), None, None, B, Ho, Wo, Cin, Cout, xs, Cout,
+                  0, 0, ACT[act], float(out_scale), 1.0, int(bool(up2x)), 1, _s())
+        CONV_TILE_STATS[0] += 1
+        return out
+    y = conv2d(x, wp, bias, stride, padding, residual, up2x, bias2d, act, out_scale, None, dilation,
+               residual2=residual2, res_scale=res_scale)
+    out.copy_((y.float().clamp(0, 1) * 255).round().to(torch.uint8))
+    return out
+
+
+def code_ok(act):
+    """activations the halo-tile kernel's epilogue applies"""
+    return ACT[act] in (0, 2, 5, 6, 8, 9)
 
 
 sig("csk_axpby_nhwc", c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_float, c_float, c_int,

@@ -236,7 +236,9 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
             # must not send a second handshake into the peer's prediction exchange
             kwargs["cfg_split"] = state["cfg"] = {"peer": int(split["peer"]), "half": int(split["half"])}
         out_type = "uint8_device" if helper else ("latent" if cfg_part and int(split["half"]) == 1 else "pil")
+        t_pipe = time.perf_counter()
         p = pipe(scheduler=sched, **dict(kwargs, output_type=out_type))
+        t_post = time.perf_counter()
     finally:
         from ..models.lora import unload_lora, unload_textual_inversion
 
@@ -284,6 +286,9 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
     if os.environ.get("SDAAS_TIMINGS"):
         t = dict(p.timings or {})
         t["load"] = load_s
+        t["setup"] = t_pipe - t0 - load_s  # scheduler / split arguments
+        t["pipe_other"] = t_post - t_pipe - sum(v for k, v in (p.timings or {}).items())
+        t["envelope"] = time.perf_counter() - t_post  # images -> encoder pool submission
         config["timings"] = {k: round(v, 4) for k, v in t.items()}
     return results, config
 

@@ -80,27 +80,48 @@ def load_esrgan(model_name: str, device: str):
     return cache().get(("esrgan", model_name, device), make)
 
 
+_GRAPH_SHAPES = 4  # captured input shapes kept per network (each holds its activations' pool)
+
+
+def _run_u8(net: RRDBNet, x: torch.Tensor) -> torch.Tensor:
+    """uint8 [1, h, w, 3] device pixels -> uint8 [1, 4h, 4w, 3]: the whole
+    network as ONE hipGraph replay per input shape (350 launches per 512^2
+    upscale otherwise paid on the host), eager on CPU / reference mode."""
+    from .graphs import CapturedCall, graphs_enabled
+
+    if not graphs_enabled(x.device):
+        return net(x, u8_out=True)
+    graphs = net.__dict__.setdefault("_u8_graphs", {})
+    key = tuple(x.shape)
+    g = graphs.pop(key, None)
+    if g is None:
+        while len(graphs) >= _GRAPH_SHAPES:
+            graphs.pop(next(iter(graphs)))  # least recently used
+        g = CapturedCall(lambda x: net(x, u8_out=True), x=x)
+    graphs[key] = g  # most recently used last
+    return g.run(x=x)
+
+
 @torch.no_grad()
 def upscale_x4(net: RRDBNet, image: Image.Image, tile: int = 1024, overlap: int = 16) -> Image.Image:
     dev = net.conv_first.weight.device
-    arr = np.asarray(image.convert("RGB"), dtype=np.float32) / 255.0
+    arr = np.array(image.convert("RGB"))  # (writable: torch.from_numpy)
     h, w = arr.shape[:2]
-    x = torch.from_numpy(arr).to(dev)[None]
+    x = torch.from_numpy(arr).to(dev, non_blocking=False)[None]  # uint8 upload; scaled on the device
     s = net.scale
     if max(h, w) <= tile:
-        y = net(x)
+        y = _run_u8(net, x)
     else:
-        y = torch.empty(1, h * s, w * s, 3, device=dev, dtype=net.conv_first.weight.dtype)
+        y = torch.empty(1, h * s, w * s, 3, device=dev, dtype=torch.uint8)
         for y0 in range(0, h, tile):
             for x0 in range(0, w, tile):
                 ys, xs = max(0, y0 - overlap), max(0, x0 - overlap)
                 ye, xe = min(h, y0 + tile + overlap), min(w, x0 + tile + overlap)
-                out = net(x[:, ys:ye, xs:xe].contiguous())
+                out = _run_u8(net, x[:, ys:ye, xs:xe].contiguous())
                 oy, ox = (y0 - ys) * s, (x0 - xs) * s
                 th, tw = min(tile, h - y0) * s, min(tile, w - x0) * s
                 y[:, y0 * s:y0 * s + th, x0 * s:x0 * s + tw] = out[:, oy:oy + th, ox:ox + tw]
-    img = (y.float().clamp(0, 1) * 255).round().to(torch.uint8)[0].cpu().numpy()
-    return Image.fromarray(img)
+    return Image.fromarray(y[0].cpu().numpy())
 
 
 def esrgan_callback(device_identifier, model_name, **kwargs):

@@ -63,6 +63,7 @@ def synchronous_do_work_function(job, device):
         done("fatal", err=e)
         return _error_result(job_id, e, content_type, True)
     try:
+        t_dev = time.perf_counter()
         with trace_range(f"job {job_id}"):
             artifacts, pipeline_config = device(worker_function, **kwargs)
     except ValueError as e:  # (b) fatal
@@ -74,6 +75,7 @@ def synchronous_do_work_function(job, device):
         done("error", err=e)
         return _error_result(job_id, e, content_type, False)
     if isinstance(pipeline_config.get("timings"), dict):  # only with SDAAS_TIMINGS=1
+        pipeline_config["timings"]["route"] = round(t_dev - t0, 4)
         pipeline_config["timings"]["total"] = round(time.perf_counter() - t0, 4)
     done("ok", pipeline_config)
     return {"id": job_id, "artifacts": artifacts, "nsfw": pipeline_config.get("nsfw", False),

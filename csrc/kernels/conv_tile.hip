@@ -50,14 +50,14 @@ constexpr int CT_HSLOT = 384;              // halo pixel slots: 24 DMA instructi
 constexpr int CT_HALO = CT_HSLOT * 64;     // bytes per stage ([pixel][4 x 16 B])
 constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per chunk (3)
 
-// per output width NOUT (32 or 64): weight rows 9 x NOUT padded to whole
-// 8-wave x 16-row DMA rounds, ring depth (3 stages at 32: 144 KB; 2 at 64: 128 KB)
+// per output width NOUT (16, 32 or 64): weight rows 9 x NOUT padded to whole
+// 8-wave x 16-row DMA rounds, ring depth (3 stages at 16 / 32: 120 / 144 KB; 2 at 64: 128 KB)
 template <int NOUT>
 struct CtGeo {
   static constexpr int WROWS = (9 * NOUT + 127) / 128 * 128;  // 384 / 640
   static constexpr int WGT = WROWS * 64;                      // bytes per stage ([tap x cout][4 x 16 B])
   static constexpr int STAGE = CT_HALO + WGT;
-  static constexpr int S = NOUT == 32 ? 3 : 2;
+  static constexpr int S = NOUT == 64 ? 2 : 3;
   static constexpr int WI = WROWS / 16 / 8;                   // weight DMA instructions per wave per chunk (3 / 5)
   static constexpr int NF = NOUT / 16;                        // output fragments per pixel row
 };
@@ -73,9 +73,15 @@ struct ConvTileArgs {
   const bf16_t* bias;  // [NOUT] or null
   bf16_t* y;           // [B][H][W] pixels, pixel stride ldc, channels [0, NOUT)
   const bf16_t* zero;  // zero page (LDS-DMA source for padding)
-  const bf16_t* res;   // [B][H][W] pixels, pixel stride ldr, or null: y = act(conv + bias) * out_scale + res
-  int B, H, W, Cin, lda, ldc, act, ldr;
-  float out_scale;
+  const bf16_t* res;   // [B][H][W] pixels, pixel stride ldr, or null
+  const bf16_t* res2;  // [B][H][W] pixels, pixel stride ldr2, or null:
+                       // y = act(conv + bias) * out_scale + res_scale * res + res2
+  int B, H, W, Cin, lda, ldc, act, ldr, ldr2;
+  int Cout;            // <= NOUT: weight rows / bias / stores of channels >= Cout are skipped
+  int u8;              // narrow outputs only: store round(clamp(y, 0, 1) * 255) as uint8 (y: unsigned char*, stride ldc bytes)
+  int up;              // 1: nearest-x2 upsampled input (x is [B][H/2][W/2]); the halo reads input pixel (iy/2, ix/2)
+  int Wi;              // input row width in pixels (W, or W/2 with up)
+  float out_scale, res_scale;
   int tiles_x, tiles_y, ntiles;
 };
 
@@ -117,7 +123,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * NOUT + output channel
     const int tap = row / NOUT, co = row % NOUT;
     const int g = (lane & 3) ^ ((row >> 2) & 3);  // source channel group landing in this lane's slot
-    wsrc[i] = row < 9 * NOUT ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
+    wsrc[i] = row < 9 * NOUT && co < a.Cout ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
   }
   // ---- halo DMA: instruction k = wv * 3 + i writes halo pixels 16 k .. 16 k + 15 ----
   const bf16_t* hsrc[CT_HI];
@@ -133,7 +139,8 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
       const int iy = ty * CT_TH - 1 + hy, ix = tx * CT_TW - 1 + hx;
       const bool ok = hp < CT_HPX && iy >= 0 && iy < H && ix >= 0 && ix < W;
       const int g = (lane & 3) ^ ((hp >> 2) & 3);
-      hsrc[i] = ok ? a.x + ((size_t)(b * H + iy) * W + ix) * a.lda + g * 8 : a.zero;
+      const int sy = iy >> a.up, sx = ix >> a.up;  // (the input grid of an upsampled conv)
+      hsrc[i] = ok ? a.x + ((size_t)(b * (H >> a.up) + sy) * a.Wi + sx) * a.lda + g * 8 : a.zero;
     }
   };
   set_halo();
@@ -164,7 +171,10 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 #pragma unroll
   for (int j = 0; j < NF; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias[j][r] = a.bias ? bf2f(a.bias[j * 16 + fq * 4 + r]) : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      const int co = j * 16 + fq * 4 + r;
+      bias[j][r] = a.bias && co < a.Cout ? bf2f(a.bias[co]) : 0.f;
+    }
 
   auto epilogue = [&](int tile) {
     const int b = tile / (a.tiles_x * a.tiles_y);
@@ -178,13 +188,36 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
       if (x >= W) continue;
       bf16_t* op = a.y + ((size_t)(b * H + y) * W + x) * a.ldc;
       const bf16_t* rp = a.res ? a.res + ((size_t)(b * H + y) * W + x) * a.ldr : nullptr;
+      const bf16_t* rp2 = a.res2 ? a.res2 + ((size_t)(b * H + y) * W + x) * a.ldr2 : nullptr;
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
+        const int c0 = j * 16 + fq * 4;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[i][j][r] + bias[j][r]) * a.out_scale;
+        if (c0 + 4 > a.Cout) {  // narrow output (Cout < 16, e.g. RGB): element stores, no residuals
+          if (a.u8) {  // image output: the upscaler's uint8 pixels straight from the accumulators
+            unsigned char* ob = reinterpret_cast<unsigned char*>(a.y) + ((size_t)(b * H + y) * W + x) * a.ldc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (c0 + r < a.Cout) ob[c0 + r] = (unsigned char)__float2int_rn(fminf(fmaxf(v[r], 0.f), 1.f) * 255.f);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (c0 + r < a.Cout) op[c0 + r] = f2bf(v[r]);
+          }
+          continue;
+        }
         if (rp) {
-          const uint2 rr = *reinterpret_cast<const uint2*>(rp + j * 16 + fq * 4);
+          const uint2 rr = *reinterpret_cast<const uint2*>(rp + c0);
+          const float rs = a.res_scale;
+          v[0] += rs * __uint_as_float(rr.x << 16);
+          v[1] += rs * __uint_as_float(rr.x & 0xffff0000u);
+          v[2] += rs * __uint_as_float(rr.y << 16);
+          v[3] += rs * __uint_as_float(rr.y & 0xffff0000u);
+        }
+        if (rp2) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(rp2 + c0);
           v[0] += __uint_as_float(rr.x << 16);
           v[1] += __uint_as_float(rr.x & 0xffff0000u);
           v[2] += __uint_as_float(rr.y << 16);
@@ -193,7 +226,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
         uint2 wd;
         wd.x = pack2(v[0], v[1]);
         wd.y = pack2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(op + j * 16 + fq * 4) = wd;
+        *reinterpret_cast<uint2*>(op + c0) = wd;
       }
     }
   };
@@ -250,21 +283,35 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 static int g_ct_cus = 0;
 
 // 1 when csk_conv_tile takes this conv: 3x3 / stride 1 / pad 1, Cout = 32 or
-// 64, Cin % 32 == 0 (<= 64 chunks), 16-byte aligned pixel strides
-CSK_API int csk_conv_tile_ok(int B, int H, int W, int Cin, int Cout, int lda, int ldc) {
-  return B > 0 && H > 0 && W > 0 && (Cout == 32 || Cout == 64) && Cin % 32 == 0 && Cin >= 32 && Cin <= 2048 && lda >= Cin &&
-         lda % 8 == 0 && ldc >= Cout && ldc % 4 == 0 && (long long)B * H * W * lda < (1ll << 31) &&
+// 64 (or <= 16: the 16-wide instance, element stores below 16, e.g. Real-ESRGAN's RGB conv_last),
+// Cin % 32 == 0 (<= 64 chunks), 16-byte aligned input pixel strides; H, W are
+// the OUTPUT size (even with up: the input is H/2 x W/2)
+CSK_API int csk_conv_tile_ok2(int B, int H, int W, int Cin, int Cout, int lda, int ldc, int up) {
+  const bool narrow = Cout > 0 && Cout < 16;
+  return B > 0 && H > 0 && W > 0 && (Cout == 16 || Cout == 32 || Cout == 64 || narrow) && Cin % 32 == 0 && Cin >= 32 &&
+         Cin <= 2048 && lda >= Cin && lda % 8 == 0 && ldc >= Cout && (narrow || ldc % 4 == 0) &&
+         (!up || (H % 2 == 0 && W % 2 == 0)) && (long long)B * H * W * lda < (1ll << 31) &&
          (long long)B * H * W * ldc < (1ll << 31);
 }
 
-// y[..., :Cout] = act(conv3x3(x[..., :Cin]) + bias) * out_scale (+ res[..., :Cout]), NHWC with
-// pixel strides lda / ldc / ldr (res may be null)
-CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bias, const void* res, int B, int H,
-                          int W, int Cin, int Cout, int lda, int ldc, int ldr, int act, float out_scale,
-                          hipStream_t stream) {
-  if (!csk_conv_tile_ok(B, H, W, Cin, Cout, lda, ldc) || !csk_zero_ptr()) return (int)hipErrorInvalidValue;
-  if ((((size_t)x) & 15) || (((size_t)y) & 7) || (((size_t)wp) & 15)) return (int)hipErrorInvalidValue;
+CSK_API int csk_conv_tile_ok(int B, int H, int W, int Cin, int Cout, int lda, int ldc) {
+  return csk_conv_tile_ok2(B, H, W, Cin, Cout, lda, ldc, 0);
+}
+
+// y[..., :Cout] = act(conv3x3(up?(x)[..., :Cin]) + bias) * out_scale (+ res_scale * res[..., :Cout])
+// (+ res2[..., :Cout]), NHWC with pixel strides lda / ldc / ldr / ldr2 (res, res2 may be null;
+// residuals need Cout >= 16; u8: Cout < 16 only, y is uint8 with pixel stride ldc bytes).  H, W: output size.
+CSK_API int csk_conv_tile2(void* y, const void* x, const void* wp, const void* bias, const void* res, const void* res2,
+                           int B, int H, int W, int Cin, int Cout, int lda, int ldc, int ldr, int ldr2, int act,
+                           float out_scale, float res_scale, int up, int u8, hipStream_t stream) {
+  if (!csk_conv_tile_ok2(B, H, W, Cin, Cout, lda, ldc, up) || !csk_zero_ptr()) return (int)hipErrorInvalidValue;
+  const bool narrow = Cout < 16;
+  if ((((size_t)x) & 15) || (!narrow && (((size_t)y) & 7)) || (((size_t)wp) & 15)) return (int)hipErrorInvalidValue;
+  if (u8 && !narrow) return (int)hipErrorInvalidValue;  // uint8 images: the Cout < 16 instance only
+  if ((res || res2) && narrow) return (int)hipErrorInvalidValue;
   if (res && ((((size_t)res) & 7) || ldr < Cout || ldr % 4 || (long long)B * H * W * ldr >= (1ll << 31)))
+    return (int)hipErrorInvalidValue;
+  if (res2 && ((((size_t)res2) & 7) || ldr2 < Cout || ldr2 % 4 || (long long)B * H * W * ldr2 >= (1ll << 31)))
     return (int)hipErrorInvalidValue;
   if ((size_t)(Cin + 64) * sizeof(bf16_t) > (size_t)csk_zero_bytes()) return (int)hipErrorInvalidValue;
   if (!g_ct_cus) {
@@ -280,13 +327,23 @@ CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bi
   a.y = (bf16_t*)y;
   a.zero = csk_zero_ptr();
   a.res = (const bf16_t*)res;
+  a.res2 = (const bf16_t*)res2;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.lda = lda; a.ldc = ldc; a.act = act;
-  a.ldr = ldr; a.out_scale = out_scale;
+  a.ldr = ldr; a.ldr2 = ldr2; a.Cout = Cout; a.up = up ? 1 : 0; a.Wi = up ? W / 2 : W; a.u8 = u8 ? 1 : 0;
+  a.out_scale = out_scale; a.res_scale = res_scale;
   a.tiles_x = (W + CT_TW - 1) / CT_TW;
   a.tiles_y = (H + CT_TH - 1) / CT_TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
   const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
   if (Cout == 64) conv_tile_kernel<64><<<G, 512, 0, stream>>>(a);
-  else conv_tile_kernel<32><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32) conv_tile_kernel<32><<<G, 512, 0, stream>>>(a);
+  else conv_tile_kernel<16><<<G, 512, 0, stream>>>(a);
   return (int)hipGetLastError();
+}
+
+CSK_API int csk_conv_tile(void* y, const void* x, const void* wp, const void* bias, const void* res, int B, int H,
+                          int W, int Cin, int Cout, int lda, int ldc, int ldr, int act, float out_scale,
+                          hipStream_t stream) {
+  return csk_conv_tile2(y, x, wp, bias, res, nullptr, B, H, W, Cin, Cout, lda, ldc, ldr, 0, act, out_scale, 1.f, 0,
+                        0, stream);
 }

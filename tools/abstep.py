@@ -90,21 +90,26 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="UNet batch (CFG: 2 x images); 2 = batch-1 jobs")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-cfg", action="store_true",
+                    help="--batch images without CFG duplication: one CFG-parallel half (batch 1 = the CFG-1 step)")
     a = ap.parse_args()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
 
     ops._lib.load()
     dev = torch.device("cuda", 0)
     p = StableDiffusion("sd21", device=dev, seed=0)
-    x = torch.randn(a.batch // 2, 64, 64, 4, device=dev).bfloat16()
-    x = torch.cat([x, x])  # identical CFG halves, as in the product loop
+    if a.no_cfg:
+        x = torch.randn(a.batch, 64, 64, 4, device=dev).bfloat16()
+    else:
+        x = torch.randn(a.batch // 2, 64, 64, 4, device=dev).bfloat16()
+        x = torch.cat([x, x])  # identical CFG halves, as in the product loop
     ctx = torch.randn(a.batch, 77, 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
     graphs = {}
     for arm in a.arms.split(","):
         for sub in arm.split("+"):  # combined knobs, e.g. gcm2+gcb1024 (settings persist into later arms)
             apply_arm(sub)
-        graphs[arm] = _UNetGraph(p.unet, x, kv, None, cfg_dup=arm != "dup0")
+        graphs[arm] = _UNetGraph(p.unet, x, kv, None, cfg_dup=arm != "dup0" and not a.no_cfg)
     res = {arm: [] for arm in graphs}
     for _ in range(a.rounds):
         for arm, g in graphs.items():

@@ -1,0 +1,22 @@
+import os, time, statistics
+os.environ.setdefault("SDAAS_ALLOW_RANDOM", "1"); os.environ.setdefault("SDAAS_OFFLINE", "1")
+import sys; sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+import numpy as np, torch
+from PIL import Image
+from chiaswarm_amd.pipelines.esrgan import load_esrgan, upscale_x4, _run_u8
+net = load_esrgan("xinntao/RealESRGAN_x4plus", "cuda:0")
+img = Image.fromarray((np.random.default_rng(0).random((512, 512, 3)) * 255).astype(np.uint8))
+for _ in range(3): upscale_x4(net, img)
+torch.cuda.synchronize()
+T = {k: [] for k in ("convert", "h2d", "graph", "d2h", "fromarray", "total", "pinned_d2h")}
+pin = torch.empty((2048, 2048, 3), dtype=torch.uint8, pin_memory=True)
+for _ in range(10):
+    t0 = time.perf_counter(); arr = np.asarray(img.convert("RGB")); t1 = time.perf_counter()
+    x = torch.from_numpy(arr).to("cuda:0")[None]; torch.cuda.synchronize(); t2 = time.perf_counter()
+    y = _run_u8(net, x); torch.cuda.synchronize(); t3 = time.perf_counter()
+    h = y[0].cpu().numpy(); t4 = time.perf_counter()
+    im = Image.fromarray(h); t5 = time.perf_counter()
+    pin.copy_(y[0], non_blocking=True); torch.cuda.synchronize(); t6 = time.perf_counter()
+    T["convert"].append(t1 - t0); T["h2d"].append(t2 - t1); T["graph"].append(t3 - t2); T["d2h"].append(t4 - t3)
+    T["fromarray"].append(t5 - t4); T["total"].append(t5 - t0); T["pinned_d2h"].append(t6 - t5)
+print({k: round(1000 * statistics.median(v), 3) for k, v in T.items()})

@@ -43,6 +43,11 @@ def flops_of(name, a):
     if name == "csk_conv_tile":  # persistent halo-tile 3x3 conv (conv_tile.hip)
         B, H, W, Cin, Cout = a[5:10]
         return f"conv-tile B{B} {H}x{W} s1 {Cin}->{Cout} k3", 2.0 * B * H * W * Cout * 9 * Cin, None
+    if name == "csk_conv_tile2":  # ... with the fused x2 upsample / second residual / narrow outputs
+        B, H, W, Cin, Cout = a[6:11]
+        tags = (" up2x" if a[18] else "") + (" res2" if a[5] else "") + (" u8" if a[19] else "")
+        return (f"conv-tile B{B} {H}x{W}{tags} s1 {Cin}->{Cout} k3", 2.0 * B * H * W * Cout * 9 * Cin,
+                None)
     if name == "csk_ff_geglu":  # fused feed-forward (ff.hip)
         M, C, inner = a[8:11]
         return f"ff fused M{M} C{C} I{inner}", 2.0 * M * C * 2 * inner + 2.0 * M * inner * C, None

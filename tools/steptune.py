@@ -60,6 +60,8 @@ def main():
                     help="sdxl: tune the SDXL step (use --batch 2 --latent 128 for 1024 px batch-1 jobs)")
     ap.add_argument("--no-cfg-dup", action="store_true",
                     help="tune the unshared step (default: the product's CFG-shared prefix, identical halves)")
+    ap.add_argument("--no-cfg", action="store_true",
+                    help="--batch images without CFG duplication: one CFG-parallel half (--batch 1: the CFG-1 step)")
     a = ap.parse_args()
     t_start = time.time()
     from chiaswarm_amd.pipelines.sd import StableDiffusion, _UNetGraph
@@ -68,8 +70,11 @@ def main():
     dev = torch.device("cuda", 0)
     sdxl = a.model == "sdxl"
     p = StableDiffusion(a.model, device=dev, seed=0)
-    x = torch.randn(a.batch // 2, a.latent, a.latent, 4, device=dev).bfloat16()
-    x = torch.cat([x, x])  # CFG halves are identical copies in the product loop
+    if a.no_cfg:
+        x = torch.randn(a.batch, a.latent, a.latent, 4, device=dev).bfloat16()
+    else:
+        x = torch.randn(a.batch // 2, a.latent, a.latent, 4, device=dev).bfloat16()
+        x = torch.cat([x, x])  # CFG halves are identical copies in the product loop
     ctx = torch.randn(a.batch, 77, 2048 if sdxl else 1024, device=dev).bfloat16()
     kv = p.unet.encode_context(ctx)
     added = None
@@ -91,7 +96,7 @@ def main():
     present0 = set(table)  # keys present before the first capture
 
     def capture():
-        return _UNetGraph(p.unet, x, kv, added, warmup=1, cfg_dup=not a.no_cfg_dup and not sdxl)
+        return _UNetGraph(p.unet, x, kv, added, warmup=1, cfg_dup=not a.no_cfg_dup and not sdxl and not a.no_cfg)
 
     def timed(g, rounds=3):
         for _ in range(2):
