@@ -28,10 +28,18 @@ class BrokenEncoderPool(RuntimeError):
     """No encoder process is alive to take (or finish) a task."""
 
 
-def _worker_main(inq, outq):
-    """Encoder process: run (task id, fn, args) items until a None arrives."""
+def _worker_main(inq, outq, parent=None):
+    """Encoder process: run (task id, fn, args) items until a None arrives (or
+    the owning process is gone: re-parented after a SIGKILL of the GPU child)."""
+    import queue
+
     while True:
-        item = inq.get()
+        try:
+            item = inq.get(timeout=1.0)
+        except queue.Empty:
+            if parent is not None and os.getppid() != parent:
+                return
+            continue
         if item is None:
             return
         tid, fn, args = item
@@ -56,7 +64,7 @@ class _ProcessPool:
         self.workers = []  # [process, task queue, pending task ids]
         for _ in range(n):
             inq = ctx.Queue()
-            proc = ctx.Process(target=_worker_main, args=(inq, self.outq), daemon=True)
+            proc = ctx.Process(target=_worker_main, args=(inq, self.outq, os.getpid()), daemon=True)
             proc.start()
             self.workers.append([proc, inq, set()])
         self.futs: dict = {}

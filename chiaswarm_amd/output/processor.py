@@ -28,13 +28,27 @@ def set_encoder_pool(pool) -> None:
     _ENCODER = pool
 
 
+_STAGER = None  # one thread: PIL -> uint8 arrays -> encoder-pool submission, off the GPU thread
+
+
+def _stager():
+    global _STAGER
+    if _STAGER is None:
+        import concurrent.futures as cf
+
+        _STAGER = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="csk-stage")
+    return _STAGER
+
+
 def resolve_artifacts(result: dict) -> dict:
-    """Replace Future-valued artifacts (deferred encoding) by their dicts."""
+    """Replace Future-valued artifacts (deferred encoding; a staged artifact is
+    a Future of the encoder pool's Future) by their dicts."""
     arts = result.get("artifacts")
     if isinstance(arts, dict):
         for k, v in list(arts.items()):
-            if hasattr(v, "result") and callable(v.result):
-                arts[k] = v.result()
+            while hasattr(v, "result") and callable(v.result):
+                v = v.result()
+            arts[k] = v
     return result
 
 
@@ -55,21 +69,27 @@ class OutputProcessor:
         """{name: artifact}.  With an encoder pool registered (the GPU worker
         process does this at startup, ``set_encoder_pool``) image artifacts are
         returned as Futures resolved by the pool's processes, so the GPU thread
-        goes straight on to the next job; the worker resolves them before posting."""
+        goes straight on to the next job; the worker resolves them before posting.
+        Even the pixel hand-over (PIL -> arrays -> pickled into the pool's pipe:
+        30.8 ms per 4 x 512^2 job on the GPU thread, profiles/bench_sup_phases_r6d.json)
+        runs on a staging thread."""
         if _ENCODER is not None and self.main_content_type.startswith("image") and all(
                 isinstance(im, Image.Image) for ims in [self.outputs] + list(self.other_outputs.values())
                 for im in ims):
             import numpy as np
 
+            ct = self.main_content_type
+
+            def stage(images):
+                return _ENCODER.submit_artifact([np.asarray(im.convert("RGB")) for im in images], ct)
+
             results = {}
             if "primary" in self.output_list:
                 grid_shape(len(self.outputs))  # >9 images: ValueError (fatal) raised here, not in the pool
-                results["primary"] = _ENCODER.submit_artifact([np.asarray(im.convert("RGB")) for im in self.outputs],
-                                                              self.main_content_type)
+                results["primary"] = _stager().submit(stage, list(self.outputs))
             for key, images in self.other_outputs.items():
                 grid_shape(len(images))
-                results[key] = _ENCODER.submit_artifact([np.asarray(im.convert("RGB")) for im in images],
-                                                        self.main_content_type)
+                results[key] = _stager().submit(stage, list(images))
             return results
         results = {}
         if "primary" in self.output_list:

@@ -109,8 +109,26 @@ def _test_hook(job):
         time.sleep(3600)
 
 
+def _watch_parent(period_s: float = 1.0) -> None:
+    """The child is not daemonic (it owns encoder processes): end it when the
+    supervisor process is gone (re-parented), whatever killed the supervisor."""
+    import threading
+    import time
+
+    parent = os.getppid()
+
+    def run():
+        while True:
+            time.sleep(period_s)
+            if os.getppid() != parent:
+                os._exit(3)
+
+    threading.Thread(target=run, daemon=True, name="csk-parent-watch").start()
+
+
 def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
     """Child entry point.  inbox: job dicts (None = stop); outbox: (gpu, job_id, result|None, err)."""
+    _watch_parent()
     if gpu_index != "cpu" and _isolated():
         os.environ["HIP_VISIBLE_DEVICES"] = str(gpu_index)
         os.environ["CUDA_VISIBLE_DEVICES"] = str(gpu_index)
@@ -121,7 +139,8 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
     from ..output.encoder import EncoderPool
     from ..output.processor import resolve_artifacts, set_encoder_pool
 
-    encoders = EncoderPool() if gpu_index != "cpu" else None
+    # (cpu children: only when asked, tests/test_worker_procs.py)
+    encoders = EncoderPool() if gpu_index != "cpu" or os.environ.get("CSK_CHILD_ENCODERS") == "1" else None
     if encoders is not None and encoders.kind == "process":
         set_encoder_pool(encoders)
     import concurrent.futures as cf
@@ -153,7 +172,8 @@ def gpu_main(gpu_index, inbox, outbox, env: dict | None = None):
         torch.cuda.set_device(_local_index(gpu_index))  # before any allocation: this child's GPU
     group = _join_group(gpu_index)
     device = Device("cpu" if gpu_index == "cpu" else _local_index(gpu_index))
-    outbox.put((gpu_index, "__ready__", None, {"desc": device.descriptor(), "group": group}))
+    outbox.put((gpu_index, "__ready__", None, {"desc": device.descriptor(), "group": group,
+                                               "encoders": "none" if encoders is None else encoders.kind}))
     while True:
         job = inbox.get()
         if job is None:

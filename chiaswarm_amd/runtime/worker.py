@@ -89,6 +89,7 @@ class ProcessExecutor:
         self.ready = threading.Event()
         self.ready_info = ""
         self.group: dict = {}  # the child's process-group status ({"gen", "rank", "world"} when joined)
+        self.encoders = "none"  # the child's result encoders: "process" | "thread" | "none" (cpu children)
         self._start()
 
     def _start(self):
@@ -98,8 +99,13 @@ class ProcessExecutor:
         self.group = {}
         self.inbox = self.ctx.Queue()
         self.outbox = self.ctx.Queue()
+        # NOT daemonic: a daemonic process may not start children, and the GPU
+        # child starts its JPEG encoder processes (output/encoder.py) — as a
+        # daemon it silently fell back to encoding on its GPU thread (30.8 ms
+        # per 4-image job, profiles/bench_sup_phases_r6d.json).  gpu_main exits
+        # by itself when this process disappears (parent watchdog).
         self.proc = self.ctx.Process(target=gpu_main, args=(self.gpu_index, self.inbox, self.outbox, self.env),
-                                     daemon=True, name=f"chiaswarm-gpu{self.gpu_index}")
+                                     daemon=False, name=f"chiaswarm-gpu{self.gpu_index}")
         self.proc.start()
         self.reader = threading.Thread(target=self._read, args=(self.outbox,), daemon=True)
         self.reader.start()
@@ -116,6 +122,7 @@ class ProcessExecutor:
             if jid == "__ready__":
                 info = err if isinstance(err, dict) else {"desc": str(err), "group": {}}
                 self.group = dict(info.get("group") or {})
+                self.encoders = info.get("encoders", "none")
                 self.ready_info = f"{info.get('desc')} [{_group_str(self.group)}]"
                 self.ready.set()
                 print(f"Started device {self.ready_info}")

@@ -72,6 +72,50 @@ def test_process_executor_recovers_from_crash_and_hang():
         ex.close()
 
 
+def test_child_owns_encoder_processes_and_dies_with_its_parent(tmp_path):
+    """The device child is not daemonic, so it can start its JPEG encoder
+    PROCESSES (a daemonic child fell back to encoding on its GPU thread); its
+    envelopes come back encoded, and an orphaned child exits by itself."""
+    import subprocess
+    import sys
+    import time
+
+    ex = ProcessExecutor("cpu", env={"CSK_CHILD_ENCODERS": "1"}, job_timeout_s=120)
+    try:
+        r = asyncio.run(ex.run({"id": "e1", **TINY, "seed": 3}))
+        assert ex.ready.wait(60) and ex.encoders == "process"
+        assert "error" not in r["pipeline_config"] and _img(r).shape == (64, 64, 3)
+    finally:
+        ex.close()
+    # orphan: a parent that starts an executor and is SIGKILLed; its child must follow
+    pidfile = tmp_path / "child.pid"
+    code = ("import sys, time, os; sys.path.insert(0, %r)\n"
+            "from chiaswarm_amd.runtime.worker import ProcessExecutor\n"
+            "ex = ProcessExecutor('cpu')\n"
+            "assert ex.ready.wait(120)\n"
+            "open(%r, 'w').write(str(ex.proc.pid))\n"
+            "time.sleep(600)\n") % (os.getcwd(), str(pidfile))
+    parent = subprocess.Popen([sys.executable, "-c", code])
+    try:
+        for _ in range(300):
+            if pidfile.exists() and pidfile.read_text():
+                break
+            time.sleep(0.5)
+        child = int(pidfile.read_text())
+    finally:
+        parent.kill()
+        parent.wait()
+    for _ in range(40):  # the watchdog polls once a second
+        try:
+            os.kill(child, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.5)
+    else:
+        os.kill(child, 9)
+        raise AssertionError("orphaned device child kept running")
+
+
 def _save_tiny_model(root):
     """A diffusers-layout tiny checkpoint under $SDAAS_ROOT/models/tiny/sd."""
     from safetensors.torch import save_file
