@@ -1,5 +1,14 @@
-// Persistent stream-K flash attention, d = 64, bf16 in / out (the
-// UNet self-attention at S = 256 .. 16384, SD2.1 / SDXL heads of 64).
+// Persistent stream-K flash attention, d = 64 or 40, bf16 in / out (SURVEY K7:
+// the UNet self-attention at S = 256 .. 16384, SD2.1 / SDXL heads of 64, the
+// SD1.5 / ControlNet 64x64-level heads of 40).
+//
+// d = 40 runs the same kernel on the d = 64 LDS images with the head zero-padded
+// in LDS: the K / V / Q DMA lanes whose 16-byte source chunk lies past the head
+// (chunks 5-7 of a row) are masked off, their LDS slots are zeroed once at kernel
+// entry and never written again (a chunk's slot depends only on the row within
+// the tile), Q's padded k-step half is zeroed in registers.  QK^T then runs 3
+// k-steps instead of 4 and only d < 40 is stored; softmax / PV / merge are the
+// d = 64 code (profiles/attn_fa_d40_r6.txt).
 //
 // Why a new kernel (attn32_kernel in attention.hip is the design it replaces
 // for these shapes): the PMC of the UNet step measured 12.5 VALU instructions
@@ -142,8 +151,11 @@ __device__ __forceinline__ unsigned long long fa_stamp() {
   return t;
 }
 
-template <int PROBE = 0>
+template <int D, int PROBE = 0>
 __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
+  static_assert(D == 64 || D == 40, "head dims 64 and 40");
+  constexpr int NCH = D / 8;         // 16-byte chunks per row that carry data (8 / 5)
+  constexpr int KS = (D + 15) / 16;  // QK^T k-steps (4 / 3)
   // (probe 256: the 4-slot ring of the first version, a barrier every unit)
   constexpr int NSLOT = (PROBE & 256) ? 4 : FA_NSLOT;
   constexpr int LEAD = (PROBE & 256) ? 3 : FA_LEAD;
@@ -164,11 +176,20 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   const int lr = lane >> 3;                        // row of the 8-row DMA piece
   const int kvrow = 8 * wv + lr;                   // tile row this lane's DMA piece fetches
   const int kvch = (lane & 7) ^ fa_f(kvrow);       // source chunk that lands in this lane's slot
+  const bool kv_on = D == 64 || kvch < NCH;         // (d = 40: chunks past the head stay zero)
   const unsigned k_lane = (unsigned)(kvrow * a.sks + kvch * 8) * 2u;  // byte offsets (32-bit: saddr + voffset)
   const unsigned v_lane = (unsigned)(kvrow * a.svs + kvch * 8) * 2u;
   int q_lane[4];                                   // Q piece i: local row 8 i + lr
 #pragma unroll
   for (int i = 0; i < 4; ++i) q_lane[i] = ((lane & 7) ^ fa_f(8 * i + lr)) * 8;
+  if constexpr (D != 64) {
+    // zero the whole LDS once: the pad slots (source chunk >= NCH) are never
+    // written by the masked DMA below; the barrier orders these stores before it
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < (int)(sizeof(smem) / 16); i += 512) reinterpret_cast<uint4*>(smem)[i] = z;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   const unsigned kv_dst = (unsigned)wv * 1024u;    // this wave's 1 KiB of a K or V tile
   const unsigned lds0 = (unsigned)(size_t)(fa_lptr_t)(void*)smem;  // LDS byte address of the array
   const unsigned q_base = QOFF + (unsigned)wv * 4096u;
@@ -206,7 +227,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
     const char* kb = (const char*)(a.k + (size_t)(d_b * a.skb + d_h * a.skh) + (size_t)(d_tile * 64 * a.sks));
     const char* vb = (const char*)(a.v + (size_t)(d_b * a.svb + d_h * a.svh) + (size_t)(d_tile * 64 * a.svs));
     unsigned char* dst = smem + (v & (NSLOT - 1)) * FA_SLOT + kv_dst;
-    if (!(PROBE & 64) || v < u0 + 2) {
+    if ((!(PROBE & 64) || v < u0 + 2) && kv_on) {
       __builtin_amdgcn_global_load_lds((fa_gptr_t)(kb + k_lane), (fa_lptr_t)dst, 16, 0, 0);
       __builtin_amdgcn_global_load_lds((fa_gptr_t)(vb + v_lane), (fa_lptr_t)(dst + 8192), 16, 0, 0);
     }
@@ -230,8 +251,9 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = min(qb * FA_ROWS + wv * 32 + 8 * i + lr, a.Sq - 1);
-      __builtin_amdgcn_global_load_lds((fa_gptr_t)(qp + (unsigned)(row * a.sqs + q_lane[i])),
-                                       (fa_lptr_t)(smem + q_base + i * 1024), 16, 0, 0);
+      if (D == 64 || q_lane[i] < 8 * NCH)
+        __builtin_amdgcn_global_load_lds((fa_gptr_t)(qp + (unsigned)(row * a.sqs + q_lane[i])),
+                                         (fa_lptr_t)(smem + q_base + i * 1024), 16, 0, 0);
     }
     issued += 4;
     q_end = issued;
@@ -239,7 +261,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
   auto wait_issue = [&](int end) { fa_vmcnt(issued - end); };
 
   // ---- registers ----
-  v8s qf[4];
+  v8s qf[KS];
   v16f o[2];
   float mref = 0.f, lsum = 0.f;
   const v16f zero16 = {0.f};
@@ -249,13 +271,16 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
 
   auto load_q = [&]() {  // this wave's 32 query rows -> B fragments, pre-scaled into log2 units
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
+    for (int ds = 0; ds < KS; ++ds) {
       const uint4 raw = *reinterpret_cast<const uint4*>(smem + q_base + koff[ds]);
       float f[8];
       unpack8(raw, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] *= sl2;
       qf[ds] = __builtin_bit_cast(v8s, pack8(f));
+      // (d = 40: the last k-step's upper half, chunk 5, is head padding; the Q
+      // region's pad slots hold stale data of no row, so zero it here)
+      if (D != 64 && 2 * ds + hh >= NCH) qf[ds] = v8s{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
   auto qk = [&](int v, v16f (&s)[2]) {  // S^T of unit v's keys (its K tile is in LDS)
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
+      for (int ds = 0; ds < KS; ++ds) {
         const v8s kf = *reinterpret_cast<const v8s*>(kb + kt * 4096 + koff[ds]);
         if constexpr ((PROBE & 8) != 0) {
           asm volatile("" ::"v"(kf), "v"(qf[ds]));
@@ -409,6 +434,7 @@ __global__ __launch_bounds__(512) void attn_fa_kernel(const FaArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int d = dt * 32 + 8 * g + 4 * hh;
+          if (D != 64 && d >= D) continue;  // (compile-time per lane half: g, dt unrolled)
           uint2 wd;
           wd.x = pack2(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
           wd.y = pack2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
@@ -639,7 +665,7 @@ CSK_API int csk_attn_fa_inject_errors(unsigned n) {
 
 // 1 when csk_attention_fa takes this shape
 CSK_API int csk_attn_fa_ok(int B, int H, int Sq, int Skv, int D, int causal, int has_kv_len) {
-  if (!g_fa_enabled || D != 64 || causal || has_kv_len || !g_fa_part) return 0;
+  if (!g_fa_enabled || (D != 64 && D != 40) || causal || has_kv_len || !g_fa_part) return 0;
   // short key ranges (S = 256: 4 tiles per block) spend more on stream-K
   // merges than they gain (profiles/attn_fa_r8a.txt: 23.4 vs 12.6 us at B8 H20)
   if (Skv % 64 != 0 || Skv < g_fa_min_skv || Sq < 128) return 0;
@@ -680,20 +706,24 @@ CSK_API int csk_attention_fa(void* o, const void* q, const void* k, const void* 
   int G = g_fa_workers;
   if (workers > 0 && workers < G) G = workers;
   if (G > a.U) G = a.U;
+  if (D == 40) {  // (no probe variants)
+    attn_fa_kernel<40><<<G, 512, 0, stream>>>(a);
+    return (int)hipGetLastError();
+  }
   switch (g_fa_probe) {
-    case 1: attn_fa_kernel<1><<<G, 512, 0, stream>>>(a); break;
-    case 2: attn_fa_kernel<2><<<G, 512, 0, stream>>>(a); break;
-    case 4: attn_fa_kernel<4><<<G, 512, 0, stream>>>(a); break;
-    case 8: attn_fa_kernel<8><<<G, 512, 0, stream>>>(a); break;
-    case 16: attn_fa_kernel<16><<<G, 512, 0, stream>>>(a); break;
-    case 32: attn_fa_kernel<32><<<G, 512, 0, stream>>>(a); break;
-    case 256: attn_fa_kernel<256><<<G, 512, 0, stream>>>(a); break;
-    case 512: attn_fa_kernel<512><<<G, 512, 0, stream>>>(a); break;
-    case 64: attn_fa_kernel<66><<<G, 512, 0, stream>>>(a); break;      // no K/V DMA (and no waits)
-    case 76: attn_fa_kernel<66 + 12><<<G, 512, 0, stream>>>(a); break; // ... and no MFMAs
-    case 77: attn_fa_kernel<66 + 13><<<G, 512, 0, stream>>>(a); break; // ... and no exp
-    case 128: attn_fa_kernel<128><<<G, 512, 0, stream>>>(a); break;    // phase stamps
-    default: attn_fa_kernel<0><<<G, 512, 0, stream>>>(a); break;
+    case 1: attn_fa_kernel<64, 1><<<G, 512, 0, stream>>>(a); break;
+    case 2: attn_fa_kernel<64, 2><<<G, 512, 0, stream>>>(a); break;
+    case 4: attn_fa_kernel<64, 4><<<G, 512, 0, stream>>>(a); break;
+    case 8: attn_fa_kernel<64, 8><<<G, 512, 0, stream>>>(a); break;
+    case 16: attn_fa_kernel<64, 16><<<G, 512, 0, stream>>>(a); break;
+    case 32: attn_fa_kernel<64, 32><<<G, 512, 0, stream>>>(a); break;
+    case 256: attn_fa_kernel<64, 256><<<G, 512, 0, stream>>>(a); break;
+    case 512: attn_fa_kernel<64, 512><<<G, 512, 0, stream>>>(a); break;
+    case 64: attn_fa_kernel<64, 66><<<G, 512, 0, stream>>>(a); break;      // no K/V DMA (and no waits)
+    case 76: attn_fa_kernel<64, 66 + 12><<<G, 512, 0, stream>>>(a); break; // ... and no MFMAs
+    case 77: attn_fa_kernel<64, 66 + 13><<<G, 512, 0, stream>>>(a); break; // ... and no exp
+    case 128: attn_fa_kernel<64, 128><<<G, 512, 0, stream>>>(a); break;    // phase stamps
+    default: attn_fa_kernel<64, 0><<<G, 512, 0, stream>>>(a); break;
   }
   return (int)hipGetLastError();
 }

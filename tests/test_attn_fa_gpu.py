@@ -1,4 +1,4 @@
-"""The persistent stream-K d = 64 attention (csrc/kernels/attn_fa.hip) against
+"""The persistent stream-K d = 64 / 40 attention (csrc/kernels/attn_fa.hip) against
 the fp32 PyTorch reference: ragged query blocks, every merge shape the
 stream-K split can produce (forced with small worker counts: one block cut into
 2..many pieces, pieces of 1 tile), strided fused-QKV views, the deferred
@@ -55,6 +55,31 @@ def test_attn_fa_shapes_and_cuts(gpu, B, Sq, Skv, H, workers):
     assert torch.isfinite(y.float()).all()
     assert rel_err(y.cpu(), _ref(q, k, v, 0.125)) < 1.5e-2
     assert hip_ops.attn_fa_errors() == 0
+
+
+@pytest.mark.parametrize("B,Sq,Skv,H", [(2, 1024, 1024, 8), (1, 4096, 4096, 2), (1, 320, 256, 3), (1, 1000, 512, 2)])
+@pytest.mark.parametrize("workers", [0, 7, 33])
+def test_attn_fa_d40_shapes_and_cuts(gpu, B, Sq, Skv, H, workers):
+    """Head dim 40 (SD1.5 / ControlNet 64x64 level) on the zero-padded d = 64 images."""
+    torch.manual_seed(B * 1000 + Sq + Skv + H + workers + 40)
+    q, k, v = (torch.randn(B, s, H, 40, device=gpu).bfloat16() for s in (Sq, Skv, Skv))
+    scale = 40 ** -0.5
+    y = _run(q, k, v, scale, workers)
+    assert y.shape == (B, Sq, H, 40)
+    assert torch.isfinite(y.float()).all()
+    assert rel_err(y.cpu(), _ref(q, k, v, scale)) < 1.5e-2
+    assert hip_ops.attn_fa_errors() == 0
+
+
+@pytest.mark.parametrize("workers", [0, 5])
+def test_attn_fa_d40_fused_qkv_strides(gpu, workers):
+    """SD1.5's fused QKV: [B, S, 3, 8, 40] views (80-byte head offsets), output
+    the head offsets are 80 bytes (16-byte aligned, not 128)."""
+    B, S, H = 2, 1024, 8
+    qkv = torch.randn(B, S, 3, H, 40, device=gpu).bfloat16()
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    y = _run(q, k, v, 40 ** -0.5, workers)
+    assert rel_err(y.cpu(), _ref(q, k, v, 40 ** -0.5)) < 1.5e-2
 
 
 @pytest.mark.parametrize("workers", [0, 5])

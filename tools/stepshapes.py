@@ -37,6 +37,9 @@ def flops_of(name, a):
     if name == "csk_attention":
         B, H, Sq, Skv, D = a[5:10]
         return f"attn B{B} H{H} Sq{Sq} Skv{Skv} D{D}", 4.0 * B * H * Sq * Skv * D, None
+    if name == "csk_attention_fa":  # persistent stream-K attention (attn_fa.hip)
+        B, H, Sq, Skv, D = a[5:10]
+        return f"attn-fa B{B} H{H} Sq{Sq} Skv{Skv} D{D}", 4.0 * B * H * Sq * Skv * D, None
     if name == "csk_xattn_block":
         M, C, rpb, Bc, Skv = a[9:14]
         return (f"xattn block M{M} C{C} Skv{Skv}", 2.0 * M * C * C * 2 + 4.0 * M * Skv * C, None)
