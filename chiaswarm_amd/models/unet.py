@@ -287,9 +287,20 @@ class UNet2DConditionModel(Prepared):
             temb = temb + self.class_embedding(class_labels.reshape(-1).long()).to(dtype).expand_as(temb)
         return temb
 
-    def forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
-                added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None,
-                cfg_dup=False, temb_proj=None):
+    def forward(self, *args, **kwargs):
+        """``_forward`` inside the model's tuning context (SDXL: its own tile
+        choices for shape keys it shares with SD2.1, ops/tuning.py::context)."""
+        ctx = "sdxl" if self.cfg.addition_embed_type == "text_time" else None
+        if ctx is None:
+            return self._forward(*args, **kwargs)
+        from ..ops import tuning
+
+        with tuning.context(ctx):
+            return self._forward(*args, **kwargs)
+
+    def _forward(self, sample, timestep, encoder_hidden_states=None, cross_kv=None,
+                 added_cond=None, down_residuals=None, mid_residual=None, class_labels=None, control=None,
+                 cfg_dup=False, temb_proj=None):
         """sample: NHWC [B, H, W, Cin]; returns NHWC [B, H, W, Cout].
 
         ``control``: a ControlNet's pre-zero-conv features

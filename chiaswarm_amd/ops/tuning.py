@@ -8,12 +8,15 @@ For every GEMM / implicit-GEMM conv shape we pick (tile, ksplit):
          shapes (UNet 16x16 / 8x8 levels) that would otherwise not fill 256 CUs.
 
 Lookup order: in-memory -> user table ($SDAAS_ROOT/csk_tune.json) -> shipped
-table (chiaswarm_amd/lib/tune_gfx950.json, measured on MI355X) -> heuristic.
+table (chiaswarm_amd/lib/tune_gfx950.json, measured on MI355X) -> heuristic;
+inside ``context("sdxl")`` (the SDXL UNet) an "sdxl|<key>" entry wins over the
+plain key.
 With CSK_AUTOTUNE=1 a miss is measured on the spot (outside graph capture)
 with hip events over every candidate and the winner is recorded.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import threading
@@ -128,10 +131,34 @@ def _time(fn, reps=10):
     return a.elapsed_time(b) / reps
 
 
+_CTX = threading.local()
+
+
+@contextlib.contextmanager
+def context(name: str | None):
+    """Tuning context of the calls inside (e.g. "sdxl": the SDXL UNet): a shape
+    key shared by two models' steps (M2048 N1280 K1280 is both SD2.1's CFG-8
+    16x16 level and SDXL's CFG-2 32x32 level) may take a different tile in each;
+    ``choose`` looks up "<context>|<key>" first, then the plain key."""
+    prev = getattr(_CTX, "name", None)
+    _CTX.name = name
+    try:
+        yield
+    finally:
+        _CTX.name = prev
+
+
+def current_context() -> str | None:
+    return getattr(_CTX, "name", None)
+
+
 def choose(key: str, M: int, N: int, K: int, runner) -> tuple[int, int]:
     """runner(tile, ksplit) launches the kernel once (used only when tuning)."""
     t = table()
-    hit = t.get(key)
+    ctx = getattr(_CTX, "name", None)
+    hit = t.get(f"{ctx}|{key}") if ctx else None
+    if hit is None:
+        hit = t.get(key)
     if hit is not None:
         return int(hit[0]), int(hit[1])
     if os.environ.get("CSK_AUTOTUNE") == "1" and not torch.cuda.is_current_stream_capturing():

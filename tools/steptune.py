@@ -60,6 +60,9 @@ def main():
                     help="sdxl: tune the SDXL step (use --batch 2 --latent 128 for 1024 px batch-1 jobs)")
     ap.add_argument("--no-cfg-dup", action="store_true",
                     help="tune the unshared step (default: the product's CFG-shared prefix, identical halves)")
+    ap.add_argument("--context", default="",
+                    help="write the winners as '<context>|<key>' (ops/tuning.py::context; sdxl: the SDXL UNet's "
+                         "own entries, leaving the keys it shares with SD2.1 alone)")
     ap.add_argument("--no-cfg", action="store_true",
                     help="--batch images without CFG duplication: one CFG-parallel half (--batch 1: the CFG-1 step)")
     a = ap.parse_args()
@@ -131,6 +134,7 @@ def main():
     changes = []
     for key in keys:
         M, N, K, cur = used[key]
+        tkey = f"{a.context}|{key}" if a.context else key  # the table entry this run writes
         only = {int(v) for v in a.only_tiles.split(",") if v}
         cands = [c for c in tuning.candidates(M, N, K) if (a.all_tiles or c[0] in SHORTLIST) and c != tuple(cur)
                  and (not only or c[0] in only)]
@@ -142,8 +146,8 @@ def main():
         for c in cands:
             if time.time() - t_start > a.budget:
                 break
-            old = table.get(key)
-            table[key] = [c[0], c[1], 0.0]
+            old = table.get(tkey)
+            table[tkey] = [c[0], c[1], 0.0]
             try:
                 g = capture()
                 tc = timed(g)
@@ -153,9 +157,9 @@ def main():
                 g = None
             finally:
                 if old is None:
-                    table.pop(key, None)
+                    table.pop(tkey, None)
                 else:
-                    table[key] = old
+                    table[tkey] = old
             if tc < best_t - a.min_gain_us / 1000:
                 # confirm against a fresh measurement of the base graph
                 tb2, tc2 = timed(base_g), timed(g)
@@ -164,7 +168,7 @@ def main():
                     base = tb2
             del g
         if best_c is not None:
-            table[key] = [best_c[0], best_c[1], round(best_t * 1000, 1)]
+            table[tkey] = [best_c[0], best_c[1], round(best_t * 1000, 1)]
             used[key] = (M, N, K, best_c)
             del base_g
             torch.cuda.empty_cache()
