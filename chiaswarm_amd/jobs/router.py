@@ -25,6 +25,7 @@ PIPELINE_TYPES = {
     "StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline", "AudioLDMPipeline",
     "TextToVideoSDPipeline", "VideoToVideoSDPipeline", "IFPipeline", "IFSuperResolutionPipeline",
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
+    "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline",
 }
 # real diffusers classes with no implementation here: a fatal error naming the
 # class (never silently run as plain SD)

@@ -179,6 +179,10 @@ class Attention(Prepared):
         b, s, _ = qkv.shape
         h, d = self.heads, self.dim_head
         qkv = qkv.view(b, s, 3, h, d)
+        store = self.__dict__.get("_store_probs")
+        if store is not None:  # SAG (pipelines/guided.py): the softmax(q k^T) map of this layer, fp32
+            q, k = qkv[:, :, 0].float().transpose(1, 2), qkv[:, :, 1].float().transpose(1, 2)
+            store.append(torch.softmax(q @ k.transpose(-1, -2) * self.scale, dim=-1))
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], self.scale, causal=causal)
         return self.to_out[0](o.reshape(b, s, h * d), residual=residual, row_stats=row_stats)
 

@@ -36,11 +36,14 @@ SD_CLASSES = {
     "StableDiffusionControlNetImg2ImgPipeline", "StableDiffusionInstructPix2PixPipeline",
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
+    # sampling-loop variants on a plain SD checkpoint (pipelines/guided.py)
+    "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline",
 }
 # checkpoints whose own class must win over a generic requested one (the
 # router defaults an image job to StableDiffusionImg2ImgPipeline; these
 # architectures cannot run as that class)
 _OWN_CLASS = {"StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline"}
+GUIDED_CLASSES = {"StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline"}  # (guided.CLASSES)
 UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
 # job kwargs the SD callback consumes itself (the rest go to the pipeline call)
 _CALLBACK_KEYS = {"model_name", "scheduler_type", "pipeline_type", "upscale", "textual_inversion", "lora",
@@ -237,7 +240,14 @@ def _diffusion(device_identifier, model_name, split, state, **kwargs):
             kwargs["cfg_split"] = state["cfg"] = {"peer": int(split["peer"]), "half": int(split["half"])}
         out_type = "uint8_device" if helper else ("latent" if cfg_part and int(split["half"]) == 1 else "pil")
         t_pipe = time.perf_counter()
-        p = pipe(scheduler=sched, **dict(kwargs, output_type=out_type))
+        if pcls in GUIDED_CLASSES:
+            if split is not None:
+                raise ValueError(f"{pcls} jobs are not split across GPUs")
+            from . import guided
+
+            p = guided.run(pcls, pipe, scheduler=sched, **dict(kwargs, output_type=out_type))
+        else:
+            p = pipe(scheduler=sched, **dict(kwargs, output_type=out_type))
         t_post = time.perf_counter()
     finally:
         from ..models.lora import unload_lora, unload_textual_inversion
@@ -403,6 +413,9 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
             raise TypeError(f"batched job: unexpected keyword arguments {bad}")
     k0 = jobs[0]
     model_name = k0["model_name"]
+    for kw in jobs:  # (runtime.worker._raw_key never batches these: their loop is not the plain one)
+        if pipeline_class_for(kw.get("pipeline_type", "DiffusionPipeline"), model_name) in GUIDED_CLASSES:
+            raise ValueError("Panorama / SAG jobs run alone, not in a denoising batch")
     pipe = load_sd(model_name, device_identifier, k0.get("revision", "main"))
     sched_type = k0.get("scheduler_type", "DPMSolverMultistepScheduler")
     sched = get_scheduler(sched_type, **pipe.family.scheduler_kwargs())

@@ -1,0 +1,272 @@
+"""Sampling-loop variants of Stable Diffusion that the hive can name as a
+diffusers class (``parameters.pipeline_type``; the reference builds any such
+name by reflection, swarm/job_arguments.py:143-145, swarm/type_helpers.py:1-3,
+swarm/diffusion/diffusion_func.py:41-46).  Both run a plain SD checkpoint on
+the resident bundle; only the denoising loop differs.
+
+* ``StableDiffusionPanoramaPipeline`` (MultiDiffusion, Bar-Tal et al. 2023):
+  the latent canvas (default 512 x 2048 px) is covered by 64 x 64 latent
+  windows at stride 8; every step each window is denoised on its own (the
+  UNet graph of a 512 x 512 image, CFG batch) with its OWN sampler state —
+  multistep samplers keep per-window history, as diffusers does since it
+  copies the scheduler state per view — and the canvas is the per-pixel mean
+  of the windows' updates.  ``circular_padding`` wraps windows around the
+  horizontal seam (360-degree panoramas) and decodes with 8 latent columns of
+  wrap-around padding on each side.  ``view_batch_size`` is accepted; windows
+  are evaluated one at a time (the same math as a batched evaluation).
+* ``StableDiffusionSAGPipeline`` (Self-Attention Guidance, Hong et al. 2023):
+  the mid-block self-attention map of the unconditional pass marks the
+  regions the model attends to (mean over heads, summed over queries > 1);
+  the predicted x0 is Gaussian-blurred there (9 taps, sigma 1, reflect
+  padding), re-noised to the current level with the predicted noise, and the
+  UNet's unconditional prediction on that degraded sample pulls the guided
+  prediction away: ``e += sag_scale * (e_uncond - e_degraded)``.  x0 / noise
+  use this sampler's own sigma (diffusers reads ``alphas_cumprod[t]``, equal
+  up to the rounding of Karras timesteps; exact for DDIM / PNDM ladders).
+
+Parity against diffusers is unpinned (diffusers is not importable here); the
+CPU tests pin the window geometry, the per-window sampler independence, the
+SAG mask / blur against their formulas, and that sag_scale = 0 and a single
+window reproduce the plain pipeline exactly.
+"""
+from __future__ import annotations
+
+import contextlib
+import copy
+import math
+
+import torch
+import torch.nn.functional as F
+
+PANORAMA = "StableDiffusionPanoramaPipeline"
+SAG = "StableDiffusionSAGPipeline"
+CLASSES = (PANORAMA, SAG)
+
+# diffusers StableDiffusionPanoramaPipeline.get_views / decode_latents_with_padding
+WINDOW, STRIDE, CIRC_PAD = 64, 8, 8
+
+
+def panorama_views(lh: int, lw: int, window: int = WINDOW, stride: int = STRIDE, circular: bool = False):
+    """(h0, h1, w0, w1) latent windows covering an lh x lw canvas; with
+    ``circular`` the windows start every ``stride`` columns all the way round
+    (w1 may exceed lw: those wrap)."""
+    nh = (lh - window) // stride + 1 if lh > window else 1
+    if circular:
+        nw = lw // stride if lw > window else 1
+    else:
+        nw = (lw - window) // stride + 1 if lw > window else 1
+    out = []
+    for i in range(nh * nw):
+        h0 = (i // nw) * stride
+        w0 = (i % nw) * stride
+        out.append((h0, h0 + window, w0, w0 + window))
+    return out
+
+
+def _take(x, v, lw):
+    h0, h1, w0, w1 = v
+    if w1 <= lw:
+        return x[:, h0:h1, w0:w1]
+    return torch.cat([x[:, h0:h1, w0:], x[:, h0:h1, :w1 - lw]], dim=2)
+
+
+def _accumulate(value, count, xv, v, lw):
+    h0, h1, w0, w1 = v
+    if w1 <= lw:
+        value[:, h0:h1, w0:w1] += xv
+        count[:, h0:h1, w0:w1] += 1
+        return
+    k = lw - w0
+    value[:, h0:h1, w0:] += xv[:, :, :k]
+    count[:, h0:h1, w0:] += 1
+    value[:, h0:h1, :w1 - lw] += xv[:, :, k:]
+    count[:, h0:h1, :w1 - lw] += 1
+
+
+def _guide(e, guidance, cfg):
+    if not cfg:
+        return e
+    e_u, e_c = e.chunk(2)
+    return e_u + guidance * (e_c - e_u)
+
+
+def window_for(pipe) -> tuple[int, int]:
+    """(window, stride) in latent pixels: diffusers' 64 / 8 for real checkpoints;
+    the family's own latent size / 8 for the test-size families."""
+    d = int(pipe.family.default_size) // 8
+    if d >= WINDOW:
+        return WINDOW, STRIDE
+    return d, max(1, d // 8)
+
+
+@torch.no_grad()
+def panorama_denoise(pipe, x, sched, cross_kv, guidance, added, generator, circular=False):
+    """MultiDiffusion loop on NHWC fp32 latents [B, lh, lw, 4]."""
+    b, lh, lw, _ = x.shape
+    window, stride = window_for(pipe)
+    views = panorama_views(lh, lw, window, stride, circular=circular)
+    cfg = guidance > 1.0
+    states = [copy.deepcopy(sched) for _ in views]  # per-window multistep history
+    while states[0].step_index < states[0].n:
+        value = torch.zeros_like(x)
+        count = torch.zeros_like(x[..., :1])
+        for v, s in zip(views, states):
+            xv = _take(x, v, lw)
+            xi = (xv * s.current_scale()).to(pipe.dtype)
+            e = pipe._unet_eval(torch.cat([xi, xi], 0) if cfg else xi, s.current_t(), cross_kv, added)
+            _accumulate(value, count, s.step(_guide(e.float(), guidance, cfg), xv, generator), v, lw)
+        x = torch.where(count > 0, value / count.clamp_min(1), value)
+    sched.step_index = sched.n
+    return x
+
+
+def gaussian_blur_nhwc(x: torch.Tensor, kernel_size: int = 9, sigma: float = 1.0) -> torch.Tensor:
+    """Depthwise Gaussian blur with reflect padding (diffusers SAG gaussian_blur_2d) on NHWC."""
+    half = (kernel_size - 1) * 0.5
+    t = torch.linspace(-half, half, kernel_size, device=x.device, dtype=torch.float32)
+    pdf = torch.exp(-0.5 * (t / sigma) ** 2)
+    k1 = pdf / pdf.sum()
+    k2 = (k1[:, None] @ k1[None, :]).to(x.dtype)
+    c = x.shape[-1]
+    w = k2.expand(c, 1, kernel_size, kernel_size)
+    xn = x.permute(0, 3, 1, 2)
+    p = kernel_size // 2
+    xn = F.pad(xn, (p, p, p, p), mode="reflect")
+    return F.conv2d(xn, w, groups=c).permute(0, 2, 3, 1)
+
+
+def sag_mask(probs: torch.Tensor, lh: int, lw: int) -> torch.Tensor:
+    """[B, heads, S, S] attention probabilities of the mid block -> [B, lh, lw, 1]
+    {0, 1} mask: keys whose attention (mean over heads, summed over queries)
+    exceeds 1, nearest-resized from the mid-block grid to the latent grid."""
+    b, _, s, _ = probs.shape
+    f = int(round(math.sqrt(lh * lw / s)))
+    mh, mw = lh // f, lw // f
+    m = (probs.mean(1).sum(1) > 1.0).to(torch.float32).reshape(b, 1, mh, mw)
+    return F.interpolate(m, (lh, lw)).permute(0, 2, 3, 1)
+
+
+def _at_sigma(sched):
+    """A view of the sampler at the sigma its NEXT evaluation sees (the second
+    stage of Heun / DPM2 evaluates between ladder points), for the x0 / noise
+    formulas of ``Scheduler.x0_coeffs`` / ``Scheduler.add_noise``."""
+    from types import SimpleNamespace
+
+    return SimpleNamespace(sigmas=[float(sched.eval_sigma())], space=sched.space, n=1,
+                           prediction_type=sched.prediction_type, name=sched.name)
+
+
+def _eps_from(view, x, x0):
+    """Noise of sample x given its x0, at the view's sigma."""
+    s = float(view.sigmas[0])
+    if view.space == "vp":
+        a = 1.0 / math.sqrt(s * s + 1.0)
+        return (x - a * x0) / (s * a)
+    return (x - x0) / s
+
+
+def _mid_attn(unet):
+    return unet.mid_block.attentions[0].transformer_blocks[0].attn1
+
+
+@torch.no_grad()
+def sag_denoise(pipe, x, sched, cross_kv, guidance, added, generator, sag_scale=0.75):
+    """Self-attention-guided loop on NHWC fp32 latents.  The UNet runs eagerly
+    (its mid-block attention map is read back every step)."""
+    b, lh, lw, _ = x.shape
+    cfg = guidance > 1.0
+    attn = _mid_attn(pipe.unet)
+    kv_ref = [t[:b] for t in cross_kv] if cfg else list(cross_kv)
+    while sched.step_index < sched.n:
+        t = sched.current_t()
+        s_in = sched.current_scale()
+        tt = torch.tensor([t], device=x.device, dtype=torch.float32)
+        xi = (x * s_in).to(pipe.dtype)
+        store: list = []
+        attn._store_probs = store
+        try:
+            e = pipe.unet(torch.cat([xi, xi], 0) if cfg else xi, tt, cross_kv=cross_kv, added_cond=added).float()
+        finally:
+            attn._store_probs = None
+        e_ref = e[:b]  # unconditional half (or the only one)
+        eg = _guide(e, guidance, cfg)
+        if sag_scale != 0.0:
+            from ..schedulers import Scheduler
+
+            view = _at_sigma(sched)
+            p, q = Scheduler.x0_coeffs(view, 0)
+            x0 = p * x + q * e_ref
+            eps = _eps_from(view, x, x0)
+            m = sag_mask(store[0][:b], lh, lw)
+            deg = gaussian_blur_nhwc(x0) * m + x0 * (1 - m)
+            deg = Scheduler.add_noise(view, deg, eps, 0)
+            ed = pipe.unet((deg * s_in).to(pipe.dtype), tt, cross_kv=kv_ref, added_cond=None).float()
+            eg = eg + sag_scale * (e_ref - ed)
+        x = sched.step(eg, x, generator)
+    return x
+
+
+@contextlib.contextmanager
+def _override(pipe, denoise, decode=None):
+    pipe._denoise_override = denoise
+    if decode is not None:
+        pipe.decode = decode
+    try:
+        yield
+    finally:
+        pipe._denoise_override = None
+        pipe.__dict__.pop("decode", None)
+
+
+def _check(pipe, cls, kwargs):
+    if pipe.family.is_xl or pipe.family.is_pix2pix or pipe.family.is_depth or pipe.unet.cfg.in_channels != 4:
+        raise ValueError(f"{cls} runs plain Stable Diffusion checkpoints, not {pipe.family.name}")
+    bad = sorted(k for k in ("image", "mask_image", "strength", "image_guidance_scale", "depth_map",
+                             "controlnet_conditioning_scale", "cfg_split") if k in kwargs)
+    if bad:
+        raise TypeError(f"{cls}.__call__() got unexpected keyword arguments {bad}")
+    if getattr(pipe, "controlnet", None) is not None:
+        raise ValueError(f"{cls} does not take a ControlNet")
+
+
+def run_panorama(pipe, height=None, width=None, view_batch_size=1, circular_padding=False, **kwargs):
+    """``StableDiffusionPanoramaPipeline.__call__`` (diffusers defaults 512 x 2048)."""
+    _check(pipe, PANORAMA, kwargs)
+    if int(view_batch_size) < 1:
+        raise ValueError("view_batch_size must be >= 1")
+    circ = bool(circular_padding)
+
+    def denoise(p, x, sched, cross_kv, guidance, added, generator, **_):
+        return panorama_denoise(p, x, sched, cross_kv, guidance, added, generator, circular=circ)
+
+    decode = None
+    if circ:
+        plain = pipe.decode
+
+        def decode(latents, to_host=True):  # wrap-around columns on both sides, cropped after the VAE
+            pad = min(CIRC_PAD, window_for(pipe)[0] // 2)  # 8 latent columns (test-size families: fewer)
+            z = torch.cat([latents[:, :, -pad:], latents, latents[:, :, :pad]], dim=2)
+            img = plain(z, to_host=False)
+            px = pad * 8
+            img = img[:, :, px:img.shape[2] - px].contiguous()
+            return img.cpu() if to_host else img
+
+    w = window_for(pipe)[0] * 8
+    with _override(pipe, denoise, decode):
+        return pipe(height=height or w, width=width or 4 * w, **kwargs)
+
+
+def run_sag(pipe, sag_scale=0.75, **kwargs):
+    """``StableDiffusionSAGPipeline.__call__``."""
+    _check(pipe, SAG, kwargs)
+    s = float(sag_scale)
+
+    def denoise(p, x, sched, cross_kv, guidance, added, generator, **_):
+        return sag_denoise(p, x, sched, cross_kv, guidance, added, generator, sag_scale=s)
+
+    with _override(pipe, denoise):
+        return pipe(**kwargs)
+
+
+def run(cls, pipe, **kwargs):
+    return run_panorama(pipe, **kwargs) if cls == PANORAMA else run_sag(pipe, **kwargs)

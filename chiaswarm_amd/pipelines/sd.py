@@ -365,6 +365,9 @@ class StableDiffusion:
         * ``cfg_split`` = {"peer": rank, "half": 0 | 1}: CFG-parallel, this rank
           evaluates one CFG half and swaps predictions with its peer each step.
         """
+        ov = self.__dict__.get("_denoise_override")
+        if ov is not None:  # a sampling-loop variant class (pipelines/guided.py: Panorama, SAG)
+            return ov(self, latents, sched, cross_kv, guidance, added, generator)
         b = latents.shape[0]
         cfg = guidance > 1.0
         three_way = image_guidance is not None
