@@ -17,6 +17,7 @@ import time
 
 import torch
 
+from ..jobs.router import GUIDED_PIPELINES
 from ..output.processor import OutputProcessor
 from ..runtime.model_cache import cache, find_weights
 from ..runtime.provision import ensure_weights
@@ -37,13 +38,13 @@ SD_CLASSES = {
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
     # sampling-loop variants on a plain SD checkpoint (pipelines/guided.py)
-    "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline",
+    "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
 }
 # checkpoints whose own class must win over a generic requested one (the
 # router defaults an image job to StableDiffusionImg2ImgPipeline; these
 # architectures cannot run as that class)
 _OWN_CLASS = {"StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline"}
-GUIDED_CLASSES = {"StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline"}  # (guided.CLASSES)
+GUIDED_CLASSES = GUIDED_PIPELINES  # (guided.CLASSES)
 UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
 # job kwargs the SD callback consumes itself (the rest go to the pipeline call)
 _CALLBACK_KEYS = {"model_name", "scheduler_type", "pipeline_type", "upscale", "textual_inversion", "lora",
@@ -415,7 +416,7 @@ def diffusion_batch(device_identifier, jobs: list[dict]) -> list[tuple[dict, dic
     model_name = k0["model_name"]
     for kw in jobs:  # (runtime.worker._raw_key never batches these: their loop is not the plain one)
         if pipeline_class_for(kw.get("pipeline_type", "DiffusionPipeline"), model_name) in GUIDED_CLASSES:
-            raise ValueError("Panorama / SAG jobs run alone, not in a denoising batch")
+            raise ValueError("Panorama / SAG / safe-latent-diffusion jobs run alone, not in a denoising batch")
     pipe = load_sd(model_name, device_identifier, k0.get("revision", "main"))
     sched_type = k0.get("scheduler_type", "DPMSolverMultistepScheduler")
     sched = get_scheduler(sched_type, **pipe.family.scheduler_kwargs())

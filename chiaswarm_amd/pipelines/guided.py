@@ -1,8 +1,8 @@
 """Sampling-loop variants of Stable Diffusion that the hive can name as a
 diffusers class (``parameters.pipeline_type``; the reference builds any such
 name by reflection, swarm/job_arguments.py:143-145, swarm/type_helpers.py:1-3,
-swarm/diffusion/diffusion_func.py:41-46).  Both run a plain SD checkpoint on
-the resident bundle; only the denoising loop differs.
+swarm/diffusion/diffusion_func.py:41-46).  All three run a plain SD
+checkpoint on the resident bundle; only the denoising loop differs.
 
 * ``StableDiffusionPanoramaPipeline`` (MultiDiffusion, Bar-Tal et al. 2023):
   the latent canvas (default 512 x 2048 px) is covered by 64 x 64 latent
@@ -23,6 +23,12 @@ the resident bundle; only the denoising loop differs.
   prediction away: ``e += sag_scale * (e_uncond - e_degraded)``.  x0 / noise
   use this sampler's own sigma (diffusers reads ``alphas_cumprod[t]``, equal
   up to the rounding of Karras timesteps; exact for DDIM / PNDM ladders).
+* ``StableDiffusionPipelineSafe`` (Safe Latent Diffusion, Schramowski et al.
+  2023; AIML-TUDA/stable-diffusion-safe): a third CFG row conditioned on a
+  safety concept text; where the text prediction comes within
+  ``sld_threshold`` of the concept's, the concept direction (scaled by
+  ``sld_guidance_scale``, clamped to 1, with momentum) is removed from the
+  guidance after ``sld_warmup_steps``.  The UNet runs as one CFG-3 graph.
 
 Parity against diffusers is unpinned (diffusers is not importable here); the
 CPU tests pin the window geometry, the per-window sampler independence, the
@@ -40,7 +46,13 @@ import torch.nn.functional as F
 
 PANORAMA = "StableDiffusionPanoramaPipeline"
 SAG = "StableDiffusionSAGPipeline"
-CLASSES = (PANORAMA, SAG)
+SAFE = "StableDiffusionPipelineSafe"
+CLASSES = (PANORAMA, SAG, SAFE)
+
+# StableDiffusionPipelineSafe's default safety concept (Schramowski et al. 2023, I2P categories)
+SAFETY_CONCEPT = ("an image showing hate, harassment, violence, suffering, humiliation, harm, suicide, sexual, nudity,"
+                  " bodily fluids, blood, obscene gestures, illegal activity, drug use, theft, vandalism, weapons,"
+                  " child abuse, brutality, cruelty")
 
 # diffusers StableDiffusionPanoramaPipeline.get_views / decode_latents_with_padding
 WINDOW, STRIDE, CIRC_PAD = 64, 8, 8
@@ -206,6 +218,39 @@ def sag_denoise(pipe, x, sched, cross_kv, guidance, added, generator, sag_scale=
     return x
 
 
+@torch.no_grad()
+def sld_denoise(pipe, x, sched, cross_kv, guidance, added, generator, safety_kv, sld_guidance_scale=1000.0,
+                sld_warmup_steps=10, sld_threshold=0.01, sld_momentum_scale=0.3, sld_mom_beta=0.4):
+    """Safe Latent Diffusion loop: CFG batch [uncond, cond, safety concept];
+    the guidance direction loses the part of the text direction that points at
+    the concept, element-wise where the text prediction is within
+    ``sld_threshold`` of the concept's (SLD eqs. 3-8), with momentum, after
+    ``sld_warmup_steps`` evaluations."""
+    b = x.shape[0]
+    kv3 = [torch.cat([kv, s], 0) for kv, s in zip(cross_kv, safety_kv)]
+    pipe._kv_static = False  # the UNet graph copies this 3-way K/V, it is not the text graph's output
+    mom = None
+    i = 0
+    while sched.step_index < sched.n:
+        xi = (x * sched.current_scale()).to(pipe.dtype)
+        e = pipe._unet_eval(torch.cat([xi, xi, xi], 0), sched.current_t(), kv3, added).float()
+        e_u, e_t, e_s = e[:b], e[b:2 * b], e[2 * b:]
+        g = e_t - e_u
+        d = e_t - e_s
+        scale = torch.clamp(d.abs() * sld_guidance_scale, max=1.0)
+        scale = torch.where(d >= sld_threshold, torch.zeros_like(scale), scale)
+        gs = (e_s - e_u) * scale
+        if mom is None:
+            mom = torch.zeros_like(g)
+        gs = gs + sld_momentum_scale * mom
+        mom = sld_mom_beta * mom + (1 - sld_mom_beta) * gs
+        if i >= sld_warmup_steps:
+            g = g - gs
+        x = sched.step(e_u + guidance * g, x, generator)
+        i += 1
+    return x
+
+
 @contextlib.contextmanager
 def _override(pipe, denoise, decode=None):
     pipe._denoise_override = denoise
@@ -268,5 +313,36 @@ def run_sag(pipe, sag_scale=0.75, **kwargs):
         return pipe(**kwargs)
 
 
+def run_safe(pipe, sld_guidance_scale=1000, sld_warmup_steps=10, sld_threshold=0.01, sld_momentum_scale=0.3,
+             sld_mom_beta=0.4, safety_concept=None, **kwargs):
+    """``StableDiffusionPipelineSafe.__call__``: safety guidance runs when
+    ``sld_guidance_scale > 1`` and classifier-free guidance is on; otherwise
+    the plain loop."""
+    _check(pipe, SAFE, kwargs)
+    concept = SAFETY_CONCEPT if safety_concept is None else str(safety_concept)
+    if not (float(sld_guidance_scale) > 1.0 and float(kwargs.get("guidance_scale", 7.5)) > 1.0):
+        return pipe(**kwargs)
+    n = max(1, int(kwargs.get("num_images_per_prompt", 1) or 1))
+    prompt = kwargs.get("prompt", "")
+    b = (len(prompt) if isinstance(prompt, list) else 1) * n
+    _, _, skv = pipe.encode([concept] * b, [""] * b, cfg=False)
+    skv = [t.clone() for t in skv]  # (the text graph's static outputs are rewritten by the next encode)
+    opts = dict(sld_guidance_scale=float(sld_guidance_scale), sld_warmup_steps=int(sld_warmup_steps),
+                sld_threshold=float(sld_threshold), sld_momentum_scale=float(sld_momentum_scale),
+                sld_mom_beta=float(sld_mom_beta))
+
+    def denoise(p, x, sched, cross_kv, guidance, added, generator, **_):
+        return sld_denoise(p, x, sched, cross_kv, guidance, added, generator, skv, **opts)
+
+    with _override(pipe, denoise):
+        out = pipe(**kwargs)
+    out.applied_safety_concept = concept
+    return out
+
+
 def run(cls, pipe, **kwargs):
-    return run_panorama(pipe, **kwargs) if cls == PANORAMA else run_sag(pipe, **kwargs)
+    if cls == PANORAMA:
+        return run_panorama(pipe, **kwargs)
+    if cls == SAFE:
+        return run_safe(pipe, **kwargs)
+    return run_sag(pipe, **kwargs)

@@ -291,7 +291,9 @@ def _raw_key(job):
         return None
     if str(job.get("model_name", "")).startswith("DeepFloyd/"):
         return None
-    if p.get("pipeline_type") in ("StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline"):
+    from ..jobs.router import GUIDED_PIPELINES
+
+    if p.get("pipeline_type") in GUIDED_PIPELINES:
         return None  # their own sampling loops (pipelines/guided.py): never batched or split
     return (job.get("model_name"), job.get("height"), job.get("width"), job.get("num_inference_steps"),
             job.get("guidance_scale"), p.get("scheduler_type"), p.get("pipeline_type"), job.get("content_type"),

@@ -1,6 +1,6 @@
 """Sampling-loop variant classes (pipelines/guided.py):
-StableDiffusionPanoramaPipeline (MultiDiffusion) and StableDiffusionSAGPipeline
-(self-attention guidance), reachable by class name like every diffusers class
+StableDiffusionPanoramaPipeline (MultiDiffusion), StableDiffusionSAGPipeline
+(self-attention guidance) and StableDiffusionPipelineSafe (safe latent diffusion), reachable by class name like every diffusers class
 the reference builds by reflection (swarm/job_arguments.py:143-145,
 swarm/type_helpers.py:1-3).
 
@@ -129,6 +129,25 @@ def test_sag_scale_zero_is_plain_and_guidance_changes_result():
     assert pipe.unet.mid_block.attentions[0].transformer_blocks[0].attn1.__dict__.get("_store_probs") is None
 
 
+def test_safe_latent_diffusion():
+    pipe = StableDiffusion("tiny", device="cpu", seed=6)
+    kw = dict(prompt="a street", num_inference_steps=4, guidance_scale=6.0, output_type="latent")
+    ref = pipe(generator=torch.Generator().manual_seed(0), **kw).latents
+    # safety guidance off (sld_guidance_scale <= 1): the plain pipeline
+    off = guided.run_safe(pipe, sld_guidance_scale=1.0, generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.equal(off.latents, ref)
+    # on, but still warming up for every step: the CFG-3 batch gives the plain CFG result
+    warm = guided.run_safe(pipe, sld_warmup_steps=100, generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.allclose(warm.latents, ref, atol=1e-5, rtol=1e-5), (warm.latents - ref).abs().max()
+    assert warm.applied_safety_concept == guided.SAFETY_CONCEPT
+    on = guided.run_safe(pipe, sld_warmup_steps=0, sld_threshold=1.0, generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.isfinite(on.latents).all() and not torch.allclose(on.latents, ref)
+    # a different concept changes the safety direction
+    other = guided.run_safe(pipe, sld_warmup_steps=0, sld_threshold=1.0, safety_concept="a cat",
+                            generator=torch.Generator().manual_seed(0), **kw)
+    assert not torch.equal(other.latents, on.latents)
+
+
 def test_routing_and_jobs_end_to_end():
     for cls in guided.CLASSES:
         _, kw = router.format_args({"model_name": "m", "parameters": {"pipeline_type": cls}})
@@ -146,6 +165,12 @@ def test_routing_and_jobs_end_to_end():
                                             scheduler_type="DPMSolverMultistepScheduler", upscale=False,
                                             supports_xformers=True)
     assert cfg["_pipeline_type"] == guided.SAG and _size(res) == (64, 64)
+    g = torch.Generator().manual_seed(0)
+    res, cfg = diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type=guided.SAFE, prompt="a beach",
+                                            num_inference_steps=2, sld_warmup_steps=0, generator=g,
+                                            scheduler_type="DPMSolverMultistepScheduler", upscale=False,
+                                            supports_xformers=True)
+    assert cfg["_pipeline_type"] == guided.SAFE and _size(res) == (64, 64)
     with pytest.raises(TypeError, match="sag_scale"):  # a Panorama-only / SAG-only kwarg elsewhere
         diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type="StableDiffusionPipeline", prompt="a",
                                      num_inference_steps=2, sag_scale=0.5, generator=torch.Generator().manual_seed(0),
@@ -162,4 +187,7 @@ def test_panorama_and_sag_on_gpu(gpu):
                               generator=torch.Generator(device=gpu).manual_seed(0))
     assert out.images[0].size == (128, 64) and torch.isfinite(out.latents).all()
     out = guided.run_sag(pipe, prompt="a", num_inference_steps=3, generator=torch.Generator(device=gpu).manual_seed(0))
+    assert len(out.images) == 1 and torch.isfinite(out.latents).all()
+    out = guided.run_safe(pipe, prompt="a", num_inference_steps=3, sld_warmup_steps=0,
+                          generator=torch.Generator(device=gpu).manual_seed(0))
     assert len(out.images) == 1 and torch.isfinite(out.latents).all()

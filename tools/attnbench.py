@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--fa", type=int, default=1, help="persistent stream-K d=64 kernel (attn_fa.hip) on / off")
     ap.add_argument("--workers", type=int, default=0, help="attn_fa workers (0: one per CU)")
     ap.add_argument("--probe", type=int, default=0, help="attn_fa profiling probe (wrong results): 1 exp 2 waits 4 PV 8 QK 16 barrier")
+    ap.add_argument("--logits", default="randn",
+                    help="query/key statistics (the lazy-rescale fast path of attn_fa depends on them): randn "
+                         "(unit logits), scale:S (logit std S, trained-model-like spread), rising:S (key norms grow "
+                         "along the sequence so every key block raises the running row max: the rescale worst case)")
     a = ap.parse_args()
     _lib.load()
     if a.short_kv >= 0:
@@ -39,7 +43,16 @@ def main():
     _lib.load().csk_set_attn_fa_probe(a.probe)
     _lib.load().csk_set_attn_fa_min_skv(128)
     B, Sq, Skv, H, D = map(int, a.shape.split(","))
-    q, k, v = (torch.randn(B, s, H, D, device="cuda").bfloat16() for s in (Sq, Skv, Skv))
+    q, k, v = (torch.randn(B, s, H, D, device="cuda") for s in (Sq, Skv, Skv))
+    kind, _, arg = a.logits.partition(":")
+    if kind == "scale":  # q.k / sqrt(D) has std = S
+        q = q * float(arg)
+    elif kind == "rising":  # a shared direction u: logit(q, k_j) ~ S j / Skv + N(0, 1), rising along the keys
+        u = torch.nn.functional.normalize(torch.randn(D, device="cuda"), dim=0)
+        ramp = float(arg) * torch.arange(Skv, device="cuda", dtype=torch.float32) / Skv
+        q = q + D ** 0.5 * u
+        k = k + ramp[None, :, None, None] * u
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
     hip_ops.ATTN_VARIANT = a.variant
     def run():
         if a.split > 1:
@@ -70,7 +83,7 @@ def main():
         print("phase cycles per unit per wave:", {k: round(v, 1) for k, v in zip(names, per)},
               "sum", round(per.sum(), 1), "seg ends", arr[:, 0, 6].sum())
     print(f"fa {a.fa} probe {a.probe} w {a.workers} attn32 {a.attn32} variant {a.variant} split {a.split} short_kv {a.short_kv} rows {a.kv_rows} {a.shape}: "
-          f"{ms * 1000:.1f} us  "
+          f"logits {a.logits}: {ms * 1000:.1f} us  "
           f"{4 * B * H * Sq * Skv * D / ms / 1e9:.1f} TF/s")
 
 
