@@ -26,6 +26,7 @@ PIPELINE_TYPES = {
     "TextToVideoSDPipeline", "VideoToVideoSDPipeline", "IFPipeline", "IFSuperResolutionPipeline",
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
+    "StableUnCLIPImg2ImgPipeline",
 }
 # SD classes with their own sampling loop (pipelines/guided.py): never batched
 # with other jobs, never split across GPUs

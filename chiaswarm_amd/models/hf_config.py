@@ -62,7 +62,7 @@ def unet_config(cfg: dict, what: str = "unet") -> UNetConfig:
                          ("mid_block_type", {"UNetMidBlock2DCrossAttn"}), ("conv_in_kernel", {3}),
                          ("conv_out_kernel", {3}), ("attention_type", {"default"}), ("act_fn", {"silu"}),
                          ("encoder_hid_dim_type", {None}), ("addition_embed_type", {None, "text_time"}),
-                         ("class_embed_type", {None, "timestep", "simple_projection"}),
+                         ("class_embed_type", {None, "timestep", "simple_projection", "projection"}),
                          ("flip_sin_to_cos", {True}), ("freq_shift", {0})):
         _expect(cfg, key, allowed, what)
     for key in ("dual_cross_attention", "only_cross_attention", "resnet_skip_time_act", "mid_block_only_cross_attention"):

@@ -37,9 +37,12 @@ class SafetyConfig:
     heads: int = 16
     mlp: int = 4096
     proj: int = 768
+    act: str = "quick_gelu"  # transformers hidden_act (OpenCLIP ViT-H/14 image encoders: "gelu")
 
 
 CLIP_L14 = SafetyConfig()
+# OpenCLIP ViT-H/14 image tower (stabilityai/stable-diffusion-2-1-unclip image_encoder/)
+CLIP_H14 = SafetyConfig(dim=1280, depth=32, heads=16, mlp=5120, proj=1024, act="gelu")
 TINY_SAFETY = SafetyConfig(image_size=28, patch=14, dim=64, depth=2, heads=2, mlp=128, proj=32)
 
 

@@ -114,6 +114,10 @@ X4_UPSCALER = UNetConfig(
     up_block_types=("CrossAttnUpBlock2D",) * 3 + ("UpBlock2D",),
     num_heads=8, cross_attention_dim=1024, num_class_embeds=1000, sample_size=128)
 TINY_X4 = dataclasses.replace(TINY, in_channels=7, num_class_embeds=1000)
+# stabilityai/stable-diffusion-2-1-unclip: SD2.1-v UNet + "projection" class
+# embedding of [noised ViT-H/14 image embedding (1024) | noise-level sinusoid (1024)]
+SD21_UNCLIP = dataclasses.replace(SD21_V, class_embed_type="projection", projection_class_embeddings_input_dim=2048)
+TINY_UNCLIP = dataclasses.replace(TINY, class_embed_type="projection", projection_class_embeddings_input_dim=64)
 # stabilityai/stable-diffusion-2-depth: latents + 1 depth channel (512 px, epsilon)
 DEPTH_SD2 = dataclasses.replace(SD21, in_channels=5)
 TINY_DEPTH = dataclasses.replace(TINY, in_channels=5)
@@ -153,6 +157,8 @@ class UNet2DConditionModel(Prepared):
             self.class_embedding = TimestepEmbedding(ch[0], temb_dim)
         elif cfg.class_embed_type == "simple_projection":  # AudioLDM: CLAP embedding -> temb
             self.class_embedding = Linear(cfg.projection_class_embeddings_input_dim, temb_dim)
+        elif cfg.class_embed_type == "projection":  # SD2.1-unCLIP: noised CLIP image embedding + level -> temb
+            self.class_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, temb_dim)
         elif cfg.num_class_embeds is not None:  # x4 upscaler: noise level as a class id
             self.class_embedding = nn.Embedding(cfg.num_class_embeds, temb_dim)
         rtemb = temb_dim * (2 if cfg.class_embeddings_concat else 1)
@@ -277,12 +283,16 @@ class UNet2DConditionModel(Prepared):
         if self.cfg.addition_embed_type == "text_time":
             ae = added_cond.get("add_emb")  # precomputed once per request (pipelines.sd._UNetGraph)
             temb = temb + (ae if ae is not None else self.add_emb(added_cond, dtype))
+        if class_labels is None and added_cond is not None:  # per-request labels carried with the added cond
+            class_labels = added_cond.get("class_labels")
         if self.cfg.class_embed_type == "timestep" and class_labels is not None:
             cl = timestep_embedding(class_labels.reshape(-1).float(), self.cfg.block_out_channels[0])
             temb = temb + self.class_embedding(cl.to(dtype))
         elif self.cfg.class_embed_type == "simple_projection" and class_labels is not None:
             cemb = self.class_embedding(class_labels.to(dtype))
             temb = torch.cat([temb, cemb], -1) if self.cfg.class_embeddings_concat else temb + cemb
+        elif self.cfg.class_embed_type == "projection" and class_labels is not None:
+            temb = temb + self.class_embedding(class_labels.to(dtype))
         elif self.cfg.num_class_embeds is not None and class_labels is not None:
             temb = temb + self.class_embedding(class_labels.reshape(-1).long()).to(dtype).expand_as(temb)
         return temb

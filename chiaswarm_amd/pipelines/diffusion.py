@@ -36,14 +36,14 @@ SD_CLASSES = {
     "StableDiffusionInpaintPipeline", "StableDiffusionInpaintPipelineLegacy", "StableDiffusionControlNetPipeline",
     "StableDiffusionControlNetImg2ImgPipeline", "StableDiffusionInstructPix2PixPipeline",
     "StableDiffusionXLPipeline", "StableDiffusionXLImg2ImgPipeline", "StableDiffusionXLInpaintPipeline",
-    "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
+    "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline", "StableUnCLIPImg2ImgPipeline",
     # sampling-loop variants on a plain SD checkpoint (pipelines/guided.py)
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
 }
 # checkpoints whose own class must win over a generic requested one (the
 # router defaults an image job to StableDiffusionImg2ImgPipeline; these
 # architectures cannot run as that class)
-_OWN_CLASS = {"StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline"}
+_OWN_CLASS = {"StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline", "StableUnCLIPImg2ImgPipeline"}
 GUIDED_CLASSES = GUIDED_PIPELINES  # (guided.CLASSES)
 UPSCALE_CLASSES = {"StableDiffusionUpscalePipeline", "StableDiffusionLatentUpscalePipeline"}
 # job kwargs the SD callback consumes itself (the rest go to the pipeline call)
@@ -65,6 +65,8 @@ def checkpoint_class(model_name: str, revision: str = "main") -> str | None:
     n = model_name.lower()
     if "image-variations" in n or (n.startswith("tiny/") and "variation" in n):
         return "StableDiffusionImageVariationPipeline"
+    if "unclip" in n:
+        return "StableUnCLIPImg2ImgPipeline"
     if "stable-diffusion-2-depth" in n or (n.startswith("tiny/") and "depth" in n):
         return "StableDiffusionDepth2ImgPipeline"
     if "x4-upscaler" in n:
@@ -128,6 +130,10 @@ def load_sd(model_name: str, device_identifier: str, revision: str = "main", con
             from .variants import ImageVariation
 
             return ImageVariation(fam, device=device_identifier, weights_dir=w, seed=stable_seed(model_name))
+        if fam.is_unclip:
+            from .variants import UnCLIPImg2Img
+
+            return UnCLIPImg2Img(fam, device=device_identifier, weights_dir=w, seed=stable_seed(model_name))
         return StableDiffusion(fam, device=device_identifier, weights_dir=w, seed=stable_seed(model_name))
 
     pipe = cache().get(("sd", model_name, revision, device_identifier), make)

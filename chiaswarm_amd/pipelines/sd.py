@@ -88,6 +88,10 @@ class Family:
     def is_image_variation(self) -> bool:  # CLIP image embedding as the only context token
         return self.pipeline_class == "StableDiffusionImageVariationPipeline"
 
+    @property
+    def is_unclip(self) -> bool:  # noised CLIP image embedding as the UNet's class embedding
+        return self.pipeline_class == "StableUnCLIPImg2ImgPipeline"
+
     def scheduler_kwargs(self) -> dict:
         kw = dict(self.sched_config)
         kw["prediction_type"] = self.prediction_type
@@ -140,7 +144,13 @@ FAMILIES = {
                         pipeline_class="StableDiffusionDepth2ImgPipeline"),
     "sd15-imagevar": Family("sd15-imagevar", unet_mod.SD15, vae_mod.SD_VAE, [],
                             pipeline_class="StableDiffusionImageVariationPipeline"),
+    # StableUnCLIPImg2ImgPipeline (stabilityai/stable-diffusion-2-1-unclip): pipelines/variants.py
+    "sd21-unclip": Family("sd21-unclip", unet_mod.SD21_UNCLIP, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H],
+                          pad_with_eos=False, default_size=768, prediction_type="v_prediction",
+                          pipeline_class="StableUnCLIPImg2ImgPipeline"),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
+    "tiny-unclip": Family("tiny-unclip", unet_mod.TINY_UNCLIP, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT],
+                          default_size=64, pipeline_class="StableUnCLIPImg2ImgPipeline"),
     "tiny-depth": Family("tiny-depth", unet_mod.TINY_DEPTH, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64,
                          pipeline_class="StableDiffusionDepth2ImgPipeline"),
     "tiny-imagevar": Family("tiny-imagevar", unet_mod.TINY, vae_mod.TINY_VAE, [], default_size=64,
@@ -159,7 +169,11 @@ def family_for_model(model_name: str) -> str:
     checkpoint is built from its own config files (``resolve_family``)."""
     n = model_name.lower()
     if n.startswith("tiny/") or n == "tiny":
+        if "unclip" in n:
+            return "tiny-unclip"
         return "tiny-depth" if "depth" in n else ("tiny-imagevar" if "variation" in n else "tiny")
+    if "unclip" in n:
+        return "sd21-unclip"
     if "image-variations" in n:
         return "sd15-imagevar"
     if "stable-diffusion-2-depth" in n:
@@ -643,7 +657,7 @@ class StableDiffusion:
         self._kv_static = (not is_pix2pix) and self.use_graphs and hasattr(self, "_text_graphs") and \
             ops.get_mode() == "hip" and ops._lib.available()
         self._req = getattr(self, "_req", 0) + 1
-        if added is not None:
+        if added is not None and self.family.is_xl:
             nrep = ctx.shape[0] // b
             added["time_ids"] = self._time_ids(nrep * b, height, width, self.device, aesthetic, b if cfg else 0)
         self._phase_sync()

@@ -20,13 +20,19 @@ swarm/diffusion/diffusion_func.py:41-46):
   tower is the safety checker's (models/safety.py) — pinned against
   transformers in tests/test_variants.py.
 
-Both run on the resident StableDiffusion bundle (UNet hipGraph step, fused
+* ``StableUnCLIPImg2ImgPipeline`` (stabilityai/stable-diffusion-2-1-unclip):
+  the SD2.1-v UNet with a "projection" class embedding fed the noised CLIP
+  ViT-H/14 image embedding of the start image plus its noise level; the
+  prompt still conditions through cross-attention.
+
+All run on the resident StableDiffusion bundle (UNet hipGraph step, fused
 sampler loop, VAE decode kernels).
 """
 from __future__ import annotations
 
 import json
 import logging
+import math
 import os
 
 import numpy as np
@@ -129,7 +135,7 @@ class CLIPImageEncoder(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.vision_model = ViT(cfg.image_size, cfg.patch, cfg.dim, cfg.depth, cfg.heads, cfg.mlp, eps=1e-5,
-                                act="quick_gelu", pre_norm=True, patch_bias=False)
+                                act=cfg.act, pre_norm=True, patch_bias=False)
         self.visual_projection = Linear(cfg.dim, cfg.proj, bias=False)
 
     def preprocess(self, images: list) -> torch.Tensor:
@@ -162,7 +168,8 @@ def image_encoder_config(d: str) -> SafetyConfig:
                         dim=int(v.get("hidden_size", base.dim)), depth=int(v.get("num_hidden_layers", base.depth)),
                         heads=int(v.get("num_attention_heads", base.heads)),
                         mlp=int(v.get("intermediate_size", base.mlp)),
-                        proj=int(raw.get("projection_dim", v.get("projection_dim", base.proj))))
+                        proj=int(raw.get("projection_dim", v.get("projection_dim", base.proj))),
+                        act=str(v.get("hidden_act", base.act)))
 
 
 def load_image_encoder(device, weights_dir: str | None, cfg: SafetyConfig | None = None, seed: int = 0):
@@ -239,3 +246,129 @@ class ImageVariation(StableDiffusion):
                                     scheduler=scheduler)
         finally:
             self._img_ctx = None
+
+
+# ---------------------------------------------------------------------------
+# StableUnCLIPImg2Img
+# ---------------------------------------------------------------------------
+def _unclip_extras(weights_dir: str | None, dim: int, device):
+    """(mean, std) of the checkpoint's ``image_normalizer`` ([1, dim] fp32;
+    0 / 1 without one) and the ``image_noising_scheduler``'s alpha-bar table
+    (its scheduler_config.json; diffusers' squaredcos_cap_v2 DDPM default)."""
+    from ..schedulers import _betas
+
+    mean = torch.zeros(1, dim, dtype=torch.float32, device=device)
+    std = torch.ones(1, dim, dtype=torch.float32, device=device)
+    cfg = {"num_train_timesteps": 1000, "beta_schedule": "squaredcos_cap_v2", "beta_start": 0.00085,
+           "beta_end": 0.012}
+    if weights_dir:
+        nd = os.path.join(weights_dir, "image_normalizer")
+        if os.path.isdir(nd):
+            from ..models.weights import _read_dir
+
+            sd = _read_dir(nd)
+            mean = sd["mean"].reshape(1, -1).float().to(device)
+            std = sd["std"].reshape(1, -1).float().to(device)
+        sp = os.path.join(weights_dir, "image_noising_scheduler", "scheduler_config.json")
+        if os.path.exists(sp):
+            with open(sp) as f:
+                cfg.update({k: v for k, v in json.load(f).items() if k in cfg})
+    betas = _betas(int(cfg["num_train_timesteps"]), float(cfg["beta_start"]), float(cfg["beta_end"]),
+                   str(cfg["beta_schedule"]))
+    return mean, std, np.cumprod(1.0 - np.asarray(betas, dtype=np.float64))
+
+
+class UnCLIPImg2Img(StableDiffusion):
+    """``StableUnCLIPImg2ImgPipeline`` (stabilityai/stable-diffusion-2-1-unclip):
+    the start image's CLIP ViT-H/14 image embedding, normalised, noised to
+    ``noise_level`` by the checkpoint's image-noising schedule, un-normalised
+    and concatenated with the level's sinusoidal embedding, is the UNet's
+    ``projection`` class embedding (zeros for the unconditional CFG half); the
+    prompt conditions through cross-attention as usual and the latents start
+    from pure noise.  The class labels ride in the UNet's added conditioning,
+    so the step stays one hipGraph replay (the device-resident loop)."""
+
+    def __init__(self, family, device="cpu", dtype=None, seed=0, weights_dir=None, image_encoder_cfg=None):
+        from ..models.safety import CLIP_H14
+
+        super().__init__(family, device=device, dtype=dtype, seed=seed, weights_dir=weights_dir)
+        d = os.path.join(weights_dir, "image_encoder") if weights_dir else None
+        if image_encoder_cfg is None and not (d and os.path.exists(os.path.join(d, "config.json"))):
+            pd = self.family.unet.projection_class_embeddings_input_dim // 2
+            image_encoder_cfg = CLIP_H14 if pd == CLIP_H14.proj else SafetyConfig(
+                image_size=28, patch=14, dim=64, depth=2, heads=2, mlp=128, proj=int(pd), act="gelu")
+        self.image_encoder = load_image_encoder(self.device, weights_dir, image_encoder_cfg, seed=seed + 19)
+        dim = self.image_encoder.cfg.proj
+        if 2 * dim != self.family.unet.projection_class_embeddings_input_dim:
+            raise ValueError(f"unCLIP: image embedding {dim} x 2 != the UNet's class input "
+                             f"{self.family.unet.projection_class_embeddings_input_dim}")
+        self.norm_mean, self.norm_std, self.noise_abar = _unclip_extras(weights_dir, dim, self.device)
+        self._class = None
+        self.config["image_encoder"] = ["chiaswarm_amd", "CLIPVisionModelWithProjection"]
+        self.config["image_normalizer"] = ["chiaswarm_amd", "StableUnCLIPImageNormalizer"]
+        self.config["image_noising_scheduler"] = ["chiaswarm_amd", "DDPMScheduler"]
+
+    @torch.no_grad()
+    def image_embeds(self, images: list) -> torch.Tensor:
+        return self.image_encoder(self.image_encoder.preprocess(images))
+
+    def noise_image_embeds(self, emb: torch.Tensor, noise_level: int, generator=None) -> torch.Tensor:
+        """diffusers ``noise_image_embeddings``: [B, 2 D] = [unscale(add_noise(scale(emb))) | sinusoid(level)]."""
+        from ..models.layers import timestep_embedding
+        from ..schedulers import batch_randn
+
+        lvl = int(noise_level)
+        if not 0 <= lvl < len(self.noise_abar):
+            raise ValueError(f"noise_level must be in [0, {len(self.noise_abar) - 1}], got {noise_level}")
+        b, dim = emb.shape
+        noise = batch_randn((b, dim), generator, emb.device)
+        x = (emb.float() - self.norm_mean) / self.norm_std
+        a = float(self.noise_abar[lvl])
+        x = math.sqrt(a) * x + math.sqrt(1.0 - a) * noise
+        x = x * self.norm_std + self.norm_mean
+        t = torch.full((b,), float(lvl), dtype=torch.float32, device=emb.device)
+        return torch.cat([x, timestep_embedding(t, dim).float()], 1)
+
+    def encode(self, prompts, negatives, cfg, with_kv=True):
+        ctx, _, kv = super().encode(prompts, negatives, cfg, with_kv)
+        cl = self._class
+        if cl is None:
+            raise ValueError("StableUnCLIPImg2ImgPipeline needs an input image (or image_embeds)")
+        cl = cl.to(self.dtype)
+        if cfg:
+            cl = torch.cat([torch.zeros_like(cl), cl], 0)
+        return ctx, {"class_labels": cl}, kv
+
+    @torch.no_grad()
+    def __call__(self, image=None, prompt="", height=None, width=None, num_inference_steps=20, guidance_scale=10.0,
+                 negative_prompt=None, num_images_per_prompt=1, eta=0.0, generator=None, latents=None,
+                 output_type="pil", scheduler=None, noise_level=0, image_embeds=None, **unexpected):
+        if unexpected:
+            raise TypeError(f"StableUnCLIPImg2ImgPipeline.__call__() got unexpected keyword arguments "
+                            f"{sorted(unexpected)}")
+        prompts = prompt if isinstance(prompt, list) else [prompt]
+        b = len(prompts) * num_images_per_prompt
+        if image_embeds is None:
+            if image is None:
+                raise ValueError("StableUnCLIPImg2ImgPipeline needs an input image (start_image_uri)")
+            images = image if isinstance(image, list) else [image]
+            emb = self.image_embeds(images)
+        else:
+            emb = torch.as_tensor(image_embeds).to(self.device)
+            emb = emb.reshape(-1, emb.shape[-1])
+        if emb.shape[0] == 1:
+            emb = emb.expand(b, -1)
+        elif emb.shape[0] == len(prompts):
+            emb = emb.repeat_interleave(num_images_per_prompt, 0)
+        elif emb.shape[0] != b:
+            raise ValueError(f"{emb.shape[0]} image embeddings for {b} images")
+        self._class = self.noise_image_embeds(emb, noise_level, generator)
+        try:
+            return super().__call__(prompt=prompts, negative_prompt=negative_prompt,
+                                    num_inference_steps=num_inference_steps, guidance_scale=guidance_scale,
+                                    num_images_per_prompt=num_images_per_prompt,
+                                    height=height or self.family.default_size, width=width or self.family.default_size,
+                                    generator=generator, eta=eta, latents=latents, output_type=output_type,
+                                    scheduler=scheduler)
+        finally:
+            self._class = None

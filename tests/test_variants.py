@@ -183,6 +183,75 @@ def test_image_variation_checkpoint_without_text_encoder(tmp_path):
     assert torch.isfinite(out.latents).all()
 
 
+def test_unclip_img2img_end_to_end_cpu():
+    """StableUnCLIPImg2ImgPipeline: the checkpoint class wins over the router's
+    Img2Img default; the class embedding is the noised, level-tagged CLIP image
+    embedding (pinned against its formula); image and noise level both steer the
+    result; the unconditional CFG half gets zero class labels."""
+    import math
+
+    from chiaswarm_amd.models.layers import timestep_embedding
+    from chiaswarm_amd.pipelines.variants import UnCLIPImg2Img
+    from chiaswarm_amd.schedulers import batch_randn
+
+    g = torch.Generator().manual_seed(0)
+    res, cfg = diffusion.diffusion_callback("cpu", "tiny/sd-unclip", pipeline_type="StableDiffusionImg2ImgPipeline",
+                                            prompt="a boat", image=_img(64), num_inference_steps=3, generator=g,
+                                            scheduler_type="DDIMScheduler", upscale=False, supports_xformers=True)
+    assert cfg["_pipeline_type"] == "StableUnCLIPImg2ImgPipeline" and _size(res) == (64, 64)
+    assert cfg.get("image_normalizer") == ["chiaswarm_amd", "StableUnCLIPImageNormalizer"]
+    pipe = diffusion.load_sd("tiny/sd-unclip", "cpu")
+    assert isinstance(pipe, UnCLIPImg2Img) and pipe.unet.cfg.class_embed_type == "projection"
+    # noise_image_embeddings against its formula (normaliser mean 0.5 / std 2, level 500)
+    m0, s0 = pipe.norm_mean, pipe.norm_std
+    pipe.norm_mean, pipe.norm_std = torch.full((1, 32), 0.5), torch.full((1, 32), 2.0)
+    try:
+        emb = torch.randn(2, 32)
+        got = pipe.noise_image_embeds(emb, 500, torch.Generator().manual_seed(3))
+        noise = batch_randn((2, 32), torch.Generator().manual_seed(3), torch.device("cpu"))
+        a = float(pipe.noise_abar[500])
+        want = (math.sqrt(a) * (emb - 0.5) / 2.0 + math.sqrt(1 - a) * noise) * 2.0 + 0.5
+        assert torch.allclose(got[:, :32], want, atol=1e-5)
+        assert torch.allclose(got[:, 32:], timestep_embedding(torch.full((2,), 500.0), 32), atol=1e-6)
+    finally:
+        pipe.norm_mean, pipe.norm_std = m0, s0
+    assert 0.999 < float(pipe.noise_abar[0]) <= 1.0 and float(pipe.noise_abar[999]) < 1e-3  # squaredcos_cap_v2
+    # the unconditional half's class labels are zeros
+    pipe._class = torch.ones(1, 64)
+    _, added, _ = pipe.encode(["a"], [""], True)
+    pipe._class = None
+    assert added["class_labels"].shape == (2, 64) and torch.count_nonzero(added["class_labels"][0]) == 0
+
+    def run(**kw):
+        g = torch.Generator().manual_seed(0)
+        return pipe(prompt="a", num_inference_steps=2, generator=g, output_type="latent", **kw).latents
+
+    base = run(image=_img(64, 1))
+    assert not torch.equal(base, run(image=_img(64, 2)))
+    assert not torch.equal(base, run(image=_img(64, 1), noise_level=600))
+    e = pipe.image_embeds([_img(64, 1)])
+    assert torch.equal(base, run(image_embeds=e))
+    with pytest.raises(ValueError, match="input image"):
+        pipe(prompt="a", num_inference_steps=2)
+    with pytest.raises(ValueError, match="noise_level"):
+        pipe(image=_img(64), num_inference_steps=2, noise_level=1000)
+
+
+def test_unet_projection_class_embedding_config():
+    from chiaswarm_amd.models import hf_config as hc
+
+    cfg = hc.unet_config({"block_out_channels": [32, 64], "down_block_types": ["CrossAttnDownBlock2D", "DownBlock2D"],
+                          "up_block_types": ["UpBlock2D", "CrossAttnUpBlock2D"], "layers_per_block": 1,
+                          "attention_head_dim": 2, "cross_attention_dim": 32, "class_embed_type": "projection",
+                          "projection_class_embeddings_input_dim": 64, "sample_size": 8, "in_channels": 4,
+                          "out_channels": 4})
+    assert cfg.class_embed_type == "projection" and cfg.projection_class_embeddings_input_dim == 64
+    from chiaswarm_amd.models.unet import UNet2DConditionModel
+
+    u = UNet2DConditionModel(cfg)
+    assert {"class_embedding.linear_1.weight", "class_embedding.linear_2.weight"} <= set(u.state_dict())
+
+
 @pytest.mark.gpu
 def test_variants_on_gpu(gpu):
     from chiaswarm_amd.pipelines.sd import StableDiffusion
@@ -192,6 +261,12 @@ def test_variants_on_gpu(gpu):
     d = StableDiffusion("tiny-depth", device=gpu, seed=1)
     out = d(prompt="a", image=_img(64), num_inference_steps=3, strength=0.8, generator=g,
             depth_map=torch.arange(64.0).repeat(64, 1))
+    assert len(out.images) == 1 and torch.isfinite(out.latents).all()
+    from chiaswarm_amd.pipelines.variants import UnCLIPImg2Img
+
+    un = UnCLIPImg2Img("tiny-unclip", device=gpu, seed=3)
+    g = torch.Generator(device=gpu).manual_seed(0)
+    out = un(image=_img(64), prompt="a", num_inference_steps=3, generator=g, noise_level=100)
     assert len(out.images) == 1 and torch.isfinite(out.latents).all()
     iv = ImageVariation("tiny-imagevar", device=gpu, seed=2)
     g = torch.Generator(device=gpu).manual_seed(0)
