@@ -281,8 +281,11 @@ class BasicTransformerBlock(nn.Module):
             folds[name] = f
         return f[1]
 
-    def forward(self, x, ctx=None, kv=None, row_stats=None, dup=False):
-        """On the HIP path every LayerNorm runs inside the GEMM that consumes it
+    def forward(self, x, ctx=None, kv=None, row_stats=None, dup=False, qkv=None):
+        """``qkv``: this block's self-attention projection LN1(x) Wqkv^T already
+        computed (the fused transformer-input kernel, Transformer2D.forward).
+
+        On the HIP path every LayerNorm runs inside the GEMM that consumes it
         (``ops.layer_norm_gemm``): each producer GEMM (proj_in, the attention
         out-projections, the FF down-projection) emits per-row statistics of its
         output, so the three LN kernels per block disappear.  ``row_stats``: emit
@@ -296,9 +299,10 @@ class BasicTransformerBlock(nn.Module):
             row_stats = hip
         a1, a2, ff = self.attn1, self.attn2, self.ff
         a1._ensure()
-        fus = ops.ln_fusable(x)
-        qkv = ops.layer_norm_gemm(x, self.norm1, a1.w_qkv, a1.b_qkv,
-                                  self._fold("qkv", a1.w_qkv, a1.b_qkv, self.norm1) if fus else None)
+        if qkv is None:
+            fus = ops.ln_fusable(x)
+            qkv = ops.layer_norm_gemm(x, self.norm1, a1.w_qkv, a1.b_qkv,
+                                      self._fold("qkv", a1.w_qkv, a1.b_qkv, self.norm1) if fus else None)
         x = a1.attend_qkv(qkv, residual=x, row_stats=hip)
         if hip and not dup and kv is not None and x.dim() == 3 and ops.xattn_fusable(x, kv, x.shape[1]):
             # LN2 + Q projection + attention over the context + out-projection +
@@ -357,25 +361,64 @@ class Transformer2D(nn.Module):
     def cross_modules(self):
         return [blk.attn2 for blk in self.transformer_blocks]
 
+    def _xin_weights(self):
+        """Packed weights of the fused transformer-input kernel (GroupNorm +
+        proj_in + block 0's LN1 + QKV, csrc/kernels/xin.hip); refolded when any
+        of them changes (e.g. a LoRA merge)."""
+        blk = self.transformer_blocks[0]
+        a1 = blk.attn1
+        a1._ensure()
+        wi = self.proj_in.weight
+        key = (wi.data_ptr(), wi._version, a1.w_qkv.data_ptr(), a1.w_qkv._version, blk.norm1.weight._version,
+               wi.device, wi.dtype)
+        hit = self.__dict__.get("_xin")
+        if hit is None or hit[0] != key:
+            w2, colsum, b2 = blk._fold("qkv", a1.w_qkv, a1.b_qkv, blk.norm1)
+            c = wi.shape[0]
+            hit = (key, ops.pack_xin_qkv(wi.detach().reshape(c, c), None if self.proj_in.bias is None
+                                         else self.proj_in.bias.detach(), w2, colsum, b2))
+            self.__dict__["_xin"] = hit
+        return hit[1]
+
+    def _xin_ok(self, x) -> bool:
+        if not ops.row_stats_wanted(x) or not self.transformer_blocks:
+            return False
+        c = x.shape[-1]
+        a1 = self.transformer_blocks[0].attn1
+        w = self.proj_in.weight
+        return (w.shape[0] == c and w.numel() == c * c and a1.to_q.weight.shape[0] == c and not a1.is_cross
+                and ops.xin_fusable(x, self.norm.num_groups))
+
     def forward(self, x, ctx=None, kvs=None, dup=False):
         """``dup``: ``x`` is one CFG half; the first block's cross-attention
         doubles the batch (BasicTransformerBlock.forward) and the output is the
-        full batch."""
+        full batch.  On the HIP path at C = 320 the GroupNorm, proj_in and block
+        0's LayerNorm + QKV projection run as ONE kernel (ops.xin_qkv)."""
         b, hh, ww, c = x.shape
-        h = self.norm(x)
         hip = ops.row_stats_wanted(x)
-        h = self.proj_in(h, row_stats=hip)  # row statistics feed block 0's fused LayerNorm
-        rows = getattr(h, "_csk_rows", None)
-        h = h.view(b, hh * ww, c)
-        if rows is not None:
-            h._csk_rows = rows
+        qkv0 = None
+        got = None
+        if self._xin_ok(x):
+            got = ops.xin_qkv(x, self.norm.weight, self.norm.bias, self.norm.num_groups, self.norm.eps,
+                              self._xin_weights(), self.transformer_blocks[0].norm1.eps)
+        if got is not None:
+            h, qkv0 = got[0].view(b, hh * ww, c), got[1].view(b, hh * ww, 3 * c)
+        else:
+            h = self.norm(x)
+            h = self.proj_in(h, row_stats=hip)  # row statistics feed block 0's fused LayerNorm
+            rows = getattr(h, "_csk_rows", None)
+            h = h.view(b, hh * ww, c)
+            if rows is not None:
+                h._csk_rows = rows
         nb = len(self.transformer_blocks)
         for i, blk in enumerate(self.transformer_blocks):
             if dup and i == 0:
-                h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb, dup=True)
+                h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb, dup=True,
+                        qkv=qkv0)
                 x, b = ops.dup2(x), 2 * b
                 continue
-            h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb)
+            h = blk(h, ctx=ctx, kv=None if kvs is None else kvs[i], row_stats=hip and i + 1 < nb,
+                    qkv=qkv0 if i == 0 else None)
         if isinstance(self.proj_out, Linear):
             return ops.gemm(h.view(b, hh, ww, c), self.proj_out.weight, self.proj_out.bias, residual=x,
                             gn_rows=hh * ww)

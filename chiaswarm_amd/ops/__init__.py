@@ -339,6 +339,94 @@ def _ref_ff_fused(x, gamma, beta, w1p, b1p, w2p, b2, eps):
     return (xf + y).to(x.dtype)
 
 
+def _a_tiles(w):
+    """[N, C] (N % 32 == 0, C % 64 == 0) -> the 32x32x16 A-operand LDS images
+    [N/32, C/64, 32, 64] of ff.hip / xin.hip: row r of a sub-image holds
+    logical 16-byte chunk c at position c ^ ((r & 7) ^ ((r >> 3) & 1))."""
+    n, c = w.shape
+    t = n // 32
+    k8, _ = _ff_keys(w.device)
+    x = w.reshape(t, 32, c // 64, 8, 8)
+    x = torch.gather(x, 3, k8[None, :, None, :, None].expand(t, 32, c // 64, 8, 8))
+    return x.permute(0, 2, 1, 3, 4).reshape(t, c // 64, 32, 64)
+
+
+def _a_untiles(p):
+    t, si = p.shape[0], p.shape[1]
+    k8, _ = _ff_keys(p.device)
+    inv8 = torch.argsort(k8, 1)
+    x = p.reshape(t, si, 32, 8, 8).permute(0, 2, 1, 3, 4)
+    return torch.gather(x, 3, inv8[None, :, None, :, None].expand(t, 32, si, 8, 8)).reshape(32 * t, 64 * si)
+
+
+def pack_xin_qkv(wi, bi, wq, colsum, bq):
+    """Weights of the fused transformer-input kernel (xin.hip) from proj_in
+    ``wi`` [C, C] (+ ``bi``) and the LN1-folded QKV projection (``wq`` [3C, C],
+    ``colsum``, ``bq`` from ``fold_layer_norm``): one bf16 buffer of the 10 + 30
+    A-operand tiles as their LDS images, Wqkv's columns permuted within every
+    16-block to the order the proj_in accumulators hand over (0-3, 8-11, 4-7,
+    12-15), and the fp32 tables (bi, colsum, bq)."""
+    c = wi.shape[0]
+    perm = torch.tensor(_FF_PERM, device=wq.device)
+    wqp = wq.reshape(wq.shape[0], c // 16, 16).index_select(2, perm).reshape(wq.shape[0], c)
+    w = torch.cat([_a_tiles(wi.reshape(c, c)), _a_tiles(wqp)], 0).contiguous()
+    f32 = lambda t, n: (torch.zeros(n, device=wi.device) if t is None else t.float()).contiguous()  # noqa: E731
+    return w, f32(bi, c), f32(colsum, wq.shape[0]), f32(bq, wq.shape[0])
+
+
+def unpack_xin_qkv(w):
+    """Inverse of ``pack_xin_qkv``'s weight buffer: (wi [C, C], wq [3C, C])."""
+    c = 64 * w.shape[1]
+    full = _a_untiles(w)
+    wi, wqp = full[:c], full[c:]
+    inv = torch.argsort(torch.tensor(_FF_PERM, device=w.device))
+    return wi, wqp.reshape(wqp.shape[0], c // 16, 16).index_select(2, inv).reshape(wqp.shape[0], c)
+
+
+def xin_fusable(x: torch.Tensor, groups: int) -> bool:
+    """The fused transformer-input kernel takes this block input (HIP path,
+    C = 320, the producer's GroupNorm statistics attached)."""
+    if not use_hip(x):
+        return False
+    from . import hip_ops
+
+    return hip_ops.xin_ok(x, groups)
+
+
+def xin_qkv(x, gn_gamma, gn_beta, groups, gn_eps, packed, ln_eps):
+    """(h, qkv): h = proj_in(GroupNorm(x)), qkv = LayerNorm1(h) Wqkv^T + b with
+    the LN1 affine folded into ``packed`` (``pack_xin_qkv``).  x: [B, ..., C];
+    h [M, C], qkv [M, 3C].  One HIP kernel (None when the producer's
+    statistics are missing), or the fp32 reference composition."""
+    w, bi, colsum, bq = packed
+    if use_hip(x):
+        from . import hip_ops
+
+        stat = hip_ops.gn_stats(x, groups, gn_eps)
+        if stat is None:
+            return None
+        return hip_ops.xin_qkv(x, stat, gn_gamma, gn_beta, w, bi, colsum, bq, ln_eps)
+    return _ref_xin_qkv(x, gn_gamma, gn_beta, groups, gn_eps, packed, ln_eps)
+
+
+def _ref_xin_qkv(x, gn_gamma, gn_beta, groups, gn_eps, packed, ln_eps):
+    """fp32 reference from the packed weights: GroupNorm, proj_in, LayerNorm
+    (affine folded into the weights), QKV projection."""
+    w, bi, colsum, bq = packed
+    wi, wq = unpack_xin_qkv(w)
+    B, C = x.shape[0], x.shape[-1]
+    xf = x.float().reshape(B, -1, C)
+    g = xf.reshape(B, -1, groups, C // groups)
+    mean = g.mean(dim=(1, 3), keepdim=True)
+    var = g.var(dim=(1, 3), keepdim=True, unbiased=False)
+    xg = ((g - mean) * torch.rsqrt(var + gn_eps)).reshape(B, -1, C)
+    xg = xg * gn_gamma.float() + (0 if gn_beta is None else gn_beta.float())
+    h = xg @ wi.float().t() + bi
+    n = torch.nn.functional.layer_norm(h, (C,), eps=ln_eps)
+    qkv = n @ wq.float().t() + bq
+    return h.reshape(-1, C).to(x.dtype), qkv.reshape(-1, 3 * C).to(x.dtype)
+
+
 def xattn_fusable(x: torch.Tensor, kv, rows_per_b: int) -> bool:
     """The fused cross-attention sub-block kernel takes this block (HIP path)."""
     if not use_hip(x):

@@ -945,3 +945,64 @@ def ff_geglu(x, gamma, beta, w1p, b1p, w2p, b2, eps):
 
 sig("csk_set_xattn_probe", c_int)
 sig("csk_set_xattn_waves", c_int)
+
+
+# Fused transformer input (csrc/kernels/xin.hip): GroupNorm apply + proj_in +
+# LN1 + QKV projection in one kernel at C = 320; the normalised input stays in
+# registers, h is stored once (the out-projection's residual).
+sig("csk_xin_qkv_ok", c_int, c_int, c_int, c_int)
+sig("csk_xin_qkv", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+    c_void_p, c_int, c_int, c_float, c_void_p)
+sig("csk_gn_finalize", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p)
+XIN_FUSED = os.environ.get("CSK_XIN_FUSED", "0") == "1"
+XIN_MIN_ROWS = int(os.environ.get("CSK_XIN_MIN_ROWS", "0"))
+
+
+def gn_stats(x, groups, eps):
+    """(mean, rstd) [B, G, 2] fp32 of a [B, ..., C] bf16 tensor from its
+    producer's fused epilogue statistics (``x._csk_gn``), or None without them."""
+    fused = getattr(x, "_csk_gn", None)
+    if fused is None:
+        return None
+    B, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (B * C)
+    part, seg = fused
+    if P % seg or part.numel() != (B * P // seg) * C * 2 or C % groups:
+        return None
+    stat = torch.empty((B, groups, 2), dtype=torch.float32, device=x.device)
+    _lib.call("csk_gn_finalize", _p(stat), _p(part), None, 0, seg, B, P, C, groups, float(eps), _s())
+    return stat
+
+
+def xin_ok(x, groups) -> bool:
+    """x: [B, P, C] (or NHWC) block input with fused GN statistics attached."""
+    if not XIN_FUSED or x.dtype != torch.bfloat16 or getattr(x, "_csk_gn", None) is None:
+        return False
+    B, C = x.shape[0], x.shape[-1]
+    M = x.numel() // C
+    return M >= XIN_MIN_ROWS and _lib.call_int("csk_xin_qkv_ok", M, C, M // B, groups) == 1
+
+
+def xin_qkv(x, stat, gamma, beta, w, bi, colsum, bq, eps):
+    """(h, qkv) = (proj_in(GroupNorm(x)), LayerNorm1(h) Wqkv^T + b) in ONE
+    kernel; weights / tables from ``ops.pack_xin_qkv``, ``stat`` from
+    ``gn_stats``.  Returns h [M, C] and qkv [M, 3C] (bf16)."""
+    _bf16(x, "xin.x")
+    _bf16(w, "xin.w")
+    _bf16(gamma, "xin.gamma")
+    B, C = x.shape[0], x.shape[-1]
+    M = x.numel() // C
+    x2 = x.reshape(M, C)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    for t, n in ((bi, "bi"), (colsum, "colsum"), (bq, "bq"), (stat, "stat")):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError(f"xin_qkv: {n} must be contiguous fp32")
+    if beta is not None:
+        _bf16(beta, "xin.beta")
+    h = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+    qkv = torch.empty((M, 3 * C), dtype=torch.bfloat16, device=x.device)
+    _lib.call("csk_xin_qkv", _p(h), _p(qkv), _p(x2), _p(stat), _p(gamma.contiguous()),
+              _p(None if beta is None else beta.contiguous()), stat.shape[1], _p(w.contiguous()), _p(bi), _p(colsum),
+              _p(bq), M, M // B, float(eps), _s())
+    return h, qkv

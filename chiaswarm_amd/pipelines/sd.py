@@ -287,6 +287,7 @@ class StableDiffusion:
         for m in [self.unet] + self.text_encoders:
             for sub in m.modules():
                 sub.__dict__.pop("_ln_folds", None)
+                sub.__dict__.pop("_xin", None)
 
     # ------------------------------------------------------------------
     def _text_fn(self, ids, with_kv=True):

@@ -642,6 +642,22 @@ CSK_API int csk_group_norm_part2(void* y, const void* x, const void* x2, int C1,
   CSK_CHECK_LAUNCH();
 }
 
+// Statistics only: (mean, rstd) per (sample, group) merged from the producer's
+// epilogue partials, for a consumer that applies the GroupNorm itself (the
+// fused transformer-input kernel, xin.hip).  stat: B*G*2 floats.
+CSK_API int csk_gn_finalize(void* stat, const void* part, const void* part2, int C1, int seg_rows, int B, int P, int C,
+                            int G, float eps, hipStream_t stream) {
+  if (C % G != 0 || seg_rows <= 0 || P % seg_rows != 0 || !stat || !part) return (int)hipErrorInvalidValue;
+  const int nseg = P / seg_rows;
+  if (nseg * (C / G) > g_gn_wg_min)
+    gn_finalize_part_wg_kernel<<<B * G, 256, 0, stream>>>((const float*)part, (float*)stat, B, C, G, nseg, seg_rows,
+                                                          eps, (const float*)part2, C1);
+  else
+    gn_finalize_part_kernel<<<(B * G + GN_THREADS / 64 - 1) / (GN_THREADS / 64), GN_THREADS, 0, stream>>>(
+        (const float*)part, (float*)stat, B, C, G, nseg, seg_rows, eps, (const float*)part2, C1);
+  return (int)hipGetLastError();
+}
+
 CSK_API int csk_group_norm_part(void* y, const void* x, const void* x2, int C1, const void* part, int seg_rows,
                                 void* stat, const void* gamma, const void* beta, int B, int P, int C, int G, int chunk,
                                 int nchunk, float eps, int silu, int affine_bstride, hipStream_t stream) {

@@ -1,0 +1,328 @@
+// Fused transformer INPUT chain of an SD UNet block at C = 320 (SURVEY K6 + K9 +
+// K11; reference call site swarm/diffusion/diffusion_func.py:96, the diffusers
+// Transformer2DModel: norm -> proj_in -> BasicTransformerBlock.norm1 ->
+// attn1.to_q / to_k / to_v):
+//
+//   xg  = GroupNorm(x)          statistics merged from the producer's epilogue
+//                               partials (csk_gn_finalize): per-sample affine
+//   h   = Wi xg + bi            -> stored: the residual of attn1's out-projection
+//   qkv = LN1(h) Wqkv^T + bqkv  -> stored [M, 960]
+//
+// ONE kernel instead of the GroupNorm apply pass, the proj_in GEMM and the
+// LN-folded QKV GEMM: the normalised input never reaches HBM, h is read back
+// by nobody but the residual, and the 960-wide QKV projection (424 TF/s as a
+// K = 320 GEMM, profiles/callprof_r6_sd21_b8.txt) runs on operands that are
+// already in registers.
+//
+// Wave layout (the fused FF's, ff.hip): 4 waves x 32 rows, one 128-row
+// workgroup per CU, 32x32x16 MFMAs whose B operand is the wave's 32 rows:
+//   * GN(x) of its rows lives in registers as 20 B fragments (lane: row l % 32,
+//     channels 16 ks + 8 h .. +7, h = l / 32);
+//   * proj_in: h^T = Wi xg^T, ten 32-channel output tiles of 20 MFMAs; each
+//     tile's accumulators (channels 8 q + 4 h + r of the lane's row) ARE two B
+//     fragments of the next GEMM in the k-slot order {4h + j, 8 + 4h + j}, so
+//     h never leaves the registers (bf16-rounded exactly as stored); Wqkv's
+//     columns are permuted the same way on the host (ops.pack_xin_qkv);
+//   * LN1 folds into the QKV epilogue (ops.fold_layer_norm):
+//     y = rstd (acc - mean colsum) + b', with the row's (mean, rstd) from the
+//     fp32 h values of the ten proj_in tiles (sum / sum of squares per lane,
+//     the two half-rows combined by one lane swap);
+//   * the 40 weight tiles (10 Wi + 30 Wqkv, 20 KB each, packed as the LDS
+//     images) stream through a 7-slot LDS-DMA ring, five tiles in flight,
+//     one barrier per tile.  The epilogue stores run while DMAs are in flight:
+//     loads retire in order among themselves, so a wait counting only the DMA
+//     pieces issued after a tile stays exact (stores can only make it wait longer).
+// MFMA floor: 800 32x32x16 MFMAs x 32 cycles per wave per 128 rows.
+#include "common.h"
+
+#include "attn_tile.h"
+
+typedef __attribute__((address_space(1))) const void* xin_gptr_t;
+typedef __attribute__((address_space(3))) void* xin_lptr_t;
+
+namespace {
+
+constexpr int XC = 320;             // channels
+constexpr int XQ = 3 * XC;          // QKV width
+constexpr int XW = 4;               // waves
+constexpr int XROWS = 32 * XW;      // rows per workgroup
+constexpr int XSLOT = 32 * XC;      // elements per weight tile (20 KB)
+constexpr int XNSLOT = 7;           // ring depth
+constexpr int XLEAD = XNSLOT - 1;   // tiles issued before the loop (5 stay in flight)
+constexpr int XTI = XC / 32;        // proj_in tiles (10)
+constexpr int XT = XTI + XQ / 32;   // all tiles (40)
+constexpr int XKS = XC / 16;        // 16-deep k-steps (20)
+constexpr int XPPW = XSLOT / 512 / XW;  // 1 KB DMA pieces per wave per tile (5)
+
+struct XinArgs {
+  const bf16_t* x;      // [M][320] block input (pre-GroupNorm)
+  const float* stat;    // [B][G][2] GroupNorm (mean, rstd)
+  const bf16_t* gamma;  // [320] GroupNorm affine
+  const bf16_t* beta;
+  const bf16_t* w;      // [40][5][32][64]: 10 Wi tiles then 30 LN1-folded Wqkv tiles (ops.pack_xin_qkv)
+  const float* bi;      // [320] proj_in bias (fp32)
+  const float* colsum;  // [960] row sums of the folded Wqkv (fp32)
+  const float* bq;      // [960] folded QKV bias (fp32)
+  bf16_t* h;            // [M][320]
+  bf16_t* qkv;          // [M][960]
+  const bf16_t* x_end;  // CSK_DEBUG bounds
+  const bf16_t* w_end;
+  int M, rows_per_b, G;
+  float eps;            // LN1 epsilon
+};
+
+template <int N>
+__device__ __forceinline__ void xin_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void xin_ld(v8s& d, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr));
+}
+__device__ __forceinline__ void xin_ldf(v4f& d, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr));
+}
+__device__ __forceinline__ void xin_wait(int n, v8s& d) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d)); break;
+    case 1: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(d)); break;
+    case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(d)); break;
+    case 3: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(d)); break;
+    case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(d)); break;
+    default: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(d)); break;
+  }
+}
+__device__ __forceinline__ void xin_waitf(v4f (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t ring[XNSLOT * XSLOT];
+  // per-channel tables (plain stores before the first DMA, asm reads after):
+  // GroupNorm scale / shift of this workgroup's sample, proj_in bias, folded
+  // QKV colsum / bias
+  __shared__ __attribute__((aligned(16))) float s_ga[XC];
+  __shared__ __attribute__((aligned(16))) float s_gb[XC];
+  __shared__ __attribute__((aligned(16))) float s_bi[XC];
+  __shared__ __attribute__((aligned(16))) float s_cs[XQ];
+  __shared__ __attribute__((aligned(16))) float s_bq[XQ];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * XROWS;
+  const int row = m0 + wid * 32 + r32;
+  const bool row_ok = row < a.M;
+  const int b = m0 / a.rows_per_b;  // every row of the workgroup is in this sample (host check)
+
+  auto dma_piece = [&](int t, int i) {
+    bf16_t* base = ring + (t % XNSLOT) * XSLOT;
+    const int p = wid + XW * i;
+    const bf16_t* src = a.w + (size_t)t * XSLOT + 512 * p + 8 * lane;
+    CSK_DCHECK(src + 8 <= a.w_end, 95, t, XT);
+    __builtin_amdgcn_global_load_lds((xin_gptr_t)src, (xin_lptr_t)(base + 512 * p), 16, 0, 0);
+  };
+
+  // ---- prologue: rows, tables, then the first XLEAD tiles in flight ----
+  uint4 xu[XKS];
+#pragma unroll
+  for (int ks = 0; ks < XKS; ++ks) {
+    xu[ks] = make_uint4(0, 0, 0, 0);
+    if (row_ok) {
+      CSK_DCHECK(a.x + (size_t)row * XC + 16 * ks + 8 * h + 8 <= a.x_end, 96, row, a.M);
+      xu[ks] = *reinterpret_cast<const uint4*>(a.x + (size_t)row * XC + 16 * ks + 8 * h);
+    }
+  }
+  {
+    const int Cg = XC / a.G;
+    for (int c = tid; c < XC; c += XW * 64) {
+      const float2 st = *reinterpret_cast<const float2*>(a.stat + ((size_t)b * a.G + c / Cg) * 2);
+      const float sc = bf2f(a.gamma[c]) * st.y;
+      s_ga[c] = sc;
+      s_gb[c] = (a.beta ? bf2f(a.beta[c]) : 0.f) - st.x * sc;
+      s_bi[c] = a.bi ? a.bi[c] : 0.f;
+    }
+    for (int c = tid; c < XQ; c += XW * 64) {
+      s_cs[c] = a.colsum[c];
+      s_bq[c] = a.bq ? a.bq[c] : 0.f;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < XLEAD; ++t)
+#pragma unroll
+    for (int i = 0; i < XPPW; ++i) dma_piece(t, i);
+
+  const unsigned ring0 = (unsigned)(size_t)(xin_lptr_t)(void*)ring;
+  const unsigned ga0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_ga;
+  const unsigned gb0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_gb;
+  const unsigned bi0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_bi;
+  const unsigned cs0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_cs;
+  const unsigned bq0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_bq;
+
+  // GN(x) -> B fragments (the table reads are asm: the compiler would order a
+  // plain LDS read after the DMAs just issued with a vmcnt(0))
+  v8s xf[XKS];
+#pragma unroll
+  for (int ks = 0; ks < XKS; ++ks) {
+    v4f sa[4];
+    const unsigned off = (unsigned)((16 * ks + 8 * h) * 4);
+    xin_ldf(sa[0], ga0 + off);
+    xin_ldf(sa[1], ga0 + off + 16);
+    xin_ldf(sa[2], gb0 + off);
+    xin_ldf(sa[3], gb0 + off + 16);
+    xin_waitf(sa);
+    float f[8], v[8];
+    unpack8(xu[ks], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __builtin_fmaf(f[j], sa[j >> 2][j & 3], sa[2 + (j >> 2)][j & 3]);
+    xf[ks] = __builtin_bit_cast(v8s, pack8(v));
+  }
+
+  unsigned wo[4];  // byte offset of k-step (4 si + j)'s A fragment inside sub-image si
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wo[j] = 2u * (unsigned)at_off64(r32, 2 * j + h);
+
+  v8s hf[XKS];  // h^T as the QKV projection's B fragments
+  float rsum = 0.f, rsq = 0.f, mean, rstd;
+  constexpr int D = 6;  // fragment reads in flight ahead of their MFMA
+
+  // wait for tile t, barrier (every wave is then done with tile t - 1, whose
+  // ring slot takes tile t + XLEAD), then acc = W tile t x B^T: 20 MFMAs with
+  // the DMA pieces of tile t + XLEAD spread over them
+  auto enter = [&](int t) {
+    // tile t landed once at most min(XLEAD - 1, XT - 1 - t) younger tiles' pieces are in flight
+    switch (min(XLEAD - 1, XT - 1 - t)) {
+      case 5: xin_vmcnt<5 * XPPW>(); break;
+      case 4: xin_vmcnt<4 * XPPW>(); break;
+      case 3: xin_vmcnt<3 * XPPW>(); break;
+      case 2: xin_vmcnt<2 * XPPW>(); break;
+      case 1: xin_vmcnt<1 * XPPW>(); break;
+      default: xin_vmcnt<0>(); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto tile_mma = [&](int t, const v8s (&bf)[XKS], v16f& acc) {
+    const bool issue = t + XLEAD < XT;
+    const unsigned sb = ring0 + (unsigned)((t % XNSLOT) * XSLOT * 2);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    v8s wf[XKS];
+#pragma unroll
+    for (int ks = 0; ks < D; ++ks) xin_ld(wf[ks], sb + wo[ks & 3] + (unsigned)((ks >> 2) * 4096));
+#pragma unroll
+    for (int ks = 0; ks < XKS; ++ks) {
+      xin_wait(ks + D - 1 < XKS ? D - 1 : XKS - 1 - ks, wf[ks]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bf[ks], acc, 0, 0, 0);
+      if (ks + D < XKS) {
+        const int k1 = ks + D;
+        xin_ld(wf[k1], sb + wo[k1 & 3] + (unsigned)((k1 >> 2) * 4096));
+      }
+      if (issue && (ks & 3) == 3) dma_piece(t + XLEAD, ks >> 2);
+    }
+    mfma_fence16(acc, acc);
+  };
+
+  // ---- proj_in: ten tiles, unrolled (tile o fills B fragments hf[2o], hf[2o + 1]) ----
+#pragma unroll
+  for (int o = 0; o < XTI; ++o) {
+    enter(o);
+    v16f acc;
+    tile_mma(o, xf, acc);
+    v4f bb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(bb[q], bi0 + (unsigned)((32 * o + 8 * q + 4 * h) * 4));
+    xin_waitf(bb);
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      v[i] = acc[i] + bb[i >> 2][i & 3];
+      rsum += v[i];
+      rsq = __builtin_fmaf(v[i], v[i], rsq);
+    }
+    const uint4 lo = pack8(v), hi = pack8(v + 8);
+    hf[2 * o] = __builtin_bit_cast(v8s, lo);
+    hf[2 * o + 1] = __builtin_bit_cast(v8s, hi);
+    if (row_ok) {  // channels 32 o + 8 q + 4 h + r
+      bf16_t* dst = a.h + (size_t)row * XC + 32 * o + 4 * h;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo.x, lo.y);
+      *reinterpret_cast<uint2*>(dst + 8) = make_uint2(lo.z, lo.w);
+      *reinterpret_cast<uint2*>(dst + 16) = make_uint2(hi.x, hi.y);
+      *reinterpret_cast<uint2*>(dst + 24) = make_uint2(hi.z, hi.w);
+    }
+  }
+  // the row's LN1 statistics: the other half-row sits in lane l ^ 32
+  rsum += __shfl_xor(rsum, 32, 64);
+  rsq += __shfl_xor(rsq, 32, 64);
+  mean = rsum * (1.0f / XC);
+  rstd = rsqrtf(fmaxf(rsq * (1.0f / XC) - mean * mean, 0.f) + a.eps);
+
+  // ---- QKV: thirty tiles, y = rstd (acc - mean colsum) + b' ----
+#pragma unroll 1
+  for (int p = 0; p < XQ / 32; ++p) {
+    const int t = XTI + p;
+    enter(t);
+    v16f acc;
+    tile_mma(t, hf, acc);
+    v4f cs[4], bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(cs[q], cs0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
+    xin_waitf(cs);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(bq[q], bq0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
+    xin_waitf(bq);
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = __builtin_fmaf(rstd, acc[i] - mean * cs[i >> 2][i & 3], bq[i >> 2][i & 3]);
+    if (row_ok) {
+      const uint4 lo = pack8(v), hi = pack8(v + 8);
+      bf16_t* dst = a.qkv + (size_t)row * XQ + 32 * p + 4 * h;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo.x, lo.y);
+      *reinterpret_cast<uint2*>(dst + 8) = make_uint2(lo.z, lo.w);
+      *reinterpret_cast<uint2*>(dst + 16) = make_uint2(hi.x, hi.y);
+      *reinterpret_cast<uint2*>(dst + 24) = make_uint2(hi.z, hi.w);
+    }
+  }
+}
+
+CSK_DEBUG_EXPORT(xin)
+
+// 1 when csk_xin_qkv takes this shape: C = 320 (QKV 960), whole 128-row
+// workgroups inside one sample
+CSK_API int csk_xin_qkv_ok(int M, int C, int rows_per_b, int G) {
+  return (C == XC && M > 0 && rows_per_b > 0 && rows_per_b % XROWS == 0 && M % rows_per_b == 0 && G > 0 &&
+          XC % G == 0)
+             ? 1
+             : 0;
+}
+
+// h = proj_in(GroupNorm(x)), qkv = LN1(h) Wqkv^T (weights packed by ops.pack_xin_qkv; stat from csk_gn_finalize)
+CSK_API int csk_xin_qkv(void* hout, void* qkv, const void* x, const void* stat, const void* gamma, const void* beta,
+                        int G, const void* w, const void* bi, const void* colsum, const void* bq, int M, int rows_per_b,
+                        float eps, hipStream_t stream) {
+  if (!csk_xin_qkv_ok(M, XC, rows_per_b, G) || !hout || !qkv || !x || !stat || !gamma || !w || !colsum)
+    return (int)hipErrorInvalidValue;
+  XinArgs a;
+  a.x = (const bf16_t*)x;
+  a.stat = (const float*)stat;
+  a.gamma = (const bf16_t*)gamma;
+  a.beta = (const bf16_t*)beta;
+  a.w = (const bf16_t*)w;
+  a.bi = (const float*)bi;
+  a.colsum = (const float*)colsum;
+  a.bq = (const float*)bq;
+  a.h = (bf16_t*)hout;
+  a.qkv = (bf16_t*)qkv;
+  a.x_end = a.x + (size_t)M * XC;
+  a.w_end = a.w + (size_t)XT * XSLOT;
+  a.M = M;
+  a.rows_per_b = rows_per_b;
+  a.G = G;
+  a.eps = eps;
+  xin_qkv_kernel<<<dim3((M + XROWS - 1) / XROWS), XW * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}

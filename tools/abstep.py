@@ -70,6 +70,8 @@ def apply_arm(arm):
         hip_ops.XATTN_FUSED = arm == "xa1"
     elif arm in ("ff0", "ff1"):  # C = 320 feed-forward: two GEMMs (0) / one fused kernel (1, ff.hip)
         hip_ops.FF_FUSED = arm == "ff1"
+    elif arm in ("xin0", "xin1"):  # C = 320 transformer input: GN + proj_in + QKV GEMMs (0) / one kernel (1, xin.hip)
+        hip_ops.XIN_FUSED = arm == "xin1"
     elif arm in ("lnoff", "lnon"):
         ops.LN_FUSE = arm == "lnon"
     elif arm in ("lnk0", "lnk1"):  # fused-LN row statistics: merge kernel (0) / in the consumer prologue (1)
