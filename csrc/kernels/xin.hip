@@ -28,14 +28,23 @@
 //     fp32 h values of the ten proj_in tiles (sum / sum of squares per lane,
 //     the two half-rows combined by one lane swap);
 //   * the 40 weight tiles (10 Wi + 30 Wqkv, 20 KB each, packed as the LDS
-//     images) stream through a 7-slot LDS-DMA ring, five tiles in flight,
-//     one barrier per tile.  The epilogue stores run while DMAs are in flight:
-//     loads retire in order among themselves, so a wait counting only the DMA
-//     pieces issued after a tile stays exact (stores can only make it wait longer).
+//     images) stream through a 6-slot LDS-DMA ring, one barrier per tile;
+//   * wave roles: 4 compute waves (no global memory traffic in the loop), 2
+//     loader waves issuing ONLY the weight DMAs, so their counted `vmcnt`
+//     waits are exact (a wave that also stores waits for its stores too:
+//     that first version spent ~14 us of a 54 us kernel there), and 2 store
+//     waves copying each finished 128 x 32 output tile from an LDS staging
+//     buffer (double-buffered, 80-byte rows) to h / qkv with 16-byte stores.
+// Measured (tools/xinbench.py, profiles/xin_fused_input_r6.txt): 47 us
+// against 85 us for the GN apply + proj_in + QKV chain at 64x64 x CFG batch 8;
+// the SD2.1 CFG-8 step 10.54 -> 10.42 ms same-box.  At 8192 rows (CFG-2) the
+// 64 workgroups lose to the GEMMs (38 vs 35 us): ops take it from 16384 rows.
 // MFMA floor: 800 32x32x16 MFMAs x 32 cycles per wave per 128 rows.
 #include "common.h"
 
 #include "attn_tile.h"
+
+#include <type_traits>
 
 typedef __attribute__((address_space(1))) const void* xin_gptr_t;
 typedef __attribute__((address_space(3))) void* xin_lptr_t;
@@ -47,12 +56,17 @@ constexpr int XQ = 3 * XC;          // QKV width
 constexpr int XW = 4;               // waves
 constexpr int XROWS = 32 * XW;      // rows per workgroup
 constexpr int XSLOT = 32 * XC;      // elements per weight tile (20 KB)
-constexpr int XNSLOT = 7;           // ring depth
-constexpr int XLEAD = XNSLOT - 1;   // tiles issued before the loop (5 stay in flight)
+constexpr int XNSLOT = 6;           // ring depth
+constexpr int XLEAD = XNSLOT - 1;   // tiles issued before the loop (4 stay in flight)
+constexpr int XDW = 2;              // loader waves (LDS-DMA only: their counted vmcnt waits are exact)
+constexpr int XSW = 2;              // store waves (staging -> global)
+constexpr int XTHREADS = 64 * (XW + XDW + XSW);
+constexpr int XSTG = 80;            // staging row stride in bytes (64 + 16: 2-way LDS conflicts at most)
 constexpr int XTI = XC / 32;        // proj_in tiles (10)
 constexpr int XT = XTI + XQ / 32;   // all tiles (40)
 constexpr int XKS = XC / 16;        // 16-deep k-steps (20)
-constexpr int XPPW = XSLOT / 512 / XW;  // 1 KB DMA pieces per wave per tile (5)
+constexpr int XDPW = XSLOT / 512 / XDW;  // 1 KB DMA pieces per loader wave per tile (10)
+constexpr int XSPL = XROWS * 4 / 64 / XSW;  // 16-byte staging chunks per store-wave lane per tile (4)
 
 struct XinArgs {
   const bf16_t* x;      // [M][320] block input (pre-GroupNorm)
@@ -89,18 +103,29 @@ __device__ __forceinline__ void xin_wait(int n, v8s& d) {
     case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(d)); break;
     case 3: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(d)); break;
     case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(d)); break;
-    default: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(d)); break;
+    case 5: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(d)); break;
+    case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(d)); break;
+    default: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(d)); break;
   }
 }
+typedef unsigned int xu2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int xu4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ xu2_t make_xu2(unsigned x, unsigned y) { return xu2_t{x, y}; }
+
 __device__ __forceinline__ void xin_waitf(v4f (&b)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
+// PROBE (profiling builds, wrong results by design; csk_set_xin_probe): 1 = no
+// global stores, 2 = no MFMAs, 4 = no weight DMA after the prologue (slots reused)
+template <int PROBE>
+__global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t ring[XNSLOT * XSLOT];
-  // per-channel tables (plain stores before the first DMA, asm reads after):
+  // output staging: two [128 rows][XSTG bytes] bf16 tiles (compute -> store waves)
+  __shared__ __attribute__((aligned(16))) unsigned char stg[2 * XROWS * XSTG];
+  // per-channel tables (plain stores in the prologue, asm reads after):
   // GroupNorm scale / shift of this workgroup's sample, proj_in bias, folded
   // QKV colsum / bias
   __shared__ __attribute__((aligned(16))) float s_ga[XC];
@@ -111,21 +136,88 @@ __global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r32 = lane & 31, h = lane >> 5;
   const int m0 = blockIdx.x * XROWS;
-  const int row = m0 + wid * 32 + r32;
-  const bool row_ok = row < a.M;
   const int b = m0 / a.rows_per_b;  // every row of the workgroup is in this sample (host check)
 
-  auto dma_piece = [&](int t, int i) {
-    bf16_t* base = ring + (t % XNSLOT) * XSLOT;
-    const int p = wid + XW * i;
-    const bf16_t* src = a.w + (size_t)t * XSLOT + 512 * p + 8 * lane;
-    CSK_DCHECK(src + 8 <= a.w_end, 95, t, XT);
-    __builtin_amdgcn_global_load_lds((xin_gptr_t)src, (xin_lptr_t)(base + 512 * p), 16, 0, 0);
-  };
+  const unsigned ring0 = (unsigned)(size_t)(xin_lptr_t)(void*)ring;
+  const unsigned stg0 = (unsigned)(size_t)(xin_lptr_t)(void*)stg;
 
-  // ---- prologue: rows, tables, then the first XLEAD tiles in flight ----
+  // ======================= loader waves (XW .. XW + XDW - 1) =======================
+  if (wid >= XW && wid < XW + XDW) {
+    const int dw = wid - XW;
+    auto dma_tile = [&](int t) {
+      bf16_t* base = ring + (t % XNSLOT) * XSLOT;
+#pragma unroll
+      for (int i = 0; i < XDPW; ++i) {
+        const int p = dw + XDW * i;
+        const bf16_t* src = a.w + (size_t)t * XSLOT + 512 * p + 8 * lane;
+        CSK_DCHECK(src + 8 <= a.w_end, 95, t, XT);
+        __builtin_amdgcn_global_load_lds((xin_gptr_t)src, (xin_lptr_t)(base + 512 * p), 16, 0, 0);
+      }
+    };
+    for (int t = 0; t < XLEAD; ++t) dma_tile(t);
+    __builtin_amdgcn_s_barrier();  // tables written
+#pragma unroll 1
+    for (int t = 0; t <= XT; ++t) {
+      if (t < XT) {
+        // tile t landed once at most min(XLEAD - 1, XT - 1 - t) younger tiles' pieces are in flight
+        switch ((PROBE & 4) ? 0 : min(XLEAD - 1, XT - 1 - t)) {
+          case 4: xin_vmcnt<4 * XDPW>(); break;
+          case 3: xin_vmcnt<3 * XDPW>(); break;
+          case 2: xin_vmcnt<2 * XDPW>(); break;
+          case 1: xin_vmcnt<1 * XDPW>(); break;
+          default: xin_vmcnt<0>(); break;
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      // every compute wave is done with tile t - 1: its ring slot takes tile t + XLEAD
+      if (!(PROBE & 4) && t + XLEAD < XT) dma_tile(t + XLEAD);
+    }
+    return;
+  }
+
+  // ============================ store waves ============================
+  if (wid >= XW + XDW) {
+    const int sw = wid - XW - XDW;
+    __builtin_amdgcn_s_barrier();  // tables written
+#pragma unroll 1
+    for (int t = 0; t <= XT; ++t) {
+      __builtin_amdgcn_s_barrier();
+      if (t == 0) continue;
+      // tile t - 1 sits in staging buffer (t - 1) & 1: 128 rows x 4 16-byte chunks
+      const int u = t - 1;
+      const unsigned sb = stg0 + (unsigned)((u & 1) * XROWS * XSTG);
+      xu4_t v[XSPL];
+#pragma unroll
+      for (int i = 0; i < XSPL; ++i) {
+        const int id = (sw * XSPL + i) * 64 + lane, r = id >> 2, c = id & 3;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(sb + (unsigned)(r * XSTG + c * 16)));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+      if (!(PROBE & 1)) {
+        bf16_t* dst;
+        int ld;
+        if (u < XTI) {
+          dst = a.h + 32 * u;
+          ld = XC;
+        } else {
+          dst = a.qkv + 32 * (u - XTI);
+          ld = XQ;
+        }
+#pragma unroll
+        for (int i = 0; i < XSPL; ++i) {
+          const int id = (sw * XSPL + i) * 64 + lane, r = id >> 2, c = id & 3;
+          if (m0 + r < a.M) *reinterpret_cast<xu4_t*>(dst + (size_t)(m0 + r) * ld + 8 * c) = v[i];
+        }
+      }
+    }
+    return;
+  }
+
+  // ============================ compute waves ============================
+  const int r32 = lane & 31, h = lane >> 5;
+  const int row = m0 + wid * 32 + r32;
+  const bool row_ok = row < a.M;
   uint4 xu[XKS];
 #pragma unroll
   for (int ks = 0; ks < XKS; ++ks) {
@@ -150,20 +242,15 @@ __global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < XLEAD; ++t)
-#pragma unroll
-    for (int i = 0; i < XPPW; ++i) dma_piece(t, i);
+  __builtin_amdgcn_s_barrier();  // tables written
 
-  const unsigned ring0 = (unsigned)(size_t)(xin_lptr_t)(void*)ring;
   const unsigned ga0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_ga;
   const unsigned gb0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_gb;
   const unsigned bi0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_bi;
   const unsigned cs0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_cs;
   const unsigned bq0 = (unsigned)(size_t)(xin_lptr_t)(void*)s_bq;
 
-  // GN(x) -> B fragments (the table reads are asm: the compiler would order a
-  // plain LDS read after the DMAs just issued with a vmcnt(0))
+  // GN(x) -> B fragments
   v8s xf[XKS];
 #pragma unroll
   for (int ks = 0; ks < XKS; ++ks) {
@@ -184,31 +271,15 @@ __global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
   unsigned wo[4];  // byte offset of k-step (4 si + j)'s A fragment inside sub-image si
 #pragma unroll
   for (int j = 0; j < 4; ++j) wo[j] = 2u * (unsigned)at_off64(r32, 2 * j + h);
+  // this lane's staging row (8-byte pieces at channel 8 q + 4 h)
+  const unsigned srow = (unsigned)((wid * 32 + r32) * XSTG + 8 * h);
 
   v8s hf[XKS];  // h^T as the QKV projection's B fragments
-  float rsum = 0.f, rsq = 0.f, mean, rstd;
-  constexpr int D = 6;  // fragment reads in flight ahead of their MFMA
+  float rsum = 0.f, rsq = 0.f;
 
-  // wait for tile t, barrier (every wave is then done with tile t - 1, whose
-  // ring slot takes tile t + XLEAD), then acc = W tile t x B^T: 20 MFMAs with
-  // the DMA pieces of tile t + XLEAD spread over them
-  auto enter = [&](int t) {
-    // tile t landed once at most min(XLEAD - 1, XT - 1 - t) younger tiles' pieces are in flight
-    switch (min(XLEAD - 1, XT - 1 - t)) {
-      case 5: xin_vmcnt<5 * XPPW>(); break;
-      case 4: xin_vmcnt<4 * XPPW>(); break;
-      case 3: xin_vmcnt<3 * XPPW>(); break;
-      case 2: xin_vmcnt<2 * XPPW>(); break;
-      case 1: xin_vmcnt<1 * XPPW>(); break;
-      default: xin_vmcnt<0>(); break;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  auto tile_mma = [&](int t, const v8s (&bf)[XKS], v16f& acc) {
-    const bool issue = t + XLEAD < XT;
-    const unsigned sb = ring0 + (unsigned)((t % XNSLOT) * XSLOT * 2);
+  auto tile_mma = [&](int t, const v8s (&bf)[XKS], v16f& acc, auto dconst) {
+    constexpr int D = decltype(dconst)::value;  // fragment reads in flight ahead of their MFMA
+    const unsigned sb = ring0 + (unsigned)(((PROBE & 4) ? t % XLEAD : t % XNSLOT) * XSLOT * 2);
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     v8s wf[XKS];
@@ -217,26 +288,37 @@ __global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
 #pragma unroll
     for (int ks = 0; ks < XKS; ++ks) {
       xin_wait(ks + D - 1 < XKS ? D - 1 : XKS - 1 - ks, wf[ks]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bf[ks], acc, 0, 0, 0);
+      if constexpr ((PROBE & 2) != 0) asm volatile("" ::"v"(wf[ks]), "v"(bf[ks]));
+      else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bf[ks], acc, 0, 0, 0);
       if (ks + D < XKS) {
         const int k1 = ks + D;
         xin_ld(wf[k1], sb + wo[k1 & 3] + (unsigned)((k1 >> 2) * 4096));
       }
-      if (issue && (ks & 3) == 3) dma_piece(t + XLEAD, ks >> 2);
     }
     mfma_fence16(acc, acc);
+  };
+  // 16 outputs (channels 8 q + 4 h + r of the lane's row) -> staging buffer t & 1
+  auto stage = [&](int t, const uint4& lo, const uint4& hi) {
+    const unsigned d = stg0 + (unsigned)((t & 1) * XROWS * XSTG) + srow;
+    asm volatile("ds_write_b64 %0, %1\n\tds_write_b64 %0, %2 offset:16\n\tds_write_b64 %0, %3 offset:32\n\t"
+                 "ds_write_b64 %0, %4 offset:48"
+                 :: "v"(d), "v"(make_xu2(lo.x, lo.y)), "v"(make_xu2(lo.z, lo.w)), "v"(make_xu2(hi.x, hi.y)),
+                    "v"(make_xu2(hi.z, hi.w))
+                 : "memory");
   };
 
   // ---- proj_in: ten tiles, unrolled (tile o fills B fragments hf[2o], hf[2o + 1]) ----
 #pragma unroll
   for (int o = 0; o < XTI; ++o) {
-    enter(o);
-    v16f acc;
-    tile_mma(o, xf, acc);
-    v4f bb[4];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    v4f bb[4];  // the tile's bias, read ahead of the MFMAs
 #pragma unroll
     for (int q = 0; q < 4; ++q) xin_ldf(bb[q], bi0 + (unsigned)((32 * o + 8 * q + 4 * h) * 4));
     xin_waitf(bb);
+    v16f acc;
+    tile_mma(o, xf, acc, std::integral_constant<int, 4>{});
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -247,49 +329,61 @@ __global__ __launch_bounds__(XW * 64, 1) void xin_qkv_kernel(const XinArgs a) {
     const uint4 lo = pack8(v), hi = pack8(v + 8);
     hf[2 * o] = __builtin_bit_cast(v8s, lo);
     hf[2 * o + 1] = __builtin_bit_cast(v8s, hi);
-    if (row_ok) {  // channels 32 o + 8 q + 4 h + r
-      bf16_t* dst = a.h + (size_t)row * XC + 32 * o + 4 * h;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(lo.x, lo.y);
-      *reinterpret_cast<uint2*>(dst + 8) = make_uint2(lo.z, lo.w);
-      *reinterpret_cast<uint2*>(dst + 16) = make_uint2(hi.x, hi.y);
-      *reinterpret_cast<uint2*>(dst + 24) = make_uint2(hi.z, hi.w);
-    }
+    stage(o, lo, hi);
   }
   // the row's LN1 statistics: the other half-row sits in lane l ^ 32
   rsum += __shfl_xor(rsum, 32, 64);
   rsq += __shfl_xor(rsq, 32, 64);
-  mean = rsum * (1.0f / XC);
-  rstd = rsqrtf(fmaxf(rsq * (1.0f / XC) - mean * mean, 0.f) + a.eps);
+  const float mean = rsum * (1.0f / XC);
+  const float rstd = rsqrtf(fmaxf(rsq * (1.0f / XC) - mean * mean, 0.f) + a.eps);
 
   // ---- QKV: thirty tiles, y = rstd (acc - mean colsum) + b' ----
+  // the tables of QKV tile p are read during tile p - 1 (no exposed LDS latency at the tile start)
+  v4f cs[4], bq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xin_ldf(cs[q], cs0 + (unsigned)((8 * q + 4 * h) * 4));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xin_ldf(bq[q], bq0 + (unsigned)((8 * q + 4 * h) * 4));
+  xin_waitf(cs);
+  xin_waitf(bq);
 #pragma unroll 1
   for (int p = 0; p < XQ / 32; ++p) {
     const int t = XTI + p;
-    enter(t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     v16f acc;
-    tile_mma(t, hf, acc);
-    v4f cs[4], bq[4];
+    tile_mma(t, hf, acc, std::integral_constant<int, 8>{});
+    v4f cn[4], bn[4];  // the next tile's tables, in flight during this epilogue
+    const int pn = p + 1 < XQ / 32 ? p + 1 : p;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xin_ldf(cs[q], cs0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
-    xin_waitf(cs);
+    for (int q = 0; q < 4; ++q) xin_ldf(cn[q], cs0 + (unsigned)((32 * pn + 8 * q + 4 * h) * 4));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xin_ldf(bq[q], bq0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
-    xin_waitf(bq);
+    for (int q = 0; q < 4; ++q) xin_ldf(bn[q], bq0 + (unsigned)((32 * pn + 8 * q + 4 * h) * 4));
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = __builtin_fmaf(rstd, acc[i] - mean * cs[i >> 2][i & 3], bq[i >> 2][i & 3]);
-    if (row_ok) {
-      const uint4 lo = pack8(v), hi = pack8(v + 8);
-      bf16_t* dst = a.qkv + (size_t)row * XQ + 32 * p + 4 * h;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(lo.x, lo.y);
-      *reinterpret_cast<uint2*>(dst + 8) = make_uint2(lo.z, lo.w);
-      *reinterpret_cast<uint2*>(dst + 16) = make_uint2(hi.x, hi.y);
-      *reinterpret_cast<uint2*>(dst + 24) = make_uint2(hi.z, hi.w);
+    stage(t, pack8(v), pack8(v + 8));
+    xin_waitf(cn);
+    xin_waitf(bn);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cs[q] = cn[q];
+      bq[q] = bn[q];
     }
   }
+  // the store waves' last round (tile XT - 1) follows this barrier
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 }
 
 CSK_DEBUG_EXPORT(xin)
+
+static int g_xin_probe = 0;
+CSK_API int csk_set_xin_probe(int p) {
+  g_xin_probe = p;
+  return 0;
+}
 
 // 1 when csk_xin_qkv takes this shape: C = 320 (QKV 960), whole 128-row
 // workgroups inside one sample
@@ -323,6 +417,13 @@ CSK_API int csk_xin_qkv(void* hout, void* qkv, const void* x, const void* stat, 
   a.rows_per_b = rows_per_b;
   a.G = G;
   a.eps = eps;
-  xin_qkv_kernel<<<dim3((M + XROWS - 1) / XROWS), XW * 64, 0, stream>>>(a);
+  const dim3 grid((M + XROWS - 1) / XROWS);
+  switch (g_xin_probe) {
+    case 1: xin_qkv_kernel<1><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 2: xin_qkv_kernel<2><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 4: xin_qkv_kernel<4><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 7: xin_qkv_kernel<7><<<grid, XTHREADS, 0, stream>>>(a); break;
+    default: xin_qkv_kernel<0><<<grid, XTHREADS, 0, stream>>>(a); break;
+  }
   return (int)hipGetLastError();
 }
