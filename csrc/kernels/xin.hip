@@ -105,7 +105,11 @@ __device__ __forceinline__ void xin_wait(int n, v8s& d) {
     case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(d)); break;
     case 5: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(d)); break;
     case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(d)); break;
-    default: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(d)); break;
+    case 7: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(d)); break;
+    case 8: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(d)); break;
+    case 9: asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(d)); break;
+    case 10: asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(d)); break;
+    default: asm volatile("s_waitcnt lgkmcnt(11)" : "+v"(d)); break;
   }
 }
 typedef unsigned int xu2_t __attribute__((ext_vector_type(2)));
@@ -119,7 +123,8 @@ __device__ __forceinline__ void xin_waitf(v4f (&b)[4]) {
 }  // namespace
 
 // PROBE (profiling builds, wrong results by design; csk_set_xin_probe): 1 = no
-// global stores, 2 = no MFMAs, 4 = no weight DMA after the prologue (slots reused)
+// global stores, 2 = no MFMAs, 4 = no weight DMA after the prologue (slots reused),
+// 8 = no barriers in the tile loop (every role runs free)
 template <int PROBE>
 __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t ring[XNSLOT * XSLOT];
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
     for (int t = 0; t < XLEAD; ++t) dma_tile(t);
     __builtin_amdgcn_s_barrier();  // tables written
 #pragma unroll 1
-    for (int t = 0; t <= XT; ++t) {
+    for (int t = 0; t <= XT + 1; ++t) {
       if (t < XT) {
         // tile t landed once at most min(XLEAD - 1, XT - 1 - t) younger tiles' pieces are in flight
         switch ((PROBE & 4) ? 0 : min(XLEAD - 1, XT - 1 - t)) {
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
           default: xin_vmcnt<0>(); break;
         }
       }
-      __builtin_amdgcn_s_barrier();
+      if constexpr ((PROBE & 8) == 0) __builtin_amdgcn_s_barrier();
       // every compute wave is done with tile t - 1: its ring slot takes tile t + XLEAD
       if (!(PROBE & 4) && t + XLEAD < XT) dma_tile(t + XLEAD);
     }
@@ -181,11 +186,12 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
     const int sw = wid - XW - XDW;
     __builtin_amdgcn_s_barrier();  // tables written
 #pragma unroll 1
-    for (int t = 0; t <= XT; ++t) {
-      __builtin_amdgcn_s_barrier();
-      if (t == 0) continue;
-      // tile t - 1 sits in staging buffer (t - 1) & 1: 128 rows x 4 16-byte chunks
-      const int u = t - 1;
+    for (int t = 0; t <= XT + 1; ++t) {
+      if constexpr ((PROBE & 8) == 0) __builtin_amdgcn_s_barrier();
+      if (t < 2) continue;
+      // tile t - 2 sits in staging buffer (t - 2) & 1 (written between barriers t - 1 and t):
+      // 128 rows x 4 16-byte chunks
+      const int u = t - 2;
       const unsigned sb = stg0 + (unsigned)((u & 1) * XROWS * XSTG);
       xu4_t v[XSPL];
 #pragma unroll
@@ -275,27 +281,20 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
   const unsigned srow = (unsigned)((wid * 32 + r32) * XSTG + 8 * h);
 
   v8s hf[XKS];  // h^T as the QKV projection's B fragments
-  float rsum = 0.f, rsq = 0.f;
+  float rsum = 0.f, rsq = 0.f, mean = 0.f, rstd = 0.f;
 
-  auto tile_mma = [&](int t, const v8s (&bf)[XKS], v16f& acc, auto dconst) {
-    constexpr int D = decltype(dconst)::value;  // fragment reads in flight ahead of their MFMA
-    const unsigned sb = ring0 + (unsigned)(((PROBE & 4) ? t % XLEAD : t % XNSLOT) * XSLOT * 2);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    v8s wf[XKS];
-#pragma unroll
-    for (int ks = 0; ks < D; ++ks) xin_ld(wf[ks], sb + wo[ks & 3] + (unsigned)((ks >> 2) * 4096));
-#pragma unroll
-    for (int ks = 0; ks < XKS; ++ks) {
-      xin_wait(ks + D - 1 < XKS ? D - 1 : XKS - 1 - ks, wf[ks]);
-      if constexpr ((PROBE & 2) != 0) asm volatile("" ::"v"(wf[ks]), "v"(bf[ks]));
-      else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bf[ks], acc, 0, 0, 0);
-      if (ks + D < XKS) {
-        const int k1 = ks + D;
-        xin_ld(wf[k1], sb + wo[k1 & 3] + (unsigned)((k1 >> 2) * 4096));
-      }
-    }
-    mfma_fence16(acc, acc);
+  // Software pipeline per tile t: barrier t (tile t landed, every wave done with
+  // tile t - 1) -> issue tile t's first D fragment reads -> the EPILOGUE of tile
+  // t - 1 (its accumulators kept in acc_prev) while they are in flight -> the
+  // MFMA chain of tile t.  The staging buffer of tile t - 1 is written between
+  // barriers t and t + 1; the store waves copy it out after barrier t + 1.
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr ((PROBE & 8) == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto slot = [&](int t) -> unsigned {
+    return ring0 + (unsigned)(((PROBE & 4) ? t % XLEAD : t % XNSLOT) * XSLOT * 2);
   };
   // 16 outputs (channels 8 q + 4 h + r of the lane's row) -> staging buffer t & 1
   auto stage = [&](int t, const uint4& lo, const uint4& hi) {
@@ -306,19 +305,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
                     "v"(make_xu2(hi.z, hi.w))
                  : "memory");
   };
-
-  // ---- proj_in: ten tiles, unrolled (tile o fills B fragments hf[2o], hf[2o + 1]) ----
-#pragma unroll
-  for (int o = 0; o < XTI; ++o) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    v4f bb[4];  // the tile's bias, read ahead of the MFMAs
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xin_ldf(bb[q], bi0 + (unsigned)((32 * o + 8 * q + 4 * h) * 4));
-    xin_waitf(bb);
-    v16f acc;
-    tile_mma(o, xf, acc, std::integral_constant<int, 4>{});
+  // proj_in epilogue of tile o: + bias -> h (staged, kept as B fragments hf[2o], hf[2o + 1], LN1 sums)
+  auto epi_in = [&](int o, v16f& acc, const v4f (&bb)[4]) {
+    mfma_fence16(acc, acc);
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -330,51 +319,115 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
     hf[2 * o] = __builtin_bit_cast(v8s, lo);
     hf[2 * o + 1] = __builtin_bit_cast(v8s, hi);
     stage(o, lo, hi);
-  }
-  // the row's LN1 statistics: the other half-row sits in lane l ^ 32
-  rsum += __shfl_xor(rsum, 32, 64);
-  rsq += __shfl_xor(rsq, 32, 64);
-  const float mean = rsum * (1.0f / XC);
-  const float rstd = rsqrtf(fmaxf(rsq * (1.0f / XC) - mean * mean, 0.f) + a.eps);
-
-  // ---- QKV: thirty tiles, y = rstd (acc - mean colsum) + b' ----
-  // the tables of QKV tile p are read during tile p - 1 (no exposed LDS latency at the tile start)
-  v4f cs[4], bq[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) xin_ldf(cs[q], cs0 + (unsigned)((8 * q + 4 * h) * 4));
-#pragma unroll
-  for (int q = 0; q < 4; ++q) xin_ldf(bq[q], bq0 + (unsigned)((8 * q + 4 * h) * 4));
-  xin_waitf(cs);
-  xin_waitf(bq);
-#pragma unroll 1
-  for (int p = 0; p < XQ / 32; ++p) {
-    const int t = XTI + p;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    v16f acc;
-    tile_mma(t, hf, acc, std::integral_constant<int, 8>{});
-    v4f cn[4], bn[4];  // the next tile's tables, in flight during this epilogue
-    const int pn = p + 1 < XQ / 32 ? p + 1 : p;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xin_ldf(cn[q], cs0 + (unsigned)((32 * pn + 8 * q + 4 * h) * 4));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xin_ldf(bn[q], bq0 + (unsigned)((32 * pn + 8 * q + 4 * h) * 4));
+  };
+  // QKV epilogue of tile t: y = rstd (acc - mean colsum) + b'
+  auto epi_qkv = [&](int t, v16f& acc, const v4f (&cs)[4], const v4f (&bq)[4]) {
+    mfma_fence16(acc, acc);
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = __builtin_fmaf(rstd, acc[i] - mean * cs[i >> 2][i & 3], bq[i >> 2][i & 3]);
     stage(t, pack8(v), pack8(v + 8));
-    xin_waitf(cn);
-    xin_waitf(bn);
+  };
+  // MFMA chain of the tile in `sb` whose first D fragment reads are in wf[0..D-1]
+  auto chain = [&](unsigned sb, v8s (&wf)[XKS], const v8s (&bf)[XKS], v16f& acc, auto dconst) {
+    constexpr int D = decltype(dconst)::value;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      cs[q] = cn[q];
-      bq[q] = bn[q];
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < XKS; ++ks) {
+      xin_wait(ks + D - 1 < XKS ? D - 1 : XKS - 1 - ks, wf[ks]);
+      if constexpr ((PROBE & 2) != 0) asm volatile("" ::"v"(wf[ks]), "v"(bf[ks]));
+      else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bf[ks], acc, 0, 0, 0);
+      if (ks + D < XKS) {
+        const int k1 = ks + D;
+        xin_ld(wf[k1], sb + wo[k1 & 3] + (unsigned)((k1 >> 2) * 4096));
+      }
     }
+  };
+  auto first_reads = [&](unsigned sb, v8s (&wf)[XKS], auto dconst) {
+    constexpr int D = decltype(dconst)::value;
+#pragma unroll
+    for (int ks = 0; ks < D; ++ks) xin_ld(wf[ks], sb + wo[ks & 3] + (unsigned)((ks >> 2) * 4096));
+  };
+  auto read_bias = [&](int o, v4f (&bb)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(bb[q], bi0 + (unsigned)((32 * o + 8 * q + 4 * h) * 4));
+  };
+  auto read_qkv_tables = [&](int p, v4f (&cs)[4], v4f (&bq)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(cs[q], cs0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xin_ldf(bq[q], bq0 + (unsigned)((32 * p + 8 * q + 4 * h) * 4));
+  };
+  using DIN = std::integral_constant<int, 8>;    // proj_in: x and h fragments both live
+  using DQKV = std::integral_constant<int, 12>;  // QKV: x fragments dead, deeper read-ahead
+
+  // table reads of the tile whose epilogue runs now are issued BEFORE this
+  // tile's first fragment reads, so a counted lgkmcnt(D) retires just them
+  auto wait_tables = [&](v4f (&x)[4], v4f (&y)[4], auto dconst) {
+    constexpr int D = decltype(dconst)::value;
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3])
+                 : "n"(D));
+  };
+  auto wait_table = [&](v4f (&x)[4], auto dconst) {  // one array: naming it twice in one asm would copy it
+    constexpr int D = decltype(dconst)::value;
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "n"(D));
+  };
+  v16f acc_prev;
+  // ---- proj_in: ten tiles, unrolled (tile o's epilogue runs in tile o + 1) ----
+#pragma unroll
+  for (int o = 0; o < XTI; ++o) {
+    barrier();
+    v8s wf[XKS];
+    const unsigned sb = slot(o);
+    v4f bb[4];
+    if (o > 0) read_bias(o - 1, bb);
+    first_reads(sb, wf, DIN{});
+    if (o > 0) {
+      wait_table(bb, DIN{});
+      epi_in(o - 1, acc_prev, bb);
+    }
+    v16f acc;
+    chain(sb, wf, xf, acc, DIN{});
+    acc_prev = acc;
   }
-  // the store waves' last round (tile XT - 1) follows this barrier
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+
+  // ---- QKV: thirty tiles (tile t's epilogue runs in tile t + 1) ----
+#pragma unroll 1
+  for (int p = 0; p < XQ / 32; ++p) {
+    const int t = XTI + p;
+    barrier();
+    v8s wf[XKS];
+    const unsigned sb = slot(t);
+    v4f cs[4], bq[4];
+    if (p == 0) read_bias(XTI - 1, cs);
+    else read_qkv_tables(p - 1, cs, bq);
+    first_reads(sb, wf, DQKV{});
+    if (p == 0) {  // the last proj_in tile, then the rows' LN1 statistics (the other half-row sits in lane l ^ 32)
+      wait_table(cs, DQKV{});
+      epi_in(XTI - 1, acc_prev, cs);
+      rsum += __shfl_xor(rsum, 32, 64);
+      rsq += __shfl_xor(rsq, 32, 64);
+      mean = rsum * (1.0f / XC);
+      rstd = rsqrtf(fmaxf(rsq * (1.0f / XC) - mean * mean, 0.f) + a.eps);
+    } else {
+      wait_tables(cs, bq, DQKV{});
+      epi_qkv(t - 1, acc_prev, cs, bq);
+    }
+    v16f acc;
+    chain(sb, wf, hf, acc, DQKV{});
+    acc_prev = acc;
+  }
+  barrier();  // barrier XT: the last tile's epilogue, then one more round for the store waves
+  {
+    v4f cs[4], bq[4];
+    read_qkv_tables(XQ / 32 - 1, cs, bq);
+    xin_waitf(cs);
+    xin_waitf(bq);
+    epi_qkv(XT - 1, acc_prev, cs, bq);
+  }
+  barrier();
 }
 
 CSK_DEBUG_EXPORT(xin)
@@ -423,6 +476,8 @@ CSK_API int csk_xin_qkv(void* hout, void* qkv, const void* x, const void* stat, 
     case 2: xin_qkv_kernel<2><<<grid, XTHREADS, 0, stream>>>(a); break;
     case 4: xin_qkv_kernel<4><<<grid, XTHREADS, 0, stream>>>(a); break;
     case 7: xin_qkv_kernel<7><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 8: xin_qkv_kernel<8><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 15: xin_qkv_kernel<15><<<grid, XTHREADS, 0, stream>>>(a); break;
     default: xin_qkv_kernel<0><<<grid, XTHREADS, 0, stream>>>(a); break;
   }
   return (int)hipGetLastError();
