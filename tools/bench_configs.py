@@ -37,16 +37,26 @@ from PIL import Image  # noqa: E402
 from chiaswarm_amd import ops  # noqa: E402
 
 
+LAST_PHASES: dict = {}
+
+
 def timed(fn, reps, warm=1):
+    """Wall latencies of ``reps`` calls; the pipelines' own phase timings
+    (text encode / prepare / denoise / decode, device-synchronised) are kept
+    as per-phase medians in LAST_PHASES."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
-    lat = []
+    lat, ph = [], {}
     for _ in range(reps):
         t = time.perf_counter()
-        fn()
+        out = fn()
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t)
+        for k, v in (getattr(out, "timings", None) or {}).items():
+            ph.setdefault(k, []).append(v)
+    LAST_PHASES.clear()
+    LAST_PHASES.update({k: round(1000 * statistics.median(v), 2) for k, v in ph.items()})
     return lat
 
 
@@ -55,6 +65,8 @@ def emit(name, imgs_per_call, lat, extra=None):
     rec = {"config": name, "images_per_s": round(imgs_per_call / p50, 4), "p50_latency_ms": round(1000 * p50, 1),
            "impl": ops.get_mode(), "reps": len(lat)}
     rec.update(extra or {})
+    if LAST_PHASES:
+        rec["phase_ms_median"] = dict(LAST_PHASES)
     print(json.dumps(rec), flush=True)
 
 
