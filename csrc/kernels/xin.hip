@@ -124,7 +124,8 @@ __device__ __forceinline__ void xin_waitf(v4f (&b)[4]) {
 
 // PROBE (profiling builds, wrong results by design; csk_set_xin_probe): 1 = no
 // global stores, 2 = no MFMAs, 4 = no weight DMA after the prologue (slots reused),
-// 8 = no barriers in the tile loop (every role runs free)
+// 8 = no barriers in the tile loop (every role runs free), 16 = the proj_in phase's
+// tiles do nothing but their barriers (h fragments left zero)
 template <int PROBE>
 __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t ring[XNSLOT * XSLOT];
@@ -379,6 +380,12 @@ __global__ __launch_bounds__(XTHREADS, 1) void xin_qkv_kernel(const XinArgs a) {
 #pragma unroll
   for (int o = 0; o < XTI; ++o) {
     barrier();
+    if constexpr ((PROBE & 16) != 0) {
+      hf[2 * o] = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      hf[2 * o + 1] = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      acc_prev = v16f{};
+      continue;
+    }
     v8s wf[XKS];
     const unsigned sb = slot(o);
     v4f bb[4];
@@ -478,6 +485,7 @@ CSK_API int csk_xin_qkv(void* hout, void* qkv, const void* x, const void* stat, 
     case 7: xin_qkv_kernel<7><<<grid, XTHREADS, 0, stream>>>(a); break;
     case 8: xin_qkv_kernel<8><<<grid, XTHREADS, 0, stream>>>(a); break;
     case 15: xin_qkv_kernel<15><<<grid, XTHREADS, 0, stream>>>(a); break;
+    case 16: xin_qkv_kernel<16><<<grid, XTHREADS, 0, stream>>>(a); break;
     default: xin_qkv_kernel<0><<<grid, XTHREADS, 0, stream>>>(a); break;
   }
   return (int)hipGetLastError();
