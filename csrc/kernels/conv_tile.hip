@@ -65,7 +65,7 @@ struct CtGeo {
 // 16-byte slot of channel group g (of 4) in LDS row r (a pixel or a (tap, cout)
 // row of 64 B): XOR-swizzled so the 16 lanes of an MFMA fragment (16
 // consecutive rows, one group) hit 16 distinct bank quads
-__device__ __forceinline__ int ct_slot(int r, int g) { return g ^ ((r >> 2) & 3); }
+__device__ __forceinline__ int ct_slot(int r, int g) { return g ^ (((r >> 2) & 1) << 1); }
 
 struct ConvTileArgs {
   const bf16_t* x;     // [B][H][W] pixels, pixel stride lda, channels [0, Cin)
@@ -97,12 +97,30 @@ __device__ __forceinline__ void ct_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+__device__ __forceinline__ void ct_ld(v8s& d, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr));
+}
+// wait until at most N LDS reads issued after the fragments f[0..R) are
+// outstanding (LDS reads return in order); names every fragment it waits for
+template <int N, int R>
+__device__ __forceinline__ void ct_wait(v8s (&f)[R]) {
+  if constexpr (R == 3) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]) : "n"(N));
+  } else if constexpr (R == 4) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N));
+  } else {
+    static_assert(R == 6, "2 + NF fragments");
+    asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5])
+                 : "n"(N));
+  }
+}
+
 }  // namespace
 
 template <int NOUT>
 __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
   using Geo = CtGeo<NOUT>;
-  constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF;
+  constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF, CT_R = 2 + NF;
   __shared__ __attribute__((aligned(16))) unsigned char smem[CT_S * CT_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -122,7 +140,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
   for (int i = 0; i < CT_WI; ++i) {
     const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * NOUT + output channel
     const int tap = row / NOUT, co = row % NOUT;
-    const int g = (lane & 3) ^ ((row >> 2) & 3);  // source channel group landing in this lane's slot
+    const int g = (lane & 3) ^ (((row >> 2) & 1) << 1);  // source channel group landing in this lane's slot
     wsrc[i] = row < 9 * NOUT && co < a.Cout ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
   }
   // ---- halo DMA: instruction k = wv * 3 + i writes halo pixels 16 k .. 16 k + 15 ----
@@ -138,7 +156,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
       const int hy = hp / CT_HW, hx = hp - hy * CT_HW;
       const int iy = ty * CT_TH - 1 + hy, ix = tx * CT_TW - 1 + hx;
       const bool ok = hp < CT_HPX && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      const int g = (lane & 3) ^ ((hp >> 2) & 3);
+      const int g = (lane & 3) ^ (((hp >> 2) & 1) << 1);
       const int sy = iy >> a.up, sx = ix >> a.up;  // (the input grid of an upsampled conv)
       hsrc[i] = ok ? a.x + ((size_t)(b * (H >> a.up) + sy) * a.Wi + sx) * a.lda + g * 8 : a.zero;
     }
@@ -231,6 +249,26 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     }
   };
 
+  // per-lane LDS byte offsets of the fragment reads inside a stage (the same
+  // for every unit): A = halo pixels of tile row wv + ky shifted by kx, B =
+  // weight rows (tap, cout)
+  const unsigned sbase = (unsigned)(size_t)(ct_lptr_t)(void*)smem;
+  unsigned aoff[9][2], boff[9][NF];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int hp = (wv + ky) * CT_HW + i * 16 + fr + kx;
+      aoff[tap][i] = (unsigned)(hp * 64 + ct_slot(hp, fq) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int row = tap * NOUT + j * 16 + fr;
+      boff[tap][j] = (unsigned)(row * 64 + ct_slot(row, fq) * 16);
+    }
+  }
+
   // ---- prologue: S - 1 units in flight ----
 #pragma unroll
   for (int k = 0; k < CT_S - 1; ++k)
@@ -243,30 +281,33 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (u + CT_S - 1 < U) issue();
-    const unsigned char* hb = smem + s * CT_STAGE;
-    const unsigned char* wb = hb + CT_HALO;
+    // nine taps, fragment reads one tap ahead of the MFMAs that consume them
+    // (inline asm, counted lgkmcnt: the compiler's own waits drained every read
+    // in front of each tap's MFMAs)
+    const unsigned hb = sbase + (unsigned)(s * CT_STAGE), wb = hb + CT_HALO;
+    v8s fr2[2][CT_R];
+    auto rd = [&](v8s (&f)[CT_R], int tap) {
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int i = 0; i < 2; ++i) ct_ld(f[i], hb + aoff[tap][i]);
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int tap = ky * 3 + kx;
-        v8s af[2], bfr[NF];
+      for (int j = 0; j < NF; ++j) ct_ld(f[2 + j], wb + boff[tap][j]);
+    };
+    rd(fr2[0], 0);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int hp = (wv + ky) * CT_HW + i * 16 + fr + kx;
-          af[i] = *reinterpret_cast<const v8s*>(hb + hp * 64 + ct_slot(hp, fq) * 16);
-        }
-#pragma unroll
-        for (int j = 0; j < NF; ++j) {
-          const int row = tap * NOUT + j * 16 + fr;
-          bfr[j] = *reinterpret_cast<const v8s*>(wb + row * 64 + ct_slot(row, fq) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < NF; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    for (int tap = 0; tap < 9; ++tap) {
+      v8s (&f)[CT_R] = fr2[tap & 1];
+      if (tap + 1 < 9) {
+        rd(fr2[(tap + 1) & 1], tap + 1);
+        ct_wait<CT_R>(f);
+      } else {
+        ct_wait<0>(f);
       }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[2 + j], f[i], acc[i][j], 0, 0, 0);
+    }
     s = s + 1 == CT_S ? 0 : s + 1;
     if (++c == nc) {
       epilogue(tile);
