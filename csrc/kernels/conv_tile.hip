@@ -21,7 +21,7 @@
 //     epilogue: the ring stays live).  Counted `vmcnt` waits, raw barriers.
 //   * LDS images are row-major, 64 B (one 32-channel chunk) per halo pixel or
 //     (tap, cout) weight row, the four 16-byte channel groups XOR-swizzled by
-//     row so the 16 lanes of an MFMA fragment hit distinct bank quads; one
+//     row (ct_slot: conflict-free on the b128 lane groups); one
 //     LDS-DMA instruction fills 16 rows (16 x 64 contiguous source bytes; a
 //     first version that filled 64 pixels of one group per instruction touched
 //     64 cache lines per 1 KB: 33.6-58.4 us against 26.7-43.9 us now);
@@ -63,8 +63,13 @@ struct CtGeo {
 };
 
 // 16-byte slot of channel group g (of 4) in LDS row r (a pixel or a (tap, cout)
-// row of 64 B): XOR-swizzled so the 16 lanes of an MFMA fragment (16
-// consecutive rows, one group) hit 16 distinct bank quads
+// row of 64 B).  A ds_read_b128 serves lanes {0-3,12-15,20-27} (and the three
+// other groups of MICROARCH §LDS) in one cycle: rows base+0..3 and base+12..15
+// of group g with rows base+4..11 of group g^1, for ANY base (the A reads sit
+// at a kx pixel offset).  Per row residue mod 4 the four rows r, r+4, r+8,
+// r+12 then need four distinct slots: g ^ 2·((r >> 2) & 1) gives them
+// (g, g^1^2, g^1, g^2); the former g ^ ((r >> 2) & 3) was 2-way on 120 of the
+// 144 A reads and on every B read
 __device__ __forceinline__ int ct_slot(int r, int g) { return g ^ (((r >> 2) & 1) << 1); }
 
 struct ConvTileArgs {
