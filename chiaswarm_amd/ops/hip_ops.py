@@ -954,6 +954,7 @@ sig("csk_xin_qkv_ok", c_int, c_int, c_int, c_int)
 sig("csk_xin_qkv", c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
     c_void_p, c_int, c_int, c_float, c_void_p)
 sig("csk_set_xin_probe", c_int)
+sig("csk_set_conv_tile_no_rw", c_int)
 sig("csk_gn_finalize", c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p)
 XIN_FUSED = os.environ.get("CSK_XIN_FUSED", "1") == "1"
 XIN_MIN_ROWS = int(os.environ.get("CSK_XIN_MIN_ROWS", "16384"))  # CFG-2 grids (8192 rows: 64 workgroups) keep the GEMMs (tools/xinbench.py)

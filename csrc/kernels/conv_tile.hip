@@ -34,6 +34,11 @@
 // stages) with the fused "* 0.2 + x" epilogue of conv5: 192 -> 64 77.9 vs 96.6
 // us, 64 -> 64 at 1024^2 / 2048^2 133 / 522 vs 158 / 622 us
 // (profiles/conv_tile64_r5.txt).
+//   * resident weights (RW instances, Cout <= 32 and Cin <= 128): the packed
+//     weight (<= 72 KB) is DMA'd once per workgroup and the ring carries halos
+//     only (per-unit LDS fill halved): 64 / 96 / 128 -> 32 in 25.6 / 29.8 /
+//     32.8 us against 27.7 / 31.5 / 37.3 us with per-unit weight DMA, same box
+//     (profiles/conv_tile_r6.txt); csk_set_conv_tile_no_rw is the A/B switch.
 //   * wave w computes tile row w (32 px = 2 MFMA row fragments) x 32 outputs
 //     with v_mfma_f32_16x16x32_bf16 (B . A order: row-layout accumulators, a
 //     lane holds one pixel's 4 consecutive outputs -> 8-byte stores).
@@ -52,13 +57,20 @@ constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per
 
 // per output width NOUT (16, 32 or 64): weight rows 9 x NOUT padded to whole
 // 8-wave x 16-row DMA rounds, ring depth (3 stages at 16 / 32: 120 / 144 KB; 2 at 64: 128 KB)
-template <int NOUT>
+//
+// RW (resident weights, NOUT <= 32 and Cin <= 128): the whole packed weight,
+// nc chunks x 9 NOUT rows, is DMA'd once per workgroup ahead of a halo-only
+// ring (the per-unit weight DMA was half of every unit's LDS fill)
+constexpr int CT_RW_MAXC = 4;  // chunks (Cin <= 128) the resident image holds
+template <int NOUT, bool RW>
 struct CtGeo {
   static constexpr int WROWS = (9 * NOUT + 127) / 128 * 128;  // 384 / 640
-  static constexpr int WGT = WROWS * 64;                      // bytes per stage ([tap x cout][4 x 16 B])
+  static constexpr int WGT = RW ? 0 : WROWS * 64;             // weight bytes per ring stage ([tap x cout][4 x 16 B])
+  static constexpr int WCH = 9 * NOUT * 64;                   // RW: bytes per resident chunk (unpadded rows)
+  static constexpr int WRES = RW ? CT_RW_MAXC * WCH : 0;      // RW: resident image (72 KB at NOUT = 32)
   static constexpr int STAGE = CT_HALO + WGT;
   static constexpr int S = NOUT == 64 ? 2 : 3;
-  static constexpr int WI = WROWS / 16 / 8;                   // weight DMA instructions per wave per chunk (3 / 5)
+  static constexpr int WI = RW ? 0 : WROWS / 16 / 8;          // weight DMA instructions per wave per chunk (3 / 5)
   static constexpr int NF = NOUT / 16;                        // output fragments per pixel row
 };
 
@@ -122,11 +134,12 @@ __device__ __forceinline__ void ct_wait(v8s (&f)[R]) {
 
 }  // namespace
 
-template <int NOUT>
+template <int NOUT, bool RW>
 __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
-  using Geo = CtGeo<NOUT>;
+  using Geo = CtGeo<NOUT, RW>;
   constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF, CT_R = 2 + NF;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[CT_S * CT_STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char smem_all[Geo::WRES + CT_S * CT_STAGE];
+  unsigned char* const smem = smem_all + Geo::WRES;  // the ring (after the resident weights)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = gridDim.x;
@@ -140,13 +153,25 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 
   // ---- weight DMA (tile-independent): instruction k = wv * 3 + i writes rows
   // 16 k .. 16 k + 15 (lane L: row 16 k + L / 4, LDS slot L % 4) ----
-  const bf16_t* wsrc[CT_WI];
+  const bf16_t* wsrc[CT_WI > 0 ? CT_WI : 1];
 #pragma unroll
   for (int i = 0; i < CT_WI; ++i) {
     const int row = (wv * CT_WI + i) * 16 + (lane >> 2);  // tap * NOUT + output channel
     const int tap = row / NOUT, co = row % NOUT;
     const int g = (lane & 3) ^ (((row >> 2) & 1) << 1);  // source channel group landing in this lane's slot
     wsrc[i] = row < 9 * NOUT && co < a.Cout ? a.w + ((size_t)co * 9 + tap) * a.Cin + g * 8 : a.zero;
+  }
+  // ---- RW: the resident weight image, DMA instruction k (k = wv, wv + 8, ...)
+  // writes flattened rows 16 k .. 16 k + 15 of [chunk][tap x cout] ----
+  if constexpr (RW) {
+    const int nrow = nc * 9 * NOUT;
+    for (int k = wv; k * 16 < nrow; k += 8) {
+      const int r = k * 16 + (lane >> 2);
+      const int c = r / (9 * NOUT), rr = r - c * (9 * NOUT);
+      const int tap = rr / NOUT, co = rr % NOUT;
+      const int g = (lane & 3) ^ (((r >> 2) & 1) << 1);
+      ct_dma(co < a.Cout ? a.w + ((size_t)co * 9 + tap) * a.Cin + c * 32 + g * 8 : a.zero, smem_all + k * 1024);
+    }
   }
   // ---- halo DMA: instruction k = wv * 3 + i writes halo pixels 16 k .. 16 k + 15 ----
   const bf16_t* hsrc[CT_HI];
@@ -172,8 +197,10 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     const int co = d_c * 32;  // channel offset of this chunk
 #pragma unroll
     for (int i = 0; i < CT_HI; ++i) ct_dma(hsrc[i] + co, st + (wv * CT_HI + i) * 1024);
+    if constexpr (!RW) {
 #pragma unroll
-    for (int i = 0; i < CT_WI; ++i) ct_dma(wsrc[i] + co, st + CT_HALO + (wv * CT_WI + i) * 1024);
+      for (int i = 0; i < CT_WI; ++i) ct_dma(wsrc[i] + co, st + CT_HALO + (wv * CT_WI + i) * 1024);
+    }
     d_s = d_s + 1 == CT_S ? 0 : d_s + 1;
     if (++d_c == nc) {
       d_c = 0;
@@ -289,7 +316,8 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     // nine taps, fragment reads one tap ahead of the MFMAs that consume them
     // (inline asm, counted lgkmcnt: the compiler's own waits drained every read
     // in front of each tap's MFMAs)
-    const unsigned hb = sbase + (unsigned)(s * CT_STAGE), wb = hb + CT_HALO;
+    const unsigned hb = sbase + (unsigned)(s * CT_STAGE);
+    const unsigned wb = RW ? sbase - (unsigned)Geo::WRES + (unsigned)(c * Geo::WCH) : hb + CT_HALO;
     v8s fr2[2][CT_R];
     auto rd = [&](v8s (&f)[CT_R], int tap) {
 #pragma unroll
@@ -327,6 +355,13 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 // host side
 // ---------------------------------------------------------------------------
 static int g_ct_cus = 0;
+static int g_ct_no_rw = 0;
+
+// A/B switch (tools/convtilebench.py --rw): 1 = per-unit weight DMA everywhere
+CSK_API int csk_set_conv_tile_no_rw(int v) {
+  g_ct_no_rw = v;
+  return 0;
+}
 
 // 1 when csk_conv_tile takes this conv: 3x3 / stride 1 / pad 1, Cout = 32 or
 // 64 (or <= 16: the 16-wide instance, element stores below 16, e.g. Real-ESRGAN's RGB conv_last),
@@ -381,9 +416,12 @@ CSK_API int csk_conv_tile2(void* y, const void* x, const void* wp, const void* b
   a.tiles_y = (H + CT_TH - 1) / CT_TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
   const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
-  if (Cout == 64) conv_tile_kernel<64><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32) conv_tile_kernel<32><<<G, 512, 0, stream>>>(a);
-  else conv_tile_kernel<16><<<G, 512, 0, stream>>>(a);
+  const bool rw = Cin <= 32 * CT_RW_MAXC && !g_ct_no_rw;  // resident weights (Cout <= 32)
+  if (Cout == 64) conv_tile_kernel<64, false><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32 && rw) conv_tile_kernel<32, true><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32) conv_tile_kernel<32, false><<<G, 512, 0, stream>>>(a);
+  else if (rw) conv_tile_kernel<16, true><<<G, 512, 0, stream>>>(a);
+  else conv_tile_kernel<16, false><<<G, 512, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rw", action="store_true", help="also time the per-unit weight DMA variant (csk_set_conv_tile_no_rw)")
     ap.add_argument("--shapes", default="", help="';'-separated hw,cin,cout (default: the four Cout = 32 convs)")
     a = ap.parse_args()
     _lib.load()
@@ -31,8 +32,10 @@ def main():
         wp = ops.pack_conv_weight((torch.randn(cout, cin, 3, 3, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16))
         b = torch.randn(cout, device=dev).to(torch.bfloat16)
         res = {}
-        for tile in (True, False):
+        arms = [(True, 0), (False, 0)] + ([(True, 1)] if a.rw else [])
+        for tile, no_rw in arms:
             hip_ops.CONV_TILE = tile
+            _lib.call("csk_set_conv_tile_no_rw", no_rw)
             run = lambda: ops.conv2d(buf[..., :cin], wp, b, act="lrelu", out=buf[..., 192:192 + cout])  # noqa: E731
             run()
             torch.cuda.synchronize()
@@ -44,11 +47,14 @@ def main():
                 ev[1].record()
                 ev[1].synchronize()
                 best = min(best, ev[0].elapsed_time(ev[1]) * 1e3 / a.iters)
-            res[tile] = best
+            res[(tile, no_rw)] = best
         del buf
         fl = 2.0 * hw * hw * cout * 9 * cin
-        print(f"conv {hw}x{hw} {cin}->{cout}: halo-tile {res[True]:7.1f} us ({fl / res[True] / 1e6:6.1f} TF/s)   "
-              f"implicit GEMM {res[False]:7.1f} us ({fl / res[False] / 1e6:6.1f} TF/s)", flush=True)
+        t, g = res[(True, 0)], res[(False, 0)]
+        extra = (f"   per-unit weight DMA {res[(True, 1)]:7.1f} us" if a.rw else "")
+        print(f"conv {hw}x{hw} {cin}->{cout}: halo-tile {t:7.1f} us ({fl / t / 1e6:6.1f} TF/s)   "
+              f"implicit GEMM {g:7.1f} us ({fl / g / 1e6:6.1f} TF/s){extra}", flush=True)
+    _lib.call("csk_set_conv_tile_no_rw", 0)
     hip_ops.CONV_TILE = True
     hip_ops.CONV_TILE64 = False
 
