@@ -34,10 +34,11 @@
 // stages) with the fused "* 0.2 + x" epilogue of conv5: 192 -> 64 77.9 vs 96.6
 // us, 64 -> 64 at 1024^2 / 2048^2 133 / 522 vs 158 / 622 us
 // (profiles/conv_tile64_r5.txt).
-//   * resident weights (RW instances, Cout <= 32 and Cin <= 128): the packed
-//     weight (<= 72 KB) is DMA'd once per workgroup and the ring carries halos
-//     only (per-unit LDS fill halved): 64 / 96 / 128 -> 32 in 25.6 / 29.8 /
-//     32.8 us against 27.7 / 31.5 / 37.3 us with per-unit weight DMA, same box
+//   * resident weights (RWC > 0 instances, Cout <= 32, Cin <= 160): the packed
+//     weight (<= 90 KB) is DMA'd once per workgroup and the ring carries halos
+//     only (per-unit LDS fill halved; Cin = 160 with a 2-stage ring): 64 / 96 /
+//     128 / 160 -> 32 in 25.2 / 29.6 / 32.6 / 36.7 us against 28.2 / 31.6 /
+//     37.0 / 41.9 us with per-unit weight DMA, same process
 //     (profiles/conv_tile_r6.txt); csk_set_conv_tile_no_rw is the A/B switch.
 //   * wave w computes tile row w (32 px = 2 MFMA row fragments) x 32 outputs
 //     with v_mfma_f32_16x16x32_bf16 (B . A order: row-layout accumulators, a
@@ -61,15 +62,16 @@ constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per
 // RW (resident weights, NOUT <= 32 and Cin <= 128): the whole packed weight,
 // nc chunks x 9 NOUT rows, is DMA'd once per workgroup ahead of a halo-only
 // ring (the per-unit weight DMA was half of every unit's LDS fill)
-constexpr int CT_RW_MAXC = 4;  // chunks (Cin <= 128) the resident image holds
-template <int NOUT, bool RW>
+constexpr int CT_RW_MAXC = 5;  // chunks (Cin <= 160) a resident image holds (5: 2-stage ring)
+template <int NOUT, int RWC>
 struct CtGeo {
+  static constexpr bool RW = RWC > 0;
   static constexpr int WROWS = (9 * NOUT + 127) / 128 * 128;  // 384 / 640
   static constexpr int WGT = RW ? 0 : WROWS * 64;             // weight bytes per ring stage ([tap x cout][4 x 16 B])
   static constexpr int WCH = 9 * NOUT * 64;                   // RW: bytes per resident chunk (unpadded rows)
-  static constexpr int WRES = RW ? CT_RW_MAXC * WCH : 0;      // RW: resident image (72 KB at NOUT = 32)
+  static constexpr int WRES = RWC * WCH;                      // RW: resident image (72 / 90 KB at NOUT = 32)
   static constexpr int STAGE = CT_HALO + WGT;
-  static constexpr int S = NOUT == 64 ? 2 : 3;
+  static constexpr int S = NOUT == 64 || RWC > 4 ? 2 : 3;
   static constexpr int WI = RW ? 0 : WROWS / 16 / 8;          // weight DMA instructions per wave per chunk (3 / 5)
   static constexpr int NF = NOUT / 16;                        // output fragments per pixel row
 };
@@ -134,9 +136,10 @@ __device__ __forceinline__ void ct_wait(v8s (&f)[R]) {
 
 }  // namespace
 
-template <int NOUT, bool RW>
+template <int NOUT, int RWC>
 __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
-  using Geo = CtGeo<NOUT, RW>;
+  using Geo = CtGeo<NOUT, RWC>;
+  constexpr bool RW = Geo::RW;
   constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF, CT_R = 2 + NF;
   __shared__ __attribute__((aligned(16))) unsigned char smem_all[Geo::WRES + CT_S * CT_STAGE];
   unsigned char* const smem = smem_all + Geo::WRES;  // the ring (after the resident weights)
@@ -416,12 +419,14 @@ CSK_API int csk_conv_tile2(void* y, const void* x, const void* wp, const void* b
   a.tiles_y = (H + CT_TH - 1) / CT_TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
   const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
-  const bool rw = Cin <= 32 * CT_RW_MAXC && !g_ct_no_rw;  // resident weights (Cout <= 32)
-  if (Cout == 64) conv_tile_kernel<64, false><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32 && rw) conv_tile_kernel<32, true><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32) conv_tile_kernel<32, false><<<G, 512, 0, stream>>>(a);
-  else if (rw) conv_tile_kernel<16, true><<<G, 512, 0, stream>>>(a);
-  else conv_tile_kernel<16, false><<<G, 512, 0, stream>>>(a);
+  // resident weights (Cout <= 32): Cin <= 128 with the 3-stage halo ring, 160 with 2 stages
+  const int rwc = g_ct_no_rw ? 0 : Cin <= 128 ? 4 : Cin <= 32 * CT_RW_MAXC ? 5 : 0;
+  if (Cout == 64) conv_tile_kernel<64, 0><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32 && rwc == 4) conv_tile_kernel<32, 4><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32 && rwc == 5) conv_tile_kernel<32, 5><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32) conv_tile_kernel<32, 0><<<G, 512, 0, stream>>>(a);
+  else if (rwc == 4) conv_tile_kernel<16, 4><<<G, 512, 0, stream>>>(a);
+  else conv_tile_kernel<16, 0><<<G, 512, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
