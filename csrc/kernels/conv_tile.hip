@@ -40,6 +40,9 @@
 //     128 / 160 -> 32 in 25.2 / 29.6 / 32.6 / 36.7 us against 28.2 / 31.6 /
 //     37.0 / 41.9 us with per-unit weight DMA, same process
 //     (profiles/conv_tile_r6.txt); csk_set_conv_tile_no_rw is the A/B switch.
+//   * Cout = 64 runs 16 x 32 tiles (TR = 2: wave w computes rows w and w + 8;
+//     80 KB stages): 192 -> 64 77.1 vs 80.6 us, 64 -> 64 at 2048^2 525.8 vs
+//     579.0 us against 8-row tiles, same process (profiles/conv_tile_r6.txt).
 //   * wave w computes tile row w (32 px = 2 MFMA row fragments) x 32 outputs
 //     with v_mfma_f32_16x16x32_bf16 (B . A order: row-layout accumulators, a
 //     lane holds one pixel's 4 consecutive outputs -> 8-byte stores).
@@ -49,12 +52,7 @@
 
 namespace {
 
-constexpr int CT_TH = 8, CT_TW = 32;       // output tile
-constexpr int CT_HW = CT_TW + 2, CT_HH = CT_TH + 2;
-constexpr int CT_HPX = CT_HH * CT_HW;      // 340 halo pixels
-constexpr int CT_HSLOT = 384;              // halo pixel slots: 24 DMA instructions of 16 pixels
-constexpr int CT_HALO = CT_HSLOT * 64;     // bytes per stage ([pixel][4 x 16 B])
-constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per chunk (3)
+constexpr int CT_TW = 32, CT_HW = CT_TW + 2;  // output tile width, halo width
 
 // per output width NOUT (16, 32 or 64): weight rows 9 x NOUT padded to whole
 // 8-wave x 16-row DMA rounds, ring depth (3 stages at 16 / 32: 120 / 144 KB; 2 at 64: 128 KB)
@@ -63,14 +61,23 @@ constexpr int CT_HI = CT_HSLOT / 16 / 8;   // halo DMA instructions per wave per
 // nc chunks x 9 NOUT rows, is DMA'd once per workgroup ahead of a halo-only
 // ring (the per-unit weight DMA was half of every unit's LDS fill)
 constexpr int CT_RW_MAXC = 5;  // chunks (Cin <= 160) a resident image holds (5: 2-stage ring)
-template <int NOUT, int RWC>
+//
+// TR = tile rows per wave (TALL tiles, TR = 2: 16 x 32 pixels; NOUT = 64 only,
+// where a 37 KB weight chunk per 8 x 32 tile was 62 % of every unit's fill):
+// halo 18 x 34 = 612 pixels in 640 slots, stage 80 KB, 2 stages = 160 KB.
+template <int NOUT, int RWC, int TR = 1>
 struct CtGeo {
   static constexpr bool RW = RWC > 0;
+  static constexpr int TH = 8 * TR;                           // output tile height
+  static constexpr int HPX = (TH + 2) * CT_HW;                // 340 / 612 halo pixels
+  static constexpr int HSLOT = (HPX + 127) / 128 * 128;       // 384 / 640 slots: whole 8-wave x 16-pixel DMA rounds
+  static constexpr int HALO = HSLOT * 64;                     // halo bytes per stage ([pixel][4 x 16 B])
+  static constexpr int HI = HSLOT / 16 / 8;                   // halo DMA instructions per wave per chunk (3 / 5)
   static constexpr int WROWS = (9 * NOUT + 127) / 128 * 128;  // 384 / 640
   static constexpr int WGT = RW ? 0 : WROWS * 64;             // weight bytes per ring stage ([tap x cout][4 x 16 B])
   static constexpr int WCH = 9 * NOUT * 64;                   // RW: bytes per resident chunk (unpadded rows)
   static constexpr int WRES = RWC * WCH;                      // RW: resident image (72 / 90 KB at NOUT = 32)
-  static constexpr int STAGE = CT_HALO + WGT;
+  static constexpr int STAGE = HALO + WGT;
   static constexpr int S = NOUT == 64 || RWC > 4 ? 2 : 3;
   static constexpr int WI = RW ? 0 : WROWS / 16 / 8;          // weight DMA instructions per wave per chunk (3 / 5)
   static constexpr int NF = NOUT / 16;                        // output fragments per pixel row
@@ -127,8 +134,12 @@ __device__ __forceinline__ void ct_wait(v8s (&f)[R]) {
     asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]) : "n"(N));
   } else if constexpr (R == 4) {
     asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N));
+  } else if constexpr (R == 8) {
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
+                 : "n"(N));
   } else {
-    static_assert(R == 6, "2 + NF fragments");
+    static_assert(R == 6, "2 TR + NF fragments");
     asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5])
                  : "n"(N));
   }
@@ -136,11 +147,12 @@ __device__ __forceinline__ void ct_wait(v8s (&f)[R]) {
 
 }  // namespace
 
-template <int NOUT, int RWC>
+template <int NOUT, int RWC, int TR>
 __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a) {
-  using Geo = CtGeo<NOUT, RWC>;
+  using Geo = CtGeo<NOUT, RWC, TR>;
   constexpr bool RW = Geo::RW;
-  constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF, CT_R = 2 + NF;
+  constexpr int CT_S = Geo::S, CT_STAGE = Geo::STAGE, CT_WI = Geo::WI, NF = Geo::NF, CT_R = 2 * TR + NF;
+  constexpr int CT_TH = Geo::TH, CT_HPX = Geo::HPX, CT_HALO = Geo::HALO, CT_HI = Geo::HI;
   __shared__ __attribute__((aligned(16))) unsigned char smem_all[Geo::WRES + CT_S * CT_STAGE];
   unsigned char* const smem = smem_all + Geo::WRES;  // the ring (after the resident weights)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -212,12 +224,14 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     }
   };
 
-  v4f acc[2][NF];
+  v4f acc[TR][2][NF];  // [tile row wv + 8 t][pixel half][output fragment]
   auto zero_acc = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int t = 0; t < TR; ++t)
 #pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[t][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
   float bias[NF][4];
@@ -233,7 +247,9 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     const int b = tile / (a.tiles_x * a.tiles_y);
     const int rem = tile - b * (a.tiles_x * a.tiles_y);
     const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
-    const int y = ty * CT_TH + wv;
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+    const int y = ty * CT_TH + wv + 8 * t;
     if (y >= H) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -247,7 +263,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
         const int c0 = j * 16 + fq * 4;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[i][j][r] + bias[j][r]) * a.out_scale;
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(a.act, acc[t][i][j][r] + bias[j][r]) * a.out_scale;
         if (c0 + 4 > a.Cout) {  // narrow output (Cout < 16, e.g. RGB): element stores, no residuals
           if (a.u8) {  // image output: the upscaler's uint8 pixels straight from the accumulators
             unsigned char* ob = reinterpret_cast<unsigned char*>(a.y) + ((size_t)(b * H + y) * W + x) * a.ldc;
@@ -282,27 +298,22 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
         *reinterpret_cast<uint2*>(op + c0) = wd;
       }
     }
+    }
   };
 
   // per-lane LDS byte offsets of the fragment reads inside a stage (the same
-  // for every unit): A = halo pixels of tile row wv + ky shifted by kx, B =
-  // weight rows (tap, cout)
+  // for every unit).  The swizzle depends on bit 2 of the row only, which
+  // whole 8-row / 16-pixel / 16-row steps keep: A (halo pixel of tile row
+  // wv + 8 t + ky, shifted by kx) = aoff[tap] + compile-time offset of (t,
+  // half); B (weight row tap x NOUT + 16 j + fr) = boff + compile-time offset.
   const unsigned sbase = (unsigned)(size_t)(ct_lptr_t)(void*)smem;
-  unsigned aoff[9][2], boff[9][NF];
+  unsigned aoff[9];
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
-    const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int hp = (wv + ky) * CT_HW + i * 16 + fr + kx;
-      aoff[tap][i] = (unsigned)(hp * 64 + ct_slot(hp, fq) * 16);
-    }
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int row = tap * NOUT + j * 16 + fr;
-      boff[tap][j] = (unsigned)(row * 64 + ct_slot(row, fq) * 16);
-    }
+    const int hp = (wv + tap / 3) * CT_HW + fr + tap % 3;
+    aoff[tap] = (unsigned)(hp * 64 + ct_slot(hp, fq) * 16);
   }
+  const unsigned boff = (unsigned)(fr * 64 + ct_slot(fr, fq) * 16);
 
   // ---- prologue: S - 1 units in flight ----
 #pragma unroll
@@ -324,9 +335,9 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
     v8s fr2[2][CT_R];
     auto rd = [&](v8s (&f)[CT_R], int tap) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) ct_ld(f[i], hb + aoff[tap][i]);
+      for (int i = 0; i < 2 * TR; ++i) ct_ld(f[i], hb + aoff[tap] + (unsigned)(((i >> 1) * 8 * CT_HW + (i & 1) * 16) * 64));
 #pragma unroll
-      for (int j = 0; j < NF; ++j) ct_ld(f[2 + j], wb + boff[tap][j]);
+      for (int j = 0; j < NF; ++j) ct_ld(f[2 * TR + j], wb + boff + (unsigned)((tap * NOUT + j * 16) * 64));
     };
     rd(fr2[0], 0);
 #pragma unroll
@@ -339,10 +350,11 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
         ct_wait<0>(f);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2 * TR; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[2 + j], f[i], acc[i][j], 0, 0, 0);
+          acc[i >> 1][i & 1][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[2 * TR + j], f[i], acc[i >> 1][i & 1][j], 0, 0, 0);
     }
     s = s + 1 == CT_S ? 0 : s + 1;
     if (++c == nc) {
@@ -360,7 +372,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile_kernel(const ConvTileArgs a)
 static int g_ct_cus = 0;
 static int g_ct_no_rw = 0;
 
-// A/B switch (tools/convtilebench.py --rw): 1 = per-unit weight DMA everywhere
+// A/B switch (tools/convtilebench.py --rw): bit 0 = per-unit weight DMA everywhere, bit 1 = 8-row tiles at Cout = 64
 CSK_API int csk_set_conv_tile_no_rw(int v) {
   g_ct_no_rw = v;
   return 0;
@@ -415,18 +427,20 @@ CSK_API int csk_conv_tile2(void* y, const void* x, const void* wp, const void* b
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.lda = lda; a.ldc = ldc; a.act = act;
   a.ldr = ldr; a.ldr2 = ldr2; a.Cout = Cout; a.up = up ? 1 : 0; a.Wi = up ? W / 2 : W; a.u8 = u8 ? 1 : 0;
   a.out_scale = out_scale; a.res_scale = res_scale;
+  const bool tall = Cout == 64 && !(g_ct_no_rw & 2);  // 16 x 32 tiles (TR = 2)
   a.tiles_x = (W + CT_TW - 1) / CT_TW;
-  a.tiles_y = (H + CT_TH - 1) / CT_TH;
+  a.tiles_y = (H + (tall ? 16 : 8) - 1) / (tall ? 16 : 8);
   a.ntiles = B * a.tiles_x * a.tiles_y;
   const int G = a.ntiles < g_ct_cus ? a.ntiles : g_ct_cus;
   // resident weights (Cout <= 32): Cin <= 128 with the 3-stage halo ring, 160 with 2 stages
-  const int rwc = g_ct_no_rw ? 0 : Cin <= 128 ? 4 : Cin <= 32 * CT_RW_MAXC ? 5 : 0;
-  if (Cout == 64) conv_tile_kernel<64, 0><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32 && rwc == 4) conv_tile_kernel<32, 4><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32 && rwc == 5) conv_tile_kernel<32, 5><<<G, 512, 0, stream>>>(a);
-  else if (Cout == 32) conv_tile_kernel<32, 0><<<G, 512, 0, stream>>>(a);
-  else if (rwc == 4) conv_tile_kernel<16, 4><<<G, 512, 0, stream>>>(a);
-  else conv_tile_kernel<16, 0><<<G, 512, 0, stream>>>(a);
+  const int rwc = (g_ct_no_rw & 1) ? 0 : Cin <= 128 ? 4 : Cin <= 32 * CT_RW_MAXC ? 5 : 0;
+  if (Cout == 64 && tall) conv_tile_kernel<64, 0, 2><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 64) conv_tile_kernel<64, 0, 1><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32 && rwc == 4) conv_tile_kernel<32, 4, 1><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32 && rwc == 5) conv_tile_kernel<32, 5, 1><<<G, 512, 0, stream>>>(a);
+  else if (Cout == 32) conv_tile_kernel<32, 0, 1><<<G, 512, 0, stream>>>(a);
+  else if (rwc == 4) conv_tile_kernel<16, 4, 1><<<G, 512, 0, stream>>>(a);
+  else conv_tile_kernel<16, 0, 1><<<G, 512, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 

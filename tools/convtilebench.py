@@ -32,7 +32,7 @@ def main():
         wp = ops.pack_conv_weight((torch.randn(cout, cin, 3, 3, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16))
         b = torch.randn(cout, device=dev).to(torch.bfloat16)
         res = {}
-        arms = [(True, 0), (False, 0)] + ([(True, 1)] if a.rw else [])
+        arms = [(True, 0), (False, 0)] + ([(True, 3)] if a.rw else [])
         for tile, no_rw in arms:
             hip_ops.CONV_TILE = tile
             _lib.call("csk_set_conv_tile_no_rw", no_rw)
@@ -51,7 +51,7 @@ def main():
         del buf
         fl = 2.0 * hw * hw * cout * 9 * cin
         t, g = res[(True, 0)], res[(False, 0)]
-        extra = (f"   per-unit weight DMA {res[(True, 1)]:7.1f} us" if a.rw else "")
+        extra = (f"   per-unit weight DMA, 8-row tiles {res[(True, 3)]:7.1f} us" if a.rw else "")
         print(f"conv {hw}x{hw} {cin}->{cout}: halo-tile {t:7.1f} us ({fl / t / 1e6:6.1f} TF/s)   "
               f"implicit GEMM {g:7.1f} us ({fl / g / 1e6:6.1f} TF/s){extra}", flush=True)
     _lib.call("csk_set_conv_tile_no_rw", 0)
