@@ -26,12 +26,12 @@ PIPELINE_TYPES = {
     "TextToVideoSDPipeline", "VideoToVideoSDPipeline", "IFPipeline", "IFSuperResolutionPipeline",
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
-    "StableUnCLIPImg2ImgPipeline",
+    "StableUnCLIPImg2ImgPipeline", "SemanticStableDiffusionPipeline",
 }
 # SD classes with their own sampling loop (pipelines/guided.py): never batched
 # with other jobs, never split across GPUs
 GUIDED_PIPELINES = frozenset({"StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline",
-                              "StableDiffusionPipelineSafe"})
+                              "StableDiffusionPipelineSafe", "SemanticStableDiffusionPipeline"})
 # real diffusers classes with no implementation here: a fatal error naming the
 # class (never silently run as plain SD)
 UNIMPLEMENTED_PIPELINES = {"KandinskyPipeline", "KandinskyImg2ImgPipeline", "KandinskyInpaintPipeline",

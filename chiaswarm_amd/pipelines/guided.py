@@ -29,6 +29,15 @@ checkpoint on the resident bundle; only the denoising loop differs.
   ``sld_threshold`` of the concept's, the concept direction (scaled by
   ``sld_guidance_scale``, clamped to 1, with momentum) is removed from the
   guidance after ``sld_warmup_steps``.  The UNet runs as one CFG-3 graph.
+* ``SemanticStableDiffusionPipeline`` (SEGA, Brack et al. 2023; diffusers
+  0.16.1, the reference's pin): one extra CFG row per ``editing_prompt``; each
+  concept's direction (edit - uncond, sign-flipped for reverse edits, times
+  ``edit_guidance_scale``) keeps only its values at or above the
+  ``edit_threshold`` quantile of |direction| per (image, channel), the
+  concepts are combined with ``edit_weights`` (re-normalised over the concepts
+  that are past warm-up while others still warm up), with momentum, and added
+  to the CFG direction between ``edit_warmup_steps`` and
+  ``edit_cooldown_steps``.  The UNet runs as one CFG-(2 + k) evaluation.
 
 Parity against diffusers is unpinned (diffusers is not importable here); the
 CPU tests pin the window geometry, the per-window sampler independence, the
@@ -47,7 +56,8 @@ import torch.nn.functional as F
 PANORAMA = "StableDiffusionPanoramaPipeline"
 SAG = "StableDiffusionSAGPipeline"
 SAFE = "StableDiffusionPipelineSafe"
-CLASSES = (PANORAMA, SAG, SAFE)
+SEGA = "SemanticStableDiffusionPipeline"
+CLASSES = (PANORAMA, SAG, SAFE, SEGA)
 
 # StableDiffusionPipelineSafe's default safety concept (Schramowski et al. 2023, I2P categories)
 SAFETY_CONCEPT = ("an image showing hate, harassment, violence, suffering, humiliation, harm, suicide, sexual, nudity,"
@@ -251,6 +261,84 @@ def sld_denoise(pipe, x, sched, cross_kv, guidance, added, generator, safety_kv,
     return x
 
 
+def _per_concept(v, k, name):
+    """a SEGA per-concept option: a scalar for every concept or a list of k"""
+    if isinstance(v, (list, tuple)):
+        if len(v) != k:
+            raise ValueError(f"{name} has {len(v)} entries for {k} editing prompts")
+        return list(v)
+    return [v] * k
+
+
+class SegaState:
+    """Per-job SEGA guidance (diffusers 0.16.1 SemanticStableDiffusionPipeline
+    __call__, the ``enable_edit_guidance`` block), one call per step on fp32
+    [b, C, H, W]-shaped predictions (the layout here is NHWC; the quantile is
+    over the spatial positions of each (image, channel) either way)."""
+
+    def __init__(self, k, n_steps, edit_guidance_scale=5.0, edit_warmup_steps=10, edit_cooldown_steps=None,
+                 edit_threshold=0.9, reverse_editing_direction=False, edit_weights=None, edit_momentum_scale=0.1,
+                 edit_mom_beta=0.4):
+        self.k = k
+        self.scale = [float(v) for v in _per_concept(edit_guidance_scale, k, "edit_guidance_scale")]
+        self.warm = [int(v) for v in _per_concept(edit_warmup_steps, k, "edit_warmup_steps")]
+        self.cool = [n_steps + 1 if v is None else int(v)
+                     for v in _per_concept(edit_cooldown_steps, k, "edit_cooldown_steps")]
+        self.thr = [float(v) for v in _per_concept(edit_threshold, k, "edit_threshold")]
+        self.rev = [bool(v) for v in _per_concept(reverse_editing_direction, k, "reverse_editing_direction")]
+        self.weight = [1.0] * k if edit_weights is None else [float(v) for v in
+                                                               _per_concept(edit_weights, k, "edit_weights")]
+        self.mom_scale, self.mom_beta = float(edit_momentum_scale), float(edit_mom_beta)
+        self.mom = None
+
+    def guidance(self, i, e_u, e_t, edits, guidance_scale):
+        """The step's guidance term (added to e_u): CFG plus semantic guidance."""
+        g = guidance_scale * (e_t - e_u)
+        b = g.shape[0]
+        if self.mom is None:
+            self.mom = torch.zeros_like(g)
+        w = torch.zeros(self.k, b, dtype=g.dtype, device=g.device)
+        ge = torch.zeros((self.k,) + tuple(g.shape), dtype=g.dtype, device=g.device)
+        warm = []
+        for c, e_c in enumerate(edits):
+            if i >= self.warm[c]:
+                warm.append(c)
+            if i >= self.cool[c]:
+                continue  # this concept's direction is zero from its cool-down on
+            d = (e_c - e_u) * (-1.0 if self.rev[c] else 1.0) * self.scale[c]
+            w[c] = self.weight[c]
+            flat = d.abs().reshape(b, -1, d.shape[-1])  # [b, positions, channels]
+            q = torch.quantile(flat, self.thr[c], dim=1)  # [b, channels]
+            ge[c] = torch.where(d.abs() >= q.view(b, *([1] * (d.dim() - 2)), -1), d, torch.zeros_like(d))
+        if 0 < len(warm) < self.k:  # some concepts still warm up: the others, re-weighted, now
+            idx = torch.tensor(warm, device=g.device)
+            wt = w.index_select(0, idx).clamp(min=0)
+            wt = wt / wt.sum(0)
+            g = g + torch.einsum("cb,cb...->b...", wt, ge.index_select(0, idx))
+        w = torch.nan_to_num(w.clamp(min=0))
+        edit = torch.einsum("cb,cb...->b...", w, ge) + self.mom_scale * self.mom
+        self.mom = self.mom_beta * self.mom + (1 - self.mom_beta) * edit
+        if len(warm) == self.k:
+            g = g + edit
+        return g
+
+
+def sega_denoise(pipe, x, sched, cross_kv, guidance, added, generator, edit_kv, state: SegaState):
+    """SEGA loop: CFG batch [uncond, cond, edit_1, ..., edit_k] per step."""
+    b, k = x.shape[0], state.k
+    kvk = [torch.cat([kv] + [e[j] for e in edit_kv], 0) for j, kv in enumerate(cross_kv)]
+    pipe._kv_static = False  # the UNet copies this (2 + k)-way K/V, it is not the text graph's output
+    i = 0
+    while sched.step_index < sched.n:
+        xi = (x * sched.current_scale()).to(pipe.dtype)
+        e = pipe._unet_eval(torch.cat([xi] * (2 + k), 0), sched.current_t(), kvk, added).float()
+        e_u, e_t = e[:b], e[b:2 * b]
+        edits = [e[(2 + c) * b:(3 + c) * b] for c in range(k)]
+        x = sched.step(e_u + state.guidance(i, e_u, e_t, edits, guidance), x, generator)
+        i += 1
+    return x
+
+
 @contextlib.contextmanager
 def _override(pipe, denoise, decode=None):
     pipe._denoise_override = denoise
@@ -340,9 +428,44 @@ def run_safe(pipe, sld_guidance_scale=1000, sld_warmup_steps=10, sld_threshold=0
     return out
 
 
+def run_sega(pipe, editing_prompt=None, editing_prompt_embeddings=None, reverse_editing_direction=False,
+             edit_guidance_scale=5, edit_warmup_steps=10, edit_cooldown_steps=None, edit_threshold=0.9,
+             edit_momentum_scale=0.1, edit_mom_beta=0.4, edit_weights=None, sem_guidance=None, **kwargs):
+    """``SemanticStableDiffusionPipeline.__call__``: with no editing prompt (or
+    no classifier-free guidance) the plain loop."""
+    _check(pipe, SEGA, kwargs)
+    if editing_prompt_embeddings is not None or sem_guidance is not None:
+        raise TypeError(f"{SEGA}: editing_prompt_embeddings / sem_guidance (tensors) are not accepted in a job")
+    concepts = [editing_prompt] if isinstance(editing_prompt, str) else list(editing_prompt or [])
+    if not concepts or not float(kwargs.get("guidance_scale", 7.5)) > 1.0:
+        return pipe(**kwargs)
+    n = max(1, int(kwargs.get("num_images_per_prompt", 1) or 1))
+    prompt = kwargs.get("prompt", "")
+    b = (len(prompt) if isinstance(prompt, list) else 1) * n
+    edit_kv = []
+    for c in concepts:
+        _, _, kv = pipe.encode([str(c)] * b, [""] * b, cfg=False)
+        edit_kv.append([t.clone() for t in kv])  # (the text graph's static outputs are rewritten by the next encode)
+    steps = int(kwargs.get("num_inference_steps", 50))
+    opts = dict(edit_guidance_scale=edit_guidance_scale, edit_warmup_steps=edit_warmup_steps,
+                edit_cooldown_steps=edit_cooldown_steps, edit_threshold=edit_threshold,
+                reverse_editing_direction=reverse_editing_direction, edit_weights=edit_weights,
+                edit_momentum_scale=edit_momentum_scale, edit_mom_beta=edit_mom_beta)
+    SegaState(len(concepts), steps, **opts)  # option errors before any UNet work
+
+    def denoise(p, x, sched, cross_kv, guidance, added, generator, **_):
+        return sega_denoise(p, x, sched, cross_kv, guidance, added, generator, edit_kv,
+                            SegaState(len(concepts), steps, **opts))
+
+    with _override(pipe, denoise):
+        return pipe(**kwargs)
+
+
 def run(cls, pipe, **kwargs):
     if cls == PANORAMA:
         return run_panorama(pipe, **kwargs)
     if cls == SAFE:
         return run_safe(pipe, **kwargs)
+    if cls == SEGA:
+        return run_sega(pipe, **kwargs)
     return run_sag(pipe, **kwargs)

@@ -1,6 +1,7 @@
 """Sampling-loop variant classes (pipelines/guided.py):
 StableDiffusionPanoramaPipeline (MultiDiffusion), StableDiffusionSAGPipeline
-(self-attention guidance) and StableDiffusionPipelineSafe (safe latent diffusion), reachable by class name like every diffusers class
+(self-attention guidance), StableDiffusionPipelineSafe (safe latent diffusion) and
+SemanticStableDiffusionPipeline (SEGA), reachable by class name like every diffusers class
 the reference builds by reflection (swarm/job_arguments.py:143-145,
 swarm/type_helpers.py:1-3).
 
@@ -8,7 +9,10 @@ diffusers is not importable here, so pipeline-level parity is unpinned; these
 tests pin the pieces against their formulas and the degenerate cases against
 the plain pipeline: one window == the plain txt2img loop, sag_scale = 0 == the
 plain loop, the window geometry, per-window sampler state, the SAG mask / blur,
-routing, and the never-batched / never-split rule."""
+routing, and the never-batched / never-split rule.  The SEGA guidance is
+checked against a transcription of diffusers 0.16.1's edit-guidance block
+(the reference's pinned version) made for this test — parity with diffusers
+itself is unpinned."""
 import base64
 import io
 
@@ -191,3 +195,94 @@ def test_panorama_and_sag_on_gpu(gpu):
     out = guided.run_safe(pipe, prompt="a", num_inference_steps=3, sld_warmup_steps=0,
                           generator=torch.Generator(device=gpu).manual_seed(0))
     assert len(out.images) == 1 and torch.isfinite(out.latents).all()
+    out = guided.run_sega(pipe, prompt="a", num_inference_steps=3, editing_prompt=["b", "c"], edit_warmup_steps=0,
+                          generator=torch.Generator(device=gpu).manual_seed(0))
+    assert len(out.images) == 1 and torch.isfinite(out.latents).all()
+
+
+def _sega_reference(i, e_u, e_t, edits, gs, opt, mom, n_steps):
+    """diffusers 0.16.1 SemanticStableDiffusionPipeline's edit-guidance block,
+    transcribed on [b, C, H, W] tensors (the layout diffusers uses)."""
+    k = len(edits)
+    lst = lambda v: list(v) if isinstance(v, (list, tuple)) else [v] * k  # noqa: E731
+    scale, warmup, thr, rev = lst(opt["edit_guidance_scale"]), lst(opt["edit_warmup_steps"]), \
+        lst(opt["edit_threshold"]), lst(opt["reverse_editing_direction"])
+    cool = [n_steps + 1 if v is None else v for v in lst(opt["edit_cooldown_steps"])]
+    wts = lst(opt["edit_weights"]) if opt["edit_weights"] is not None else [1.0] * k
+    ng = gs * (e_t - e_u)
+    cw = torch.zeros(k, ng.shape[0])
+    nge = torch.zeros((k,) + tuple(ng.shape))
+    warm = []
+    for c, ec in enumerate(edits):
+        if i >= warmup[c]:
+            warm.append(c)
+        if i >= cool[c]:
+            nge[c] = torch.zeros_like(ec)
+            continue
+        t = ec - e_u
+        if rev[c]:
+            t = t * -1
+        cw[c, :] = wts[c]
+        t = t * scale[c]
+        q = torch.quantile(torch.abs(t).flatten(start_dim=2), thr[c], dim=2, keepdim=False)
+        nge[c] = torch.where(torch.abs(t) >= q[:, :, None, None], t, torch.zeros_like(t))
+    wi = torch.tensor(warm, dtype=torch.long)
+    if k > wi.shape[0] > 0:
+        cwt = torch.index_select(cw, 0, wi)
+        cwt = torch.where(cwt < 0, torch.zeros_like(cwt), cwt)
+        cwt = cwt / cwt.sum(dim=0)
+        ng = ng + torch.einsum("cb,cbijk->bijk", cwt, torch.index_select(nge, 0, wi))
+    cw = torch.nan_to_num(torch.where(cw < 0, torch.zeros_like(cw), cw))
+    edit = torch.einsum("cb,cbijk->bijk", cw, nge) + opt["edit_momentum_scale"] * mom
+    mom = opt["edit_mom_beta"] * mom + (1 - opt["edit_mom_beta"]) * edit
+    if wi.shape[0] == k:
+        ng = ng + edit
+    return ng, mom
+
+
+@pytest.mark.parametrize("opt", [
+    dict(edit_guidance_scale=5.0, edit_warmup_steps=1, edit_cooldown_steps=None, edit_threshold=0.9,
+         reverse_editing_direction=False, edit_weights=None, edit_momentum_scale=0.1, edit_mom_beta=0.4),
+    dict(edit_guidance_scale=[3.0, 7.0], edit_warmup_steps=[0, 2], edit_cooldown_steps=[None, 3],
+         edit_threshold=[0.8, 0.95], reverse_editing_direction=[True, False], edit_weights=[0.7, 1.6],
+         edit_momentum_scale=0.3, edit_mom_beta=0.6),
+])
+def test_sega_guidance_matches_the_diffusers_block(opt):
+    torch.manual_seed(0)
+    b, C, H, W, steps = 2, 4, 8, 8, 5
+    k = 2 if isinstance(opt["edit_guidance_scale"], list) else 1
+    st = guided.SegaState(k, steps, **opt)
+    mom = torch.zeros(b, C, H, W)
+    for i in range(steps):
+        e_u, e_t = torch.randn(b, C, H, W), torch.randn(b, C, H, W)
+        edits = [torch.randn(b, C, H, W) for _ in range(k)]
+        want, mom = _sega_reference(i, e_u, e_t, edits, 7.5, opt, mom, steps)
+        nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731  (this repo's latent layout)
+        got = st.guidance(i, nhwc(e_u), nhwc(e_t), [nhwc(e) for e in edits], 7.5)
+        assert torch.allclose(got, nhwc(want), atol=1e-5, rtol=1e-5), (i, (got - nhwc(want)).abs().max())
+
+
+def test_sega_pipeline():
+    pipe = StableDiffusion("tiny", device="cpu", seed=7)
+    kw = dict(prompt="a house", num_inference_steps=4, guidance_scale=6.0, output_type="latent")
+    ref = pipe(generator=torch.Generator().manual_seed(0), **kw).latents
+    plain = guided.run_sega(pipe, generator=torch.Generator().manual_seed(0), **kw)  # no editing prompt
+    assert torch.equal(plain.latents, ref)
+    # edits still warming up for every step: the CFG-(2 + k) batch gives the plain CFG result
+    warm = guided.run_sega(pipe, editing_prompt=["snow", "night"], edit_warmup_steps=100,
+                           generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.allclose(warm.latents, ref, atol=1e-5, rtol=1e-5), (warm.latents - ref).abs().max()
+    on = guided.run_sega(pipe, editing_prompt="snow", edit_warmup_steps=0,
+                         generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.isfinite(on.latents).all() and not torch.allclose(on.latents, ref)
+    rev = guided.run_sega(pipe, editing_prompt="snow", edit_warmup_steps=0, reverse_editing_direction=True,
+                          generator=torch.Generator().manual_seed(0), **kw)
+    assert not torch.allclose(rev.latents, on.latents)
+    with pytest.raises(ValueError, match="edit_weights"):
+        guided.run_sega(pipe, editing_prompt=["a", "b"], edit_weights=[1.0], **kw)
+    g = torch.Generator().manual_seed(0)
+    res, cfg = diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type=guided.SEGA, prompt="a beach",
+                                            num_inference_steps=2, editing_prompt=["sunset"], edit_warmup_steps=0,
+                                            generator=g, scheduler_type="DDIMScheduler", upscale=False,
+                                            supports_xformers=True)
+    assert cfg["_pipeline_type"] == guided.SEGA and _size(res) == (64, 64)
