@@ -27,6 +27,8 @@ PIPELINE_TYPES = {
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline",
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
     "StableUnCLIPImg2ImgPipeline", "SemanticStableDiffusionPipeline",
+    # its __call__ is StableDiffusionPipeline's (edits happen through edit_model(), which no job reaches)
+    "StableDiffusionModelEditingPipeline",
 }
 # SD classes with their own sampling loop (pipelines/guided.py): never batched
 # with other jobs, never split across GPUs
@@ -36,7 +38,18 @@ GUIDED_PIPELINES = frozenset({"StableDiffusionPanoramaPipeline", "StableDiffusio
 # class (never silently run as plain SD)
 UNIMPLEMENTED_PIPELINES = {"KandinskyPipeline", "KandinskyImg2ImgPipeline", "KandinskyInpaintPipeline",
                            "KandinskyV22Pipeline", "UnCLIPPipeline", "UnCLIPImageVariationPipeline",
-                           "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline"}
+                           "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline",
+                           # diffusers 0.16.1 classes needing gradients through the UNet, their own
+                           # model families or packages the reference does not install
+                           "StableDiffusionAttendAndExcitePipeline", "StableDiffusionPix2PixZeroPipeline",
+                           "StableDiffusionKDiffusionPipeline", "PaintByExamplePipeline", "StableUnCLIPPipeline",
+                           "VersatileDiffusionPipeline", "VersatileDiffusionTextToImagePipeline",
+                           "VersatileDiffusionImageVariationPipeline", "VersatileDiffusionDualGuidedPipeline",
+                           "LDMTextToImagePipeline", "LDMSuperResolutionPipeline", "DiTPipeline",
+                           "VQDiffusionPipeline", "RePaintPipeline", "DDPMPipeline", "DDIMPipeline",
+                           "PNDMPipeline", "ScoreSdeVePipeline", "KarrasVePipeline", "DanceDiffusionPipeline",
+                           "AudioDiffusionPipeline", "SpectrogramDiffusionPipeline", "LDMPipeline",
+                           "StableDiffusionOnnxPipeline", "OnnxStableDiffusionPipeline"}
 
 
 class PipelineType(str):

@@ -28,10 +28,22 @@ def _size(res):
     return Image.open(io.BytesIO(base64.b64decode(res["primary"]["blob"]))).size
 
 
-@pytest.mark.parametrize("cls", ["KandinskyPipeline", "UnCLIPPipeline", "AltDiffusionPipeline"])
+@pytest.mark.parametrize("cls", ["KandinskyPipeline", "UnCLIPPipeline", "AltDiffusionPipeline",
+                                 "StableDiffusionAttendAndExcitePipeline", "PaintByExamplePipeline"])
 def test_unimplemented_classes_are_fatal(cls):
     with pytest.raises(ValueError, match=cls):
         router.format_args({"model_name": "m", "parameters": {"pipeline_type": cls}})
+
+
+def test_model_editing_class_runs_as_plain_sd():
+    """StableDiffusionModelEditingPipeline.__call__ is StableDiffusionPipeline's
+    (the edits go through edit_model(), which a job cannot call): same image."""
+    kw = dict(prompt="a", num_inference_steps=2, scheduler_type="DDIMScheduler", upscale=False, supports_xformers=True)
+    a, _ = diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type="StableDiffusionPipeline",
+                                        generator=torch.Generator().manual_seed(0), **kw)
+    b, cfg = diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type="StableDiffusionModelEditingPipeline",
+                                          generator=torch.Generator().manual_seed(0), **kw)
+    assert a["primary"]["blob"] == b["primary"]["blob"]
 
 
 def test_class_resolution():
