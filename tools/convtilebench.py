@@ -18,7 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--rw", action="store_true", help="also time the per-unit weight DMA variant (csk_set_conv_tile_no_rw)")
+    ap.add_argument("--rw", action="store_true", help="also time the per-unit weight DMA, 8-row tile variant (switch 3)")
+    ap.add_argument("--switch", default="", help="','-separated extra csk_set_conv_tile_no_rw values to time (bit 0: per-unit weight DMA, bit 1: 8-row tiles)")
     ap.add_argument("--shapes", default="", help="';'-separated hw,cin,cout (default: the four Cout = 32 convs)")
     a = ap.parse_args()
     _lib.load()
@@ -32,7 +33,8 @@ def main():
         wp = ops.pack_conv_weight((torch.randn(cout, cin, 3, 3, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16))
         b = torch.randn(cout, device=dev).to(torch.bfloat16)
         res = {}
-        arms = [(True, 0), (False, 0)] + ([(True, 3)] if a.rw else [])
+        extra = [int(v) for v in a.switch.split(",") if v]
+        arms = [(True, 0), (False, 0)] + ([(True, 3)] if a.rw else []) + [(True, v) for v in extra]
         for tile, no_rw in arms:
             hip_ops.CONV_TILE = tile
             _lib.call("csk_set_conv_tile_no_rw", no_rw)
@@ -51,9 +53,10 @@ def main():
         del buf
         fl = 2.0 * hw * hw * cout * 9 * cin
         t, g = res[(True, 0)], res[(False, 0)]
-        extra = (f"   per-unit weight DMA, 8-row tiles {res[(True, 3)]:7.1f} us" if a.rw else "")
+        extra_s = (f"   per-unit weight DMA, 8-row tiles {res[(True, 3)]:7.1f} us" if a.rw else "")
+        extra_s += "".join(f"   switch {v}: {res[(True, v)]:7.1f} us" for v in extra)
         print(f"conv {hw}x{hw} {cin}->{cout}: halo-tile {t:7.1f} us ({fl / t / 1e6:6.1f} TF/s)   "
-              f"implicit GEMM {g:7.1f} us ({fl / g / 1e6:6.1f} TF/s){extra}", flush=True)
+              f"implicit GEMM {g:7.1f} us ({fl / g / 1e6:6.1f} TF/s){extra_s}", flush=True)
     _lib.call("csk_set_conv_tile_no_rw", 0)
     hip_ops.CONV_TILE = True
     hip_ops.CONV_TILE64 = False
