@@ -85,3 +85,25 @@ def test_bench_through_supervisor_cpu(tmp_path):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["p50_job_latency_ms"] > 0
     assert "Supervisor" in rec["path"] and rec["config"]["global_batch"] == 2
+
+
+def test_bench_under_torchrun_cpu():
+    """The driver's launch form: ``python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus
+    N ...`` — ranks come from torchrun's env, rank 0 prints the one line."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--device", "cpu", "--family", "tiny", "--steps", "2", "--warmup", "1", "--denoise-steps", "2",
+                        "--res", "64", "--batch", "1"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["parallelism"] == "dp2" and len(rec["ms_per_step_per_rank"]) == 2
