@@ -28,20 +28,21 @@ PIPELINE_TYPES = {
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
     "StableUnCLIPImg2ImgPipeline", "SemanticStableDiffusionPipeline",
     # its __call__ is StableDiffusionPipeline's (edits happen through edit_model(), which no job reaches)
-    "StableDiffusionModelEditingPipeline",
+    "StableDiffusionModelEditingPipeline", "StableDiffusionAttendAndExcitePipeline",
 }
 # SD classes with their own sampling loop (pipelines/guided.py): never batched
 # with other jobs, never split across GPUs
 GUIDED_PIPELINES = frozenset({"StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline",
-                              "StableDiffusionPipelineSafe", "SemanticStableDiffusionPipeline"})
+                              "StableDiffusionPipelineSafe", "SemanticStableDiffusionPipeline",
+                              "StableDiffusionAttendAndExcitePipeline"})
 # real diffusers classes with no implementation here: a fatal error naming the
 # class (never silently run as plain SD)
 UNIMPLEMENTED_PIPELINES = {"KandinskyPipeline", "KandinskyImg2ImgPipeline", "KandinskyInpaintPipeline",
                            "KandinskyV22Pipeline", "UnCLIPPipeline", "UnCLIPImageVariationPipeline",
                            "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline",
-                           # diffusers 0.16.1 classes needing gradients through the UNet, their own
+                           # diffusers 0.16.1 classes needing an inversion / captioner loop, their own
                            # model families or packages the reference does not install
-                           "StableDiffusionAttendAndExcitePipeline", "StableDiffusionPix2PixZeroPipeline",
+                           "StableDiffusionPix2PixZeroPipeline",
                            "StableDiffusionKDiffusionPipeline", "PaintByExamplePipeline", "StableUnCLIPPipeline",
                            "VersatileDiffusionPipeline", "VersatileDiffusionTextToImagePipeline",
                            "VersatileDiffusionImageVariationPipeline", "VersatileDiffusionDualGuidedPipeline",

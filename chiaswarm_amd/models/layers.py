@@ -193,6 +193,10 @@ class Attention(Prepared):
         h, d = self.heads, self.dim_head
         if kv is None:  # no context given: attend to itself (diffusers attn2 semantics)
             kv = self.context_kv(ctx)
+        store = self.__dict__.get("_store_probs")
+        if store is not None:  # Attend-and-Excite (pipelines/guided.py): softmax(q k^T), fp32, in the autograd graph
+            qf, kf = q.view(b, s, h, d).float().transpose(1, 2), kv[:, :, 0].float().transpose(1, 2)
+            store.append(torch.softmax(qf @ kf.transpose(-1, -2) * self.scale, dim=-1))
         o = ops.attention(q.view(b, s, h, d), kv[:, :, 0], kv[:, :, 1], self.scale)
         return self.to_out[0](o.reshape(b, s, h * d), residual=residual, row_stats=row_stats)
 

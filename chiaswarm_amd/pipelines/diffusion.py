@@ -39,7 +39,7 @@ SD_CLASSES = {
     "StableDiffusionDepth2ImgPipeline", "StableDiffusionImageVariationPipeline", "StableUnCLIPImg2ImgPipeline",
     # sampling-loop variants on a plain SD checkpoint (pipelines/guided.py)
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
-    "SemanticStableDiffusionPipeline", "StableDiffusionModelEditingPipeline",
+    "SemanticStableDiffusionPipeline", "StableDiffusionModelEditingPipeline", "StableDiffusionAttendAndExcitePipeline",
 }
 # checkpoints whose own class must win over a generic requested one (the
 # router defaults an image job to StableDiffusionImg2ImgPipeline; these

@@ -38,6 +38,16 @@ checkpoint on the resident bundle; only the denoising loop differs.
   that are past warm-up while others still warm up), with momentum, and added
   to the CFG direction between ``edit_warmup_steps`` and
   ``edit_cooldown_steps``.  The UNet runs as one CFG-(2 + k) evaluation.
+* ``StableDiffusionAttendAndExcitePipeline`` (Chefer et al. 2023; diffusers
+  0.16.1): for the first ``max_iter_to_alter`` steps the text-conditioned UNet
+  runs once more with autograd (the torch implementation of every op: the HIP
+  kernels have no backward), the cross-attention maps at 16 x 16 queries are
+  averaged over heads and layers, softmaxed over the prompt tokens (x100,
+  start / end token dropped), Gaussian-smoothed, and the latents take a
+  gradient step against max over ``token_indices`` of (1 - max attention),
+  step ``scale_factor * sqrt(linspace(1, 0.5))``, with up to 20 refinement
+  iterations at the ``thresholds`` steps; the denoising step itself is the
+  plain CFG graph.
 
 Parity against diffusers is unpinned (diffusers is not importable here); the
 CPU tests pin the window geometry, the per-window sampler independence, the
@@ -57,7 +67,8 @@ PANORAMA = "StableDiffusionPanoramaPipeline"
 SAG = "StableDiffusionSAGPipeline"
 SAFE = "StableDiffusionPipelineSafe"
 SEGA = "SemanticStableDiffusionPipeline"
-CLASSES = (PANORAMA, SAG, SAFE, SEGA)
+AE = "StableDiffusionAttendAndExcitePipeline"
+CLASSES = (PANORAMA, SAG, SAFE, SEGA, AE)
 
 # StableDiffusionPipelineSafe's default safety concept (Schramowski et al. 2023, I2P categories)
 SAFETY_CONCEPT = ("an image showing hate, harassment, violence, suffering, humiliation, harm, suicide, sexual, nudity,"
@@ -339,6 +350,120 @@ def sega_denoise(pipe, x, sched, cross_kv, guidance, added, generator, edit_kv, 
     return x
 
 
+def ae_gauss_kernel(kernel_size=3, sigma=0.5):
+    """The prompt-to-prompt GaussianSmoothing kernel diffusers' A&E uses:
+    exp(-((x - mu) / (2 sigma))^2) per axis (its quirk: 2 sigma, not 2 sigma^2),
+    outer product, normalised to sum 1."""
+    g = torch.arange(kernel_size, dtype=torch.float32) - (kernel_size - 1) / 2
+    g = torch.exp(-((g / (2 * sigma)) ** 2)) / (sigma * math.sqrt(2 * math.pi))
+    k = g[:, None] * g[None, :]
+    return k / k.sum()
+
+
+def ae_max_attention(maps, indices, res):
+    """Per token index, the max over the (res x res) map of the smoothed,
+    token-softmaxed cross-attention (diffusers 0.16.1
+    _compute_max_attention_per_index on AttentionStore.aggregate_attention)."""
+    a = torch.cat([m.reshape(-1, res, res, m.shape[-1]) for m in maps], 0)
+    a = a.sum(0) / a.shape[0]
+    t = torch.softmax(a[:, :, 1:-1] * 100, dim=-1)
+    ker = ae_gauss_kernel().to(t)[None, None]
+    out = []
+    for i in indices:
+        img = F.pad(t[:, :, int(i) - 1][None, None], (1, 1, 1, 1), mode="reflect")
+        out.append(F.conv2d(img, ker)[0, 0].max())
+    return out
+
+
+def ae_loss(maxes):
+    return torch.stack([torch.clamp(1.0 - m, min=0.0) for m in maxes]).max()
+
+
+@contextlib.contextmanager
+def _reference_ops():
+    from .. import ops
+
+    prev = ops.get_mode()
+    ops.set_mode("reference")
+    try:
+        yield
+    finally:
+        ops.set_mode(prev)
+
+
+def _ae_maxes(pipe, x, t, kv_cond, indices, res):
+    """One text-conditioned UNet pass with autograd from ``x`` (leaf with
+    grad): the maxima per token index, in the graph."""
+    from ..models.layers import Attention
+
+    mods = [m for m in pipe.unet.modules() if isinstance(m, Attention) and m.is_cross]
+    store: list = []
+    for m in mods:
+        m._store_probs = store
+    try:
+        with torch.enable_grad(), _reference_ops():
+            tt = torch.tensor([float(t)], device=x.device, dtype=torch.float32)
+            pipe.unet(x.to(pipe.dtype), tt, cross_kv=kv_cond, added_cond=None)
+    finally:
+        for m in mods:
+            m.__dict__.pop("_store_probs", None)
+    maps = [p for p in store if p.shape[-2] == res * res]
+    if not maps:
+        raise ValueError(f"{AE}: no cross-attention maps at {res} x {res} (attn_res) for this image size")
+    with torch.enable_grad():
+        return ae_max_attention(maps, indices, res)
+
+
+def _ae_step(x, loss, step):
+    g, = torch.autograd.grad(loss, [x])
+    return (x - step * g).detach().requires_grad_(True)
+
+
+def ae_denoise(pipe, x, sched, cross_kv, guidance, added, generator, token_indices, max_iter_to_alter=25,
+               thresholds=None, scale_factor=20.0, attn_res=16, max_refinement_steps=20):
+    """Attend-and-Excite loop (diffusers 0.16.1 __call__ / _perform_iterative_refinement_step)."""
+    import numpy as np
+
+    thresholds = {0: 0.05, 10: 0.5, 20: 0.8} if thresholds is None else {int(k): float(v)
+                                                                         for k, v in thresholds.items()}
+    b = x.shape[0]
+    cfg = guidance > 1.0
+    kv_cond = [kv[b:] if cfg else kv for kv in cross_kv]
+    steps = scale_factor * np.sqrt(np.linspace(1.0, 0.5, sched.n))
+    i = 0
+    while sched.step_index < sched.n:
+        t = sched.current_t()
+        if i < max_iter_to_alter:
+            with torch.enable_grad():  # (the pipeline's denoise runs under no_grad)
+                xg = x.detach().requires_grad_(True)
+                maxes = _ae_maxes(pipe, xg, t, kv_cond, token_indices, attn_res)
+                loss = ae_loss(maxes)
+                if i in thresholds and loss.item() > 1.0 - thresholds[i]:
+                    target, it = max(0.0, 1.0 - thresholds[i]), 0
+                    while loss.item() > target:
+                        it += 1
+                        xg = xg.detach().requires_grad_(True)
+                        loss = ae_loss(_ae_maxes(pipe, xg, t, kv_cond, token_indices, attn_res))
+                        if loss.item() != 0:
+                            xg = _ae_step(xg, loss, float(steps[i]))
+                        if it >= max_refinement_steps:
+                            break
+                    xg = xg.detach().requires_grad_(True)  # one more pass: the loss the step below uses
+                    maxes = _ae_maxes(pipe, xg, t, kv_cond, token_indices, attn_res)
+                loss = ae_loss(maxes)
+                if loss.item() != 0:
+                    xg = _ae_step(xg, loss, float(steps[i]))
+            x = xg.detach()
+        xi = (x * sched.current_scale()).to(pipe.dtype)
+        e = pipe._unet_eval(torch.cat([xi, xi], 0) if cfg else xi, t, cross_kv, added).float()
+        if cfg:
+            e_u, e_t = e.chunk(2)
+            e = e_u + guidance * (e_t - e_u)
+        x = sched.step(e, x, generator)
+        i += 1
+    return x
+
+
 @contextlib.contextmanager
 def _override(pipe, denoise, decode=None):
     pipe._denoise_override = denoise
@@ -461,7 +586,32 @@ def run_sega(pipe, editing_prompt=None, editing_prompt_embeddings=None, reverse_
         return pipe(**kwargs)
 
 
+def run_attend_and_excite(pipe, token_indices=None, max_iter_to_alter=25, thresholds=None, scale_factor=20,
+                          attn_res=16, **kwargs):
+    """``StableDiffusionAttendAndExcitePipeline.__call__`` (one prompt, one image,
+    as diffusers 0.16.1 runs it: its gradient pass takes prompt_embeds[1])."""
+    _check(pipe, AE, kwargs)
+    if token_indices is None or not list(token_indices):
+        raise TypeError(f"{AE}.__call__() missing required argument 'token_indices'")
+    idx = [int(i) for i in token_indices]
+    if min(idx) < 1 or max(idx) > 75:
+        raise ValueError(f"{AE}: token_indices must lie in 1..75 (prompt tokens after the start token)")
+    prompt = kwargs.get("prompt", "")
+    if isinstance(prompt, list) and len(prompt) != 1 or int(kwargs.get("num_images_per_prompt", 1) or 1) != 1:
+        raise ValueError(f"{AE} runs one prompt and one image per call")
+    opts = dict(token_indices=idx, max_iter_to_alter=int(max_iter_to_alter), thresholds=thresholds,
+                scale_factor=float(scale_factor), attn_res=int(attn_res))
+
+    def denoise(p, x, sched, cross_kv, guidance, added, generator, **_):
+        return ae_denoise(p, x, sched, cross_kv, guidance, added, generator, **opts)
+
+    with _override(pipe, denoise):
+        return pipe(**kwargs)
+
+
 def run(cls, pipe, **kwargs):
+    if cls == AE:
+        return run_attend_and_excite(pipe, **kwargs)
     if cls == PANORAMA:
         return run_panorama(pipe, **kwargs)
     if cls == SAFE:

@@ -29,7 +29,7 @@ def _size(res):
 
 
 @pytest.mark.parametrize("cls", ["KandinskyPipeline", "UnCLIPPipeline", "AltDiffusionPipeline",
-                                 "StableDiffusionAttendAndExcitePipeline", "PaintByExamplePipeline"])
+                                 "StableDiffusionPix2PixZeroPipeline", "PaintByExamplePipeline"])
 def test_unimplemented_classes_are_fatal(cls):
     with pytest.raises(ValueError, match=cls):
         router.format_args({"model_name": "m", "parameters": {"pipeline_type": cls}})

@@ -1,7 +1,7 @@
 """Sampling-loop variant classes (pipelines/guided.py):
 StableDiffusionPanoramaPipeline (MultiDiffusion), StableDiffusionSAGPipeline
-(self-attention guidance), StableDiffusionPipelineSafe (safe latent diffusion) and
-SemanticStableDiffusionPipeline (SEGA), reachable by class name like every diffusers class
+(self-attention guidance), StableDiffusionPipelineSafe (safe latent diffusion),
+SemanticStableDiffusionPipeline (SEGA) and StableDiffusionAttendAndExcitePipeline, reachable by class name like every diffusers class
 the reference builds by reflection (swarm/job_arguments.py:143-145,
 swarm/type_helpers.py:1-3).
 
@@ -198,6 +198,15 @@ def test_panorama_and_sag_on_gpu(gpu):
     out = guided.run_sega(pipe, prompt="a", num_inference_steps=3, editing_prompt=["b", "c"], edit_warmup_steps=0,
                           generator=torch.Generator(device=gpu).manual_seed(0))
     assert len(out.images) == 1 and torch.isfinite(out.latents).all()
+    # Attend-and-Excite: the gradient passes run the torch implementation of the ops on the HIP-prepared
+    # model (mode switched for those passes only), the denoising steps the HIP graph
+    from chiaswarm_amd import ops
+
+    kw = dict(prompt="a cat and a frog", num_inference_steps=3, height=128, width=128, output_type="latent")
+    ref = pipe(generator=torch.Generator(device=gpu).manual_seed(0), **kw).latents
+    out = guided.run_attend_and_excite(pipe, token_indices=[2, 5], max_iter_to_alter=2, thresholds={0: 0.99},
+                                       generator=torch.Generator(device=gpu).manual_seed(0), **kw)
+    assert ops.get_mode() == "hip" and torch.isfinite(out.latents).all() and not torch.allclose(out.latents, ref)
 
 
 def _sega_reference(i, e_u, e_t, edits, gs, opt, mom, n_steps):
@@ -286,3 +295,44 @@ def test_sega_pipeline():
                                             generator=g, scheduler_type="DDIMScheduler", upscale=False,
                                             supports_xformers=True)
     assert cfg["_pipeline_type"] == guided.SEGA and _size(res) == (64, 64)
+
+
+def test_attend_and_excite_pieces():
+    k = guided.ae_gauss_kernel()
+    g = torch.exp(-((torch.tensor([-1.0, 0.0, 1.0]) / 1.0) ** 2))  # (x / (2 * 0.5))^2
+    want = g[:, None] * g[None, :]
+    assert torch.allclose(k, want / want.sum(), atol=1e-7)
+    # one map, all queries attend to token 3 (index 3 = the 3rd prompt token): its max is ~1, the others ~0
+    res, skv = 4, 8
+    p = torch.full((1, 2, res * res, skv), 1e-4)
+    p[..., 3] = 1.0
+    m = guided.ae_max_attention([p], [3, 5], res)
+    assert m[0].item() > 0.99 and m[1].item() < 0.01
+    assert abs(guided.ae_loss(m).item() - (1 - m[1].item())) < 1e-6
+
+
+def test_attend_and_excite_pipeline():
+    pipe = StableDiffusion("tiny", device="cpu", seed=8)
+    kw = dict(prompt="a cat and a frog", num_inference_steps=4, guidance_scale=6.0, height=128, width=128,
+              output_type="latent")
+    ref = pipe(generator=torch.Generator().manual_seed(0), **kw).latents
+    off = guided.run_attend_and_excite(pipe, token_indices=[2, 5], max_iter_to_alter=0,
+                                       generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.allclose(off.latents, ref, atol=1e-5, rtol=1e-5), (off.latents - ref).abs().max()
+    on = guided.run_attend_and_excite(pipe, token_indices=[2, 5], max_iter_to_alter=3, thresholds={"0": 0.99},
+                                      generator=torch.Generator().manual_seed(0), **kw)
+    assert torch.isfinite(on.latents).all() and not torch.allclose(on.latents, ref)
+    for m in pipe.unet.modules():
+        assert "_store_probs" not in m.__dict__
+    with pytest.raises(TypeError, match="token_indices"):
+        guided.run_attend_and_excite(pipe, **kw)
+    with pytest.raises(ValueError, match="one prompt"):
+        guided.run_attend_and_excite(pipe, token_indices=[2], num_images_per_prompt=2, **kw)
+    with pytest.raises(ValueError, match="attn_res"):  # 64 px: no 16 x 16 maps
+        guided.run_attend_and_excite(pipe, token_indices=[2], prompt="a", num_inference_steps=2, height=64, width=64)
+    g = torch.Generator().manual_seed(0)
+    res, cfg = diffusion.diffusion_callback("cpu", "tiny/sd", pipeline_type=guided.AE, prompt="a red cube",
+                                            token_indices=[2], max_iter_to_alter=1, height=128, width=128,
+                                            num_inference_steps=2, generator=g, scheduler_type="DDIMScheduler",
+                                            upscale=False, supports_xformers=True)
+    assert cfg["_pipeline_type"] == guided.AE and _size(res) == (128, 128)
