@@ -29,6 +29,7 @@ PIPELINE_TYPES = {
     "StableUnCLIPImg2ImgPipeline", "SemanticStableDiffusionPipeline",
     # its __call__ is StableDiffusionPipeline's (edits happen through edit_model(), which no job reaches)
     "StableDiffusionModelEditingPipeline", "StableDiffusionAttendAndExcitePipeline",
+    "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline",
 }
 # SD classes with their own sampling loop (pipelines/guided.py): never batched
 # with other jobs, never split across GPUs
@@ -39,7 +40,6 @@ GUIDED_PIPELINES = frozenset({"StableDiffusionPanoramaPipeline", "StableDiffusio
 # class (never silently run as plain SD)
 UNIMPLEMENTED_PIPELINES = {"KandinskyPipeline", "KandinskyImg2ImgPipeline", "KandinskyInpaintPipeline",
                            "KandinskyV22Pipeline", "UnCLIPPipeline", "UnCLIPImageVariationPipeline",
-                           "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline",
                            # diffusers 0.16.1 classes needing an inversion / captioner loop, their own
                            # model families or packages the reference does not install
                            "StableDiffusionPix2PixZeroPipeline",

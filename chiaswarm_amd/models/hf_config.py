@@ -24,6 +24,7 @@ import json
 import os
 
 from .clip import CLIPTextConfig
+from .xlmr import is_xlmr_config, xlmr_text_config
 from .unet import UNetConfig
 from .vae import VAEConfig
 
@@ -217,8 +218,16 @@ def pipeline_spec(weights_dir: str) -> PipelineSpec | None:
         if tc is None:
             raise UnsupportedConfig(f"{weights_dir}: {sub}/config.json is missing")
         cls = (comps[sub][1] if len(comps[sub]) > 1 else "") or ""
+        if cls == "RobertaSeriesModelWithTransformation" or (not cls.startswith("CLIPTextModel")
+                                                             and is_xlmr_config(tc)):
+            # AltDiffusion: XLM-RoBERTa + transformation (models/xlmr.py)
+            text.append(xlmr_text_config(tc, sub))
+            names.append(sub)
+            pads.append("<pad>")
+            continue
         if cls and not cls.startswith("CLIPTextModel"):
-            raise UnsupportedConfig(f"{sub}: {cls} is not supported (CLIPTextModel[WithProjection] only)")
+            raise UnsupportedConfig(f"{sub}: {cls} is not supported (CLIPTextModel[WithProjection] / "
+                                    "RobertaSeriesModelWithTransformation only)")
         if cls == "CLIPTextModelWithProjection":
             tc = dict(tc)
             tc.setdefault("architectures", [cls])

@@ -224,7 +224,7 @@ def load_sd_weights(pipe, weights_dir: str) -> bool:
     tnames = fam.text_components if fam is not None else \
         ["text_encoder" if i == 0 else f"text_encoder_{i + 1}" for i in range(len(pipe.text_encoders))]
     for name, te in zip(tnames, pipe.text_encoders):
-        parts.append((name, te, None))
+        parts.append((name, te, getattr(te, "hf_renames", None)))  # (AltDiffusion's XLM-R: transformers names)
     present = [sub for sub, _, _ in parts if weight_files(os.path.join(weights_dir, sub))[1]]
     if not present:
         return False
@@ -259,5 +259,5 @@ def tokenizer_dir(weights_dir: str | None, sub: str = "tokenizer") -> str | None
     if not weights_dir:
         return None
     d = os.path.join(weights_dir, sub)
-    return d if os.path.exists(os.path.join(d, "vocab.json")) or os.path.exists(os.path.join(d, "spiece.model")) \
-        else None
+    return d if any(os.path.exists(os.path.join(d, f)) for f in ("vocab.json", "spiece.model",
+                                                                  "sentencepiece.bpe.model")) else None

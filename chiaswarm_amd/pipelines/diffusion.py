@@ -40,6 +40,8 @@ SD_CLASSES = {
     # sampling-loop variants on a plain SD checkpoint (pipelines/guided.py)
     "StableDiffusionPanoramaPipeline", "StableDiffusionSAGPipeline", "StableDiffusionPipelineSafe",
     "SemanticStableDiffusionPipeline", "StableDiffusionModelEditingPipeline", "StableDiffusionAttendAndExcitePipeline",
+    # SD1.x UNet + XLM-RoBERTa text encoder (models/xlmr.py)
+    "AltDiffusionPipeline", "AltDiffusionImg2ImgPipeline",
 }
 # checkpoints whose own class must win over a generic requested one (the
 # router defaults an image job to StableDiffusionImg2ImgPipeline; these
@@ -87,7 +89,8 @@ def pipeline_class_for(pipeline_type: str, model_name: str, revision: str = "mai
         ck = checkpoint_class(model_name, revision)
         if ck in UPSCALE_CLASSES or (ck is not None and ck not in SD_CLASSES) or ck in _OWN_CLASS:
             cls = ck
-    elif cls in ("StableDiffusionPipeline", "StableDiffusionImg2ImgPipeline"):
+    elif cls in ("StableDiffusionPipeline", "StableDiffusionImg2ImgPipeline", "AltDiffusionPipeline",
+                 "AltDiffusionImg2ImgPipeline"):
         ck = checkpoint_class(model_name, revision)
         if ck in _OWN_CLASS:
             cls = ck

@@ -34,6 +34,7 @@ from ..models import unet as unet_mod
 from ..models import vae as vae_mod
 from ..models.layers import init_random_fast_, prepare_model
 from ..models.tokenizer import CLIPTokenizer
+from ..models.xlmr import TINY_XLMR, XLMR_LARGE, XLMRConfig, XLMRobertaSeries, XLMRTokenizer
 from ..schedulers import Scheduler, batch_randn, get_scheduler
 from ..utils.trace import trace_range
 
@@ -148,7 +149,12 @@ FAMILIES = {
     "sd21-unclip": Family("sd21-unclip", unet_mod.SD21_UNCLIP, vae_mod.SD_VAE, [clip_mod.OPENCLIP_H],
                           pad_with_eos=False, default_size=768, prediction_type="v_prediction",
                           pipeline_class="StableUnCLIPImg2ImgPipeline"),
+    # AltDiffusion (BAAI): the SD1.x UNet / VAE conditioned on XLM-RoBERTa-large + transformation
+    "altdiffusion": Family("altdiffusion", unet_mod.SD15, vae_mod.SD_VAE, [XLMR_LARGE], pad_with_eos=False,
+                           pipeline_class="AltDiffusionPipeline"),
     "tiny": Family("tiny", unet_mod.TINY, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64),
+    "tiny-alt": Family("tiny-alt", unet_mod.TINY, vae_mod.TINY_VAE, [TINY_XLMR], default_size=64, pad_with_eos=False,
+                       pipeline_class="AltDiffusionPipeline"),
     "tiny-unclip": Family("tiny-unclip", unet_mod.TINY_UNCLIP, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT],
                           default_size=64, pipeline_class="StableUnCLIPImg2ImgPipeline"),
     "tiny-depth": Family("tiny-depth", unet_mod.TINY_DEPTH, vae_mod.TINY_VAE, [clip_mod.TINY_TEXT], default_size=64,
@@ -169,9 +175,13 @@ def family_for_model(model_name: str) -> str:
     checkpoint is built from its own config files (``resolve_family``)."""
     n = model_name.lower()
     if n.startswith("tiny/") or n == "tiny":
+        if "altdiffusion" in n:
+            return "tiny-alt"
         if "unclip" in n:
             return "tiny-unclip"
         return "tiny-depth" if "depth" in n else ("tiny-imagevar" if "variation" in n else "tiny")
+    if "altdiffusion" in n:
+        return "altdiffusion"
     if "unclip" in n:
         return "sd21-unclip"
     if "image-variations" in n:
@@ -234,7 +244,8 @@ class StableDiffusion:
         with torch.device(self.device):
             self.unet = unet_mod.UNet2DConditionModel(fam.unet).to(dtype)
             self.vae = vae_mod.AutoencoderKL(fam.vae, with_encoder=with_encoder).to(dtype)
-            self.text_encoders = [clip_mod.CLIPTextModel(c).to(dtype) for c in fam.text]
+            self.text_encoders = [(XLMRobertaSeries(c) if isinstance(c, XLMRConfig) else clip_mod.CLIPTextModel(c))
+                                  .to(dtype) for c in fam.text]
         for i, m in enumerate([self.unet, self.vae] + self.text_encoders):
             m.eval().requires_grad_(False)
             init_random_fast_(m, seed=seed + i)
@@ -258,7 +269,8 @@ class StableDiffusion:
             # real text-encoder weights fed hash-fallback token ids = a random prompt
             raise CheckpointMismatch(f"{weights_dir}: tokenizer files (vocab.json / merges.txt) missing for "
                                      f"{[t for t, d in zip(tnames, tdirs) if d is None]}")
-        self.tokenizers = [CLIPTokenizer(tdirs[i], 77, pad_with_eos=fam.pad_with_eos and i == 0,
+        self.tokenizers = [XLMRTokenizer(tdirs[i], 77, vocab_size=c.vocab_size) if isinstance(c, XLMRConfig) else
+                           CLIPTokenizer(tdirs[i], 77, pad_with_eos=fam.pad_with_eos and i == 0,
                                          vocab_size=c.vocab_size)
                            for i, c in enumerate(fam.text)]
         self.controlnet = controlnet
@@ -311,7 +323,9 @@ class StableDiffusion:
         """(context, added_cond or None, cross-attention K/V tuple)."""
         texts = (negatives + prompts) if cfg else prompts
         ids = tuple(tok(texts).to(self.device) for tok in self.tokenizers)
-        if self.use_graphs and with_kv:
+        # (XLM-RoBERTa cuts each prompt's keys to its real tokens, a host-side
+        # length: that encoder runs eagerly, not as a captured graph)
+        if self.use_graphs and with_kv and not any(isinstance(c, XLMRConfig) for c in self.family.text):
             if not hasattr(self, "_text_graphs"):
                 from .graphs import GraphCache
 

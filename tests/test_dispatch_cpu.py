@@ -28,7 +28,7 @@ def _size(res):
     return Image.open(io.BytesIO(base64.b64decode(res["primary"]["blob"]))).size
 
 
-@pytest.mark.parametrize("cls", ["KandinskyPipeline", "UnCLIPPipeline", "AltDiffusionPipeline",
+@pytest.mark.parametrize("cls", ["KandinskyPipeline", "UnCLIPPipeline", "VersatileDiffusionPipeline",
                                  "StableDiffusionPix2PixZeroPipeline", "PaintByExamplePipeline"])
 def test_unimplemented_classes_are_fatal(cls):
     with pytest.raises(ValueError, match=cls):
