@@ -293,6 +293,34 @@ def test_sdxl_empty_negative_prompt_is_zero_embeddings():
         assert torch.allclose(c[0], a[0], rtol=1e-4, atol=1e-3) and torch.allclose(c[1], b[0], rtol=1e-4, atol=1e-3)
 
 
+def test_sdxl_zero_negative_kv_cache_matches_full_recompute():
+    """The zero-negative K/V rows come from a per-pipeline cache (a zero
+    context row's K/V is the projection bias): bitwise what re-running every
+    K/V projection on the zeroed context gave, for leading and non-leading
+    zero rows."""
+    from chiaswarm_amd.pipelines.sd import StableDiffusion
+
+    pipe = StableDiffusion("tiny-xl", device="cpu", seed=3)
+
+    def recompute(ctx, n):
+        idx = (ctx.abs().sum((1, 2)) == 0).nonzero().flatten()
+        return [t[idx].clone() for t in pipe.unet.encode_context(ctx)]
+
+    for negs in ([None, None], ["blurry", None], [None, "blurry"]):
+        kw = dict(prompt=["a fox", "a cat"], negative_prompt=negs, num_inference_steps=2, guidance_scale=6.0,
+                  output_type="latent")
+        a = pipe(generator=torch.Generator().manual_seed(0), **kw).latents
+        cached = pipe._zero_rows_kv
+        pipe._zero_rows_kv = recompute
+        try:
+            b = pipe(generator=torch.Generator().manual_seed(0), **kw).latents
+        finally:
+            pipe._zero_rows_kv = cached
+        assert torch.equal(a, b), negs
+    pipe.invalidate_graphs()
+    assert "_zero_kv" not in pipe.__dict__
+
+
 def test_txt2vid_uses_the_checkpoint_scheduler_config(monkeypatch):
     """reference: scheduler_type.from_config(pipeline.scheduler.config,
     use_karras_sigmas=True) (swarm/video/tx2vid.py:32-34)"""
